@@ -1,0 +1,145 @@
+/*
+ * slam_ekf.h — C-ABI of the MI355X-native EKF-SLAM update (libslam_ekf.so).
+ *
+ * Drop-in boundary for HuaiLeiTang/slam_ros `class Robot` (slam_ros/Robot.h:21-77). The
+ * reference has no FFI: its interface is the C++ class, so every entry point below names the
+ * member (file:line) it replaces. Plain pointers and sizes only; no GSL/ROS/torch types.
+ *
+ * One context = E independent EKF instances (an ensemble) of capacity N landmarks on one
+ * HIP device, one HIP stream. State n = 3 + 2N (Robot.h:13-14 LINESIZE/SLAMSIZE, runtime here).
+ * Contexts are not thread-safe (the reference is single-threaded, main.cpp:130-179).
+ *
+ * Errors: every call returns an int status (EKF_OK == 0). The reference's localize() returns
+ * void and only prints GSL error codes (Robot.cpp:128, 909-917); per-instance numeric
+ * conditions (singular S, capacity overflow) are reported in ekf_result.status instead, and
+ * the state is always committed, as in the reference.
+ */
+#ifndef SLAM_EKF_H
+#define SLAM_EKF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SLAM_EKF_ABI_VERSION 1
+#define EKF_MAX_LINES 64 /* lines per scan per instance; main.cpp:99 reserves 20 */
+
+/* status codes */
+enum {
+    EKF_OK = 0,
+    EKF_EINVAL = 1,   /* bad argument */
+    EKF_ENOMEM = 2,   /* device / host allocation failed */
+    EKF_EDEVICE = 3,  /* HIP runtime error / no device */
+    EKF_ERANGE = 4,   /* instance index / line count out of range */
+};
+/* ekf_result.status bits (per instance, per call) */
+enum {
+    EKF_ST_SINGULAR_S = 1, /* gsl_linalg_LU_invert → GSL_EDOM on some candidate (Robot.cpp:454) */
+    EKF_ST_CAPACITY = 2,   /* augmentation beyond capacity (UB in the reference, Robot.cpp:802) */
+    EKF_ST_NONSYM = 4,     /* EKF_R_AS_WRITTEN only: a line with index 1 or 2 matched. Its R has a
+                              single off-diagonal entry (Robot.cpp:302-304), so the reference's
+                              K·S·Kᵀ — and from then on its P — is not symmetric; the packed
+                              symmetric storage keeps the upper triangle. */
+};
+
+/* storage precision of the landmark-landmark covariance block */
+enum { EKF_PREC_F64 = 0, EKF_PREC_F32 = 1 };
+/* R source inside the association loop (SURVEY.md §8a parity-mode flags) */
+enum { EKF_R_INTENDED = 0, EKF_R_AS_WRITTEN = 1 };
+
+typedef struct ekf_config {
+    int32_t capacity;      /* N = LINESIZE (Robot.h:13); landmarks per instance */
+    int32_t instances;     /* E: independent EKF instances in this context */
+    int32_t precision;     /* EKF_PREC_* for the landmark block of P */
+    int32_t device;        /* HIP device ordinal, -1 = current */
+    int32_t max_lines;     /* per-scan line capacity per instance, <= EKF_MAX_LINES */
+    int32_t r_mode;        /* EKF_R_* */
+    int32_t reset_margin;  /* map wiped when savedLineCount > N - margin (Robot.cpp:893: 10) */
+    int32_t reserved;
+    double mahalanobis;    /* MAHALANOBIS gate, Robot.h:15 (0.4) */
+    double encoder_noise;  /* ENCODERNOISE, Robot.h:17 (0.024) */
+} ekf_config;
+
+/* One observed line: the fields of `line` (simplifyPath.h:62-79) that localize reads. */
+typedef struct ekf_line {
+    double alpha; /* line.alfa, robot frame */
+    double r;     /* line.r */
+    double R[4];  /* *line.C_AR, 2x2 row-major */
+} ekf_line;
+
+/* Per-instance outcome of one localize (what Robot exposes after the call). */
+typedef struct ekf_result {
+    double pose[3];            /* xPos, yPos, thetaPos (Robot.h:54-56) */
+    int32_t matches;           /* matchesNum (Robot.h:36) */
+    int32_t new_landmarks;     /* extraLines.size() (Robot.cpp:291) */
+    int32_t saved;             /* savedLineCount after the call (Robot.h:28) */
+    int32_t reset;             /* 1 if the capacity reset ran (Robot.cpp:893-904) */
+    int32_t status;            /* EKF_ST_* bits */
+    int32_t nlines;
+    int32_t match[EKF_MAX_LINES]; /* matched saved index per line, -1 = appended as new */
+} ekf_result;
+
+typedef struct ekf_ctx ekf_ctx;
+
+void ekf_config_init(ekf_config* cfg);
+const char* ekf_strerror(int status);
+int ekf_abi_version(void);
+
+/* Robot::Robot(x, y, theta) for every instance (Robot.cpp:20-35), y/P/savedLineCount zeroed. */
+int ekf_create(const ekf_config* cfg, ekf_ctx** out);
+int ekf_destroy(ekf_ctx* ctx);
+/* Order all work after/before the caller's stream (e.g. torch's current stream). NULL = own. */
+int ekf_set_stream(ekf_ctx* ctx, void* hip_stream);
+int ekf_sync(ekf_ctx* ctx);
+
+/* Robot::Robot(x, y, theta) on one instance (e < 0: all instances). */
+int ekf_reset_instance(ekf_ctx* ctx, int e, double x, double y, double theta);
+
+/* Robot::localize(lines, rot, encoder) (Robot.h:74, Robot.cpp:126-904) on every instance.
+ * Host buffers: encoder[E*3] (realRoboPose, main.cpp:84-89), lines[E*max_lines] (instance e
+ * uses lines[e*max_lines ... + nlines[e]-1]), nlines[E]. out[E] optional. Synchronous.
+ * `rot` (wheel rotations) is not an input: SIMULATIONOFF == true (Robot.h:18) never uses it. */
+int ekf_localize(ekf_ctx* ctx, const double* encoder, const ekf_line* lines,
+                 const int32_t* nlines, ekf_result* out);
+/* Same, with all three inputs already resident in device memory; asynchronous on the
+ * context stream. Results stay on the device until ekf_read_results(). */
+int ekf_localize_device(ekf_ctx* ctx, const double* d_encoder, const ekf_line* d_lines,
+                        const int32_t* d_nlines);
+/* The two halves of localize: predict = Robot.cpp:130-286 (motion model and
+ * P_pre), update = Robot.cpp:288-904 (association, Kalman updates, augmentation, reset).
+ * predict followed by update == localize. */
+int ekf_predict(ekf_ctx* ctx, const double* encoder);
+int ekf_update(ekf_ctx* ctx, const ekf_line* lines, const int32_t* nlines, ekf_result* out);
+int ekf_read_results(ekf_ctx* ctx, ekf_result* out);
+
+/* State transfer (fixtures, tests, checkpoints). P_full is the reference's dense row-major
+ * n×n P_t0 (Robot.h:62) in fp64; y is Robot::y (Robot.h:26); pose = xPos/yPos/thetaPos. */
+int ekf_upload_state(ekf_ctx* ctx, int e, const double* P_full, const double* y, int saved,
+                     const double pose[3]);
+int ekf_download_state(ekf_ctx* ctx, int e, double* P_full, double* y, int* saved,
+                       double pose[3]);
+/* Device-side initialisation P = diag(d) + U·Uᵀ (U: n×rank row-major, host pointers). */
+int ekf_init_lowrank(ekf_ctx* ctx, int e, const double* diag, const double* U, int rank,
+                     const double* y, int saved, const double pose[3]);
+/* P_t0[0:3,0:3] of instance e (what getEllipse reads, Robot.cpp:75-77). */
+int ekf_get_pose_cov(ekf_ctx* ctx, int e, double P33[9]);
+/* Robot::getEllipse(axii, angle) (Robot.h:73, Robot.cpp:73-124). Returns 1 on success, 0 if
+ * the 2x2 eigenproblem failed (as the reference's bool), negative on API error. */
+int ekf_get_ellipse(ekf_ctx* ctx, int e, float axii[2], float* angle);
+
+/* Introspection for the benchmark's roofline accounting. */
+size_t ekf_landmark_block_bytes(const ekf_ctx* ctx); /* stored bytes of P_ll per instance */
+int ekf_state_dim(const ekf_ctx* ctx);                /* n */
+/* Per-kernel HIP-event timing on the context stream (0 = off). Averages are over the
+ * launches recorded since the last enable. */
+int ekf_profile_enable(ekf_ctx* ctx, int enable);
+int ekf_profile_read(ekf_ctx* ctx, double* scan_ms, double* downdate_ms, double* augment_ms,
+                     int* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLAM_EKF_H */

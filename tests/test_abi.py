@@ -1,0 +1,111 @@
+"""CPU checks of the drop-in boundary: the C-ABI library builds, loads and exports exactly the
+entry points include/slam_ekf.h declares (no compute calls: no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "slam_ekf.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b(ekf_[a-z_0-9]+)\s*\(", src)
+    return sorted(set(names))
+
+
+def test_header_declares_expected_surface():
+    names = declared_functions()
+    for must in ("ekf_create", "ekf_localize", "ekf_predict", "ekf_update", "ekf_get_ellipse",
+                 "ekf_download_state", "ekf_upload_state", "ekf_localize_device"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(ekf_mod):
+    lib = ctypes.CDLL(ekf_mod.LIB_PATH)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    assert sorted(ekf_mod.EXPORTED) == declared_functions()
+
+
+def test_library_is_gfx950_code_object(ekf_mod):
+    """The device code embedded in the .so targets gfx950 (and only gfx950)."""
+    data = open(ekf_mod.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    for other in (b"gfx942", b"gfx90a", b"sm_"):
+        assert b"amdgcn-amd-amdhsa--" + other not in data
+
+
+def test_cpu_only_calls(ekf_mod):
+    lib = ekf_mod.load_library()
+    assert lib.ekf_abi_version() == 1
+    assert lib.ekf_strerror(0) == b"ok"
+    cfg = ekf_mod.EkfConfig()
+    lib.ekf_config_init(ctypes.byref(cfg))
+    # defaults are the reference's compile-time constants (Robot.h:13-17, Robot.cpp:893)
+    assert cfg.capacity == 100 and cfg.reset_margin == 10
+    assert cfg.mahalanobis == 0.4 and cfg.encoder_noise == 0.024
+    h = ctypes.c_void_p()
+    bad = ekf_mod.EkfConfig()
+    lib.ekf_config_init(ctypes.byref(bad))
+    bad.max_lines = 1000
+    assert lib.ekf_create(ctypes.byref(bad), ctypes.byref(h)) == 1   # EKF_EINVAL before any HIP call
+
+
+def test_struct_layouts_match_header():
+    # ekf_line is 6 doubles; ekf_result as declared
+    from slam_ros_amd import ekf
+    assert ctypes.sizeof(ekf.EkfLine) == 48
+    assert ctypes.sizeof(ekf.EkfConfig) == 48
+    assert ctypes.sizeof(ekf.EkfResult) == 24 + 6 * 4 + 4 * ekf.EKF_MAX_LINES
+
+
+def test_layout_header_bijective(tmp_path):
+    """Host-compile ekf_layout.h and check the packed tile maps are bijections."""
+    src = tmp_path / "t.cpp"
+    src.write_text(r'''
+#include "ekf_layout.h"
+#include <cstdio>
+#include <vector>
+using namespace ekf;
+int main() {
+  for (int r = 0; r < 32; r++) for (int c = 0; c < 32; c++) {
+    if (tile_off_f32(r, c) < 0 || tile_off_f32(r, c) >= 1024) return 1;
+    if (tile_off_f64(r, c) < 0 || tile_off_f64(r, c) >= 1024) return 1;
+  }
+  std::vector<int> s32(1024, 0), s64(1024, 0);
+  for (int r = 0; r < 32; r++) for (int c = 0; c < 32; c++) { s32[tile_off_f32(r,c)]++; s64[tile_off_f64(r,c)]++; }
+  for (int k = 0; k < 1024; k++) if (s32[k] != 1 || s64[k] != 1) return 2;
+  const int M = 200, nb = (M + 31) / 32;
+  std::vector<int> hit((size_t)nb * (nb + 1) / 2 * 1024, 0);
+  for (int i = 0; i < M; i++) for (int j = 0; j < M; j++) {
+    if (ll_offset<float>(i, j, nb) != ll_offset<float>(j, i, nb) && (i >> 5) != (j >> 5)) return 3;
+    hit[ll_offset<float>(i, j, nb)]++;
+  }
+  for (int i = 0; i < M; i++) for (int j = 0; j < M; j++) {
+    int want = ((i >> 5) == (j >> 5)) ? 1 : 2;
+    if (hit[ll_offset<float>(i, j, nb)] != want) return 4;
+  }
+  for (int bi = 0; bi < nb; bi++) for (int bj = bi; bj < nb; bj++)
+    if (tile_index(bi, bj, nb) < 0 || tile_index(bi, bj, nb) >= (long)nb*(nb+1)/2) return 5;
+  if (tile_index(nb - 1, nb - 1, nb) != (long)nb*(nb+1)/2 - 1) return 6;
+  // operand maps stay inside their per-row-block slab
+  const int kmax = 16;
+  for (int row = 0; row < 64; row++) for (int k = 0; k < kmax; k++) {
+    long a = op_index_f32(row, k, kmax), b = op_index_f64(row, k, kmax);
+    if (a < (row >> 5) * 64L * (kmax / 2) || a >= ((row >> 5) + 1) * 64L * (kmax / 2)) return 7;
+    if (b < (row >> 5) * 64L * (kmax / 2) || b >= ((row >> 5) + 1) * 64L * (kmax / 2)) return 8;
+  }
+  puts("ok");
+  return 0;
+}
+''')
+    exe = tmp_path / "t"
+    inc = os.path.join(ROOT, "slam_ros_amd", "csrc")
+    subprocess.run(["g++", "-std=c++17", "-O1", f"-I{inc}", str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.returncode

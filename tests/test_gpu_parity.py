@@ -1,0 +1,288 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU restatement (oracle/).
+
+Tolerances (BASELINE.json north_star): per scan from identical inputs,
+‖P − P_ref‖_F / ‖P_ref‖_F ≤ 1e-6 and ‖y − y_ref‖₂ / ‖y_ref‖₂ ≤ 1e-8, association identical.
+fp64 storage is held to 1e-10 over whole trajectories.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from slam_ros_amd import scan_gen as G
+
+pytestmark = pytest.mark.gpu
+
+P_TOL = {0: 1e-10, 1: 1e-6}    # precision → per-scan relative Frobenius bound on P
+Y_TOL = 1e-8
+
+
+def rel(a, b):
+    nb = np.linalg.norm(b)
+    return np.linalg.norm(a - b) / (nb if nb > 0 else 1.0)
+
+
+def make_pair(ekf, oracle, N, prec, state=None, r_mode=0, max_lines=16, mode=None,
+              reset_margin=10):
+    ens = ekf.Ensemble(N, 1, prec, max_lines=max_lines, r_mode=r_mode, reset_margin=reset_margin)
+    ref = oracle.OracleRobot(N, mode=oracle.FAST if mode is None else mode, r_mode=r_mode)
+    if state is not None:
+        P0, y0, s0, pose0 = state
+        ens.upload_state(0, P0, y0, s0, pose0)
+        Pg, yg, sg, pg = ens.download_state(0)
+        ref.set_state(Pg, yg, sg, pg)
+    return ens, ref
+
+
+def check_same(ens, ref, prec, res=None, mref=None, where=""):
+    if res is not None:
+        assert res["match"] == mref, (where, res["match"], mref)
+    P, y, saved, pose = ens.download_state(0)
+    assert saved == ref.savedLineCount, where
+    rp = rel(P, ref.P_t0)
+    ry = rel(y, ref.y)
+    assert rp <= P_TOL[prec], (where, "P", rp)
+    assert ry <= Y_TOL, (where, "y", ry)
+    np.testing.assert_allclose(pose, ref.pose, rtol=0, atol=1e-9 if prec else 1e-12)
+    return P, y, saved, pose
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("N", [5, 37, 64, 100])
+def test_state_roundtrip(ekf_mod, prec, N):
+    n = 3 + 2 * N
+    rng = np.random.default_rng(N)
+    A = rng.normal(size=(n, n))
+    P = A @ A.T
+    P = (P + P.T) / 2                           # exactly symmetric (packed storage)
+    y = rng.normal(size=n)
+    ens = ekf_mod.Ensemble(N, 1, prec)
+    ens.upload_state(0, P, y, N // 2, [1.0, 2.0, 0.3])
+    Pg, yg, sg, pg = ens.download_state(0)
+    assert sg == N // 2 and list(pg) == [1.0, 2.0, 0.3]
+    np.testing.assert_array_equal(yg, y)
+    if prec == 0:
+        np.testing.assert_array_equal(Pg, P)
+    else:
+        np.testing.assert_array_equal(Pg[:3], P[:3])            # robot strip kept in fp64
+        np.testing.assert_allclose(Pg[3:, 3:], P[3:, 3:].astype(np.float32), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+def test_lowrank_init_equals_dense(ekf_mod, prec):
+    N = 48
+    w = G.make_world(N)
+    st = G.initial_state(w)
+    a = ekf_mod.Ensemble(N, 1, prec)
+    a.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
+    Pa = a.download_state(0)[0]
+    ref = st.dense_P()
+    tol = 1e-14 if prec == 0 else 1e-7
+    assert rel(Pa, ref) <= tol
+
+
+def test_ctor_state_matches_reference(ekf_mod, oracle_mod):
+    ens = ekf_mod.Ensemble(12, 2, 0)
+    ens.reset(1, 1.5, -2.0, 0.25)
+    ref = oracle_mod.OracleRobot(12, 1.5, -2.0, 0.25)
+    P, y, s, pose = ens.download_state(1)
+    np.testing.assert_array_equal(P, ref.P_t0)
+    np.testing.assert_array_equal(y, ref.y)
+    assert s == 0 and list(pose) == [1.5, -2.0, 0.25]
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+def test_map_from_scratch(ekf_mod, oracle_mod, prec):
+    """Robot(0,0,0) → first scan augments every line → later scans match and augment.
+    fp64: one trajectory vs the faithful dense restatement. fp32: per scan from identical state."""
+    N = 24
+    rng = np.random.default_rng(1)
+    ens, ref = make_pair(ekf_mod, oracle_mod, N, prec, mode=oracle_mod.FAITHFUL)
+    first = G.random_lines(rng, 5)
+    res = ens.localize([0.01, 0.0, 0.0], first[None], [5])[0]
+    m = ref.localize(first, [0.01, 0.0, 0.0])
+    check_same(ens, ref, prec, res, m, "first")
+    assert res["new_landmarks"] == 5 and res["saved"] == 5
+    for step in range(15):
+        y = ref.y
+        lines = []
+        for j in rng.choice(ref.savedLineCount, size=min(3, ref.savedLineCount), replace=False):
+            a, rr = y[3 + 2 * j], y[4 + 2 * j]
+            lines.append([G.wrap_pi(a - ref.thetaPos),
+                          rr - (ref.xPos * math.cos(a) + ref.yPos * math.sin(a)), 1e-2, 0, 0, 1e-2])
+        lines = np.array(lines + list(G.random_lines(rng, 1)))
+        enc = [ref.xPos - 0.01, ref.yPos, ref.thetaPos + 0.001]
+        res = ens.localize(enc, lines[None], [len(lines)])[0]
+        m = ref.localize(lines, enc)
+        P, yg, s, pose = check_same(ens, ref, prec, res, m, f"step {step}")
+        if prec == 1:
+            ref.set_state(P, yg, s, pose)
+
+
+def test_trajectory_fp64_with_reset(ekf_mod, oracle_mod):
+    """25 scans at N=64 in fp64 incl. augmentation and the capacity reset (Robot.cpp:893-904)."""
+    N = 64
+    w = G.make_world(N, active=N - 13)
+    st = G.initial_state(w)
+    ens, ref = make_pair(ekf_mod, oracle_mod, N, 0, (st.dense_P(), st.y, st.saved, st.pose),
+                         mode=oracle_mod.FAITHFUL)
+    rng = np.random.default_rng(3)
+    resets = 0
+    for step in range(1, 26):
+        enc, lines, _ = G.make_scan(w, step, lines=6)
+        ln = np.concatenate([lines[0], G.random_lines(rng, 1)])
+        res = ens.localize(enc, ln[None], [len(ln)])[0]
+        m = ref.localize(ln, enc[0])
+        check_same(ens, ref, 0, res, m, f"step {step}")
+        resets += res["reset"]
+    assert resets >= 1
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("N", [64, 256, 1024])
+def test_per_scan_parity(ekf_mod, oracle_mod, prec, N):
+    w = G.make_world(N)
+    st = G.initial_state(w)
+    ens, ref = make_pair(ekf_mod, oracle_mod, N, prec, (st.dense_P(), st.y, st.saved, st.pose),
+                         max_lines=8)
+    for step in range(1, 4):
+        enc, lines, nl = G.make_scan(w, step)
+        res = ens.localize(enc, lines, nl)[0]
+        m = ref.localize(lines[0], enc[0])
+        assert res["matches"] == 8
+        P, y, s, pose = check_same(ens, ref, prec, res, m, f"N={N} step {step}")
+        ref.set_state(P, y, s, pose)
+
+
+def test_n4096_fp32_scan(ekf_mod, oracle_mod):
+    """Headline size (N=4096, n=8195): one fp32 scan from identical state vs the restatement."""
+    N = 4096
+    w = G.make_world(N)
+    st = G.initial_state(w)
+    ens = ekf_mod.Ensemble(N, 1, 1, max_lines=8)
+    ens.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
+    P0, y0, s0, pose0 = ens.download_state(0)
+    ref = oracle_mod.OracleRobot(N)
+    ref.set_state(P0, y0, s0, pose0)
+    del P0
+    enc, lines, nl = G.make_scan(w, 1)
+    res = ens.localize(enc, lines, nl)[0]
+    m = ref.localize(lines[0], enc[0])
+    assert res["matches"] == 8
+    check_same(ens, ref, 1, res, m, "N=4096")
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+def test_predict_then_update_equals_localize(ekf_mod, prec):
+    N = 64
+    w = G.make_world(N)
+    st = G.initial_state(w)
+    a = ekf_mod.Ensemble(N, 1, prec, max_lines=8)
+    b = ekf_mod.Ensemble(N, 1, prec, max_lines=8)
+    for e in (a, b):
+        e.upload_state(0, st.dense_P(), st.y, st.saved, st.pose)
+    for step in range(1, 4):
+        enc, lines, nl = G.make_scan(w, step)
+        ra = a.localize(enc, lines, nl)[0]
+        b.predict(enc)
+        rb = b.update(lines, nl)[0]
+        assert ra["match"] == rb["match"]
+        Pa, ya, _, pa = a.download_state(0)
+        Pb, yb, _, pb = b.download_state(0)
+        np.testing.assert_array_equal(Pa, Pb)
+        np.testing.assert_array_equal(ya, yb)
+        np.testing.assert_array_equal(pa, pb)
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+def test_ensemble_instances_are_independent(ekf_mod, prec):
+    N, E = 64, 3
+    w = G.make_world(N)
+    st = G.initial_state(w)
+    ens = ekf_mod.Ensemble(N, E, prec, max_lines=8)
+    singles = [ekf_mod.Ensemble(N, 1, prec, max_lines=8) for _ in range(E)]
+    for e in range(E):
+        ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+        singles[e].init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
+    for step in range(1, 4):
+        enc, lines, nl = G.make_scan(w, step, instances=E)
+        nl[1] = 5                                  # ragged line counts across instances
+        rs = ens.localize(enc, lines, nl)
+        for e in range(E):
+            r1 = singles[e].localize(enc[e:e + 1], lines[e:e + 1], nl[e:e + 1])[0]
+            assert rs[e]["match"] == r1["match"]
+    for e in range(E):
+        Pa, ya, _, _ = ens.download_state(e)
+        Pb, yb, _, _ = singles[e].download_state(0)
+        np.testing.assert_array_equal(Pa, Pb)
+        np.testing.assert_array_equal(ya, yb)
+
+
+def test_as_written_r_mode(ekf_mod, oracle_mod):
+    """Robot.cpp:302-304 as written (zero-initialised stack): exact whenever the as-written R is
+    symmetric. Lines 1 and 2 get a single OFF-diagonal R entry; if such a line matches, the
+    reference's P turns non-symmetric and the GPU flags EKF_ST_NONSYM instead of pretending."""
+    N = 40
+    w = G.make_world(N, active=20)
+    st = G.initial_state(w)
+    state = (st.dense_P(), st.y, st.saved, st.pose)
+    enc, lines, _ = G.make_scan(w, 1, lines=6, var_alpha=2e-4, var_r=3e-4)
+    far = np.array([[0.123, 55.0, 1e-4, 0, 0, 1e-4], [-2.0, 40.0, 1e-4, 0, 0, 2e-4]])
+    for L, ln in ((1, lines[0][:1]), (6, np.concatenate([lines[0][:1], far, lines[0][3:]]))):
+        ens, ref = make_pair(ekf_mod, oracle_mod, N, 0, state, r_mode=1)
+        res = ens.localize(enc, ln[None], [L])[0]
+        m = ref.localize(ln, enc[0])
+        check_same(ens, ref, 0, res, m, f"as_written L={L}")
+        assert not res["status"] & ekf_mod.ST_NONSYM
+    ens, ref = make_pair(ekf_mod, oracle_mod, N, 0, state, r_mode=1)
+    res = ens.localize(enc, lines[:, :3], [3])[0]
+    assert res["match"][1] >= 0 and res["status"] & ekf_mod.ST_NONSYM
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+def test_edge_cases(ekf_mod, oracle_mod, prec):
+    N = 30
+    w = G.make_world(N, active=12)
+    st = G.initial_state(w)
+    state = (st.dense_P(), st.y, st.saved, st.pose)
+    # no lines: prediction committed (Robot.cpp:702-716)
+    ens, ref = make_pair(ekf_mod, oracle_mod, N, prec, state)
+    res = ens.localize([0.05, -0.02, 0.3], np.zeros((1, 0, 6)), [0])[0]
+    ref.localize(np.zeros((0, 6)), [0.05, -0.02, 0.3])
+    assert res["matches"] == 0 and res["new_landmarks"] == 0
+    check_same(ens, ref, prec, where="no lines")
+    # every line rejected by the gate → all appended
+    ens, ref = make_pair(ekf_mod, oracle_mod, N, prec, state)
+    far = np.array([[0.123, 55.0, 1e-4, 0, 0, 1e-4], [-2.0, 40.0, 1e-4, 0, 0, 2e-4]])
+    res = ens.localize([0, 0, 0], far[None], [2])[0]
+    m = ref.localize(far, [0, 0, 0])
+    assert m == [-1, -1]
+    check_same(ens, ref, prec, res, m, "gate reject")
+    # capacity overflow: s = N - 1 with 3 unmatched lines and no reset margin
+    ens, ref = make_pair(ekf_mod, oracle_mod, N, prec, reset_margin=0,
+                         state=None)
+    ref = oracle_mod.OracleRobot(N)  # reset margin is fixed at 10 in the reference
+    w2 = G.make_world(N, active=N - 1)
+    st2 = G.initial_state(w2)
+    ens.upload_state(0, st2.dense_P(), st2.y, st2.saved, st2.pose)
+    lines = np.array([[0.1, 60.0, 1e-4, 0, 0, 1e-4], [0.2, 61.0, 1e-4, 0, 0, 1e-4],
+                      [0.3, 62.0, 1e-4, 0, 0, 1e-4]])
+    res = ens.localize([0, 0, 0], lines[None], [3])[0]
+    assert res["saved"] == N and res["status"] & ekf_mod.ST_CAPACITY
+
+
+def test_ellipse_matches_eigen(ekf_mod):
+    N = 8
+    ens = ekf_mod.Ensemble(N, 1, 0)
+    n = 3 + 2 * N
+    P = np.eye(n) * 0.01
+    P[:2, :2] = [[0.04, 0.012], [0.012, 0.01]]
+    ens.upload_state(0, P, np.zeros(n), 0, [0, 0, 0])
+    ok, axii, angle = ens.ellipse(0)
+    lam, vec = np.linalg.eigh(P[:2, :2])
+    assert ok
+    np.testing.assert_allclose(axii, 2 * np.sqrt(5.991 * np.abs(lam)), rtol=1e-6)
+    v = vec[:, 1]
+    want = math.atan2(v[0], v[1])
+    d = (angle - want) % math.pi
+    assert min(d, math.pi - d) < 1e-5          # GSL eigenvector sign: parity modulo π

@@ -1,0 +1,203 @@
+"""CPU tests of the checker (oracle/): known answers from the reference, internal cross-checks.
+
+Pinning: the reference's only known-answer data is the MATLAB quiz in Robot.h:146-178
+(tests/golden/kat_matlab.json). The SLAM-specific structure is pinned by the statement-level
+restatement (faithful mode, Robot.cpp:126-904) and its sparse equivalent (fast mode), which
+must agree bit for bit.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from slam_ros_amd import scan_gen as G
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _kat():
+    with open(os.path.join(GOLDEN, "kat_matlab.json")) as f:
+        return json.load(f)
+
+
+def test_kat_uncertainty_propagation(oracle_mod):
+    """Robot.h:146-156 via the gslcblas-style dgemm used at Robot.cpp:242-258."""
+    k = _kat()["propagation"]
+    Fx, Fu, P, Q = (np.array(k[n]) for n in ("Fx", "Fu", "P", "Q"))
+    dg = oracle_mod.dgemm
+    FxP = dg(False, False, Fx, P)
+    Pp = dg(False, True, FxP, Fx)
+    FuQ = dg(False, False, Fu, Q)
+    Pp = Pp + dg(False, True, FuQ, Fu)
+    np.testing.assert_array_equal(Pp, np.array(k["P_prior"]))
+
+
+def test_kat_update(oracle_mod):
+    """Robot.h:158-178 with the reference's own update form P − (K·S)·Kᵀ (Robot.cpp:560-568)."""
+    k = _kat()["update"]
+    Hx, Pp, R = np.array(k["Hx"]), np.array(k["P_prior"]), np.array(k["R"])
+    z, h, x = np.array(k["z"]), np.array(k["h"]), np.array(k["x_prior"])
+    dg = oracle_mod.dgemm
+    HP = dg(False, False, Hx, Pp)
+    S = dg(False, True, HP, Hx) + R
+    np.testing.assert_allclose(S, np.array(k["S"]), rtol=0, atol=1e-15)
+    Si, rc = oracle_mod.lu_invert2(S)
+    assert rc == 0
+    PHt = dg(False, True, Pp, Hx)          # the quiz's P*Hx (Hx symmetric here)
+    K = dg(False, False, PHt, Si)
+    np.testing.assert_allclose(K, np.array(k["K"]), rtol=1e-14, atol=1e-15)
+    v = (z - h).reshape(2, 1)
+    xp = x + dg(False, False, K, v).ravel()
+    np.testing.assert_allclose(xp, np.array(k["x_posterior"]), rtol=1e-14)
+    KS = dg(False, False, K, S)
+    Ppost = Pp - dg(False, True, KS, K)
+    np.testing.assert_allclose(Ppost, np.array(k["P_posterior"]), rtol=1e-13, atol=1e-15)
+
+
+@pytest.mark.parametrize("x", [0.0, 1.0, -1.0, math.pi, -math.pi, 3.2, -3.2, 7.0, -7.0, 13.0,
+                               -13.0, 2 * math.pi, -2 * math.pi])
+def test_normalize_radian_quirk(oracle_mod, x):
+    """Robot.cpp:62-71, including its non-standard result for |rad| >= 2π."""
+    if x > math.pi:
+        want = x - (2.0 * math.pi + math.floor(x / (2.0 * math.pi)) * 2.0 * math.pi)
+    elif x < -math.pi:
+        want = x + (2.0 * math.pi + math.floor(abs(x) / (2.0 * math.pi)) * 2.0 * math.pi)
+    else:
+        want = x
+    assert oracle_mod.normalize_radian(x) == want
+
+
+def test_lu_invert_pivot_and_singular(oracle_mod):
+    S = np.array([[1e-3, 2.0], [3.0, 4.0]])    # forces the row swap
+    Si, rc = oracle_mod.lu_invert2(S)
+    assert rc == 0
+    np.testing.assert_allclose(Si @ S, np.eye(2), atol=1e-12)
+    Si, rc = oracle_mod.lu_invert2(np.array([[1.0, 2.0], [2.0, 4.0]]))
+    assert rc == 1                             # GSL_EDOM, output untouched
+    assert np.all(Si == 0)
+
+
+def _pair(oracle_mod, N, r_mode=0):
+    f = oracle_mod.OracleRobot(N, mode=oracle_mod.FAITHFUL, r_mode=r_mode)
+    s = oracle_mod.OracleRobot(N, mode=oracle_mod.FAST, r_mode=r_mode)
+    return f, s
+
+
+def _same(a, b):
+    np.testing.assert_array_equal(a.P_t0, b.P_t0)
+    np.testing.assert_array_equal(a.y, b.y)
+    np.testing.assert_array_equal(a.pose, b.pose)
+    assert a.savedLineCount == b.savedLineCount
+
+
+def test_ctor_state(oracle_mod):
+    r = oracle_mod.OracleRobot(8, 1.0, 2.0, 0.5)
+    P = r.P_t0
+    assert P[0, 0] == 0.05 and P[1, 1] == 0.05 and P[2, 2] == 0.0
+    assert np.count_nonzero(P) == 2 and not r.y.any() and r.savedLineCount == 0
+    assert list(r.pose) == [1.0, 2.0, 0.5]
+
+
+def test_faithful_equals_fast_from_ctor(oracle_mod):
+    """Map built from scratch: first scan augments everything, later scans match/augment."""
+    rng = np.random.default_rng(0)
+    f, s = _pair(oracle_mod, 24)
+    first = G.random_lines(rng, 5)
+    for r in (f, s):
+        m = r.localize(first, [0.01, 0.0, 0.0])
+        assert m == [-1] * 5
+    _same(f, s)
+    assert s.savedLineCount == 5
+    for step in range(12):
+        lines = []
+        y = s.y
+        for j in rng.choice(s.savedLineCount, size=min(3, s.savedLineCount), replace=False):
+            a, rr = y[3 + 2 * j], y[4 + 2 * j]
+            lines.append([G.wrap_pi(a - s.thetaPos), rr - (s.xPos * math.cos(a) + s.yPos * math.sin(a)),
+                          1e-2, 0, 0, 1e-2])
+        lines = np.array(lines + list(G.random_lines(rng, 1)))
+        enc = [s.xPos - 0.01, s.yPos, s.thetaPos + 0.001]
+        mf = f.localize(lines, enc)
+        ms = s.localize(lines, enc)
+        assert mf == ms
+        _same(f, s)
+
+
+def test_faithful_equals_fast_synthetic_world_with_reset(oracle_mod):
+    N = 40
+    w = G.make_world(N, active=N - 12)
+    st = G.initial_state(w)
+    f, s = _pair(oracle_mod, N)
+    P0 = st.dense_P()
+    for r in (f, s):
+        r.set_state(P0, st.y, st.saved, st.pose)
+    rng = np.random.default_rng(5)
+    saw_reset = False
+    for step in range(1, 8):
+        enc, lines, _ = G.make_scan(w, step, lines=4)
+        ln = np.concatenate([lines[0], G.random_lines(rng, 1)])
+        before = s.savedLineCount
+        mf = f.localize(ln, enc[0])
+        ms = s.localize(ln, enc[0])
+        assert mf == ms
+        _same(f, s)
+        if before and s.savedLineCount == 0:
+            saw_reset = True
+            assert not s.y[3:].any()
+            assert not s.P_t0[3:, :].any() and not s.P_t0[:, 3:].any()
+    assert saw_reset
+
+
+def test_no_lines_commits_prediction(oracle_mod):
+    """Robot.cpp:702-716: pose = x_pre (θ normalised), y[2] left as is, P_t0 = P_pre."""
+    f, s = _pair(oracle_mod, 6)
+    for r in (f, s):
+        r.set_state(None, None, 0, [0.0, 0.0, 3.1])
+        r.localize(np.zeros((0, 6)), [-0.1, 0.0, -0.2])
+    _same(f, s)
+    # u2 = 3.1 - (-0.2) = 3.3 → x_pre θ = 6.4 → normalizeRadian quirk
+    assert s.thetaPos == pytest.approx(oracle_mod.normalize_radian(6.4))
+    assert s.y[2] == pytest.approx(6.4)
+
+
+def test_gate_rejects_far_lines(oracle_mod):
+    N = 30
+    w = G.make_world(N, active=10)
+    st = G.initial_state(w)
+    f, s = _pair(oracle_mod, N)
+    for r in (f, s):
+        r.set_state(st.dense_P(), st.y, st.saved, st.pose)
+    far = np.array([[0.123, 55.0, 1e-4, 0, 0, 1e-4]])
+    for r in (f, s):
+        assert r.localize(far, [0.0, 0.0, 0.0]) == [-1]
+    _same(f, s)
+    assert s.savedLineCount == 11
+
+
+def test_as_written_r_mode(oracle_mod):
+    """Robot.cpp:302-304 as written: R[i] = C_AR[3] for the line index i < 4, else zero."""
+    N = 30
+    w = G.make_world(N, active=12)
+    st = G.initial_state(w)
+    for L in (3, 6):
+        f, s = _pair(oracle_mod, N, r_mode=oracle_mod.R_AS_WRITTEN)
+        for r in (f, s):
+            r.set_state(st.dense_P(), st.y, st.saved, st.pose)
+        enc, lines, _ = G.make_scan(w, 1, lines=L, var_alpha=2e-4, var_r=3e-4)
+        assert f.localize(lines[0], enc[0]) == s.localize(lines[0], enc[0])
+        _same(f, s)
+
+
+def test_synthetic_scans_associate_to_truth(oracle_mod):
+    """The benchmark generator's observations match their true landmarks."""
+    N = 64
+    w = G.make_world(N)
+    st = G.initial_state(w)
+    r = oracle_mod.OracleRobot(N)
+    r.set_state(st.dense_P(), st.y, st.saved, st.pose)
+    for step in range(1, 30):
+        enc, lines, _ = G.make_scan(w, step)
+        pick = np.random.default_rng(7 + step).choice(w.active, size=8, replace=False)
+        assert r.localize(lines[0], enc[0]) == list(pick)
