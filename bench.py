@@ -1,0 +1,254 @@
+"""Benchmark: EKF-SLAM updates/s at N=4096 landmarks on MI355X (BASELINE.json metric).
+
+One step = one scan on every EKF instance: Robot::localize (slam_ros/Robot.cpp:126-904) with
+L = m = 8 matched lines per instance, s = N - 10 active landmarks, fp32 covariance storage.
+Weak scaling: 8 instances per GPU (configs[3]: batch 64 across 8 GPUs). For N > 1 GPUs, rank 0
+holds the pre-generated scan payloads and broadcasts each step's payload (all instances) over
+RCCL/xGMI; every rank runs its slice of instances (no other collective on the data path).
+
+Inputs are resident in HBM before the timed region. `value` = instances × steps (all ranks)
+÷ max-over-ranks wall time of the K timed steps.
+
+roofline: the dominant kernel is the packed rank-2m covariance downdate. Algorithmic bytes per
+launch = instances_per_gpu × n(n+1) × 4 (read + write of the packed symmetric P once, SURVEY.md
+§8d); its average duration comes from HIP events recorded on the stream it runs on.
+cpu_baseline (rank 0, N=1 only): the CPU restatement (oracle/, fast mode, fp64, 1 thread) on a
+bounded sample of the same scans of instance 0; the same scans also give the per-scan parity
+numbers (‖P−P_ref‖_F/‖P_ref‖_F, state, association) from identical inputs.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "EKF updates/s at N=4096 landmarks, 1→8 MI355X; ‖P−P_ref‖_F rel-err"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+L_LINES = 8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--capacity", type=int, default=4096)
+    ap.add_argument("--instances", type=int, default=8, help="EKF instances per GPU")
+    ap.add_argument("--precision", choices=["f32", "f64"], default="f32")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="1: overlap step k's association with step k-1's downdate")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    return ap.parse_args()
+
+
+def rel(a, b):
+    nb = np.linalg.norm(b)
+    return float(np.linalg.norm(a - b) / (nb if nb > 0 else 1.0))
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from slam_ros_amd import ekf, scan_gen as G
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    N, E, K, W = args.capacity, args.instances, args.steps, args.warmup
+    prec = ekf.PREC_F32 if args.precision == "f32" else ekf.PREC_F64
+    bpe = 4 if prec == ekf.PREC_F32 else 8
+    E_total = E * world
+    n = 3 + 2 * N
+
+    world_map = G.make_world(N)
+    st = G.initial_state(world_map)
+
+    ens = ekf.Ensemble(N, E, prec, max_lines=L_LINES, device=local, pipeline=bool(args.pipeline))
+    stream = torch.cuda.current_stream(dev)
+    ens.set_stream(stream.cuda_stream)
+    for e in range(E):
+        ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+
+    # ---- pre-generated scan payloads, resident in HBM (rank 0 is the sensor) ----
+    steps_total = W + K
+    per_step = E_total * 3 + E_total * L_LINES * 6
+    payload = torch.empty((steps_total, per_step), dtype=torch.float64, device=dev)
+    if rank == 0:
+        host = np.zeros((steps_total, per_step))
+        for s in range(steps_total):
+            enc, lines, _ = G.make_scan(world_map, s + 1, instances=E_total, lines=L_LINES)
+            host[s, : E_total * 3] = enc.ravel()
+            host[s, E_total * 3:] = lines.ravel()
+        payload.copy_(torch.from_numpy(host))
+    recv = payload if world == 1 else torch.empty((2, per_step), dtype=torch.float64, device=dev)
+    nlines = torch.full((E,), L_LINES, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+
+    def step(s):
+        if world == 1:
+            buf = payload[s]
+        else:
+            buf = recv[s & 1]
+            if rank == 0:
+                buf.copy_(payload[s], non_blocking=True)
+            dist.broadcast(buf, src=0)
+        base = buf.data_ptr()
+        enc_ptr = base + (rank * E * 3) * 8
+        lines_ptr = base + (E_total * 3 + rank * E * L_LINES * 6) * 8
+        ens.localize_device(enc_ptr, lines_ptr, nlines.data_ptr())
+
+    for s in range(W):
+        step(s)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    ens.profile(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for s in range(W, W + K):
+        step(s)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = ens.profile_read()
+    ens.profile(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    res = ens.read_results()
+    all_matched = all(r["matches"] == L_LINES and r["saved"] == st.saved and not r["reset"]
+                      for r in res)
+    if world > 1:
+        ok = torch.tensor([1 if all_matched else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        all_matched = bool(ok.item())
+
+    value = E_total * K / elapsed
+    dd_ms = prof["downdate_ms"]
+    alg_bytes = E * n * (n + 1) * bpe
+    achieved = alg_bytes / (dd_ms * 1e-3) / 1e9 if dd_ms > 0 else None
+    traffic = None
+    traffic_src = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("capacity") == N and tj.get("instances") == E and tj.get("precision") == args.precision:
+                traffic = tj.get("hbm_bytes_per_launch")
+                traffic_src = os.path.relpath(args.traffic_json, ROOT)
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "updates/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic (seeded line-landmark world and scans, SURVEY.md §8d)",
+        "config": {
+            "workload": f"N={N} landmarks (n={n}), {E} EKF instances/GPU, L=m={L_LINES} matched "
+                        f"lines/scan, s=N-10 active, {args.precision} covariance storage",
+            "capacity": N, "instances_per_gpu": E, "global_batch": E_total,
+            "lines_per_scan": L_LINES, "parallelism": f"ensemble x{world} (RCCL broadcast of scans)",
+            "pipeline": bool(args.pipeline),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic": traffic,
+            "kernel": "downdate_f32_kernel" if prec == ekf.PREC_F32 else "downdate_f64_kernel",
+            "alg_bytes_per_launch": alg_bytes,
+            "traffic_source": traffic_src,
+        },
+        "kernel_ms": {"scan": prof["scan_ms"], "downdate": dd_ms, "augment": prof["augment_ms"]},
+        "all_lines_matched": all_matched,
+        "cpu_baseline": None,
+    }
+    if not all_matched:
+        out["last_step_results"] = [{"matches": r["matches"], "saved": r["saved"],
+                                     "reset": r["reset"], "status": r["status"]} for r in res]
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle import oracle as O
+        # identical inputs: instance 0 restarted from the state it stores (fp32-rounded P0)
+        ens.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
+        P0, y0, s0, pose0 = ens.download_state(0)
+        ref = O.OracleRobot(N, mode=O.FAST)
+        ref.set_state(P0, y0, s0, pose0)
+        del P0
+        host = payload.cpu().numpy()
+        scans = 0
+        t_cpu = 0.0
+        parity = None
+        while True:
+            enc = host[scans, :3]
+            lines = host[scans, E_total * 3: E_total * 3 + L_LINES * 6].reshape(L_LINES, 6)
+            t1 = time.perf_counter()
+            mref = ref.localize(lines, enc)
+            t_cpu += time.perf_counter() - t1
+            scans += 1
+            if parity is None:
+                # the GPU runs the same first scan from the same state (all instances step; 0 compared)
+                ens.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
+                for e in range(1, E):
+                    ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+                ens.set_stream(None)
+                g = ens.localize(host[0, : E * 3].reshape(E, 3),
+                                 host[0, E_total * 3: E_total * 3 + E * L_LINES * 6].reshape(E, L_LINES, 6),
+                                 [L_LINES] * E)[0]
+                Pg, yg, _, poseg = ens.download_state(0)
+                parity = {"p_rel_err": rel(Pg, ref.P_t0), "y_rel_err": rel(yg, ref.y),
+                          "pose_abs_err": float(np.abs(poseg - ref.pose).max()),
+                          "association_identical": g["match"] == mref,
+                          "scope": "instance 0, first scan, identical fp32-rounded P0"}
+                del Pg
+            if t_cpu >= args.cpu_seconds or scans >= steps_total:
+                break
+        out["cpu_baseline"] = {
+            "value": scans / t_cpu, "unit": "updates/s", "cores": 1, "kind": "port",
+            "sample": f"{scans} consecutive scans of instance 0 (N={N}, L=m={L_LINES}) through "
+                      f"oracle/ekf_oracle.c fast mode (fp64, sparse predict/gating, dense O(n^2) "
+                      f"update per match), {t_cpu:.1f} s",
+        }
+        out["parity"] = parity
+        out["speedup_vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
+
+    if rank == 0:
+        print(json.dumps(out))
+    ens.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -58,7 +58,9 @@ typedef struct ekf_config {
     int32_t max_lines;     /* per-scan line capacity per instance, <= EKF_MAX_LINES */
     int32_t r_mode;        /* EKF_R_* */
     int32_t reset_margin;  /* map wiped when savedLineCount > N - margin (Robot.cpp:893: 10) */
-    int32_t reserved;
+    int32_t pipeline;      /* 1: double-buffer the landmark block so that a step's association
+                              kernel overlaps the previous step's covariance downdate (applying
+                              it on read, bit-identically); 0: in-place, strictly sequential */
     double mahalanobis;    /* MAHALANOBIS gate, Robot.h:15 (0.4) */
     double encoder_noise;  /* ENCODERNOISE, Robot.h:17 (0.024) */
 } ekf_config;

@@ -1,9 +1,15 @@
 // ekf_api.hip — C-ABI (include/slam_ekf.h) over the gfx950 kernels in ekf_kernels.hip.
 //
-// A context owns E instances' state in HBM (packed landmark block, robot strip, y, pose,
-// savedLineCount), the per-scan scratch, and one HIP stream. localize() enqueues three
-// kernels (association/gain, MFMA downdate, augmentation); nothing is copied back unless the
-// caller asks for results.
+// A context owns E instances' state in HBM and two HIP streams:
+//   S  association/gain kernels (scan_kernel) — all state except the landmark block;
+//   D  landmark-block kernels (downdate_kernel, patch_kernel).
+// The landmark block ping-pongs between X[0] and X[1]: step k's downdate reads X[w_{k-1}] and
+// writes X[w_k] = the other buffer, while step k+1's association already runs on S reading the
+// older buffer plus step k's pending downdate (see ekf_kernels.hip). Per-step scratch (gain
+// operands, patch rows, results) alternates between two slots. Events order the streams:
+//   downdate_k  waits for scan_k           (needs its operands)
+//   scan_{k+1}  waits for downdate_{k-1}   (reads the buffer that downdate wrote; reuses its slot)
+// Any call that reads or replaces the landmark block drains both streams first.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -23,27 +29,28 @@ struct EvPair {
     hipEvent_t a, b;
 };
 
+struct SlotBuf {
+    ekf::Slot s;
+};
+
 struct ekf_ctx {
     ekf_config cfg;
     Dims d;
     int device;
-    hipStream_t own_stream;
-    hipStream_t stream;
-    size_t elem;      // bytes per stored P_ll element
-    size_t pll_inst;  // elements per instance
-    size_t op_inst;   // operand elements per instance
-    void* Pll;
+    hipStream_t own_stream;   // S unless the caller supplies one
+    hipStream_t stream;       // S
+    hipStream_t dstream;      // D
+    size_t elem;              // bytes per stored landmark-block element
+    size_t pll_inst;          // elements per instance
+    size_t op_inst;           // operand elements per instance
+    void* X[2];
     double* Rs;
     double* y;
     double* pose;
     double* xpre;
     int* saved;
     double* D;
-    double* Ust;
-    double* Vst;
-    void* Uop;
-    void* Vop;
-    int* res;
+    SlotBuf slot[2];
     int2* tile_rc;
     double* d_enc;
     ekf_line* d_lines;
@@ -51,18 +58,27 @@ struct ekf_ctx {
     int* h_res;
     double* h_pose;
     int dd_grid;
+    // pipeline state
+    int cur;                  // buffer holding the newest landmark block (in stream order)
+    int pending;              // 1: a step was enqueued since the last drain
+    long long step;           // steps enqueued (slot = step & 1)
+    int have_results;
+    hipEvent_t ev_scan[2];    // recorded on S after scan of slot p
+    hipEvent_t ev_dd[2];      // recorded on D after downdate+patch of slot p
+    int ev_dd_valid[2];
+    // profiling
     int prof;
-    std::vector<EvPair> ev[3];   // scan, downdate, augment
+    std::vector<EvPair> ev[3];   // scan, downdate, patch
     std::vector<EvPair> pool;
 };
 
-#define HIP_TRY(expr)                                  \
-    do {                                               \
-        hipError_t _e = (expr);                        \
-        if (_e != hipSuccess) {                        \
-            fprintf(stderr, "slam_ekf: %s failed: %s\n", #expr, hipGetErrorString(_e)); \
-            return EKF_EDEVICE;                        \
-        }                                              \
+#define HIP_TRY(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess) {                                                             \
+            fprintf(stderr, "slam_ekf: %s failed: %s\n", #expr, hipGetErrorString(_e));     \
+            return EKF_EDEVICE;                                                             \
+        }                                                                                   \
     } while (0)
 
 extern "C" {
@@ -71,15 +87,15 @@ void ekf_config_init(ekf_config* c)
 {
     if (!c) return;
     memset(c, 0, sizeof(*c));
-    c->capacity = 100;       // Robot.h:13
+    c->capacity = 100;        // Robot.h:13
     c->instances = 1;
     c->precision = EKF_PREC_F64;
     c->device = -1;
-    c->max_lines = 20;       // main.cpp:99 lines.reserve(20)
+    c->max_lines = 20;        // main.cpp:99 lines.reserve(20)
     c->r_mode = EKF_R_INTENDED;
-    c->reset_margin = 10;    // Robot.cpp:893
-    c->mahalanobis = 0.4;    // Robot.h:15
-    c->encoder_noise = 0.024;// Robot.h:17
+    c->reset_margin = 10;     // Robot.cpp:893
+    c->mahalanobis = 0.4;     // Robot.h:15
+    c->encoder_noise = 0.024; // Robot.h:17
 }
 
 const char* ekf_strerror(int s)
@@ -100,8 +116,17 @@ int ekf_abi_version(void) { return SLAM_EKF_ABI_VERSION; }
 
 static void free_all(ekf_ctx* c)
 {
-    void* ptrs[] = {c->Pll, c->Rs, c->y, c->pose, c->xpre, c->saved, c->D, c->Ust, c->Vst,
-                    c->Uop, c->Vop, c->res, c->tile_rc, c->d_enc, c->d_lines, c->d_nlines};
+    std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->pose, c->xpre, c->saved, c->D,
+                               c->tile_rc, c->d_enc, c->d_lines, c->d_nlines};
+    for (auto& sb : c->slot) {
+        ptrs.push_back(sb.s.Ust);
+        ptrs.push_back(sb.s.Vst);
+        ptrs.push_back(sb.s.Uop);
+        ptrs.push_back(sb.s.Vop);
+        ptrs.push_back(sb.s.patch);
+        ptrs.push_back(sb.s.patch_diag);
+        ptrs.push_back(sb.s.res);
+    }
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->h_res) (void)hipHostFree(c->h_res);
@@ -109,7 +134,22 @@ static void free_all(ekf_ctx* c)
     for (auto& v : c->ev)
         for (auto& pr : v) { (void)hipEventDestroy(pr.a); (void)hipEventDestroy(pr.b); }
     for (auto& pr : c->pool) { (void)hipEventDestroy(pr.a); (void)hipEventDestroy(pr.b); }
+    for (int k = 0; k < 2; k++) {
+        if (c->ev_scan[k]) (void)hipEventDestroy(c->ev_scan[k]);
+        if (c->ev_dd[k]) (void)hipEventDestroy(c->ev_dd[k]);
+    }
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    if (c->dstream) (void)hipStreamDestroy(c->dstream);
+}
+
+// Wait for everything on both streams; afterwards X[cur] is the materialised landmark block.
+static int drain(ekf_ctx* c)
+{
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(c->dstream));
+    c->pending = 0;
+    c->ev_dd_valid[0] = c->ev_dd_valid[1] = 0;
+    return EKF_OK;
 }
 
 static int set_robot_ctor(ekf_ctx* c, int e, double x, double y, double th)
@@ -117,7 +157,7 @@ static int set_robot_ctor(ekf_ctx* c, int e, double x, double y, double th)
     // Robot::Robot (Robot.cpp:20-35): P_t0[0][0] = P_t0[1][1] = 0.05, P_t0[2][2] = 0, the rest
     // (and y, savedLineCount) zero.
     const Dims& d = c->d;
-    HIP_TRY(hipMemsetAsync((char*)c->Pll + (size_t)e * c->pll_inst * c->elem, 0,
+    HIP_TRY(hipMemsetAsync((char*)c->X[c->cur] + (size_t)e * c->pll_inst * c->elem, 0,
                            c->pll_inst * c->elem, c->stream));
     HIP_TRY(hipMemsetAsync(c->Rs + (size_t)e * 3 * d.n, 0, sizeof(double) * 3 * d.n, c->stream));
     HIP_TRY(hipMemsetAsync(c->y + (size_t)e * d.n, 0, sizeof(double) * d.n, c->stream));
@@ -139,11 +179,13 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
 {
     if (!cfg || !out) return EKF_EINVAL;
     *out = nullptr;
-    if (cfg->capacity < 1 || cfg->instances < 1 || cfg->max_lines < 1 ||
+    // capacity bound: each association thread tracks its <= 64 landmarks' matched flags in a
+    // 64-bit mask (N <= 64 × 512 = 32768, i.e. n <= 65539)
+    if (cfg->capacity < 1 || cfg->capacity > 64 * ekf::SCAN_THREADS || cfg->instances < 1 ||
+        cfg->max_lines < 1 ||
         cfg->max_lines > EKF_MAX_LINES ||
         (cfg->precision != EKF_PREC_F64 && cfg->precision != EKF_PREC_F32) ||
-        (cfg->r_mode != EKF_R_INTENDED && cfg->r_mode != EKF_R_AS_WRITTEN) ||
-        cfg->capacity > (1 << 20))
+        (cfg->r_mode != EKF_R_INTENDED && cfg->r_mode != EKF_R_AS_WRITTEN))
         return EKF_EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return EKF_EDEVICE;
@@ -158,31 +200,35 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     }
     (void)hipGetDevice(&c->device);
     c->d = ekf::make_dims(cfg->capacity, cfg->max_lines);
-    // operands: k columns rounded to a multiple of 16 (8 f32 k-steps / 4 f64 k-steps per chunk)
-    c->d.kmax = ((2 * cfg->max_lines + 15) / 16) * 16;
     const Dims& d = c->d;
     const int E = cfg->instances;
     c->elem = (cfg->precision == EKF_PREC_F64) ? 8 : 4;
     c->pll_inst = (size_t)d.ntiles * ekf::TILE_ELEMS;
     c->op_inst = (size_t)d.nb * 64 * (d.kmax / 2);
     int rc = EKF_ENOMEM;
-#define ALLOC(ptr, bytes)                                                      \
-    do {                                                                       \
-        if (hipMalloc((void**)&(ptr), (bytes)) != hipSuccess) goto fail;       \
-        if (hipMemset((ptr), 0, (bytes)) != hipSuccess) goto fail;             \
+#define ALLOC(ptr, bytes)                                                       \
+    do {                                                                        \
+        if (hipMalloc((void**)&(ptr), (bytes)) != hipSuccess) goto fail;        \
+        if (hipMemset((void*)(ptr), 0, (bytes)) != hipSuccess) goto fail;       \
     } while (0)
-    ALLOC(c->Pll, c->pll_inst * c->elem * E);
+    ALLOC(c->X[0], c->pll_inst * c->elem * E);
+    if (cfg->pipeline) ALLOC(c->X[1], c->pll_inst * c->elem * E);
+    else c->X[1] = nullptr;
     ALLOC(c->Rs, sizeof(double) * 3 * d.n * E);
     ALLOC(c->y, sizeof(double) * d.n * E);
     ALLOC(c->pose, sizeof(double) * 3 * E);
     ALLOC(c->xpre, sizeof(double) * 3 * E);
     ALLOC(c->saved, sizeof(int) * E);
     ALLOC(c->D, sizeof(double) * 4 * d.N * E);
-    ALLOC(c->Ust, sizeof(double) * d.max_lines * 2 * d.n * E);
-    ALLOC(c->Vst, sizeof(double) * d.max_lines * 2 * d.n * E);
-    ALLOC(c->Uop, c->op_inst * c->elem * E);
-    ALLOC(c->Vop, c->op_inst * c->elem * E);
-    ALLOC(c->res, sizeof(int) * ekf::RES_STRIDE * E);
+    for (auto& sb : c->slot) {
+        ALLOC(sb.s.Ust, sizeof(double) * d.max_lines * d.n * 2 * E);
+        ALLOC(sb.s.Vst, sizeof(double) * d.max_lines * d.n * 2 * E);
+        ALLOC(sb.s.Uop, c->op_inst * c->elem * E);
+        ALLOC(sb.s.Vop, c->op_inst * c->elem * E);
+        ALLOC(sb.s.patch, sizeof(double) * d.max_lines * 2 * d.M * E);
+        ALLOC(sb.s.patch_diag, sizeof(double) * d.max_lines * 4 * E);
+        ALLOC(sb.s.res, sizeof(int) * ekf::RES_STRIDE * E);
+    }
     ALLOC(c->tile_rc, sizeof(int2) * d.ntiles);
     ALLOC(c->d_enc, sizeof(double) * 3 * E);
     ALLOC(c->d_lines, sizeof(ekf_line) * d.max_lines * E);
@@ -192,7 +238,12 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     if (hipHostMalloc((void**)&c->h_pose, sizeof(double) * 3 * E) != hipSuccess) goto fail;
     rc = EKF_EDEVICE;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) goto fail;
+    if (hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking) != hipSuccess) goto fail;
     c->stream = c->own_stream;
+    for (int k = 0; k < 2; k++) {
+        if (hipEventCreateWithFlags(&c->ev_scan[k], hipEventDisableTiming) != hipSuccess) goto fail;
+        if (hipEventCreateWithFlags(&c->ev_dd[k], hipEventDisableTiming) != hipSuccess) goto fail;
+    }
     {
         std::vector<int2> rcv((size_t)d.ntiles);
         for (int bi = 0; bi < d.nb; bi++)
@@ -211,6 +262,7 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) goto fail;
         c->dd_grid = prop.multiProcessorCount * 8;
     }
+    c->cur = 0;
     for (int e = 0; e < E; e++)
         if (set_robot_ctor(c, e, 0.0, 0.0, 0.0) != EKF_OK) goto fail;
     *out = c;
@@ -225,6 +277,7 @@ extern "C" int ekf_destroy(ekf_ctx* c)
 {
     if (!c) return EKF_EINVAL;
     (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->dstream);
     free_all(c);
     delete c;
     return EKF_OK;
@@ -233,6 +286,8 @@ extern "C" int ekf_destroy(ekf_ctx* c)
 extern "C" int ekf_set_stream(ekf_ctx* c, void* s)
 {
     if (!c) return EKF_EINVAL;
+    int rc = drain(c);
+    if (rc) return rc;
     c->stream = s ? (hipStream_t)s : c->own_stream;
     return EKF_OK;
 }
@@ -241,6 +296,7 @@ extern "C" int ekf_sync(ekf_ctx* c)
 {
     if (!c) return EKF_EINVAL;
     HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(c->dstream));
     return EKF_OK;
 }
 
@@ -248,9 +304,11 @@ extern "C" int ekf_reset_instance(ekf_ctx* c, int e, double x, double y, double 
 {
     if (!c) return EKF_EINVAL;
     if (e >= c->cfg.instances) return EKF_ERANGE;
+    int rc = drain(c);
+    if (rc) return rc;
     if (e < 0) {
         for (int k = 0; k < c->cfg.instances; k++) {
-            int rc = set_robot_ctor(c, k, x, y, th);
+            rc = set_robot_ctor(c, k, x, y, th);
             if (rc) return rc;
         }
         return EKF_OK;
@@ -258,36 +316,7 @@ extern "C" int ekf_reset_instance(ekf_ctx* c, int e, double x, double y, double 
     return set_robot_ctor(c, e, x, y, th);
 }
 
-static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
-                                   const ekf_line* lines, const int* nlines)
-{
-    ekf::ScanParams p;
-    p.d = c->d;
-    p.E = c->cfg.instances;
-    p.phase = phase;
-    p.r_mode = c->cfg.r_mode;
-    p.reset_margin = c->cfg.reset_margin;
-    p.gate = c->cfg.mahalanobis;
-    p.enc_noise = c->cfg.encoder_noise;
-    p.Pll = c->Pll;
-    p.Rs = c->Rs;
-    p.y = c->y;
-    p.pose = c->pose;
-    p.xpre = c->xpre;
-    p.saved = c->saved;
-    p.D = c->D;
-    p.Ust = c->Ust;
-    p.Vst = c->Vst;
-    p.Uop = c->Uop;
-    p.Vop = c->Vop;
-    p.res = c->res;
-    p.enc = enc;
-    p.lines = lines;
-    p.nlines = nlines;
-    return p;
-}
-
-static EvPair* prof_begin(ekf_ctx* c, int kind)
+static EvPair* prof_begin(ekf_ctx* c, int kind, hipStream_t st)
 {
     if (!c->prof) return nullptr;
     EvPair pr;
@@ -299,55 +328,127 @@ static EvPair* prof_begin(ekf_ctx* c, int kind)
         if (hipEventCreate(&pr.b) != hipSuccess) return nullptr;
     }
     c->ev[kind].push_back(pr);
-    (void)hipEventRecord(pr.a, c->stream);
+    (void)hipEventRecord(pr.a, st);
     return &c->ev[kind].back();
 }
 
-static void prof_end(ekf_ctx* c, EvPair* pr)
+static void prof_end(ekf_ctx* c, EvPair* pr, hipStream_t st)
 {
-    if (pr) (void)hipEventRecord(pr->b, c->stream);
+    if (pr) (void)hipEventRecord(pr->b, st);
 }
 
+static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
+                                   const ekf_line* lines, const int* nlines)
+{
+    ekf::ScanParams p;
+    memset(&p, 0, sizeof(p));
+    p.d = c->d;
+    p.E = c->cfg.instances;
+    p.phase = phase;
+    p.r_mode = c->cfg.r_mode;
+    p.reset_margin = c->cfg.reset_margin;
+    p.gate = c->cfg.mahalanobis;
+    p.enc_noise = c->cfg.encoder_noise;
+    p.Rs = c->Rs;
+    p.y = c->y;
+    p.pose = c->pose;
+    p.xpre = c->xpre;
+    p.saved = c->saved;
+    p.D = c->D;
+    p.enc = enc;
+    p.lines = lines;
+    p.nlines = nlines;
+    return p;
+}
+
+// Enqueue one localize step (or its predict / update half).
 static int enqueue(ekf_ctx* c, int phase, const double* enc, const ekf_line* lines,
                    const int* nlines)
 {
     ekf::ScanParams sp = scan_params(c, phase, enc, lines, nlines);
-    EvPair* pr = prof_begin(c, 0);
+    if (!(phase & ekf::PHASE_UPDATE)) {
+        EvPair* pr = prof_begin(c, 0, c->stream);
+        HIP_TRY(ekf::launch_scan(sp, c->cfg.precision, c->stream));
+        prof_end(c, pr, c->stream);
+        return EKF_OK;
+    }
+    const int sl = (int)(c->step & 1);
+    int rbuf, wbuf;
+    if (!c->cfg.pipeline) {
+        // sequential: scan_k after downdate_{k-1} (+patch), in-place downdate
+        rbuf = wbuf = c->cur;
+        sp.pending = 0;
+        if (c->ev_dd_valid[1 - sl]) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_dd[1 - sl], 0));
+    } else if (c->pending) {
+        // previous step wrote X[cur] (maybe still running on D): read the other buffer + its
+        // pending downdate, and let this step's downdate write the other buffer again.
+        rbuf = 1 - c->cur;
+        wbuf = 1 - c->cur;
+        sp.pending = 1;
+        sp.prev = c->slot[1 - sl].s;
+    } else {
+        rbuf = c->cur;
+        wbuf = 1 - c->cur;
+        sp.pending = 0;
+    }
+    sp.Pread = c->X[rbuf];
+    sp.cur = c->slot[sl].s;
+    // scan_k reuses slot sl and reads X[rbuf]: both were last used by downdate_{k-2}
+    if (c->ev_dd_valid[sl]) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_dd[sl], 0));
+    EvPair* pr = prof_begin(c, 0, c->stream);
     HIP_TRY(ekf::launch_scan(sp, c->cfg.precision, c->stream));
-    prof_end(c, pr);
-    if (!(phase & ekf::PHASE_UPDATE)) return EKF_OK;
+    prof_end(c, pr, c->stream);
+    HIP_TRY(hipEventRecord(c->ev_scan[sl], c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->dstream, c->ev_scan[sl], 0));
+
     ekf::DowndateParams dp;
     dp.d = c->d;
     dp.E = c->cfg.instances;
-    dp.Pll = c->Pll;
-    dp.Uop = c->Uop;
-    dp.Vop = c->Vop;
-    dp.res = c->res;
+    dp.Pin = c->X[c->cur];
+    dp.Pout = c->X[wbuf];
+    dp.Uop = c->slot[sl].s.Uop;
+    dp.Vop = c->slot[sl].s.Vop;
+    dp.res = c->slot[sl].s.res;
     dp.tile_rc = c->tile_rc;
-    pr = prof_begin(c, 1);
-    HIP_TRY(ekf::launch_downdate(dp, c->cfg.precision, c->dd_grid, c->stream));
-    prof_end(c, pr);
-    pr = prof_begin(c, 2);
-    HIP_TRY(ekf::launch_augment(sp, c->cfg.precision, c->stream));
-    prof_end(c, pr);
+    pr = prof_begin(c, 1, c->dstream);
+    HIP_TRY(ekf::launch_downdate(dp, c->cfg.precision, c->dd_grid, c->dstream));
+    prof_end(c, pr, c->dstream);
+    ekf::PatchParams pp;
+    pp.d = c->d;
+    pp.E = c->cfg.instances;
+    pp.P = c->X[wbuf];
+    pp.patch = c->slot[sl].s.patch;
+    pp.patch_diag = c->slot[sl].s.patch_diag;
+    pp.res = c->slot[sl].s.res;
+    pr = prof_begin(c, 2, c->dstream);
+    HIP_TRY(ekf::launch_patch(pp, c->cfg.precision, c->dstream));
+    prof_end(c, pr, c->dstream);
+    HIP_TRY(hipEventRecord(c->ev_dd[sl], c->dstream));
+    c->ev_dd_valid[sl] = 1;
+    c->cur = wbuf;
+    c->pending = 1;
+    c->step++;
+    c->have_results = 1;
     return EKF_OK;
 }
 
 static int stage_inputs(ekf_ctx* c, const double* enc, const ekf_line* lines, const int* nlines)
 {
     const int E = c->cfg.instances;
+    if (nlines)
+        for (int e = 0; e < E; e++)
+            if (nlines[e] < 0 || nlines[e] > c->d.max_lines) return EKF_ERANGE;
+    // the previous step's association kernel may still read the staging buffers
+    HIP_TRY(hipStreamSynchronize(c->stream));
     if (enc)
         HIP_TRY(hipMemcpyAsync(c->d_enc, enc, sizeof(double) * 3 * E, hipMemcpyHostToDevice,
                                c->stream));
     if (lines)
         HIP_TRY(hipMemcpyAsync(c->d_lines, lines, sizeof(ekf_line) * c->d.max_lines * E,
                                hipMemcpyHostToDevice, c->stream));
-    if (nlines) {
-        for (int e = 0; e < E; e++)
-            if (nlines[e] < 0 || nlines[e] > c->d.max_lines) return EKF_ERANGE;
+    if (nlines)
         HIP_TRY(hipMemcpyAsync(c->d_nlines, nlines, sizeof(int) * E, hipMemcpyHostToDevice,
                                c->stream));
-    }
     return EKF_OK;
 }
 
@@ -355,7 +456,12 @@ extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
 {
     if (!c) return EKF_EINVAL;
     const int E = c->cfg.instances;
-    HIP_TRY(hipMemcpyAsync(c->h_res, c->res, sizeof(int) * ekf::RES_STRIDE * E,
+    if (!c->have_results) {
+        if (out) memset(out, 0, sizeof(ekf_result) * E);
+        return EKF_OK;
+    }
+    const int sl = (int)((c->step - 1) & 1);
+    HIP_TRY(hipMemcpyAsync(c->h_res, c->slot[sl].s.res, sizeof(int) * ekf::RES_STRIDE * E,
                            hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_pose, c->pose, sizeof(double) * 3 * E, hipMemcpyDeviceToHost,
                            c->stream));
@@ -374,7 +480,8 @@ extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
         o.reset = r[ekf::RES_RESET];
         o.status = r[ekf::RES_STATUS];
         o.nlines = r[ekf::RES_NLINES];
-        for (int i = 0; i < EKF_MAX_LINES; i++) o.match[i] = (i < o.nlines) ? r[ekf::RES_MATCH + i] : -1;
+        for (int i = 0; i < EKF_MAX_LINES; i++)
+            o.match[i] = (i < o.nlines) ? r[ekf::RES_MATCH + i] : -1;
     }
     return EKF_OK;
 }
@@ -408,7 +515,7 @@ extern "C" int ekf_predict(ekf_ctx* c, const double* enc)
 extern "C" int ekf_update(ekf_ctx* c, const ekf_line* lines, const int32_t* nlines,
                           ekf_result* out)
 {
-    if (!c || !nlines) return EKF_EINVAL;
+    if (!c || !lines || !nlines) return EKF_EINVAL;
     int rc = stage_inputs(c, nullptr, lines, nlines);
     if (rc) return rc;
     rc = enqueue(c, ekf::PHASE_UPDATE, c->d_enc, c->d_lines, c->d_nlines);
@@ -422,6 +529,8 @@ extern "C" int ekf_upload_state(ekf_ctx* c, int e, const double* P, const double
     if (!c) return EKF_EINVAL;
     if (e < 0 || e >= c->cfg.instances) return EKF_ERANGE;
     if (saved < 0 || saved > c->d.N) return EKF_ERANGE;
+    int rc = drain(c);
+    if (rc) return rc;
     const Dims& d = c->d;
     if (P) {
         double* tmp = nullptr;
@@ -430,7 +539,7 @@ extern "C" int ekf_upload_state(ekf_ctx* c, int e, const double* P, const double
                                         c->stream);
         if (err == hipSuccess)
             err = ekf::launch_pack(d, c->cfg.precision, tmp,
-                                   (char*)c->Pll + (size_t)e * c->pll_inst * c->elem,
+                                   (char*)c->X[c->cur] + (size_t)e * c->pll_inst * c->elem,
                                    c->Rs + (size_t)e * 3 * d.n, c->tile_rc, c->stream);
         if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
         (void)hipFree(tmp);
@@ -455,12 +564,14 @@ extern "C" int ekf_download_state(ekf_ctx* c, int e, double* P, double* y, int* 
 {
     if (!c) return EKF_EINVAL;
     if (e < 0 || e >= c->cfg.instances) return EKF_ERANGE;
+    int rc = drain(c);
+    if (rc) return rc;
     const Dims& d = c->d;
     if (P) {
         double* tmp = nullptr;
         HIP_TRY(hipMalloc((void**)&tmp, sizeof(double) * d.n * d.n));
         hipError_t err = ekf::launch_unpack(d, c->cfg.precision, tmp,
-                                            (const char*)c->Pll + (size_t)e * c->pll_inst * c->elem,
+                                            (const char*)c->X[c->cur] + (size_t)e * c->pll_inst * c->elem,
                                             c->Rs + (size_t)e * 3 * d.n, c->stream);
         if (err == hipSuccess)
             err = hipMemcpyAsync(P, tmp, sizeof(double) * d.n * d.n, hipMemcpyDeviceToHost,
@@ -486,6 +597,8 @@ extern "C" int ekf_init_lowrank(ekf_ctx* c, int e, const double* diag, const dou
 {
     if (!c || !diag || (rank > 0 && !U) || rank < 0) return EKF_EINVAL;
     if (e < 0 || e >= c->cfg.instances) return EKF_ERANGE;
+    int rc = drain(c);
+    if (rc) return rc;
     const Dims& d = c->d;
     double *dd = nullptr, *du = nullptr;
     HIP_TRY(hipMalloc((void**)&dd, sizeof(double) * d.n));
@@ -496,7 +609,7 @@ extern "C" int ekf_init_lowrank(ekf_ctx* c, int e, const double* diag, const dou
         err = hipMemcpyAsync(du, U, sizeof(double) * d.n * rank, hipMemcpyHostToDevice, c->stream);
     if (err == hipSuccess)
         err = ekf::launch_lowrank(d, c->cfg.precision, dd, du, rank,
-                                  (char*)c->Pll + (size_t)e * c->pll_inst * c->elem,
+                                  (char*)c->X[c->cur] + (size_t)e * c->pll_inst * c->elem,
                                   c->Rs + (size_t)e * 3 * d.n, c->tile_rc, c->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
     (void)hipFree(dd);
@@ -532,16 +645,18 @@ extern "C" int ekf_get_ellipse(ekf_ctx* c, int e, float axii[2], float* angle)
     if (!isfinite(a) || !isfinite(b) || !isfinite(cc) || !isfinite(dd)) return 0;
     const double tr = 0.5 * (a + dd);
     const double disc = 0.25 * (a - dd) * (a - dd) + b * cc;
-    if (disc < 0) return 0;  // complex pair: not produced by a covariance block
+    if (disc < 0) return 0;   // complex pair: not produced by a covariance block
     const double sq = sqrt(disc);
     double lam[2] = {tr - sq, tr + sq};
     if (fabs(lam[0]) > fabs(lam[1])) {
-        double t = lam[0]; lam[0] = lam[1]; lam[1] = t;
+        double t = lam[0];
+        lam[0] = lam[1];
+        lam[1] = t;
     }
     double vx = 1.0, vy = 0.0;
     {
         const double l = lam[1];
-        double x1 = b, y1 = l - a, x2 = l - dd, y2 = cc;
+        const double x1 = b, y1 = l - a, x2 = l - dd, y2 = cc;
         const double n1 = hypot(x1, y1), n2 = hypot(x2, y2);
         if (n1 >= n2 && n1 > 0) { vx = x1 / n1; vy = y1 / n1; }
         else if (n2 > 0) { vx = x2 / n2; vy = y2 / n2; }
@@ -564,6 +679,7 @@ extern "C" int ekf_profile_enable(ekf_ctx* c, int enable)
 {
     if (!c) return EKF_EINVAL;
     (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->dstream);
     for (auto& v : c->ev) {
         for (auto& pr : v) c->pool.push_back(pr);
         v.clear();
@@ -577,6 +693,7 @@ extern "C" int ekf_profile_read(ekf_ctx* c, double* scan_ms, double* dd_ms, doub
 {
     if (!c) return EKF_EINVAL;
     HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(c->dstream));
     double avg[3] = {0, 0, 0};
     for (int k = 0; k < 3; k++) {
         double sum = 0;

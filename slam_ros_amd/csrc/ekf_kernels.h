@@ -14,16 +14,29 @@ enum { EKF_ST_SINGULAR = EKF_ST_SINGULAR_S, EKF_ST_CAP = EKF_ST_CAPACITY, EKF_ST
 // per-instance result record in device memory (ints)
 enum {
     RES_M = 0,        // matches
-    RES_NEXTRA = 1,   // lines appended as new landmarks
-    RES_SAVED_IN = 2, // savedLineCount before augmentation
+    RES_NEXTRA = 1,   // lines appended to extraLines (Robot.cpp:291)
+    RES_SAVED_IN = 2, // savedLineCount before augmentation (first new landmark index)
     RES_SAVED = 3,    // savedLineCount after the call
     RES_RESET = 4,
     RES_STATUS = 5,
     RES_NLINES = 6,
     RES_KSTEPS = 7,   // MFMA k-steps of the downdate (0 = no downdate)
-    RES_MATCH = 8,                      // [EKF_MAX_LINES]
-    RES_EXTRA = 8 + EKF_MAX_LINES,      // [EKF_MAX_LINES] line indices, in order
-    RES_STRIDE = 8 + 2 * EKF_MAX_LINES,
+    RES_NADD = 8,     // landmarks actually added (patch rows)
+    RES_MATCH = 16,                     // [EKF_MAX_LINES]
+    RES_EXTRA = 16 + EKF_MAX_LINES,     // [EKF_MAX_LINES] line indices, in order
+    RES_STRIDE = 16 + 2 * EKF_MAX_LINES,
+};
+
+// Per-step scratch ("slot"): two slots alternate so that step k's association kernel can run
+// while step k-1's downdate still reads its operands.
+struct Slot {
+    double* Ust;        // [E][max_lines][n][2]   U_t = K_t·S_t  (fp64)
+    double* Vst;        // [E][max_lines][n][2]   V_t = K_t      (fp64)
+    void* Uop;          // [E][nb][64][kmax/2]    -U in MFMA operand order (storage precision)
+    void* Vop;          //                         V in MFMA operand order
+    double* patch;      // [E][max_lines][2][M]   rows of landmarks added by this step
+    double* patch_diag; // [E][max_lines][4]      their 2x2 diagonal blocks
+    int* res;           // [E][RES_STRIDE]
 };
 
 struct ScanParams {
@@ -32,38 +45,46 @@ struct ScanParams {
     int phase;
     int r_mode;
     int reset_margin;
+    int pending;          // 1: Pread is X_{k-2}; the previous slot's downdate is applied on read
     double gate;
     double enc_noise;
-    void* Pll;        // [E][ntiles][1024] storage precision
-    double* Rs;       // [E][3][n]
-    double* y;        // [E][n]
-    double* pose;     // [E][3]
-    double* xpre;     // [E][3]
-    int* saved;       // [E]
-    double* D;        // [E][4][N]
-    double* Ust;      // [E][max_lines][2][n]
-    double* Vst;      // [E][max_lines][2][n]
-    void* Uop;        // [E][nb][64][kmax/2]
-    void* Vop;
-    int* res;         // [E][RES_STRIDE]
-    const double* enc;       // [E][3]
-    const ekf_line* lines;   // [E][max_lines]
-    const int* nlines;       // [E]
+    const void* Pread;    // [E][ntiles][1024] landmark block to read
+    double* Rs;           // [E][3][n]  robot strip (rows 0..2 of P)
+    double* y;            // [E][n]
+    double* pose;         // [E][3]
+    double* xpre;         // [E][3]
+    int* saved;           // [E]
+    double* D;            // [E][N][4]  landmark 2x2 diagonal blocks (per scan)
+    Slot cur;             // this step's slot
+    Slot prev;            // previous step's slot (read only, used when pending)
+    const double* enc;    // [E][3]
+    const ekf_line* lines;// [E][max_lines]
+    const int* nlines;    // [E]
 };
 
 struct DowndateParams {
     Dims d;
     int E;
-    void* Pll;
+    const void* Pin;      // X_{k-1}
+    void* Pout;           // X_k (may equal Pin: in place)
     const void* Uop;
     const void* Vop;
     const int* res;
-    const int2* tile_rc;   // [ntiles] (bi, bj)
+    const int2* tile_rc;  // [ntiles] (bi, bj)
+};
+
+struct PatchParams {
+    Dims d;
+    int E;
+    void* P;              // X_k
+    const double* patch;
+    const double* patch_diag;
+    const int* res;
 };
 
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st);
 hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st);
-hipError_t launch_augment(const ScanParams& p, int precision, hipStream_t st);
+hipError_t launch_patch(const PatchParams& p, int precision, hipStream_t st);
 hipError_t launch_pack(const Dims& d, int precision, const double* Pfull, void* Pll, double* Rs,
                        const int2* tile_rc, hipStream_t st);
 hipError_t launch_unpack(const Dims& d, int precision, double* Pfull, const void* Pll,

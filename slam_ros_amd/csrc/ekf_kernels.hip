@@ -1,20 +1,28 @@
 // ekf_kernels.hip — gfx950 kernels of the EKF-SLAM update (slam_ros Robot::localize).
 //
-// Per scan, three launches on one stream, all E ensemble instances at once:
-//   1. scan_kernel     (1 workgroup of 1024 threads per instance)
-//        predict of the robot strip (Robot.cpp:130-286, only rows 0..2 of Fx differ from I),
-//        then for every observed line in order: Mahalanobis gating of all unmatched saved
-//        landmarks in parallel with a min-index reduction (== the reference's first-passing
-//        candidate, Robot.cpp:313-504), and for a match the gain chain in deferred low-rank
-//        form (Robot.cpp:515-602): W_t = P_{t-1}·H_tᵀ from the robot strip + two landmark
-//        columns of P_ll corrected by the earlier matches of this scan, K_t = W_t·S_t⁻¹,
-//        U_t = K_t·S_t, y += K_t·v_t. The robot strip and the landmark 2×2 diagonal blocks are
-//        downdated eagerly (O(n) per match); the landmark block P_ll is not touched.
-//   2. downdate_kernel (grid-stride over E × packed 32×32 tiles, one tile per wave)
-//        P_ll ← P_ll − Σ_t U_t·V_tᵀ (rank 2m) on MFMA, reading and writing every stored tile
-//        once — the reference's m dense n×n passes (Robot.cpp:560-572) fused into one.
-//        Also performs the capacity reset of P_ll (Robot.cpp:893-904).
-//   3. augment_kernel  (1 workgroup per instance): new landmarks (Robot.cpp:776-866).
+// Per scan (one "step"), all E ensemble instances at once:
+//   1. scan_kernel     (one 1024-thread workgroup per instance, stream S)
+//        predict of the robot strip (Robot.cpp:130-286: Fx = I outside rows 0..2), then for
+//        every observed line in order: Mahalanobis gating of all unmatched saved landmarks in
+//        parallel + min-index reduction (== the reference's first passing candidate,
+//        Robot.cpp:313-504); for a match the gain chain in deferred low-rank form
+//        (Robot.cpp:515-602): W_t = P_{t-1}·H_tᵀ, K_t = W_t·S_t⁻¹, U_t = K_t·S_t, y += K_t·v_t.
+//        Thread tid OWNS landmarks j ≡ tid (mod 1024): their gating, their two rows of W/K/U/y,
+//        their robot-strip columns and their 2×2 diagonal block. The robot 3×3 block and the
+//        pose are computed redundantly by every thread. Cross-thread traffic per line is the
+//        winner's candidate (LDS) and the matched landmark's columns (uniform loads), so a line
+//        costs two workgroup barriers. Landmark augmentation (Robot.cpp:776-866) runs at the end
+//        of the same kernel; its rows of the landmark block go to a patch buffer.
+//   2. downdate_kernel (grid-stride over E × packed 32×32 tiles, one tile per wave, stream D)
+//        X_k = X_{k-1} − Σ_t U_t·V_tᵀ (rank 2m) on MFMA, reading and writing each stored tile
+//        once: the reference's m dense n×n passes (Robot.cpp:560-572) fused into one. Also the
+//        capacity reset of the landmark block (Robot.cpp:893-904).
+//   3. patch_kernel    (stream D): writes the augmented landmark rows into X_k.
+//
+// Cross-scan pipelining: X ping-pongs between two buffers, so scan k can read X_{k-2} while
+// downdate k-1 writes X_{k-1}; scan k then applies step k-1's downdate itself, element by
+// element, as the same k-ordered fp32/fp64 FMA chain the MFMA executes (bit-identical to the
+// value downdate k-1 stores), plus step k-1's patch and reset.
 #include <hip/hip_runtime.h>
 
 #include "ekf_kernels.h"
@@ -34,7 +42,7 @@ __device__ __forceinline__ double normalize_radian(double rad)
     return rad;
 }
 
-// gsl_linalg_LU_decomp + LU_invert on 2x2 (Robot.cpp:449-457); returns false when singular
+// gsl_linalg_LU_decomp + LU_invert on 2x2 (Robot.cpp:449-457); false when U is singular
 // (GSL_EDOM), leaving Si untouched.
 __device__ __forceinline__ bool lu_invert2(const double S[4], double Si[4])
 {
@@ -66,78 +74,265 @@ __device__ __forceinline__ bool lu_invert2(const double S[4], double Si[4])
 }
 
 template <typename T>
-__device__ __forceinline__ double ll_get(const T* P, int i, int j, int nb)
-{
-    return (double)P[ll_offset<T>(i, j, nb)];
-}
-
-template <typename T>
 __device__ __forceinline__ void ll_store_sym(T* P, int i, int j, int nb, double v)
 {
     P[ll_offset<T>(i, j, nb)] = (T)v;
     if ((i >> 5) == (j >> 5) && i != j) P[ll_offset<T>(j, i, nb)] = (T)v;
 }
 
+// ---------------------------------------------------------------------------------------
+// Landmark block as seen by step k: X plus step k-1's pending downdate / patch / reset
+// (pipeline mode; in sequential mode pend_ks = pend_reset = pn = 0 and X is current).
+// ---------------------------------------------------------------------------------------
+template <typename T>
+struct PllView {
+    const T* X;
+    int nb, kmax, M;
+    int pend_ks;      // k-steps of the pending downdate (0: none)
+    int pend_reset;
+    const T* pU;      // pending operands (this instance)
+    const T* pV;
+    int ps0, pn;      // landmarks added by the previous step
+    const double* patch;
+    const double* pdiag;
+};
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef double f64x2v __attribute__((ext_vector_type(2)));
+
+// 2x2 block (i0, i0+1) × (j0, j0+1) of the landmark block, i0 and j0 even.
+template <typename T>
+__device__ __forceinline__ void pll_block(const PllView<T>& v, int i0, int j0, double out[4])
+{
+    if (v.pend_reset) {
+        out[0] = out[1] = out[2] = out[3] = 0.0;
+        return;
+    }
+    const int li = i0 >> 1, lj = j0 >> 1;
+    if (v.pn > 0) {
+        const int hi = li > lj ? li : lj;
+        if (hi >= v.ps0 && hi < v.ps0 + v.pn) {
+            // values as patch_kernel stores them (rounded to the storage precision)
+            const int q = hi - v.ps0;
+            double raw[4];
+            if (li == lj) {
+                raw[0] = v.pdiag[q * 4 + 0]; raw[1] = v.pdiag[q * 4 + 1];
+                raw[2] = v.pdiag[q * 4 + 2]; raw[3] = v.pdiag[q * 4 + 3];
+            } else if (li > lj) {
+                const double* r0 = v.patch + (size_t)(q * 2) * v.M;
+                raw[0] = r0[j0]; raw[1] = r0[j0 + 1];
+                raw[2] = r0[v.M + j0]; raw[3] = r0[v.M + j0 + 1];
+            } else {
+                const double* r0 = v.patch + (size_t)(q * 2) * v.M;
+                raw[0] = r0[i0]; raw[1] = r0[v.M + i0];
+                raw[2] = r0[i0 + 1]; raw[3] = r0[v.M + i0 + 1];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) out[k] = (double)(T)raw[k];
+            return;
+        }
+    }
+    // stored orientation: rows a0, a0+1 and columns b0, b0+1 of one tile
+    const bool swap = (i0 >> 5) > (j0 >> 5);
+    const int a0 = swap ? j0 : i0, b0 = swap ? i0 : j0;
+    double st[4];   // stored (a0+p, b0+c) at st[p*2+c]
+    T x[4];
+#pragma unroll
+    for (int p = 0; p < 2; p++)
+#pragma unroll
+        for (int c = 0; c < 2; c++) x[p * 2 + c] = v.X[ll_offset<T>(a0 + p, b0 + c, v.nb)];
+    if (v.pend_ks == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) st[q] = (double)x[q];
+    } else if constexpr (sizeof(T) == 4) {
+        // v_mfma_f32_32x32x2_f32 is bit-for-bit a k-ordered fmaf chain (k0 lanes 0-31, then k1)
+        const int kh = v.kmax / 2;
+        const float* ua = v.pU + ((size_t)(a0 >> 5) * 64 + (a0 & 31)) * kh;   // row a0; a0+1 at +kh
+        const float* vb = v.pV + ((size_t)(b0 >> 5) * 64 + (b0 & 31)) * kh;
+        float acc[4] = {x[0], x[1], x[2], x[3]};
+        for (int s0 = 0; s0 < v.pend_ks; s0 += 4) {
+            const f32x4v ae0 = *reinterpret_cast<const f32x4v*>(ua + s0);
+            const f32x4v ae1 = *reinterpret_cast<const f32x4v*>(ua + kh + s0);
+            const f32x4v ao0 = *reinterpret_cast<const f32x4v*>(ua + 32 * kh + s0);
+            const f32x4v ao1 = *reinterpret_cast<const f32x4v*>(ua + 33 * kh + s0);
+            const f32x4v be0 = *reinterpret_cast<const f32x4v*>(vb + s0);
+            const f32x4v be1 = *reinterpret_cast<const f32x4v*>(vb + kh + s0);
+            const f32x4v bo0 = *reinterpret_cast<const f32x4v*>(vb + 32 * kh + s0);
+            const f32x4v bo1 = *reinterpret_cast<const f32x4v*>(vb + 33 * kh + s0);
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                if (s0 + s >= v.pend_ks) break;
+                acc[0] = fmaf(ao0[s], bo0[s], fmaf(ae0[s], be0[s], acc[0]));
+                acc[1] = fmaf(ao0[s], bo1[s], fmaf(ae0[s], be1[s], acc[1]));
+                acc[2] = fmaf(ao1[s], bo0[s], fmaf(ae1[s], be0[s], acc[2]));
+                acc[3] = fmaf(ao1[s], bo1[s], fmaf(ae1[s], be1[s], acc[3]));
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) st[q] = (double)acc[q];
+    } else {
+        const int kq = v.kmax / 4;
+        const double* ua = v.pU + ((size_t)(a0 >> 5) * 64 + (a0 & 15)) * (2 * kq) + ((a0 >> 4) & 1) * kq;
+        const double* vb = v.pV + ((size_t)(b0 >> 5) * 64 + (b0 & 15)) * (2 * kq) + ((b0 >> 4) & 1) * kq;
+        double acc[4] = {(double)x[0], (double)x[1], (double)x[2], (double)x[3]};
+        for (int s = 0; s < v.pend_ks; s++)
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                const size_t o = (size_t)16 * kk * 2 * kq + s;
+                const double a_0 = ua[o], a_1 = ua[o + 2 * kq];
+                const double b_0 = vb[o], b_1 = vb[o + 2 * kq];
+                acc[0] = fma(a_0, b_0, acc[0]);
+                acc[1] = fma(a_0, b_1, acc[1]);
+                acc[2] = fma(a_1, b_0, acc[2]);
+                acc[3] = fma(a_1, b_1, acc[3]);
+            }
+#pragma unroll
+        for (int q = 0; q < 4; q++) st[q] = acc[q];
+    }
+    if (swap) {
+        out[0] = st[0]; out[1] = st[2]; out[2] = st[1]; out[3] = st[3];
+    } else {
+        out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
+    }
+}
+
+// Uniform per-line package published by the matching thread (LDS).
+enum {
+    C_S = 0, C_SI = 4, C_V = 8, C_H = 10, C_KR = 13, C_UR = 19, C_WORDS = 25,
+};
+
 struct Cand {
     double S[4];
     double Si[4];
     double v[2];
     double h10, h11, h1l;
-    bool pass;
-    bool singular;
+    int pass;
+    int singular;
 };
 
-// One association candidate (line z vs saved landmark j), Robot.cpp:367-489, on the 5×5
-// block {0,1,2, 3+2j, 4+2j} of the current P (robot strip + diagonal cache).
-__device__ __forceinline__ void eval_candidate(int j, const double* Rs, int n, const double* D,
-                                               int Nc, const double* y, const double xp[3],
-                                               double za, double zr, const double Rm[4],
-                                               double gate, Cand& c)
+// 5×5 block {0,1,2, 3+2j, 4+2j} of the current P: robot 3×3 (R33), robot–landmark columns
+// (Rs, owned), landmark diagonal block (Dj, owned), and H·P·Hᵀ + R for given H row 1.
+struct Block5 {
+    double p00, p01, p02, p10, p11, p12, p20, p21, p22;
+    double p0a, p1a, p2a, p0b, p1b, p2b;
+    double daa, dab, dba, dbb;
+};
+
+__device__ __forceinline__ void load_block5(Block5& b, int j, const double* R33, const double* Rs,
+                                            int n, const double Dj[4])
 {
-    const int l0 = 3 + 2 * j, l1 = l0 + 1;
-    const double ma = y[l0], mr = y[l1];
+    const int l0 = 3 + 2 * j;
+    b.p00 = R33[0]; b.p01 = R33[1]; b.p02 = R33[2];
+    b.p10 = R33[3]; b.p11 = R33[4]; b.p12 = R33[5];
+    b.p20 = R33[6]; b.p21 = R33[7]; b.p22 = R33[8];
+    const double2 ra = *reinterpret_cast<const double2*>(Rs + l0);
+    const double2 rb = *reinterpret_cast<const double2*>(Rs + n + l0);
+    const double2 rc = *reinterpret_cast<const double2*>(Rs + 2 * n + l0);
+    b.p0a = ra.x; b.p0b = ra.y;
+    b.p1a = rb.x; b.p1b = rb.y;
+    b.p2a = rc.x; b.p2b = rc.y;
+    b.daa = Dj[0]; b.dab = Dj[1]; b.dba = Dj[2]; b.dbb = Dj[3];
+}
+
+// S = H·P5·Hᵀ + R in the reference's summation order (Robot.cpp:397-405); also returns the
+// intermediate rows hp0 = hr0·P5, hp1 = hr1·P5 (hr0 = (0,0,-1,1,0), hr1 = (h10,h11,0,h1l,1)).
+__device__ __forceinline__ void innovation_cov(const Block5& b, double h10, double h11, double h1l,
+                                               const double Rm[4], double S[4], double hp0[5],
+                                               double hp1[5])
+{
+    hp0[0] = -b.p20 + b.p0a; hp0[1] = -b.p21 + b.p1a; hp0[2] = -b.p22 + b.p2a;
+    hp0[3] = -b.p2a + b.daa; hp0[4] = -b.p2b + b.dab;
+    hp1[0] = h10 * b.p00 + h11 * b.p10 + h1l * b.p0a + b.p0b;
+    hp1[1] = h10 * b.p01 + h11 * b.p11 + h1l * b.p1a + b.p1b;
+    hp1[2] = h10 * b.p02 + h11 * b.p12 + h1l * b.p2a + b.p2b;
+    hp1[3] = h10 * b.p0a + h11 * b.p1a + h1l * b.daa + b.dba;
+    hp1[4] = h10 * b.p0b + h11 * b.p1b + h1l * b.dab + b.dbb;
+    S[0] = -hp0[2] + hp0[3] + Rm[0];
+    S[1] = hp0[0] * h10 + hp0[1] * h11 + hp0[3] * h1l + hp0[4] + Rm[1];
+    S[2] = -hp1[2] + hp1[3] + Rm[2];
+    S[3] = hp1[0] * h10 + hp1[1] * h11 + hp1[3] * h1l + hp1[4] + Rm[3];
+}
+
+__device__ __forceinline__ double innovation_angle(double za, double ma, double xp2)
+{
+    // h0 (Robot.cpp:423-426) and the 2π fold of v0 (Robot.cpp:465-475)
+    const double h0 = normalize_radian(ma - xp2);
+    double v0 = za - h0;
+    if (fabs(v0 - 2.0 * EKF_PI) < fabs(v0)) v0 -= 2.0 * EKF_PI;
+    else if (fabs(v0 + 2.0 * EKF_PI) < fabs(v0)) v0 += 2.0 * EKF_PI;
+    return v0;
+}
+
+// Exact candidate evaluation in fp64 (Robot.cpp:367-489).
+__device__ __forceinline__ void eval_candidate(const Block5& b, double ma, double mr,
+                                               const double xp[3], double za, double zr,
+                                               const double Rm[4], double gate, Cand& c)
+{
     double sn, cs;
     sincos(ma, &sn, &cs);
     c.h10 = -cs;
     c.h11 = -sn;
     c.h1l = xp[0] * sn - xp[1] * cs;
-    // P rows: P[a][b] for a,b<3 from the strip; P[a][L] = Rs[a][L]; P[L][a] = Rs[a][L];
-    // P[L][L'] from the diagonal cache.
-    const double p00 = Rs[0], p01 = Rs[1], p02 = Rs[2];
-    const double p10 = Rs[n + 0], p11 = Rs[n + 1], p12 = Rs[n + 2];
-    const double p20 = Rs[2 * n + 0], p21 = Rs[2 * n + 1], p22 = Rs[2 * n + 2];
-    const double p0a = Rs[l0], p1a = Rs[n + l0], p2a = Rs[2 * n + l0];
-    const double p0b = Rs[l1], p1b = Rs[n + l1], p2b = Rs[2 * n + l1];
-    const double daa = D[j], dab = D[Nc + j], dba = D[2 * Nc + j], dbb = D[3 * Nc + j];
-    // hp0 = hr0·P5 with hr0 = (0,0,-1,1,0); hp1 = hr1·P5 with hr1 = (h10,h11,0,h1l,1)
-    const double hp0_0 = -p20 + p0a, hp0_1 = -p21 + p1a, hp0_2 = -p22 + p2a;
-    const double hp0_3 = -p2a + daa, hp0_4 = -p2b + dab;
-    const double hp1_0 = c.h10 * p00 + c.h11 * p10 + c.h1l * p0a + p0b;
-    const double hp1_1 = c.h10 * p01 + c.h11 * p11 + c.h1l * p1a + p1b;
-    const double hp1_2 = c.h10 * p02 + c.h11 * p12 + c.h1l * p2a + p2b;
-    const double hp1_3 = c.h10 * p0a + c.h11 * p1a + c.h1l * daa + dba;
-    const double hp1_4 = c.h10 * p0b + c.h11 * p1b + c.h1l * dab + dbb;
-    (void)hp0_4;
-    c.S[0] = -hp0_2 + hp0_3 + Rm[0];
-    c.S[1] = hp0_0 * c.h10 + hp0_1 * c.h11 + hp0_3 * c.h1l + hp0_4 + Rm[1];
-    c.S[2] = -hp1_2 + hp1_3 + Rm[2];
-    c.S[3] = hp1_0 * c.h10 + hp1_1 * c.h11 + hp1_3 * c.h1l + hp1_4 + Rm[3];
-    // h (Robot.cpp:423-426), S⁻¹ (Robot.cpp:443-457), v and its 2π fold (Robot.cpp:465-475)
-    double h0 = normalize_radian(ma - xp[2]);
+    double hp0[5], hp1[5];
+    innovation_cov(b, c.h10, c.h11, c.h1l, Rm, c.S, hp0, hp1);
     const double h1 = mr - (xp[0] * cs + xp[1] * sn);
     c.Si[0] = c.Si[1] = c.Si[2] = c.Si[3] = 0.0;
-    c.singular = !lu_invert2(c.S, c.Si);
-    double v0 = za - h0;
+    c.singular = lu_invert2(c.S, c.Si) ? 0 : 1;
+    const double v0 = innovation_angle(za, ma, xp[2]);
     const double v1 = zr - h1;
-    if (fabs(v0 - 2.0 * EKF_PI) < fabs(v0)) v0 -= 2.0 * EKF_PI;
-    else if (fabs(v0 + 2.0 * EKF_PI) < fabs(v0)) v0 += 2.0 * EKF_PI;
     c.v[0] = v0;
     c.v[1] = v1;
-    // vᵀ·S⁻¹·v (Robot.cpp:479-486); gate (Robot.cpp:489): NaN passes, as in the reference
+    // vᵀ·S⁻¹·v (Robot.cpp:479-486); gate (:489): a NaN distance passes, as in the reference
     const double vs0 = v0 * c.Si[0] + v1 * c.Si[2];
     const double vs1 = v0 * c.Si[1] + v1 * c.Si[3];
     const double d2 = vs0 * v0 + vs1 * v1;
     c.pass = !(sqrt(fabs(d2)) > gate);
+}
+
+// Certified rejection without fp64 transcendentals: true only if the exact evaluation is
+// guaranteed to fail the gate. cos/sin come from fp32 sincosf (|error| <= EPS for |ma| <= 8);
+// the resulting error in S and v is bounded explicitly and d² = q/det is bounded from below by
+// interval arithmetic. Requires a symmetric R and a determinant that is not tiny relative to
+// |S00·S11| + |S01·S10| (so that the reference's LU-based d² is within 1e-9 of q/det).
+__device__ __forceinline__ bool certified_reject(const Block5& b, double ma, double mr,
+                                                 const double xp[3], double za, double zr,
+                                                 const double Rm[4], double gate)
+{
+    if (!(fabs(ma) <= 8.0) || Rm[1] != Rm[2]) return false;
+    const double EPS = 1e-5;
+    float sf, cf;
+    sincosf((float)ma, &sf, &cf);
+    const double sn = sf, cs = cf;
+    const double h10 = -cs, h11 = -sn, h1l = xp[0] * sn - xp[1] * cs;
+    double S[4], hp0[5], hp1[5];
+    innovation_cov(b, h10, h11, h1l, Rm, S, hp0, hp1);
+    const double v0 = innovation_angle(za, ma, xp[2]);
+    const double v1 = zr - (mr - (xp[0] * cs + xp[1] * sn));
+    const double ex = EPS * (fabs(xp[0]) + fabs(xp[1]));
+    double Pm = fmax(fmax(fmax(fabs(b.p00), fabs(b.p01)), fmax(fabs(b.p02), fabs(b.p10))),
+                     fmax(fmax(fabs(b.p11), fabs(b.p12)), fmax(fabs(b.p20), fabs(b.p21))));
+    Pm = fmax(Pm, fmax(fmax(fmax(fabs(b.p22), fabs(b.p0a)), fmax(fabs(b.p1a), fabs(b.p2a))),
+                       fmax(fmax(fabs(b.p0b), fabs(b.p1b)), fabs(b.p2b))));
+    Pm = fmax(Pm, fmax(fmax(fabs(b.daa), fabs(b.dab)), fmax(fabs(b.dba), fabs(b.dbb))));
+    const double dh = (2.0 * EPS + ex) * Pm;                   // |Δ hp1[b]|
+    const double dS01 = EPS * (fabs(hp0[0]) + fabs(hp0[1])) + ex * fabs(hp0[3]);
+    const double dS10 = 2.0 * dh;
+    const double dS11 = dh * (3.0 + fabs(h1l) + ex) + EPS * (fabs(hp1[0]) + fabs(hp1[1])) +
+                        ex * fabs(hp1[3]);
+    const double dv1 = ex;
+    const double q = v0 * v0 * S[3] - v0 * v1 * (S[1] + S[2]) + v1 * v1 * S[0];
+    const double det = S[0] * S[3] - S[1] * S[2];
+    const double mag_det = fabs(S[0] * S[3]) + fabs(S[1] * S[2]);
+    const double mag_q = v0 * v0 * fabs(S[3]) + fabs(v0 * v1) * (fabs(S[1]) + fabs(S[2])) +
+                         v1 * v1 * fabs(S[0]);
+    const double dq = v0 * v0 * dS11 + fabs(v0) * (fabs(v1) + dv1) * (dS01 + dS10) +
+                      fabs(v0) * dv1 * fabs(S[1] + S[2]) +
+                      (2.0 * fabs(v1) * dv1 + dv1 * dv1) * fabs(S[0]) + 1e-9 * mag_q;
+    const double ddet = fabs(S[0]) * dS11 + fabs(S[1]) * dS10 + fabs(S[2]) * dS01 +
+                        dS01 * dS10 + 1e-9 * mag_det;
+    const double det_lo = det - ddet;
+    if (!(det_lo > 1e-6 * mag_det)) return false;              // also false for NaN / Inf
+    return (q - dq) > gate * gate * (1.0 + 1e-6) * (det + ddet);
 }
 
 __device__ __forceinline__ int wave_min(int v)
@@ -147,33 +342,27 @@ __device__ __forceinline__ int wave_min(int v)
     return v;
 }
 
-// --------------------------------------------------------------------------------------
-// 1. association + gain chain
-// --------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------
+// 1. association + gain chain + augmentation
+// ---------------------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
 {
     const Dims d = p.d;
     const int e = blockIdx.x;
     const int tid = threadIdx.x;
-    const int n = d.n, N = d.N;
+    const int n = d.n, N = d.N, M = d.M;
     double* Rs = p.Rs + (size_t)e * 3 * n;
     double* y = p.y + (size_t)e * n;
     double* D = p.D + (size_t)e * 4 * N;
-    double* Ust = p.Ust + (size_t)e * d.max_lines * 2 * n;
-    double* Vst = p.Vst + (size_t)e * d.max_lines * 2 * n;
-    const size_t opstride = (size_t)d.nb * 64 * (d.kmax / 2);
-    T* Uop = reinterpret_cast<T*>(p.Uop) + (size_t)e * opstride;
-    T* Vop = reinterpret_cast<T*>(p.Vop) + (size_t)e * opstride;
-    const T* Pll = reinterpret_cast<const T*>(p.Pll) + (size_t)e * d.ntiles * TILE_ELEMS;
-    int* res = p.res + (size_t)e * RES_STRIDE;
 
-    __shared__ double sh_xp[3];
-    __shared__ double sh_u[6];     // U_t rows 0..2 (k = 0, 1)
-    __shared__ int sh_red[SCAN_THREADS / 64];
-    extern __shared__ unsigned int sh_matched[];  // bitmask over N landmarks
+    __shared__ double sh_R33[9];        // robot 3×3 block of the current P
+    __shared__ double sh_xp[3];         // current x_pre
+    __shared__ double sh_c[C_WORDS];    // the matched candidate's uniform package
+    __shared__ int sh_red[2][SCAN_THREADS / 64];
+    __shared__ int sh_extra[EKF_MAX_LINES];
+    __shared__ int sh_status;
 
-    double xp[3];
     if (p.phase & PHASE_PREDICT) {
         // Robot.cpp:130-148 (SIMULATIONOFF == true: `rot` unused)
         const double x0 = p.pose[3 * e + 0], y0 = p.pose[3 * e + 1], t0 = p.pose[3 * e + 2];
@@ -181,22 +370,32 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         const double u2 = t0 - enc[2];
         const double dx = x0 - enc[0], dy = y0 - enc[1];
         const double u0 = sqrt(dx * dx + dy * dy);
-        xp[0] = x0 + u0 * cos(t0 + u2 / 2.0);
-        xp[1] = y0 + u0 * sin(t0 + u2 / 2.0);
-        xp[2] = t0 + u2;
         const double c = u2 / 2.0 + t0;
         double sc, cc;
         sincos(c, &sc, &cc);
         const double F3[9] = {1, 0, -u0 * sc, 0, 1, u0 * cc, 0, 0, 1};
-        // robot–landmark block: rows 0..2 of Fx·P (Robot.cpp:242); columns b >= 3
-        for (int b = 3 + tid; b < n; b += SCAN_THREADS) {
-            const double r0 = Rs[b], r1 = Rs[n + b], r2 = Rs[2 * n + b];
-            Rs[b] = F3[0] * r0 + F3[1] * r1 + F3[2] * r2;
-            Rs[n + b] = F3[3] * r0 + F3[4] * r1 + F3[5] * r2;
-            Rs[2 * n + b] = F3[6] * r0 + F3[7] * r1 + F3[8] * r2;
+        // rows 0..2 of Fx·P for the owned landmark columns (Robot.cpp:242)
+        for (int j = tid; j < N; j += SCAN_THREADS) {
+            const int b = 3 + 2 * j;
+            const double2 r0 = *reinterpret_cast<const double2*>(Rs + b);
+            const double2 r1 = *reinterpret_cast<const double2*>(Rs + n + b);
+            const double2 r2 = *reinterpret_cast<const double2*>(Rs + 2 * n + b);
+            double2 o0, o1, o2;
+            o0.x = F3[0] * r0.x + F3[1] * r1.x + F3[2] * r2.x;
+            o0.y = F3[0] * r0.y + F3[1] * r1.y + F3[2] * r2.y;
+            o1.x = F3[3] * r0.x + F3[4] * r1.x + F3[5] * r2.x;
+            o1.y = F3[3] * r0.y + F3[4] * r1.y + F3[5] * r2.y;
+            o2.x = F3[6] * r0.x + F3[7] * r1.x + F3[8] * r2.x;
+            o2.y = F3[6] * r0.y + F3[7] * r1.y + F3[8] * r2.y;
+            *reinterpret_cast<double2*>(Rs + b) = o0;
+            *reinterpret_cast<double2*>(Rs + n + b) = o1;
+            *reinterpret_cast<double2*>(Rs + 2 * n + b) = o2;
         }
         if (tid == 0) {
-            // 3×3 block: F3·P33·F3ᵀ + Fu3·Q·Fu3ᵀ (Robot.cpp:178-258)
+            // x_pre (Robot.cpp:148); 3×3 block F3·P33·F3ᵀ + Fu3·Q·Fu3ᵀ (Robot.cpp:178-258)
+            sh_xp[0] = x0 + u0 * cos(t0 + u2 / 2.0);
+            sh_xp[1] = y0 + u0 * sin(t0 + u2 / 2.0);
+            sh_xp[2] = t0 + u2;
             const double Fu3[9] = {cc, 0, -u0 * sc / 2.0, sc, 1, u0 * cc / 2.0, 0, 0, 1};
             const double qs = (-1.0 / (1 + fabs(u0)) + 1);
             const double Q[9] = {p.enc_noise * qs, 0, 0, 0, 2 * p.enc_noise * qs, 0, 0, 0,
@@ -220,212 +419,387 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
                         s += FP[a * 3 + k] * F3[b * 3 + k];
                         t += FuQ[a * 3 + k] * Fu3[b * 3 + k];
                     }
-                    Rs[a * n + b] = s + t;
+                    sh_R33[a * 3 + b] = s + t;
                 }
             if (!(p.phase & PHASE_UPDATE)) {
-                p.xpre[3 * e + 0] = xp[0];
-                p.xpre[3 * e + 1] = xp[1];
-                p.xpre[3 * e + 2] = xp[2];
+                for (int a = 0; a < 9; a++) Rs[(a / 3) * n + (a % 3)] = sh_R33[a];
+                p.xpre[3 * e + 0] = sh_xp[0];
+                p.xpre[3 * e + 1] = sh_xp[1];
+                p.xpre[3 * e + 2] = sh_xp[2];
             }
         }
-        __syncthreads();
-    } else {
-        xp[0] = p.xpre[3 * e + 0];
-        xp[1] = p.xpre[3 * e + 1];
-        xp[2] = p.xpre[3 * e + 2];
+        if (!(p.phase & PHASE_UPDATE)) return;
+    } else if (tid == 0) {
+        for (int a = 0; a < 9; a++) sh_R33[a] = Rs[(a / 3) * n + (a % 3)];
+        sh_xp[0] = p.xpre[3 * e + 0];
+        sh_xp[1] = p.xpre[3 * e + 1];
+        sh_xp[2] = p.xpre[3 * e + 2];
     }
-    if (!(p.phase & PHASE_UPDATE)) return;
+    if (tid == 0) sh_status = 0;
 
     // ---------------- association / update (Robot.cpp:288-904) ----------------
+    const size_t opstride = (size_t)d.nb * 64 * (d.kmax / 2);
+    double* Ust = p.cur.Ust + (size_t)e * d.max_lines * n * 2;
+    double* Vst = p.cur.Vst + (size_t)e * d.max_lines * n * 2;
+    T* Uop = reinterpret_cast<T*>(p.cur.Uop) + (size_t)e * opstride;
+    T* Vop = reinterpret_cast<T*>(p.cur.Vop) + (size_t)e * opstride;
+    double* patch = p.cur.patch + (size_t)e * d.max_lines * 2 * M;
+    double* pdiag = p.cur.patch_diag + (size_t)e * d.max_lines * 4;
+    int* res = p.cur.res + (size_t)e * RES_STRIDE;
+
+    PllView<T> pv;
+    pv.X = reinterpret_cast<const T*>(p.Pread) + (size_t)e * d.ntiles * TILE_ELEMS;
+    pv.nb = d.nb;
+    pv.kmax = d.kmax;
+    pv.M = M;
+    pv.pend_ks = 0;
+    pv.pend_reset = 0;
+    pv.pU = pv.pV = nullptr;
+    pv.ps0 = pv.pn = 0;
+    pv.patch = pv.pdiag = nullptr;
+    if (p.pending) {
+        const int* pres = p.prev.res + (size_t)e * RES_STRIDE;
+        pv.pend_ks = pres[RES_KSTEPS];
+        pv.pend_reset = pres[RES_RESET];
+        pv.pU = reinterpret_cast<const T*>(p.prev.Uop) + (size_t)e * opstride;
+        pv.pV = reinterpret_cast<const T*>(p.prev.Vop) + (size_t)e * opstride;
+        pv.ps0 = pres[RES_SAVED_IN];
+        pv.pn = pres[RES_NADD];
+        pv.patch = p.prev.patch + (size_t)e * d.max_lines * 2 * M;
+        pv.pdiag = p.prev.patch_diag + (size_t)e * d.max_lines * 4;
+    }
+
     int L = p.nlines[e];
     L = L < 0 ? 0 : (L > d.max_lines ? d.max_lines : L);
     const int s = p.saved[e];
     const ekf_line* lines = p.lines + (size_t)e * d.max_lines;
 
-    // diagonal cache of P_ll and matched bitmask
+    // diagonal 2x2 blocks of the owned saved landmarks
     for (int j = tid; j < s; j += SCAN_THREADS) {
-        D[j] = ll_get(Pll, 2 * j, 2 * j, d.nb);
-        D[N + j] = ll_get(Pll, 2 * j, 2 * j + 1, d.nb);
-        D[2 * N + j] = ll_get(Pll, 2 * j + 1, 2 * j, d.nb);
-        D[3 * N + j] = ll_get(Pll, 2 * j + 1, 2 * j + 1, d.nb);
+        double blk[4];
+        pll_block(pv, 2 * j, 2 * j, blk);
+        *reinterpret_cast<double4*>(D + 4 * j) = make_double4(blk[0], blk[1], blk[2], blk[3]);
     }
-    const int nwords = (N + 31) / 32;
-    for (int w = tid; w < nwords; w += SCAN_THREADS) sh_matched[w] = 0u;
-    __syncthreads();
+    __syncthreads();   // sh_R33 / sh_xp / sh_status
 
+    unsigned long long mbits = 0ull;   // matched flags of the owned landmarks
     int m = 0, nextra = 0, status = 0;
     for (int i = 0; i < L; ++i) {
         const ekf_line ln = lines[i];
         double Rm[4] = {0, 0, 0, 0};
         if (p.r_mode == 1) {
-            if (i < 4) Rm[i] = ln.R[3];   // Robot.cpp:302-304 as written (zero-init stack)
+            if (i < 4) Rm[i] = ln.R[3];   // Robot.cpp:302-304 as written (zero-initialised stack)
         } else {
             Rm[0] = ln.R[0]; Rm[1] = ln.R[1]; Rm[2] = ln.R[2]; Rm[3] = ln.R[3];
         }
-        // parallel gating, first passing unmatched j wins (Robot.cpp:313-498)
+        // gating over owned candidates, first passing unmatched j (Robot.cpp:313-498)
         int best = 0x7fffffff;
-        bool sing = false;
-        for (int j = tid; j < s; j += SCAN_THREADS) {
-            if (sh_matched[j >> 5] & (1u << (j & 31))) continue;
-            Cand c;
-            eval_candidate(j, Rs, n, D, N, y, xp, ln.alpha, ln.r, Rm, p.gate, c);
-            sing |= c.singular;
-            if (c.pass) { best = j; break; }
-        }
-        if (sing) status |= EKF_ST_SINGULAR;
-        best = wave_min(best);
-        if ((tid & 63) == 0) sh_red[tid >> 6] = best;
-        __syncthreads();
-        int jstar = sh_red[0];
+        {
+            double R33[9], xp[3];
 #pragma unroll
-        for (int w = 1; w < SCAN_THREADS / 64; w++) jstar = min(jstar, sh_red[w]);
-        if (jstar == 0x7fffffff) {
-            // no match (or s == 0): the line goes to extraLines (Robot.cpp:308-310, 492-496)
-            if (tid == 0) {
-                res[RES_MATCH + i] = -1;
-                res[RES_EXTRA + nextra] = i;
-            }
-            nextra++;
-            __syncthreads();   // sh_red reuse
-            continue;
-        }
-        // ---- match (Robot.cpp:500-641) in deferred low-rank form ----
-        Cand c;
-        eval_candidate(jstar, Rs, n, D, N, y, xp, ln.alpha, ln.r, Rm, p.gate, c);
-        const int t = m;
-        const int l0 = 3 + 2 * jstar, l1 = l0 + 1;
-        if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
-        double* Ut0 = Ust + (size_t)(2 * t) * n;
-        double* Ut1 = Ut0 + n;
-        double* Vt0 = Vst + (size_t)(2 * t) * n;
-        double* Vt1 = Vt0 + n;
-        for (int b = tid; b < n; b += SCAN_THREADS) {
-            double pb0, pb1, pb2, pba, pbb;
-            if (b < 3) {
-                pb0 = Rs[b * n + 0]; pb1 = Rs[b * n + 1]; pb2 = Rs[b * n + 2];
-                pba = Rs[b * n + l0]; pbb = Rs[b * n + l1];
-            } else {
-                pb0 = Rs[b]; pb1 = Rs[n + b]; pb2 = Rs[2 * n + b];
-                pba = ll_get(Pll, b - 3, l0 - 3, d.nb);
-                pbb = ll_get(Pll, b - 3, l1 - 3, d.nb);
-                for (int q = 0; q < t; q++) {   // earlier matches of this scan, in order
-                    const double* Uq = Ust + (size_t)(2 * q) * n;
-                    const double* Vq = Vst + (size_t)(2 * q) * n;
-                    pba -= Uq[b] * Vq[l0] + Uq[n + b] * Vq[n + l0];
-                    pbb -= Uq[b] * Vq[l1] + Uq[n + b] * Vq[n + l1];
+            for (int a = 0; a < 9; a++) R33[a] = sh_R33[a];
+            xp[0] = sh_xp[0]; xp[1] = sh_xp[1]; xp[2] = sh_xp[2];
+            int r = 0;
+            for (int j = tid; j < s; j += SCAN_THREADS, r++) {
+                if ((mbits >> r) & 1ull) continue;
+                const double4 dj = *reinterpret_cast<const double4*>(D + 4 * j);
+                const double Dj[4] = {dj.x, dj.y, dj.z, dj.w};
+                Block5 b5;
+                load_block5(b5, j, R33, Rs, n, Dj);
+                const double2 m2 = *reinterpret_cast<const double2*>(y + 3 + 2 * j);
+                if (certified_reject(b5, m2.x, m2.y, xp, ln.alpha, ln.r, Rm, p.gate)) continue;
+                Cand c;
+                eval_candidate(b5, m2.x, m2.y, xp, ln.alpha, ln.r, Rm, p.gate, c);
+                status |= c.singular ? EKF_ST_SINGULAR : 0;
+                if (c.pass) {
+                    best = j;
+                    break;
                 }
             }
-            // W = P·Hᵀ (Robot.cpp:522), K = W·S⁻¹ (:526), U = K·S (:560)
-            const double w0 = -pb2 + pba;
-            const double w1 = c.h10 * pb0 + c.h11 * pb1 + c.h1l * pba + pbb;
-            const double k0 = w0 * c.Si[0] + w1 * c.Si[2];
-            const double k1 = w0 * c.Si[1] + w1 * c.Si[3];
-            const double u0 = k0 * c.S[0] + k1 * c.S[2];
-            const double u1 = k0 * c.S[1] + k1 * c.S[3];
-            Ut0[b] = u0; Ut1[b] = u1;
-            Vt0[b] = k0; Vt1[b] = k1;
-            // y = x_pre ⊕ y_landmarks + K·v (Robot.cpp:579-592)
-            const double yb = (b < 3) ? xp[b] : y[b];
-            y[b] = yb + (k0 * c.v[0] + k1 * c.v[1]);
-            if (b < 3) {
-                sh_u[b] = u0;
-                sh_u[3 + b] = u1;
-            } else {
-                const int lr = b - 3;
-                if constexpr (sizeof(T) == 4) {
-                    Uop[op_index_f32(lr, 2 * t, d.kmax)] = (T)(-u0);
-                    Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (T)(-u1);
-                    Vop[op_index_f32(lr, 2 * t, d.kmax)] = (T)k0;
-                    Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (T)k1;
-                } else {
-                    Uop[op_index_f64(lr, 2 * t, d.kmax)] = (T)(-u0);
-                    Uop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (T)(-u1);
-                    Vop[op_index_f64(lr, 2 * t, d.kmax)] = (T)k0;
-                    Vop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (T)k1;
+            const int wbest = wave_min(best);
+            if ((tid & 63) == 0) sh_red[i & 1][tid >> 6] = wbest;
+            __syncthreads();
+            int jstar = sh_red[i & 1][0];
+#pragma unroll
+            for (int w = 1; w < SCAN_THREADS / 64; w++) jstar = min(jstar, sh_red[i & 1][w]);
+            if (jstar == 0x7fffffff) {
+                // no match (or s == 0): the line goes to extraLines (Robot.cpp:308-310, 492-496)
+                if (tid == 0) {
+                    res[RES_MATCH + i] = -1;
+                    res[RES_EXTRA + nextra] = i;
+                    sh_extra[nextra] = i;
                 }
+                nextra++;
+                continue;
             }
+            best = jstar;
         }
-        __syncthreads();
-        // eager downdate of the robot strip and the diagonal cache (Robot.cpp:568)
-        for (int b = tid; b < n; b += SCAN_THREADS) {
-            const double k0 = Vt0[b], k1 = Vt1[b];
-            Rs[b] -= sh_u[0] * k0 + sh_u[3] * k1;
-            Rs[n + b] -= sh_u[1] * k0 + sh_u[4] * k1;
-            Rs[2 * n + b] -= sh_u[2] * k0 + sh_u[5] * k1;
-        }
-        for (int j = tid; j < s; j += SCAN_THREADS) {
-            const int a = 3 + 2 * j, bb = a + 1;
-            const double ua0 = Ut0[a], ua1 = Ut1[a], ub0 = Ut0[bb], ub1 = Ut1[bb];
-            const double va0 = Vt0[a], va1 = Vt1[a], vb0 = Vt0[bb], vb1 = Vt1[bb];
-            D[j] -= ua0 * va0 + ua1 * va1;
-            D[N + j] -= ua0 * vb0 + ua1 * vb1;
-            D[2 * N + j] -= ub0 * va0 + ub1 * va1;
-            D[3 * N + j] -= ub0 * vb0 + ub1 * vb1;
-        }
-        if (tid == 0) {
-            y[2] = normalize_radian(y[2]);     // Robot.cpp:596
-            sh_xp[0] = y[0];
-            sh_xp[1] = y[1];
-            sh_xp[2] = y[2];
-            sh_matched[jstar >> 5] |= (1u << (jstar & 31));
+        const int jstar = best;
+        if ((jstar % SCAN_THREADS) == tid) {
+            // the owner of j*: exact re-evaluation, the uniform gain of the robot rows
+            // (Robot.cpp:522-602 for rows 0..2) and the new x_pre, published through LDS
+            const double4 dj = *reinterpret_cast<const double4*>(D + 4 * jstar);
+            const double Dj[4] = {dj.x, dj.y, dj.z, dj.w};
+            double R33[9], xp[3];
+#pragma unroll
+            for (int a = 0; a < 9; a++) R33[a] = sh_R33[a];
+            xp[0] = sh_xp[0]; xp[1] = sh_xp[1]; xp[2] = sh_xp[2];
+            Block5 b5;
+            load_block5(b5, jstar, R33, Rs, n, Dj);
+            const double2 m2 = *reinterpret_cast<const double2*>(y + 3 + 2 * jstar);
+            Cand c;
+            eval_candidate(b5, m2.x, m2.y, xp, ln.alpha, ln.r, Rm, p.gate, c);
+            const double RL0[3] = {b5.p0a, b5.p1a, b5.p2a};
+            const double RL1[3] = {b5.p0b, b5.p1b, b5.p2b};
+            double Kr[6], Ur[6], yn[3];
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                // W = P·Hᵀ (Robot.cpp:522), K = W·S⁻¹ (:526), U = K·S (:560)
+                const double w0 = -R33[a * 3 + 2] + RL0[a];
+                const double w1 = c.h10 * R33[a * 3 + 0] + c.h11 * R33[a * 3 + 1] + c.h1l * RL0[a] + RL1[a];
+                const double k0 = w0 * c.Si[0] + w1 * c.Si[2];
+                const double k1 = w0 * c.Si[1] + w1 * c.Si[3];
+                Kr[2 * a] = k0;
+                Kr[2 * a + 1] = k1;
+                Ur[2 * a] = k0 * c.S[0] + k1 * c.S[2];
+                Ur[2 * a + 1] = k0 * c.S[1] + k1 * c.S[3];
+                yn[a] = xp[a] + (k0 * c.v[0] + k1 * c.v[1]);   // Robot.cpp:579-592
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                sh_c[C_S + q] = c.S[q];
+                sh_c[C_SI + q] = c.Si[q];
+            }
+            sh_c[C_V] = c.v[0];
+            sh_c[C_V + 1] = c.v[1];
+            sh_c[C_H] = c.h10;
+            sh_c[C_H + 1] = c.h11;
+            sh_c[C_H + 2] = c.h1l;
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                sh_c[C_KR + q] = Kr[q];
+                sh_c[C_UR + q] = Ur[q];
+            }
+#pragma unroll
+            for (int a = 0; a < 3; a++)
+#pragma unroll
+                for (int cc = 0; cc < 3; cc++)
+                    sh_R33[a * 3 + cc] = R33[a * 3 + cc] - (Ur[2 * a] * Kr[2 * cc] + Ur[2 * a + 1] * Kr[2 * cc + 1]);
+            sh_xp[0] = yn[0];
+            sh_xp[1] = yn[1];
+            sh_xp[2] = normalize_radian(yn[2]);   // Robot.cpp:596
+            mbits |= 1ull << (jstar / SCAN_THREADS);
             res[RES_MATCH + i] = jstar;
         }
+        if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
         __syncthreads();
-        xp[0] = sh_xp[0];
-        xp[1] = sh_xp[1];
-        xp[2] = sh_xp[2];
+        const double S0 = sh_c[C_S], S1 = sh_c[C_S + 1], S2 = sh_c[C_S + 2], S3 = sh_c[C_S + 3];
+        const double Si0 = sh_c[C_SI], Si1 = sh_c[C_SI + 1], Si2 = sh_c[C_SI + 2], Si3 = sh_c[C_SI + 3];
+        const double v0 = sh_c[C_V], v1 = sh_c[C_V + 1];
+        const double h10 = sh_c[C_H], h11 = sh_c[C_H + 1], h1l = sh_c[C_H + 2];
+        const int t = m;
+        const int l0 = 3 + 2 * jstar;
+
+        // owned landmark rows
+        for (int j = tid; j < N; j += SCAN_THREADS) {
+            const int b0 = 3 + 2 * j;
+            double blk[4];
+            pll_block(pv, 2 * j, 2 * jstar, blk);
+            for (int q = 0; q < t; q++) {   // earlier matches of this scan, in order
+                const double4 uq = *reinterpret_cast<const double4*>(Ust + ((size_t)q * n + b0) * 2);
+                const double4 vq = *reinterpret_cast<const double4*>(Vst + ((size_t)q * n + l0) * 2);
+                blk[0] -= uq.x * vq.x + uq.y * vq.y;
+                blk[1] -= uq.x * vq.z + uq.y * vq.w;
+                blk[2] -= uq.z * vq.x + uq.w * vq.y;
+                blk[3] -= uq.z * vq.z + uq.w * vq.w;
+            }
+            double2 rr[3];
+#pragma unroll
+            for (int a = 0; a < 3; a++) rr[a] = *reinterpret_cast<const double2*>(Rs + a * n + b0);
+            double2 yb = *reinterpret_cast<const double2*>(y + b0);
+            double kk[4], uu[4];
+#pragma unroll
+            for (int pp = 0; pp < 2; pp++) {
+                const double pb0 = pp ? rr[0].y : rr[0].x;
+                const double pb1 = pp ? rr[1].y : rr[1].x;
+                const double pb2 = pp ? rr[2].y : rr[2].x;
+                const double pba = blk[pp * 2 + 0], pbb = blk[pp * 2 + 1];
+                const double w0 = -pb2 + pba;
+                const double w1 = h10 * pb0 + h11 * pb1 + h1l * pba + pbb;
+                const double k0 = w0 * Si0 + w1 * Si2;
+                const double k1 = w0 * Si1 + w1 * Si3;
+                kk[2 * pp] = k0;
+                kk[2 * pp + 1] = k1;
+                uu[2 * pp] = k0 * S0 + k1 * S2;
+                uu[2 * pp + 1] = k0 * S1 + k1 * S3;
+                const double dy = k0 * v0 + k1 * v1;
+                if (pp) yb.y += dy; else yb.x += dy;
+            }
+            *reinterpret_cast<double2*>(y + b0) = yb;
+            *reinterpret_cast<double4*>(Ust + ((size_t)t * n + b0) * 2) = make_double4(uu[0], uu[1], uu[2], uu[3]);
+            *reinterpret_cast<double4*>(Vst + ((size_t)t * n + b0) * 2) = make_double4(kk[0], kk[1], kk[2], kk[3]);
+#pragma unroll
+            for (int pp = 0; pp < 2; pp++) {
+                const int lr = 2 * j + pp;
+                if constexpr (sizeof(T) == 4) {
+                    Uop[op_index_f32(lr, 2 * t, d.kmax)] = (T)(-uu[2 * pp]);
+                    Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (T)(-uu[2 * pp + 1]);
+                    Vop[op_index_f32(lr, 2 * t, d.kmax)] = (T)kk[2 * pp];
+                    Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (T)kk[2 * pp + 1];
+                } else {
+                    Uop[op_index_f64(lr, 2 * t, d.kmax)] = (T)(-uu[2 * pp]);
+                    Uop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (T)(-uu[2 * pp + 1]);
+                    Vop[op_index_f64(lr, 2 * t, d.kmax)] = (T)kk[2 * pp];
+                    Vop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (T)kk[2 * pp + 1];
+                }
+            }
+            // eager downdate of the owned robot-strip columns (Robot.cpp:568)
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                const double ua0 = sh_c[C_UR + 2 * a], ua1 = sh_c[C_UR + 2 * a + 1];
+                rr[a].x -= ua0 * kk[0] + ua1 * kk[1];
+                rr[a].y -= ua0 * kk[2] + ua1 * kk[3];
+                *reinterpret_cast<double2*>(Rs + a * n + b0) = rr[a];
+            }
+            if (j < s) {
+                double4 dj = *reinterpret_cast<const double4*>(D + 4 * j);
+                dj.x -= uu[0] * kk[0] + uu[1] * kk[1];
+                dj.y -= uu[0] * kk[2] + uu[1] * kk[3];
+                dj.z -= uu[2] * kk[0] + uu[3] * kk[1];
+                dj.w -= uu[2] * kk[2] + uu[3] * kk[3];
+                *reinterpret_cast<double4*>(D + 4 * j) = dj;
+            }
+        }
         m++;
     }
 
-    // ---------------- commit (Robot.cpp:702-716, 893-904) ----------------
-    const int added = min(nextra, N - s);
-    const int reset = (s + added > N - p.reset_margin) ? 1 : 0;
+    // ---------------- commit (Robot.cpp:702-716) ----------------
+    __syncthreads();   // sh_extra, sh_xp, sh_R33 final
+    double xp[3] = {sh_xp[0], sh_xp[1], sh_xp[2]};
+    double pose[3] = {xp[0], xp[1], xp[2]};
+    if (L == 0 || m == 0) pose[2] = normalize_radian(xp[2]);   // y[2] stays un-normalised
     if (tid == 0) {
-        if (L == 0 || m == 0) {
-            y[0] = xp[0];
-            y[1] = xp[1];
-            y[2] = xp[2];
-            p.pose[3 * e + 0] = xp[0];
-            p.pose[3 * e + 1] = xp[1];
-            p.pose[3 * e + 2] = normalize_radian(xp[2]);
-        } else {
-            p.pose[3 * e + 0] = y[0];
-            p.pose[3 * e + 1] = y[1];
-            p.pose[3 * e + 2] = y[2];
+        y[0] = xp[0];
+        y[1] = xp[1];
+        y[2] = xp[2];
+        p.pose[3 * e + 0] = pose[0];
+        p.pose[3 * e + 1] = pose[1];
+        p.pose[3 * e + 2] = pose[2];
+    }
+    const int nadd = min(nextra, N - s);
+    const int reset = (s + nadd > N - p.reset_margin) ? 1 : 0;
+    if (nextra > nadd) status |= EKF_ST_CAP;
+    double R33[9];
+#pragma unroll
+    for (int a = 0; a < 9; a++) R33[a] = sh_R33[a];
+
+    // ---------------- augmentation (Robot.cpp:776-866) ----------------
+    if (!reset) {
+        for (int q = 0; q < nadd; q++) {
+            const ekf_line ln = lines[sh_extra[q]];
+            const int sq = s + q;
+            const int l0 = 3 + 2 * sq;
+            double alfa = ln.alpha;
+            const double r = ln.r + (pose[0] * cos(alfa) + pose[1] * sin(alfa));
+            alfa += pose[2];
+            double sa, ca;
+            sincos(alfa, &sa, &ca);
+            // landmark columns of P[l0:l0+2, 0:l0] = Gx·P[0:3, 0:l0] (Robot.cpp:852-862) → patch
+            double* prow = patch + (size_t)(q * 2) * M;
+            for (int jc = tid; jc < sq; jc += SCAN_THREADS) {
+                const int c = 3 + 2 * jc;
+                const double2 r0 = *reinterpret_cast<const double2*>(Rs + c);
+                const double2 r1 = *reinterpret_cast<const double2*>(Rs + n + c);
+                const double2 r2 = *reinterpret_cast<const double2*>(Rs + 2 * n + c);
+                *reinterpret_cast<double2*>(prow + 2 * jc) = r2;
+                double2 g;
+                g.x = ca * r0.x + sa * r1.x;
+                g.y = ca * r0.y + sa * r1.y;
+                *reinterpret_cast<double2*>(prow + M + 2 * jc) = g;
+            }
+            if ((sq % SCAN_THREADS) == tid) {
+                // the new landmark's owner: its robot-strip columns (robot part of the same
+                // product, stored transposed) and its mean (Robot.cpp:801-803)
+                double2 c0, c1, c2;
+                c0.x = R33[6]; c0.y = ca * R33[0] + sa * R33[3];
+                c1.x = R33[7]; c1.y = ca * R33[1] + sa * R33[4];
+                c2.x = R33[8]; c2.y = ca * R33[2] + sa * R33[5];
+                *reinterpret_cast<double2*>(Rs + l0) = c0;
+                *reinterpret_cast<double2*>(Rs + n + l0) = c1;
+                *reinterpret_cast<double2*>(Rs + 2 * n + l0) = c2;
+                y[l0] = normalize_radian(alfa);
+                y[l0 + 1] = r;
+            }
+            if (tid == 0) {
+                // P_ll = Gx·Prr·Gxᵀ + Gl·R·Glᵀ (Robot.cpp:813-847); Gx = [[0,0,1],[ca,sa,0]],
+                // Gl = [[1,0],[y1·ca − y0·sa, 1]]
+                const double Gx[6] = {0, 0, 1, ca, sa, 0};
+                const double Gl[4] = {1.0, 0, xp[1] * ca - xp[0] * sa, 1};
+                double GP[6], GlR[4];
+                for (int a = 0; a < 2; a++)
+                    for (int b = 0; b < 3; b++) {
+                        double acc = 0.0;
+                        for (int k = 0; k < 3; k++) acc += Gx[a * 3 + k] * R33[k * 3 + b];
+                        GP[a * 3 + b] = acc;
+                    }
+                for (int a = 0; a < 2; a++)
+                    for (int b = 0; b < 2; b++)
+                        GlR[a * 2 + b] = Gl[a * 2 + 0] * ln.R[0 * 2 + b] + Gl[a * 2 + 1] * ln.R[1 * 2 + b];
+                for (int a = 0; a < 2; a++)
+                    for (int b = 0; b < 2; b++) {
+                        double g = 0.0;
+                        for (int k = 0; k < 3; k++) g += GP[a * 3 + k] * Gx[b * 3 + k];
+                        const double h = GlR[a * 2 + 0] * Gl[b * 2 + 0] + GlR[a * 2 + 1] * Gl[b * 2 + 1];
+                        pdiag[q * 4 + a * 2 + b] = g + h;
+                    }
+            }
         }
-        if (nextra > added) status |= EKF_ST_CAP;
+    }
+    // status: OR over the workgroup
+    {
+        int st = status;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) st |= __shfl_xor(st, off, 64);
+        if ((tid & 63) == 0 && st) atomicOr(&sh_status, st);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int a = 0; a < 9; a++) Rs[(a / 3) * n + (a % 3)] = R33[a];
+        res[RES_STATUS] = sh_status;
         res[RES_M] = m;
         res[RES_NEXTRA] = nextra;
         res[RES_SAVED_IN] = s;
-        res[RES_SAVED] = reset ? 0 : s + added;
+        res[RES_SAVED] = reset ? 0 : s + nadd;
         res[RES_RESET] = reset;
-        res[RES_STATUS] = status;
+        res[RES_NADD] = reset ? 0 : nadd;
         res[RES_NLINES] = L;
         res[RES_KSTEPS] = (sizeof(T) == 4) ? m : (m + 1) / 2;
-        if (reset) p.saved[e] = 0;
+        p.saved[e] = reset ? 0 : s + nadd;
     }
     // f64 operands: zero the odd tail column pair of the last 4-wide k-step
     if (sizeof(T) == 8 && (m & 1)) {
-        for (int lr = tid; lr < d.M; lr += SCAN_THREADS) {
+        for (int lr = tid; lr < M; lr += SCAN_THREADS) {
             Uop[op_index_f64(lr, 2 * m, d.kmax)] = (T)0;
             Uop[op_index_f64(lr, 2 * m + 1, d.kmax)] = (T)0;
             Vop[op_index_f64(lr, 2 * m, d.kmax)] = (T)0;
             Vop[op_index_f64(lr, 2 * m + 1, d.kmax)] = (T)0;
         }
     }
-    if (reset) {
-        for (int b = 3 + tid; b < n; b += SCAN_THREADS) {
-            y[b] = 0.0;
-            Rs[b] = 0.0;
-            Rs[n + b] = 0.0;
-            Rs[2 * n + b] = 0.0;
+    if (reset) {   // Robot.cpp:893-904 (the landmark block is zeroed by downdate_kernel)
+        for (int j = tid; j < N; j += SCAN_THREADS) {
+            const int b = 3 + 2 * j;
+            const double2 z = make_double2(0.0, 0.0);
+            *reinterpret_cast<double2*>(y + b) = z;
+            *reinterpret_cast<double2*>(Rs + b) = z;
+            *reinterpret_cast<double2*>(Rs + n + b) = z;
+            *reinterpret_cast<double2*>(Rs + 2 * n + b) = z;
         }
     }
 }
 
-// --------------------------------------------------------------------------------------
-// 2. packed rank-2m covariance downdate on MFMA
-// --------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------
+// 2. packed rank-2m covariance downdate on MFMA (out of place: X_{k-1} → X_k)
+// ---------------------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
@@ -445,20 +819,28 @@ __global__ __launch_bounds__(DD_THREADS) void downdate_f32_kernel(DowndateParams
         const int* res = p.res + (size_t)e * RES_STRIDE;
         const int ks = res[RES_KSTEPS];
         const int reset = res[RES_RESET];
-        if (!reset && ks == 0) continue;
-        float* tile = reinterpret_cast<float*>(p.Pll) + ((size_t)e * d.ntiles + t) * TILE_ELEMS;
-        f32x4* tv = reinterpret_cast<f32x4*>(tile) + lane;
+        const size_t toff = ((size_t)e * d.ntiles + t) * TILE_ELEMS;
+        const f32x4* src = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.Pin) + toff) + lane;
+        f32x4* dst = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.Pout) + toff) + lane;
         if (reset) {
             const f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int q = 0; q < 4; q++) __builtin_nontemporal_store(z, tv + q * 64);
+            for (int q = 0; q < 4; q++) __builtin_nontemporal_store(z, dst + q * 64);
+            continue;
+        }
+        if (ks == 0) {
+            if (p.Pin != p.Pout) {   // no match: X_k = X_{k-1} (P_t0 ← P_pre, Robot.cpp:713)
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    __builtin_nontemporal_store(__builtin_nontemporal_load(src + q * 64), dst + q * 64);
+            }
             continue;
         }
         const int2 rc = p.tile_rc[t];
         f32x16 acc;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const f32x4 v = __builtin_nontemporal_load(tv + q * 64);
+            const f32x4 v = __builtin_nontemporal_load(src + q * 64);
             acc[4 * q + 0] = v[0];
             acc[4 * q + 1] = v[1];
             acc[4 * q + 2] = v[2];
@@ -483,7 +865,7 @@ __global__ __launch_bounds__(DD_THREADS) void downdate_f32_kernel(DowndateParams
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const f32x4 v = {acc[4 * q + 0], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
-            __builtin_nontemporal_store(v, tv + q * 64);
+            __builtin_nontemporal_store(v, dst + q * 64);
         }
     }
 }
@@ -503,15 +885,25 @@ __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams
         const int* res = p.res + (size_t)e * RES_STRIDE;
         const int ks = res[RES_KSTEPS];
         const int reset = res[RES_RESET];
-        if (!reset && ks == 0) continue;
-        double* tile = reinterpret_cast<double*>(p.Pll) + ((size_t)e * d.ntiles + t) * TILE_ELEMS;
-        f64x2* tv = reinterpret_cast<f64x2*>(tile) + 2 * lane;
+        const size_t toff = ((size_t)e * d.ntiles + t) * TILE_ELEMS;
+        const f64x2* src = reinterpret_cast<const f64x2*>(reinterpret_cast<const double*>(p.Pin) + toff) + 2 * lane;
+        f64x2* dst = reinterpret_cast<f64x2*>(reinterpret_cast<double*>(p.Pout) + toff) + 2 * lane;
         if (reset) {
             const f64x2 z = {0.0, 0.0};
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                __builtin_nontemporal_store(z, tv + q * 128);
-                __builtin_nontemporal_store(z, tv + q * 128 + 1);
+                __builtin_nontemporal_store(z, dst + q * 128);
+                __builtin_nontemporal_store(z, dst + q * 128 + 1);
+            }
+            continue;
+        }
+        if (ks == 0) {
+            if (p.Pin != p.Pout) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    __builtin_nontemporal_store(__builtin_nontemporal_load(src + q * 128), dst + q * 128);
+                    __builtin_nontemporal_store(__builtin_nontemporal_load(src + q * 128 + 1), dst + q * 128 + 1);
+                }
             }
             continue;
         }
@@ -519,8 +911,8 @@ __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams
         f64x4 acc[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const f64x2 v0 = __builtin_nontemporal_load(tv + q * 128);
-            const f64x2 v1 = __builtin_nontemporal_load(tv + q * 128 + 1);
+            const f64x2 v0 = __builtin_nontemporal_load(src + q * 128);
+            const f64x2 v1 = __builtin_nontemporal_load(src + q * 128 + 1);
             acc[q][0] = v0[0];
             acc[q][1] = v0[1];
             acc[q][2] = v1[0];
@@ -543,105 +935,59 @@ __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams
         for (int q = 0; q < 4; q++) {
             const f64x2 v0 = {acc[q][0], acc[q][1]};
             const f64x2 v1 = {acc[q][2], acc[q][3]};
-            __builtin_nontemporal_store(v0, tv + q * 128);
-            __builtin_nontemporal_store(v1, tv + q * 128 + 1);
+            __builtin_nontemporal_store(v0, dst + q * 128);
+            __builtin_nontemporal_store(v1, dst + q * 128 + 1);
         }
     }
 }
 
-// --------------------------------------------------------------------------------------
-// 3. landmark augmentation (Robot.cpp:776-866)
-// --------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------
+// 3. augmented landmark rows into X_k (after the downdate, Robot.cpp:845-862)
+// ---------------------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(SCAN_THREADS) void augment_kernel(ScanParams p)
+__global__ __launch_bounds__(SCAN_THREADS) void patch_kernel(PatchParams p)
 {
     const Dims d = p.d;
     const int e = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int n = d.n, N = d.N;
-    int* res = p.res + (size_t)e * RES_STRIDE;
-    const int nextra = res[RES_NEXTRA];
-    if (res[RES_RESET] || nextra == 0) return;
-    double* Rs = p.Rs + (size_t)e * 3 * n;
-    double* y = p.y + (size_t)e * n;
-    T* Pll = reinterpret_cast<T*>(p.Pll) + (size_t)e * d.ntiles * TILE_ELEMS;
-    const ekf_line* lines = p.lines + (size_t)e * d.max_lines;
-    const double px = p.pose[3 * e + 0], py = p.pose[3 * e + 1], pt = p.pose[3 * e + 2];
-    int s = res[RES_SAVED_IN];
-    for (int q = 0; q < nextra; q++) {
-        if (s >= N) break;   // capacity (flagged by scan_kernel)
-        const ekf_line ln = lines[res[RES_EXTRA + q]];
-        double alfa = ln.alpha;
-        const double r = ln.r + (px * cos(alfa) + py * sin(alfa));
-        alfa += pt;
-        double sa, ca;
-        sincos(alfa, &sa, &ca);
-        const double y0 = y[0], y1 = y[1];
-        const double gl10 = y1 * ca - y0 * sa;
-        const int l0 = 3 + 2 * s;
-        // P_ll = Gx·Prr·Gxᵀ + Gl·R·Glᵀ (Robot.cpp:813-847); Gx = [[0,0,1],[ca,sa,0]],
-        // Gl = [[1,0],[gl10,1]]
-        double Prr[9];
-        for (int a = 0; a < 9; a++) Prr[a] = Rs[(a / 3) * n + (a % 3)];
-        const double Gx[6] = {0, 0, 1, ca, sa, 0};
-        double GP[6];
-        for (int a = 0; a < 2; a++)
-            for (int b = 0; b < 3; b++) {
-                double acc = 0.0;
-                for (int k = 0; k < 3; k++) acc += Gx[a * 3 + k] * Prr[k * 3 + b];
-                GP[a * 3 + b] = acc;
-            }
-        const double Gl[4] = {1.0, 0, gl10, 1};
-        double GlR[4];
-        for (int a = 0; a < 2; a++)
-            for (int b = 0; b < 2; b++)
-                GlR[a * 2 + b] = Gl[a * 2 + 0] * ln.R[0 * 2 + b] + Gl[a * 2 + 1] * ln.R[1 * 2 + b];
-        double Pnew[4];
-        for (int a = 0; a < 2; a++)
-            for (int b = 0; b < 2; b++) {
-                double g = 0.0;
-                for (int k = 0; k < 3; k++) g += GP[a * 3 + k] * Gx[b * 3 + k];
-                const double h = GlR[a * 2 + 0] * Gl[b * 2 + 0] + GlR[a * 2 + 1] * Gl[b * 2 + 1];
-                Pnew[a * 2 + b] = g + h;
-            }
-        // P[l0:l0+2, 0:l0] = Gx·P[0:3, 0:l0] and its transpose (Robot.cpp:852-862)
-        for (int c = tid; c < l0; c += SCAN_THREADS) {
-            const double v0 = Rs[2 * n + c];
-            const double v1 = ca * Rs[c] + sa * Rs[n + c];
-            if (c >= 3) {
-                ll_store_sym(Pll, l0 - 3, c - 3, d.nb, v0);
-                ll_store_sym(Pll, l0 - 2, c - 3, d.nb, v1);
-            }
+    const int* res = p.res + (size_t)e * RES_STRIDE;
+    const int nadd = res[RES_NADD];
+    if (res[RES_RESET] || nadd == 0) return;
+    const int s0 = res[RES_SAVED_IN];
+    T* P = reinterpret_cast<T*>(p.P) + (size_t)e * d.ntiles * TILE_ELEMS;
+    const double* patch = p.patch + (size_t)e * d.max_lines * 2 * d.M;
+    const double* pdiag = p.patch_diag + (size_t)e * d.max_lines * 4;
+    for (int q = 0; q < nadd; q++) {
+        const int i0 = 2 * (s0 + q);
+        for (int c = threadIdx.x; c < i0; c += SCAN_THREADS) {
+            ll_store_sym(P, i0, c, d.nb, patch[(size_t)(q * 2) * d.M + c]);
+            ll_store_sym(P, i0 + 1, c, d.nb, patch[(size_t)(q * 2 + 1) * d.M + c]);
         }
-        __syncthreads();
-        if (tid < 3) {
-            const int c = tid;
-            const double v0 = Rs[2 * n + c];
-            const double v1 = ca * Rs[c] + sa * Rs[n + c];
-            Rs[c * n + l0] = v0;
-            Rs[c * n + l0 + 1] = v1;
+        if (threadIdx.x == 0) {
+            P[ll_offset<T>(i0, i0, d.nb)] = (T)pdiag[q * 4 + 0];
+            P[ll_offset<T>(i0, i0 + 1, d.nb)] = (T)pdiag[q * 4 + 1];
+            P[ll_offset<T>(i0 + 1, i0, d.nb)] = (T)pdiag[q * 4 + 2];
+            P[ll_offset<T>(i0 + 1, i0 + 1, d.nb)] = (T)pdiag[q * 4 + 3];
         }
-        if (tid == 0) {
-            const int i0 = l0 - 3;
-            Pll[ll_offset<T>(i0, i0, d.nb)] = (T)Pnew[0];
-            Pll[ll_offset<T>(i0, i0 + 1, d.nb)] = (T)Pnew[1];
-            Pll[ll_offset<T>(i0 + 1, i0, d.nb)] = (T)Pnew[2];
-            Pll[ll_offset<T>(i0 + 1, i0 + 1, d.nb)] = (T)Pnew[3];
-            y[l0] = normalize_radian(alfa);
-            y[l0 + 1] = r;
-        }
-        __syncthreads();
-        s++;
-    }
-    if (tid == 0) {
-        p.saved[e] = s;
-        res[RES_SAVED] = s;
     }
 }
 
-// --------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------
 // state transfer / initialisation
-// --------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void tile_rc_of(int rem, int& r, int& c)
+{
+    if (sizeof(T) == 4) {
+        const int q = rem & 3, lane = (rem >> 2) & 63, grp = rem >> 8;
+        c = lane & 31;
+        r = q + 4 * (lane >> 5) + 8 * grp;
+    } else {
+        const int reg = rem & 3, lane = (rem >> 2) & 63, blk = rem >> 8;
+        c = (lane & 15) + 16 * (blk & 1);
+        r = (lane >> 4) + 4 * reg + 16 * (blk >> 1);
+    }
+}
+
 template <typename T>
 __global__ void pack_kernel(Dims d, const double* __restrict__ Pfull, T* __restrict__ Pll,
                             double* __restrict__ Rs, const int2* __restrict__ tile_rc)
@@ -650,18 +996,8 @@ __global__ void pack_kernel(Dims d, const double* __restrict__ Pfull, T* __restr
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
          g += (int64_t)gridDim.x * blockDim.x) {
         const int64_t t = g / TILE_ELEMS;
-        const int rem = (int)(g - t * TILE_ELEMS);
-        // invert the intra-tile layout by brute force over (r, c): map rem → (r, c)
         int r, c;
-        if (sizeof(T) == 4) {
-            const int q = rem & 3, lane = (rem >> 2) & 63, grp = rem >> 8;
-            c = lane & 31;
-            r = q + 4 * (lane >> 5) + 8 * grp;
-        } else {
-            const int reg = rem & 3, lane = (rem >> 2) & 63, blk = rem >> 8;
-            c = (lane & 15) + 16 * (blk & 1);
-            r = (lane >> 4) + 4 * reg + 16 * (blk >> 1);
-        }
+        tile_rc_of<T>((int)(g - t * TILE_ELEMS), r, c);
         const int2 rc = tile_rc[t];
         const int i = rc.x * TILE + r, j = rc.y * TILE + c;
         double v = 0.0;
@@ -700,17 +1036,8 @@ __global__ void lowrank_kernel(Dims d, const double* __restrict__ diag,
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
          g += (int64_t)gridDim.x * blockDim.x) {
         const int64_t t = g / TILE_ELEMS;
-        const int rem = (int)(g - t * TILE_ELEMS);
         int r, c;
-        if (sizeof(T) == 4) {
-            const int q = rem & 3, lane = (rem >> 2) & 63, grp = rem >> 8;
-            c = lane & 31;
-            r = q + 4 * (lane >> 5) + 8 * grp;
-        } else {
-            const int reg = rem & 3, lane = (rem >> 2) & 63, blk = rem >> 8;
-            c = (lane & 15) + 16 * (blk & 1);
-            r = (lane >> 4) + 4 * reg + 16 * (blk >> 1);
-        }
+        tile_rc_of<T>((int)(g - t * TILE_ELEMS), r, c);
         const int2 rc = tile_rc[t];
         const int i = rc.x * TILE + r, j = rc.y * TILE + c;
         double v = 0.0;
@@ -734,16 +1061,15 @@ __global__ void lowrank_kernel(Dims d, const double* __restrict__ diag,
     }
 }
 
-// --------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------
 // launchers
-// --------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 {
-    const size_t lds = sizeof(unsigned int) * (size_t)((p.d.N + 31) / 32);
     if (precision == 0)
-        hipLaunchKernelGGL(scan_kernel<double>, dim3(p.E), dim3(SCAN_THREADS), lds, st, p);
+        hipLaunchKernelGGL(scan_kernel<double>, dim3(p.E), dim3(SCAN_THREADS), 0, st, p);
     else
-        hipLaunchKernelGGL(scan_kernel<float>, dim3(p.E), dim3(SCAN_THREADS), lds, st, p);
+        hipLaunchKernelGGL(scan_kernel<float>, dim3(p.E), dim3(SCAN_THREADS), 0, st, p);
     return hipGetLastError();
 }
 
@@ -756,12 +1082,12 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     return hipGetLastError();
 }
 
-hipError_t launch_augment(const ScanParams& p, int precision, hipStream_t st)
+hipError_t launch_patch(const PatchParams& p, int precision, hipStream_t st)
 {
     if (precision == 0)
-        hipLaunchKernelGGL(augment_kernel<double>, dim3(p.E), dim3(SCAN_THREADS), 0, st, p);
+        hipLaunchKernelGGL(patch_kernel<double>, dim3(p.E), dim3(SCAN_THREADS), 0, st, p);
     else
-        hipLaunchKernelGGL(augment_kernel<float>, dim3(p.E), dim3(SCAN_THREADS), 0, st, p);
+        hipLaunchKernelGGL(patch_kernel<float>, dim3(p.E), dim3(SCAN_THREADS), 0, st, p);
     return hipGetLastError();
 }
 

@@ -31,7 +31,7 @@ namespace ekf {
 
 constexpr int TILE = 32;            // tile edge (both precisions)
 constexpr int TILE_ELEMS = TILE * TILE;
-constexpr int SCAN_THREADS = 1024;  // association kernel: one workgroup per instance
+constexpr int SCAN_THREADS = 512;   // association kernel: one workgroup per instance
 constexpr int DD_THREADS = 256;     // downdate kernel: 4 waves, one tile per wave
 
 struct Dims {
@@ -41,7 +41,7 @@ struct Dims {
     int nb;       // tile rows = ceil(M / 32)
     int64_t ntiles;   // nb(nb+1)/2
     int max_lines;
-    int kmax;     // 2*max_lines rounded up to a multiple of 4 (operand k columns)
+    int kmax;     // operand k columns: 2*max_lines rounded up to a multiple of 16
 };
 
 EKF_HD Dims make_dims(int N, int max_lines)
@@ -53,7 +53,7 @@ EKF_HD Dims make_dims(int N, int max_lines)
     d.nb = (d.M + TILE - 1) / TILE;
     d.ntiles = (int64_t)d.nb * (d.nb + 1) / 2;
     d.max_lines = max_lines;
-    d.kmax = ((2 * max_lines + 3) / 4) * 4;
+    d.kmax = ((2 * max_lines + 15) / 16) * 16;   // 8 f32 / 4 f64 k-steps per operand chunk
     return d;
 }
 

@@ -90,8 +90,14 @@ def truth_pose(step: int, speed: float = 1e-3, wobble: float = 2e-4) -> np.ndarr
     return np.array([speed * step, 0.0, wobble * math.sin(step / 10.0)])
 
 
+def _noise(rng: np.random.Generator, sigma: float, size, clip: float = 2.5) -> np.ndarray:
+    """Gaussian noise truncated at ±clip·sigma, so that no draw lands near the 0.4 gate
+    (association must be precision-robust)."""
+    return np.clip(rng.normal(0.0, sigma, size), -clip * sigma, clip * sigma)
+
+
 def make_scan(world: World, step: int, instances: int = 1, lines: int = 8, seed: int = 7,
-              z_noise: float = 1e-3, enc_noise: float = 1e-4, var_alpha: float = 1e-4,
+              z_noise: float = 5e-4, enc_noise: float = 1e-4, var_alpha: float = 1e-4,
               var_r: float = 1e-4, first_instance: int = 0):
     """Returns (encoder[E,3], lines[E,L,6], nlines[E]) for one scan of `instances` EKFs."""
     s = world.active
@@ -102,10 +108,10 @@ def make_scan(world: World, step: int, instances: int = 1, lines: int = 8, seed:
     out = np.zeros((instances, lines, LINE_FIELDS))
     for e in range(instances):
         rng = np.random.default_rng([1000 + first_instance + e, step])
-        enc[e] = pose + rng.normal(0.0, enc_noise, 3) * np.array([1.0, 1.0, 0.1])
+        enc[e] = pose + _noise(rng, enc_noise, 3) * np.array([1.0, 1.0, 0.1])
         a = world.alpha[pick]
-        z_a = wrap_pi(a - pose[2] + rng.normal(0.0, z_noise, L))
-        z_r = world.r[pick] - (pose[0] * np.cos(a) + pose[1] * np.sin(a)) + rng.normal(0.0, z_noise, L)
+        z_a = wrap_pi(a - pose[2] + _noise(rng, z_noise, L))
+        z_r = world.r[pick] - (pose[0] * np.cos(a) + pose[1] * np.sin(a)) + _noise(rng, z_noise, L)
         out[e, :L, 0] = z_a
         out[e, :L, 1] = z_r
         out[e, :L, 2] = var_alpha

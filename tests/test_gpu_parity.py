@@ -139,6 +139,46 @@ def test_trajectory_fp64_with_reset(ekf_mod, oracle_mod):
 
 
 @pytest.mark.parametrize("prec", [0, 1])
+def test_pipelined_equals_drained(ekf_mod, oracle_mod, prec):
+    """Back-to-back steps (step k's association overlaps step k-1's downdate and applies it
+    on read) give bit-identical state to draining after every step; fp64 also vs the oracle.
+    Covers matches, augmentation (patch rows) and the capacity reset across the pipeline."""
+    N = 64
+    w = G.make_world(N, active=N - 14)
+    st = G.initial_state(w)
+    a = ekf_mod.Ensemble(N, 2, prec, max_lines=8, pipeline=True)
+    b = ekf_mod.Ensemble(N, 2, prec, max_lines=8, pipeline=True)
+    for ens in (a, b):
+        for e in range(2):
+            ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+    ref = oracle_mod.OracleRobot(N)
+    ref.set_state(*b.download_state(0))
+    rng = np.random.default_rng(11)
+    resets = 0
+    for step in range(1, 21):
+        enc, lines, nl = G.make_scan(w, step, instances=2, lines=6)
+        extra = G.random_lines(rng, 2)[None].repeat(2, axis=0) if step % 3 == 0 else np.zeros((2, 0, 6))
+        ln = np.concatenate([lines, extra], axis=1)
+        nl = np.full(2, ln.shape[1], dtype=np.int32)
+        ra = a.localize(enc, ln, nl)
+        rb = b.localize(enc, ln, nl)
+        b.download_state(0, with_P=False)          # drains b's pipeline every step
+        m = ref.localize(ln[0], enc[0])
+        assert ra[0]["match"] == rb[0]["match"] == m, (step, ra[0]["match"], m)
+        resets += ra[0]["reset"]
+    assert resets >= 1
+    for e in range(2):
+        Pa, ya, sa, pa = a.download_state(e)
+        Pb, yb, sb, pb = b.download_state(e)
+        bad = np.argwhere(Pa != Pb)
+        assert bad.size == 0, (e, bad[:12].tolist(), rel(Pa, Pb))
+        np.testing.assert_array_equal(ya, yb)
+        assert sa == sb
+    if prec == 0:
+        check_same(a, ref, 0, where="pipelined fp64 trajectory")
+
+
+@pytest.mark.parametrize("prec", [0, 1])
 @pytest.mark.parametrize("N", [64, 256, 1024])
 def test_per_scan_parity(ekf_mod, oracle_mod, prec, N):
     w = G.make_world(N)
