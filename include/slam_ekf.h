@@ -43,6 +43,8 @@ enum {
                               single off-diagonal entry (Robot.cpp:302-304), so the reference's
                               K·S·Kᵀ — and from then on its P — is not symmetric; the packed
                               symmetric storage keeps the upper triangle. */
+    EKF_ST_SYNC_TIMEOUT = 8, /* the instance's cooperating workgroups did not all arrive at an
+                                exchange within the spin bound (results of that call invalid) */
 };
 
 /* storage precision of the landmark-landmark covariance block */
@@ -140,6 +142,11 @@ int ekf_state_dim(const ekf_ctx* ctx);                /* n */
 int ekf_profile_enable(ekf_ctx* ctx, int enable);
 int ekf_profile_read(ekf_ctx* ctx, double* scan_ms, double* downdate_ms, double* augment_ms,
                      int* launches);
+/* Diagnostic: association-kernel phase timers (sum over instances, 100 MHz ticks), collected
+ * only when the environment had EKF_SCAN_STAMPS=1 at ekf_create. Slots: 0 predict, 1 diagonal
+ * gather + barrier, 2 gating, 3 min-reduction barrier, 4 winner package, 5 broadcast barrier,
+ * 6 gain rows, 7 commit/augmentation, 8 total, 9 launches. */
+int ekf_debug_scan_stamps(ekf_ctx* ctx, unsigned long long out[16]);
 
 #ifdef __cplusplus
 }

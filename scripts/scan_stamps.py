@@ -1,0 +1,18 @@
+"""Phase breakdown of the association kernel (EKF_SCAN_STAMPS=1), N=4096 f32, 8 instances."""
+import os, sys, json
+os.environ["EKF_SCAN_STAMPS"] = "1"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from slam_ros_amd import ekf, scan_gen as G
+N = int(os.environ.get("N", 4096)); E = 8
+names = ["predict", "diag+barrier", "gating", "reduce-barrier", "winner", "bcast-barrier",
+         "gain-rows", "commit", "total"]
+w = G.make_world(N); st = G.initial_state(w)
+ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8)
+for e in range(E):
+    ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+for s in range(1, 11):
+    enc, lines, nl = G.make_scan(w, s, instances=E)
+    r = ens.localize(enc, lines, nl)
+st_ = ens.scan_stamps()
+launches = st_[9] or 1
+print(json.dumps({k: st_[i] * 10e-3 / launches for i, k in enumerate(names)}))  # µs per launch (per instance)

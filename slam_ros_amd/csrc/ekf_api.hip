@@ -58,6 +58,12 @@ struct ekf_ctx {
     int* h_res;
     double* h_pose;
     int dd_grid;
+    int G;                    // association workgroups per instance
+    int mbw;                  // mailbox words per workgroup slot
+    int scan_batch;           // instances per association launch (co-residency bound)
+    double* mbox;
+    int* sync;
+    unsigned long long* dbg;  // association-kernel phase timers (EKF_SCAN_STAMPS=1)
     // pipeline state
     int cur;                  // buffer holding the newest landmark block (in stream order)
     int pending;              // 1: a step was enqueued since the last drain
@@ -117,7 +123,8 @@ int ekf_abi_version(void) { return SLAM_EKF_ABI_VERSION; }
 static void free_all(ekf_ctx* c)
 {
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->pose, c->xpre, c->saved, c->D,
-                               c->tile_rc, c->d_enc, c->d_lines, c->d_nlines};
+                               c->tile_rc, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->mbox,
+                               c->sync};
     for (auto& sb : c->slot) {
         ptrs.push_back(sb.s.Ust);
         ptrs.push_back(sb.s.Vst);
@@ -179,9 +186,10 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
 {
     if (!cfg || !out) return EKF_EINVAL;
     *out = nullptr;
-    // capacity bound: each association thread tracks its <= 64 landmarks' matched flags in a
-    // 64-bit mask (N <= 64 × 512 = 32768, i.e. n <= 65539)
-    if (cfg->capacity < 1 || cfg->capacity > 64 * ekf::SCAN_THREADS || cfg->instances < 1 ||
+    // capacity bound: one association thread per landmark, at most MAX_GROUPS workgroups of
+    // SCAN_THREADS per instance (N <= 32768, i.e. n <= 65539)
+    if (cfg->capacity < 1 || cfg->capacity > ekf::MAX_GROUPS * ekf::SCAN_THREADS ||
+        cfg->instances < 1 ||
         cfg->max_lines < 1 ||
         cfg->max_lines > EKF_MAX_LINES ||
         (cfg->precision != EKF_PREC_F64 && cfg->precision != EKF_PREC_F32) ||
@@ -233,6 +241,12 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     ALLOC(c->d_enc, sizeof(double) * 3 * E);
     ALLOC(c->d_lines, sizeof(ekf_line) * d.max_lines * E);
     ALLOC(c->d_nlines, sizeof(int) * E);
+    c->G = (d.N + ekf::SCAN_THREADS - 1) / ekf::SCAN_THREADS;
+    c->mbw = ((ekf::MB_WORDS_FIXED + 4 * d.max_lines + 15) / 16) * 16;   // whole 128-B lines
+    ALLOC(c->mbox, sizeof(double) * 2 * c->G * c->mbw * E);
+    ALLOC(c->sync, sizeof(int) * ekf::SYNC_WORDS * E);
+    if (getenv("EKF_SCAN_STAMPS") && atoi(getenv("EKF_SCAN_STAMPS")))
+        ALLOC(c->dbg, sizeof(unsigned long long) * 16 * E);
 #undef ALLOC
     if (hipHostMalloc((void**)&c->h_res, sizeof(int) * ekf::RES_STRIDE * E) != hipSuccess) goto fail;
     if (hipHostMalloc((void**)&c->h_pose, sizeof(double) * 3 * E) != hipSuccess) goto fail;
@@ -261,6 +275,19 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) goto fail;
         c->dd_grid = prop.multiProcessorCount * 8;
+        // all G workgroups of an instance must be co-resident (they exchange per line): bound
+        // the instances per association launch by the occupancy the hardware admits, less one
+        // workgroup per CU of margin (MI355X_MICROARCH.md: the API can over-report by one)
+        int per_cu = ekf::scan_blocks_per_cu(cfg->precision);
+        if (per_cu > 1) per_cu -= 1;
+        if (per_cu < 1) per_cu = 1;
+        const int resident = prop.multiProcessorCount * per_cu;
+        c->scan_batch = resident / c->G;
+        if (c->scan_batch < 1) {
+            rc = EKF_EINVAL;   // one instance does not fit the device
+            goto fail;
+        }
+        if (c->scan_batch > E) c->scan_batch = E;
     }
     c->cur = 0;
     for (int e = 0; e < E; e++)
@@ -358,7 +385,26 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.enc = enc;
     p.lines = lines;
     p.nlines = nlines;
+    p.dbg = c->dbg;
+    p.G = c->G;
+    p.mbw = c->mbw;
+    p.mbox = c->mbox;
+    p.sync = c->sync;
     return p;
+}
+
+// The association kernel in batches of co-resident instances: grid (G, batch). Its per-line
+// exchange counters are zeroed on the stream first.
+static hipError_t launch_scans(ekf_ctx* c, ekf::ScanParams sp)
+{
+    const int E = c->cfg.instances;
+    hipError_t err = hipMemsetAsync(c->sync, 0, sizeof(int) * ekf::SYNC_WORDS * E, c->stream);
+    for (int e0 = 0; err == hipSuccess && e0 < E; e0 += c->scan_batch) {
+        sp.e0 = e0;
+        sp.E = (E - e0 < c->scan_batch) ? E - e0 : c->scan_batch;
+        err = ekf::launch_scan(sp, c->cfg.precision, c->stream);
+    }
+    return err;
 }
 
 // Enqueue one localize step (or its predict / update half).
@@ -368,7 +414,7 @@ static int enqueue(ekf_ctx* c, int phase, const double* enc, const ekf_line* lin
     ekf::ScanParams sp = scan_params(c, phase, enc, lines, nlines);
     if (!(phase & ekf::PHASE_UPDATE)) {
         EvPair* pr = prof_begin(c, 0, c->stream);
-        HIP_TRY(ekf::launch_scan(sp, c->cfg.precision, c->stream));
+        HIP_TRY(launch_scans(c, sp));
         prof_end(c, pr, c->stream);
         return EKF_OK;
     }
@@ -396,7 +442,7 @@ static int enqueue(ekf_ctx* c, int phase, const double* enc, const ekf_line* lin
     // scan_k reuses slot sl and reads X[rbuf]: both were last used by downdate_{k-2}
     if (c->ev_dd_valid[sl]) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_dd[sl], 0));
     EvPair* pr = prof_begin(c, 0, c->stream);
-    HIP_TRY(ekf::launch_scan(sp, c->cfg.precision, c->stream));
+    HIP_TRY(launch_scans(c, sp));
     prof_end(c, pr, c->stream);
     HIP_TRY(hipEventRecord(c->ev_scan[sl], c->stream));
     HIP_TRY(hipStreamWaitEvent(c->dstream, c->ev_scan[sl], 0));
@@ -465,7 +511,12 @@ extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
                            hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_pose, c->pose, sizeof(double) * 3 * E, hipMemcpyDeviceToHost,
                            c->stream));
+    std::vector<int> hs((size_t)ekf::SYNC_WORDS * E);
+    HIP_TRY(hipMemcpyAsync(hs.data(), c->sync, sizeof(int) * hs.size(), hipMemcpyDeviceToHost,
+                           c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int e = 0; e < E; e++)
+        c->h_res[(size_t)e * ekf::RES_STRIDE + ekf::RES_STATUS] |= hs[(size_t)e * ekf::SYNC_WORDS + ekf::SYNC_STATUS];
     if (!out) return EKF_OK;
     for (int e = 0; e < E; e++) {
         const int* r = c->h_res + (size_t)e * ekf::RES_STRIDE;
@@ -708,5 +759,20 @@ extern "C" int ekf_profile_read(ekf_ctx* c, double* scan_ms, double* dd_ms, doub
     if (dd_ms) *dd_ms = avg[1];
     if (aug_ms) *aug_ms = avg[2];
     if (launches) *launches = (int)c->ev[1].size();
+    return EKF_OK;
+}
+
+extern "C" int ekf_debug_scan_stamps(ekf_ctx* c, unsigned long long out[16])
+{
+    // Diagnostic: association-kernel phase times summed over instances (100 MHz ticks) since
+    // context creation, when built with EKF_SCAN_STAMPS=1 in the environment; zeros otherwise.
+    if (!c || !out) return EKF_EINVAL;
+    memset(out, 0, sizeof(unsigned long long) * 16);
+    if (!c->dbg) return EKF_OK;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::vector<unsigned long long> h((size_t)16 * c->cfg.instances);
+    HIP_TRY(hipMemcpy(h.data(), c->dbg, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+    for (int e = 0; e < c->cfg.instances; e++)
+        for (int k = 0; k < 16; k++) out[k] += h[(size_t)e * 16 + k];
     return EKF_OK;
 }

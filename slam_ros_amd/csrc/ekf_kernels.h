@@ -9,7 +9,13 @@
 namespace ekf {
 
 enum { PHASE_PREDICT = 1, PHASE_UPDATE = 2, PHASE_BOTH = 3 };
-enum { EKF_ST_SINGULAR = EKF_ST_SINGULAR_S, EKF_ST_CAP = EKF_ST_CAPACITY, EKF_ST_NSYM = EKF_ST_NONSYM };
+enum { EKF_ST_SINGULAR = EKF_ST_SINGULAR_S, EKF_ST_CAP = EKF_ST_CAPACITY, EKF_ST_NSYM = EKF_ST_NONSYM,
+       EKF_ST_TIMEOUT_BIT = EKF_ST_SYNC_TIMEOUT };
+
+// per-instance synchronisation words of the association kernel (zeroed before every launch)
+enum { SYNC_ARRIVE = 0, SYNC_STATUS = 1, SYNC_START = 2, SYNC_WORDS = 4 };
+constexpr int MAX_GROUPS = 128;   // workgroups per instance (N <= 128 × 256)
+constexpr int MB_WORDS_FIXED = 26; // mailbox words before the V-history (see ekf_kernels.hip)
 
 // per-instance result record in device memory (ints)
 enum {
@@ -41,7 +47,12 @@ struct Slot {
 
 struct ScanParams {
     Dims d;
-    int E;
+    int E;                // instances in this launch (grid.y)
+    int e0;               // first instance of this launch
+    int G;                // workgroups per instance (grid.x) = ceil(N / SCAN_THREADS)
+    int mbw;              // mailbox words per workgroup slot
+    double* mbox;         // [E][2][G][mbw] per-line candidate exchange
+    int* sync;            // [E][SYNC_WORDS]
     int phase;
     int r_mode;
     int reset_margin;
@@ -60,6 +71,7 @@ struct ScanParams {
     const double* enc;    // [E][3]
     const ekf_line* lines;// [E][max_lines]
     const int* nlines;    // [E]
+    unsigned long long* dbg;  // optional [E][16] phase timers (s_memrealtime ticks, 100 MHz)
 };
 
 struct DowndateParams {
@@ -83,6 +95,7 @@ struct PatchParams {
 };
 
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st);
+int scan_blocks_per_cu(int precision);
 hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st);
 hipError_t launch_patch(const PatchParams& p, int precision, hipStream_t st);
 hipError_t launch_pack(const Dims& d, int precision, const double* Pfull, void* Pll, double* Rs,

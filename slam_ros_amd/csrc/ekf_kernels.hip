@@ -335,6 +335,16 @@ __device__ __forceinline__ bool certified_reject(const Block5& b, double ma, dou
     return (q - dq) > gate * gate * (1.0 + 1e-6) * (det + ddet);
 }
 
+// Diagnostic phase timers (thread 0 of each workgroup; only when p.dbg is set).
+#define EKF_STAMP(k)                                                            \
+    do {                                                                        \
+        if (dbg) {                                                              \
+            const unsigned long long _t = __builtin_amdgcn_s_memrealtime();     \
+            dbg[k] += _t - t_last;                                              \
+            t_last = _t;                                                        \
+        }                                                                       \
+    } while (0)
+
 __device__ __forceinline__ int wave_min(int v)
 {
 #pragma unroll
@@ -343,25 +353,89 @@ __device__ __forceinline__ int wave_min(int v)
 }
 
 // ---------------------------------------------------------------------------------------
-// 1. association + gain chain + augmentation
+// 1. association + gain chain + augmentation: ⌈N/256⌉ cooperating workgroups per instance
 // ---------------------------------------------------------------------------------------
+// Thread (g, tid) of instance e OWNS landmark j = 256·g + tid: its gating candidate, its two
+// rows of W/K/U/y, its robot-strip columns and its 2×2 diagonal block, all kept in registers
+// for the whole scan. The robot 3×3 block and x_pre are uniform and recomputed identically by
+// every thread. Per observed line the instance's workgroups exchange one mailbox slot each
+// (their best passing candidate and, from its owner, the uniform gain package), written with
+// 8-byte agent-scope atomic stores (sc1) and read after an arrival counter reaches G·(line+1)
+// (MI355X_MICROARCH.md "Valid forms": sc1 stores drained by s_waitcnt before the counter add,
+// sc1 poll, workgroup barrier, sc1 loads). Every spin is bounded; a timeout sets a status bit.
+__device__ __forceinline__ void mb_store(double* p, double v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ double mb_load(const double* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// mailbox slot words
+enum { MB_BEST = 0, MB_S = 1, MB_SI = 5, MB_V = 9, MB_H = 11, MB_KR = 14, MB_UR = 20, MB_VH = 26 };
+
+// Each workgroup announces that it has read the instance's shared inputs (after its loads
+// returned); the lead waits for all G before overwriting them. Bounded spin.
+__device__ __forceinline__ void signal_started(int* sync, int tid)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+        __hip_atomic_fetch_add(&sync[SYNC_START], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void wait_all_started(int* sync, int G)
+{
+    int polls = 0;
+    while (__hip_atomic_load(&sync[SYNC_START], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++polls > (1 << 24)) {
+            __hip_atomic_fetch_or(&sync[SYNC_STATUS], EKF_ST_TIMEOUT_BIT, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
 {
     const Dims d = p.d;
-    const int e = blockIdx.x;
+    const int g = blockIdx.x;
+    const int e = p.e0 + blockIdx.y;
+    const int G = p.G;
     const int tid = threadIdx.x;
+    const int j = g * SCAN_THREADS + tid;      // owned landmark
+    const bool own = j < d.N;
     const int n = d.n, N = d.N, M = d.M;
+    const int b0 = 3 + 2 * j;                   // its first row of P
     double* Rs = p.Rs + (size_t)e * 3 * n;
     double* y = p.y + (size_t)e * n;
-    double* D = p.D + (size_t)e * 4 * N;
+    int* sync = p.sync + (size_t)e * SYNC_WORDS;
+    double* mbox = p.mbox + (size_t)e * 2 * G * p.mbw;
+    const bool lead = (g == 0 && tid == 0);
 
-    __shared__ double sh_R33[9];        // robot 3×3 block of the current P
-    __shared__ double sh_xp[3];         // current x_pre
-    __shared__ double sh_c[C_WORDS];    // the matched candidate's uniform package
-    __shared__ int sh_red[2][SCAN_THREADS / 64];
+    __shared__ double sh_pkg[MB_VH + 4 * EKF_MAX_LINES];
+    __shared__ int sh_red[SCAN_THREADS / 64];
+    __shared__ int sh_best[MAX_GROUPS];
     __shared__ int sh_extra[EKF_MAX_LINES];
-    __shared__ int sh_status;
+    unsigned long long* dbg = (p.dbg && lead) ? p.dbg + (size_t)e * 16 : nullptr;
+    unsigned long long t_last = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const unsigned long long t_first = t_last;
+
+    // owned state, in registers for the whole scan
+    double2 rr0 = make_double2(0, 0), rr1 = rr0, rr2 = rr0, yb = rr0;
+    if (own) {
+        rr0 = *reinterpret_cast<const double2*>(Rs + b0);
+        rr1 = *reinterpret_cast<const double2*>(Rs + n + b0);
+        rr2 = *reinterpret_cast<const double2*>(Rs + 2 * n + b0);
+        yb = *reinterpret_cast<const double2*>(y + b0);
+    }
+    double R33[9], xp[3];
+#pragma unroll
+    for (int a = 0; a < 9; a++) R33[a] = Rs[(a / 3) * n + (a % 3)];
 
     if (p.phase & PHASE_PREDICT) {
         // Robot.cpp:130-148 (SIMULATIONOFF == true: `rot` unused)
@@ -374,68 +448,66 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         double sc, cc;
         sincos(c, &sc, &cc);
         const double F3[9] = {1, 0, -u0 * sc, 0, 1, u0 * cc, 0, 0, 1};
+        xp[0] = x0 + u0 * cos(t0 + u2 / 2.0);
+        xp[1] = y0 + u0 * sin(t0 + u2 / 2.0);
+        xp[2] = t0 + u2;
         // rows 0..2 of Fx·P for the owned landmark columns (Robot.cpp:242)
-        for (int j = tid; j < N; j += SCAN_THREADS) {
-            const int b = 3 + 2 * j;
-            const double2 r0 = *reinterpret_cast<const double2*>(Rs + b);
-            const double2 r1 = *reinterpret_cast<const double2*>(Rs + n + b);
-            const double2 r2 = *reinterpret_cast<const double2*>(Rs + 2 * n + b);
-            double2 o0, o1, o2;
-            o0.x = F3[0] * r0.x + F3[1] * r1.x + F3[2] * r2.x;
-            o0.y = F3[0] * r0.y + F3[1] * r1.y + F3[2] * r2.y;
-            o1.x = F3[3] * r0.x + F3[4] * r1.x + F3[5] * r2.x;
-            o1.y = F3[3] * r0.y + F3[4] * r1.y + F3[5] * r2.y;
-            o2.x = F3[6] * r0.x + F3[7] * r1.x + F3[8] * r2.x;
-            o2.y = F3[6] * r0.y + F3[7] * r1.y + F3[8] * r2.y;
-            *reinterpret_cast<double2*>(Rs + b) = o0;
-            *reinterpret_cast<double2*>(Rs + n + b) = o1;
-            *reinterpret_cast<double2*>(Rs + 2 * n + b) = o2;
+        {
+            const double2 a0 = rr0, a1 = rr1, a2 = rr2;
+            rr0.x = F3[0] * a0.x + F3[1] * a1.x + F3[2] * a2.x;
+            rr0.y = F3[0] * a0.y + F3[1] * a1.y + F3[2] * a2.y;
+            rr1.x = F3[3] * a0.x + F3[4] * a1.x + F3[5] * a2.x;
+            rr1.y = F3[3] * a0.y + F3[4] * a1.y + F3[5] * a2.y;
+            rr2.x = F3[6] * a0.x + F3[7] * a1.x + F3[8] * a2.x;
+            rr2.y = F3[6] * a0.y + F3[7] * a1.y + F3[8] * a2.y;
         }
-        if (tid == 0) {
-            // x_pre (Robot.cpp:148); 3×3 block F3·P33·F3ᵀ + Fu3·Q·Fu3ᵀ (Robot.cpp:178-258)
-            sh_xp[0] = x0 + u0 * cos(t0 + u2 / 2.0);
-            sh_xp[1] = y0 + u0 * sin(t0 + u2 / 2.0);
-            sh_xp[2] = t0 + u2;
-            const double Fu3[9] = {cc, 0, -u0 * sc / 2.0, sc, 1, u0 * cc / 2.0, 0, 0, 1};
-            const double qs = (-1.0 / (1 + fabs(u0)) + 1);
-            const double Q[9] = {p.enc_noise * qs, 0, 0, 0, 2 * p.enc_noise * qs, 0, 0, 0,
-                                 p.enc_noise * qs};
-            double P33[9], FP[9], FuQ[9];
-            for (int a = 0; a < 9; a++) P33[a] = Rs[(a / 3) * n + (a % 3)];
-            for (int a = 0; a < 3; a++)
-                for (int b = 0; b < 3; b++) {
-                    double s = 0.0, t = 0.0;
-                    for (int k = 0; k < 3; k++) {
-                        s += F3[a * 3 + k] * P33[k * 3 + b];
-                        t += Fu3[a * 3 + k] * Q[k * 3 + b];
-                    }
-                    FP[a * 3 + b] = s;
-                    FuQ[a * 3 + b] = t;
+        // 3×3 block: F3·P33·F3ᵀ + Fu3·Q·Fu3ᵀ (Robot.cpp:178-258)
+        const double Fu3[9] = {cc, 0, -u0 * sc / 2.0, sc, 1, u0 * cc / 2.0, 0, 0, 1};
+        const double qs = (-1.0 / (1 + fabs(u0)) + 1);
+        const double Q[9] = {p.enc_noise * qs, 0, 0, 0, 2 * p.enc_noise * qs, 0, 0, 0,
+                             p.enc_noise * qs};
+        double FP[9], FuQ[9];
+        for (int a = 0; a < 3; a++)
+            for (int b = 0; b < 3; b++) {
+                double s = 0.0, t = 0.0;
+                for (int k = 0; k < 3; k++) {
+                    s += F3[a * 3 + k] * R33[k * 3 + b];
+                    t += Fu3[a * 3 + k] * Q[k * 3 + b];
                 }
-            for (int a = 0; a < 3; a++)
-                for (int b = 0; b < 3; b++) {
-                    double s = 0.0, t = 0.0;
-                    for (int k = 0; k < 3; k++) {
-                        s += FP[a * 3 + k] * F3[b * 3 + k];
-                        t += FuQ[a * 3 + k] * Fu3[b * 3 + k];
-                    }
-                    sh_R33[a * 3 + b] = s + t;
-                }
-            if (!(p.phase & PHASE_UPDATE)) {
-                for (int a = 0; a < 9; a++) Rs[(a / 3) * n + (a % 3)] = sh_R33[a];
-                p.xpre[3 * e + 0] = sh_xp[0];
-                p.xpre[3 * e + 1] = sh_xp[1];
-                p.xpre[3 * e + 2] = sh_xp[2];
+                FP[a * 3 + b] = s;
+                FuQ[a * 3 + b] = t;
             }
+        for (int a = 0; a < 3; a++)
+            for (int b = 0; b < 3; b++) {
+                double s = 0.0, t = 0.0;
+                for (int k = 0; k < 3; k++) {
+                    s += FP[a * 3 + k] * F3[b * 3 + k];
+                    t += FuQ[a * 3 + k] * Fu3[b * 3 + k];
+                }
+                R33[a * 3 + b] = s + t;
+            }
+        if (!(p.phase & PHASE_UPDATE)) {
+            if (own) {
+                *reinterpret_cast<double2*>(Rs + b0) = rr0;
+                *reinterpret_cast<double2*>(Rs + n + b0) = rr1;
+                *reinterpret_cast<double2*>(Rs + 2 * n + b0) = rr2;
+            }
+            signal_started(sync, tid);
+            if (lead) {
+                wait_all_started(sync, G);
+                for (int a = 0; a < 9; a++) Rs[(a / 3) * n + (a % 3)] = R33[a];
+                p.xpre[3 * e + 0] = xp[0];
+                p.xpre[3 * e + 1] = xp[1];
+                p.xpre[3 * e + 2] = xp[2];
+            }
+            return;
         }
-        if (!(p.phase & PHASE_UPDATE)) return;
-    } else if (tid == 0) {
-        for (int a = 0; a < 9; a++) sh_R33[a] = Rs[(a / 3) * n + (a % 3)];
-        sh_xp[0] = p.xpre[3 * e + 0];
-        sh_xp[1] = p.xpre[3 * e + 1];
-        sh_xp[2] = p.xpre[3 * e + 2];
+    } else {
+        xp[0] = p.xpre[3 * e + 0];
+        xp[1] = p.xpre[3 * e + 1];
+        xp[2] = p.xpre[3 * e + 2];
     }
-    if (tid == 0) sh_status = 0;
+    EKF_STAMP(0);
 
     // ---------------- association / update (Robot.cpp:288-904) ----------------
     const size_t opstride = (size_t)d.nb * 64 * (d.kmax / 2);
@@ -473,16 +545,14 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     L = L < 0 ? 0 : (L > d.max_lines ? d.max_lines : L);
     const int s = p.saved[e];
     const ekf_line* lines = p.lines + (size_t)e * d.max_lines;
+    // all per-instance inputs that the lead rewrites at the end (robot 3×3, pose, saved) are read
+    signal_started(sync, tid);
 
-    // diagonal 2x2 blocks of the owned saved landmarks
-    for (int j = tid; j < s; j += SCAN_THREADS) {
-        double blk[4];
-        pll_block(pv, 2 * j, 2 * j, blk);
-        *reinterpret_cast<double4*>(D + 4 * j) = make_double4(blk[0], blk[1], blk[2], blk[3]);
-    }
-    __syncthreads();   // sh_R33 / sh_xp / sh_status
+    double Dj[4] = {0, 0, 0, 0};   // owned diagonal block
+    if (own && j < s) pll_block(pv, 2 * j, 2 * j, Dj);
+    EKF_STAMP(1);
 
-    unsigned long long mbits = 0ull;   // matched flags of the owned landmarks
+    bool matched = false;
     int m = 0, nextra = 0, status = 0;
     for (int i = 0; i < L; ++i) {
         const ekf_line ln = lines[i];
@@ -492,66 +562,46 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         } else {
             Rm[0] = ln.R[0]; Rm[1] = ln.R[1]; Rm[2] = ln.R[2]; Rm[3] = ln.R[3];
         }
-        // gating over owned candidates, first passing unmatched j (Robot.cpp:313-498)
+        // gating of the owned candidate (Robot.cpp:313-498); the first passing unmatched j wins
         int best = 0x7fffffff;
-        {
-            double R33[9], xp[3];
-#pragma unroll
-            for (int a = 0; a < 9; a++) R33[a] = sh_R33[a];
-            xp[0] = sh_xp[0]; xp[1] = sh_xp[1]; xp[2] = sh_xp[2];
-            int r = 0;
-            for (int j = tid; j < s; j += SCAN_THREADS, r++) {
-                if ((mbits >> r) & 1ull) continue;
-                const double4 dj = *reinterpret_cast<const double4*>(D + 4 * j);
-                const double Dj[4] = {dj.x, dj.y, dj.z, dj.w};
-                Block5 b5;
-                load_block5(b5, j, R33, Rs, n, Dj);
-                const double2 m2 = *reinterpret_cast<const double2*>(y + 3 + 2 * j);
-                if (certified_reject(b5, m2.x, m2.y, xp, ln.alpha, ln.r, Rm, p.gate)) continue;
-                Cand c;
-                eval_candidate(b5, m2.x, m2.y, xp, ln.alpha, ln.r, Rm, p.gate, c);
+        Cand c;
+        Block5 b5;
+        if (own && j < s && !matched) {
+            b5.p00 = R33[0]; b5.p01 = R33[1]; b5.p02 = R33[2];
+            b5.p10 = R33[3]; b5.p11 = R33[4]; b5.p12 = R33[5];
+            b5.p20 = R33[6]; b5.p21 = R33[7]; b5.p22 = R33[8];
+            b5.p0a = rr0.x; b5.p0b = rr0.y;
+            b5.p1a = rr1.x; b5.p1b = rr1.y;
+            b5.p2a = rr2.x; b5.p2b = rr2.y;
+            b5.daa = Dj[0]; b5.dab = Dj[1]; b5.dba = Dj[2]; b5.dbb = Dj[3];
+            if (!certified_reject(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate)) {
+                eval_candidate(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate, c);
                 status |= c.singular ? EKF_ST_SINGULAR : 0;
-                if (c.pass) {
-                    best = j;
-                    break;
-                }
+                if (c.pass) best = j;
             }
-            const int wbest = wave_min(best);
-            if ((tid & 63) == 0) sh_red[i & 1][tid >> 6] = wbest;
-            __syncthreads();
-            int jstar = sh_red[i & 1][0];
-#pragma unroll
-            for (int w = 1; w < SCAN_THREADS / 64; w++) jstar = min(jstar, sh_red[i & 1][w]);
-            if (jstar == 0x7fffffff) {
-                // no match (or s == 0): the line goes to extraLines (Robot.cpp:308-310, 492-496)
-                if (tid == 0) {
-                    res[RES_MATCH + i] = -1;
-                    res[RES_EXTRA + nextra] = i;
-                    sh_extra[nextra] = i;
-                }
-                nextra++;
-                continue;
-            }
-            best = jstar;
         }
-        const int jstar = best;
-        if ((jstar % SCAN_THREADS) == tid) {
-            // the owner of j*: exact re-evaluation, the uniform gain of the robot rows
-            // (Robot.cpp:522-602 for rows 0..2) and the new x_pre, published through LDS
-            const double4 dj = *reinterpret_cast<const double4*>(D + 4 * jstar);
-            const double Dj[4] = {dj.x, dj.y, dj.z, dj.w};
-            double R33[9], xp[3];
+        EKF_STAMP(2);
+        const int wbest = wave_min(best);
+        if ((tid & 63) == 0) sh_red[tid >> 6] = wbest;
+        __syncthreads();
+        int gbest = sh_red[0];
 #pragma unroll
-            for (int a = 0; a < 9; a++) R33[a] = sh_R33[a];
-            xp[0] = sh_xp[0]; xp[1] = sh_xp[1]; xp[2] = sh_xp[2];
-            Block5 b5;
-            load_block5(b5, jstar, R33, Rs, n, Dj);
-            const double2 m2 = *reinterpret_cast<const double2*>(y + 3 + 2 * jstar);
-            Cand c;
-            eval_candidate(b5, m2.x, m2.y, xp, ln.alpha, ln.r, Rm, p.gate, c);
-            const double RL0[3] = {b5.p0a, b5.p1a, b5.p2a};
-            const double RL1[3] = {b5.p0b, b5.p1b, b5.p2b};
-            double Kr[6], Ur[6], yn[3];
+        for (int w = 1; w < SCAN_THREADS / 64; w++) gbest = min(gbest, sh_red[w]);
+        const int par = i & 1;
+        double* slot = mbox + ((size_t)par * G + g) * p.mbw;
+        if (best != 0x7fffffff && best == gbest) {
+            // this workgroup's candidate: the uniform gain package of the robot rows
+            // (Robot.cpp:522-602 for rows 0..2) and the V rows of the candidate for the
+            // earlier matches of this scan (Robot.cpp:560-568 corrections)
+            const double RL0[3] = {rr0.x, rr1.x, rr2.x};
+            const double RL1[3] = {rr0.y, rr1.y, rr2.y};
+            mb_store(slot + MB_S + 0, c.S[0]); mb_store(slot + MB_S + 1, c.S[1]);
+            mb_store(slot + MB_S + 2, c.S[2]); mb_store(slot + MB_S + 3, c.S[3]);
+            mb_store(slot + MB_SI + 0, c.Si[0]); mb_store(slot + MB_SI + 1, c.Si[1]);
+            mb_store(slot + MB_SI + 2, c.Si[2]); mb_store(slot + MB_SI + 3, c.Si[3]);
+            mb_store(slot + MB_V + 0, c.v[0]); mb_store(slot + MB_V + 1, c.v[1]);
+            mb_store(slot + MB_H + 0, c.h10); mb_store(slot + MB_H + 1, c.h11);
+            mb_store(slot + MB_H + 2, c.h1l);
 #pragma unroll
             for (int a = 0; a < 3; a++) {
                 // W = P·Hᵀ (Robot.cpp:522), K = W·S⁻¹ (:526), U = K·S (:560)
@@ -559,70 +609,93 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
                 const double w1 = c.h10 * R33[a * 3 + 0] + c.h11 * R33[a * 3 + 1] + c.h1l * RL0[a] + RL1[a];
                 const double k0 = w0 * c.Si[0] + w1 * c.Si[2];
                 const double k1 = w0 * c.Si[1] + w1 * c.Si[3];
-                Kr[2 * a] = k0;
-                Kr[2 * a + 1] = k1;
-                Ur[2 * a] = k0 * c.S[0] + k1 * c.S[2];
-                Ur[2 * a + 1] = k0 * c.S[1] + k1 * c.S[3];
-                yn[a] = xp[a] + (k0 * c.v[0] + k1 * c.v[1]);   // Robot.cpp:579-592
+                mb_store(slot + MB_KR + 2 * a, k0);
+                mb_store(slot + MB_KR + 2 * a + 1, k1);
+                mb_store(slot + MB_UR + 2 * a, k0 * c.S[0] + k1 * c.S[2]);
+                mb_store(slot + MB_UR + 2 * a + 1, k0 * c.S[1] + k1 * c.S[3]);
             }
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                sh_c[C_S + q] = c.S[q];
-                sh_c[C_SI + q] = c.Si[q];
+            for (int q = 0; q < m; q++) {
+                const double4 vq = *reinterpret_cast<const double4*>(Vst + ((size_t)q * n + b0) * 2);
+                mb_store(slot + MB_VH + 4 * q + 0, vq.x);
+                mb_store(slot + MB_VH + 4 * q + 1, vq.y);
+                mb_store(slot + MB_VH + 4 * q + 2, vq.z);
+                mb_store(slot + MB_VH + 4 * q + 3, vq.w);
             }
-            sh_c[C_V] = c.v[0];
-            sh_c[C_V + 1] = c.v[1];
-            sh_c[C_H] = c.h10;
-            sh_c[C_H + 1] = c.h11;
-            sh_c[C_H + 2] = c.h1l;
-#pragma unroll
-            for (int q = 0; q < 6; q++) {
-                sh_c[C_KR + q] = Kr[q];
-                sh_c[C_UR + q] = Ur[q];
-            }
-#pragma unroll
-            for (int a = 0; a < 3; a++)
-#pragma unroll
-                for (int cc = 0; cc < 3; cc++)
-                    sh_R33[a * 3 + cc] = R33[a * 3 + cc] - (Ur[2 * a] * Kr[2 * cc] + Ur[2 * a + 1] * Kr[2 * cc + 1]);
-            sh_xp[0] = yn[0];
-            sh_xp[1] = yn[1];
-            sh_xp[2] = normalize_radian(yn[2]);   // Robot.cpp:596
-            mbits |= 1ull << (jstar / SCAN_THREADS);
-            res[RES_MATCH + i] = jstar;
         }
-        if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
+        if (tid == 0) mb_store(slot + MB_BEST, gbest == 0x7fffffff ? -1.0 : (double)gbest);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        const double S0 = sh_c[C_S], S1 = sh_c[C_S + 1], S2 = sh_c[C_S + 2], S3 = sh_c[C_S + 3];
-        const double Si0 = sh_c[C_SI], Si1 = sh_c[C_SI + 1], Si2 = sh_c[C_SI + 2], Si3 = sh_c[C_SI + 3];
-        const double v0 = sh_c[C_V], v1 = sh_c[C_V + 1];
-        const double h10 = sh_c[C_H], h11 = sh_c[C_H + 1], h1l = sh_c[C_H + 2];
+        EKF_STAMP(3);
+        if (tid == 0) {
+            __hip_atomic_fetch_add(&sync[SYNC_ARRIVE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int target = G * (i + 1);
+            int polls = 0;
+            while (__hip_atomic_load(&sync[SYNC_ARRIVE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++polls > (1 << 24)) {   // ~seconds: a workgroup never arrived
+                    __hip_atomic_fetch_or(&sync[SYNC_STATUS], EKF_ST_TIMEOUT_BIT, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        if (tid < G) {
+            const double bv = mb_load(mbox + ((size_t)par * G + tid) * p.mbw + MB_BEST);
+            sh_best[tid] = bv < 0.0 ? 0x7fffffff : (int)bv;
+        }
+        __syncthreads();
+        int jstar = 0x7fffffff, gstar = 0;
+        for (int k = 0; k < G; k++) {
+            const int v = sh_best[k];
+            if (v < jstar) { jstar = v; gstar = k; }
+        }
+        EKF_STAMP(4);
+        if (jstar == 0x7fffffff) {
+            // no match (or s == 0): the line goes to extraLines (Robot.cpp:308-310, 492-496)
+            if (lead) {
+                res[RES_MATCH + i] = -1;
+                res[RES_EXTRA + nextra] = i;
+            }
+            if (tid == 0) sh_extra[nextra] = i;
+            nextra++;
+            continue;
+        }
+        // ---- match (Robot.cpp:500-641) ----
+        const double* ps = mbox + ((size_t)par * G + gstar) * p.mbw;
+        for (int k = tid; k < MB_VH + 4 * m; k += SCAN_THREADS) sh_pkg[k] = mb_load(ps + k);
+        __syncthreads();
+        const double S0 = sh_pkg[MB_S], S1 = sh_pkg[MB_S + 1], S2 = sh_pkg[MB_S + 2], S3 = sh_pkg[MB_S + 3];
+        const double Si0 = sh_pkg[MB_SI], Si1 = sh_pkg[MB_SI + 1], Si2 = sh_pkg[MB_SI + 2], Si3 = sh_pkg[MB_SI + 3];
+        const double v0 = sh_pkg[MB_V], v1 = sh_pkg[MB_V + 1];
+        const double h10 = sh_pkg[MB_H], h11 = sh_pkg[MB_H + 1], h1l = sh_pkg[MB_H + 2];
+        double Kr[6], Ur[6];
+#pragma unroll
+        for (int q = 0; q < 6; q++) {
+            Kr[q] = sh_pkg[MB_KR + q];
+            Ur[q] = sh_pkg[MB_UR + q];
+        }
         const int t = m;
-        const int l0 = 3 + 2 * jstar;
+        if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
 
         // owned landmark rows
-        for (int j = tid; j < N; j += SCAN_THREADS) {
-            const int b0 = 3 + 2 * j;
+        if (own) {
             double blk[4];
             pll_block(pv, 2 * j, 2 * jstar, blk);
             for (int q = 0; q < t; q++) {   // earlier matches of this scan, in order
                 const double4 uq = *reinterpret_cast<const double4*>(Ust + ((size_t)q * n + b0) * 2);
-                const double4 vq = *reinterpret_cast<const double4*>(Vst + ((size_t)q * n + l0) * 2);
-                blk[0] -= uq.x * vq.x + uq.y * vq.y;
-                blk[1] -= uq.x * vq.z + uq.y * vq.w;
-                blk[2] -= uq.z * vq.x + uq.w * vq.y;
-                blk[3] -= uq.z * vq.z + uq.w * vq.w;
+                const double* vh = sh_pkg + MB_VH + 4 * q;
+                blk[0] -= uq.x * vh[0] + uq.y * vh[1];
+                blk[1] -= uq.x * vh[2] + uq.y * vh[3];
+                blk[2] -= uq.z * vh[0] + uq.w * vh[1];
+                blk[3] -= uq.z * vh[2] + uq.w * vh[3];
             }
-            double2 rr[3];
-#pragma unroll
-            for (int a = 0; a < 3; a++) rr[a] = *reinterpret_cast<const double2*>(Rs + a * n + b0);
-            double2 yb = *reinterpret_cast<const double2*>(y + b0);
             double kk[4], uu[4];
 #pragma unroll
             for (int pp = 0; pp < 2; pp++) {
-                const double pb0 = pp ? rr[0].y : rr[0].x;
-                const double pb1 = pp ? rr[1].y : rr[1].x;
-                const double pb2 = pp ? rr[2].y : rr[2].x;
+                const double pb0 = pp ? rr0.y : rr0.x;
+                const double pb1 = pp ? rr1.y : rr1.x;
+                const double pb2 = pp ? rr2.y : rr2.x;
                 const double pba = blk[pp * 2 + 0], pbb = blk[pp * 2 + 1];
                 const double w0 = -pb2 + pba;
                 const double w1 = h10 * pb0 + h11 * pb1 + h1l * pba + pbb;
@@ -632,10 +705,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
                 kk[2 * pp + 1] = k1;
                 uu[2 * pp] = k0 * S0 + k1 * S2;
                 uu[2 * pp + 1] = k0 * S1 + k1 * S3;
-                const double dy = k0 * v0 + k1 * v1;
-                if (pp) yb.y += dy; else yb.x += dy;
+                const double dyv = k0 * v0 + k1 * v1;   // y += K·v (Robot.cpp:585-589)
+                if (pp) yb.y += dyv; else yb.x += dyv;
             }
-            *reinterpret_cast<double2*>(y + b0) = yb;
             *reinterpret_cast<double4*>(Ust + ((size_t)t * n + b0) * 2) = make_double4(uu[0], uu[1], uu[2], uu[3]);
             *reinterpret_cast<double4*>(Vst + ((size_t)t * n + b0) * 2) = make_double4(kk[0], kk[1], kk[2], kk[3]);
 #pragma unroll
@@ -653,84 +725,71 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
                     Vop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (T)kk[2 * pp + 1];
                 }
             }
-            // eager downdate of the owned robot-strip columns (Robot.cpp:568)
-#pragma unroll
-            for (int a = 0; a < 3; a++) {
-                const double ua0 = sh_c[C_UR + 2 * a], ua1 = sh_c[C_UR + 2 * a + 1];
-                rr[a].x -= ua0 * kk[0] + ua1 * kk[1];
-                rr[a].y -= ua0 * kk[2] + ua1 * kk[3];
-                *reinterpret_cast<double2*>(Rs + a * n + b0) = rr[a];
-            }
-            if (j < s) {
-                double4 dj = *reinterpret_cast<const double4*>(D + 4 * j);
-                dj.x -= uu[0] * kk[0] + uu[1] * kk[1];
-                dj.y -= uu[0] * kk[2] + uu[1] * kk[3];
-                dj.z -= uu[2] * kk[0] + uu[3] * kk[1];
-                dj.w -= uu[2] * kk[2] + uu[3] * kk[3];
-                *reinterpret_cast<double4*>(D + 4 * j) = dj;
-            }
+            // eager downdate of the owned robot-strip columns and diagonal block (Robot.cpp:568)
+            rr0.x -= Ur[0] * kk[0] + Ur[1] * kk[1];
+            rr0.y -= Ur[0] * kk[2] + Ur[1] * kk[3];
+            rr1.x -= Ur[2] * kk[0] + Ur[3] * kk[1];
+            rr1.y -= Ur[2] * kk[2] + Ur[3] * kk[3];
+            rr2.x -= Ur[4] * kk[0] + Ur[5] * kk[1];
+            rr2.y -= Ur[4] * kk[2] + Ur[5] * kk[3];
+            Dj[0] -= uu[0] * kk[0] + uu[1] * kk[1];
+            Dj[1] -= uu[0] * kk[2] + uu[1] * kk[3];
+            Dj[2] -= uu[2] * kk[0] + uu[3] * kk[1];
+            Dj[3] -= uu[2] * kk[2] + uu[3] * kk[3];
         }
+        // uniform: robot 3×3 block and x_pre = y[0..2] (Robot.cpp:568, 579-602)
+        double yn[3];
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            yn[a] = xp[a] + (Kr[2 * a] * v0 + Kr[2 * a + 1] * v1);
+#pragma unroll
+            for (int cc = 0; cc < 3; cc++)
+                R33[a * 3 + cc] -= Ur[2 * a] * Kr[2 * cc] + Ur[2 * a + 1] * Kr[2 * cc + 1];
+        }
+        xp[0] = yn[0];
+        xp[1] = yn[1];
+        xp[2] = normalize_radian(yn[2]);   // Robot.cpp:596
+        if (j == jstar) matched = true;
+        if (lead) res[RES_MATCH + i] = jstar;
         m++;
+        EKF_STAMP(6);
     }
 
     // ---------------- commit (Robot.cpp:702-716) ----------------
-    __syncthreads();   // sh_extra, sh_xp, sh_R33 final
-    double xp[3] = {sh_xp[0], sh_xp[1], sh_xp[2]};
+    __syncthreads();   // sh_extra
     double pose[3] = {xp[0], xp[1], xp[2]};
     if (L == 0 || m == 0) pose[2] = normalize_radian(xp[2]);   // y[2] stays un-normalised
-    if (tid == 0) {
-        y[0] = xp[0];
-        y[1] = xp[1];
-        y[2] = xp[2];
-        p.pose[3 * e + 0] = pose[0];
-        p.pose[3 * e + 1] = pose[1];
-        p.pose[3 * e + 2] = pose[2];
-    }
     const int nadd = min(nextra, N - s);
     const int reset = (s + nadd > N - p.reset_margin) ? 1 : 0;
-    if (nextra > nadd) status |= EKF_ST_CAP;
-    double R33[9];
-#pragma unroll
-    for (int a = 0; a < 9; a++) R33[a] = sh_R33[a];
 
     // ---------------- augmentation (Robot.cpp:776-866) ----------------
     if (!reset) {
         for (int q = 0; q < nadd; q++) {
             const ekf_line ln = lines[sh_extra[q]];
             const int sq = s + q;
-            const int l0 = 3 + 2 * sq;
             double alfa = ln.alpha;
             const double r = ln.r + (pose[0] * cos(alfa) + pose[1] * sin(alfa));
             alfa += pose[2];
             double sa, ca;
             sincos(alfa, &sa, &ca);
-            // landmark columns of P[l0:l0+2, 0:l0] = Gx·P[0:3, 0:l0] (Robot.cpp:852-862) → patch
-            double* prow = patch + (size_t)(q * 2) * M;
-            for (int jc = tid; jc < sq; jc += SCAN_THREADS) {
-                const int c = 3 + 2 * jc;
-                const double2 r0 = *reinterpret_cast<const double2*>(Rs + c);
-                const double2 r1 = *reinterpret_cast<const double2*>(Rs + n + c);
-                const double2 r2 = *reinterpret_cast<const double2*>(Rs + 2 * n + c);
-                *reinterpret_cast<double2*>(prow + 2 * jc) = r2;
-                double2 g;
-                g.x = ca * r0.x + sa * r1.x;
-                g.y = ca * r0.y + sa * r1.y;
-                *reinterpret_cast<double2*>(prow + M + 2 * jc) = g;
+            if (own && j < sq) {
+                // landmark columns of P[l0:l0+2, 0:l0] = Gx·P[0:3, 0:l0] (Robot.cpp:852-862)
+                double* prow = patch + (size_t)(q * 2) * M;
+                *reinterpret_cast<double2*>(prow + 2 * j) = rr2;
+                double2 gx;
+                gx.x = ca * rr0.x + sa * rr1.x;
+                gx.y = ca * rr0.y + sa * rr1.y;
+                *reinterpret_cast<double2*>(prow + M + 2 * j) = gx;
             }
-            if ((sq % SCAN_THREADS) == tid) {
-                // the new landmark's owner: its robot-strip columns (robot part of the same
-                // product, stored transposed) and its mean (Robot.cpp:801-803)
-                double2 c0, c1, c2;
-                c0.x = R33[6]; c0.y = ca * R33[0] + sa * R33[3];
-                c1.x = R33[7]; c1.y = ca * R33[1] + sa * R33[4];
-                c2.x = R33[8]; c2.y = ca * R33[2] + sa * R33[5];
-                *reinterpret_cast<double2*>(Rs + l0) = c0;
-                *reinterpret_cast<double2*>(Rs + n + l0) = c1;
-                *reinterpret_cast<double2*>(Rs + 2 * n + l0) = c2;
-                y[l0] = normalize_radian(alfa);
-                y[l0 + 1] = r;
+            if (j == sq) {
+                // the new landmark: robot part of the same product (its robot-strip columns) and
+                // its mean (Robot.cpp:801-803)
+                rr0 = make_double2(R33[6], ca * R33[0] + sa * R33[3]);
+                rr1 = make_double2(R33[7], ca * R33[1] + sa * R33[4]);
+                rr2 = make_double2(R33[8], ca * R33[2] + sa * R33[5]);
+                yb = make_double2(normalize_radian(alfa), r);
             }
-            if (tid == 0) {
+            if (lead) {
                 // P_ll = Gx·Prr·Gxᵀ + Gl·R·Glᵀ (Robot.cpp:813-847); Gx = [[0,0,1],[ca,sa,0]],
                 // Gl = [[1,0],[y1·ca − y0·sa, 1]]
                 const double Gx[6] = {0, 0, 1, ca, sa, 0};
@@ -747,25 +806,53 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
                         GlR[a * 2 + b] = Gl[a * 2 + 0] * ln.R[0 * 2 + b] + Gl[a * 2 + 1] * ln.R[1 * 2 + b];
                 for (int a = 0; a < 2; a++)
                     for (int b = 0; b < 2; b++) {
-                        double g = 0.0;
-                        for (int k = 0; k < 3; k++) g += GP[a * 3 + k] * Gx[b * 3 + k];
+                        double gsum = 0.0;
+                        for (int k = 0; k < 3; k++) gsum += GP[a * 3 + k] * Gx[b * 3 + k];
                         const double h = GlR[a * 2 + 0] * Gl[b * 2 + 0] + GlR[a * 2 + 1] * Gl[b * 2 + 1];
-                        pdiag[q * 4 + a * 2 + b] = g + h;
+                        pdiag[q * 4 + a * 2 + b] = gsum + h;
                     }
             }
         }
     }
-    // status: OR over the workgroup
+    // write back the owned state (reset: Robot.cpp:893-904 zeroes landmark entries of y and P)
+    if (own) {
+        if (reset) {
+            rr0 = rr1 = rr2 = yb = make_double2(0.0, 0.0);
+        }
+        *reinterpret_cast<double2*>(Rs + b0) = rr0;
+        *reinterpret_cast<double2*>(Rs + n + b0) = rr1;
+        *reinterpret_cast<double2*>(Rs + 2 * n + b0) = rr2;
+        *reinterpret_cast<double2*>(y + b0) = yb;
+        if (sizeof(T) == 8 && (m & 1)) {
+            // f64 operands: zero the odd tail column pair of the last 4-wide k-step
+#pragma unroll
+            for (int pp = 0; pp < 2; pp++) {
+                Uop[op_index_f64(2 * j + pp, 2 * m, d.kmax)] = (T)0;
+                Uop[op_index_f64(2 * j + pp, 2 * m + 1, d.kmax)] = (T)0;
+                Vop[op_index_f64(2 * j + pp, 2 * m, d.kmax)] = (T)0;
+                Vop[op_index_f64(2 * j + pp, 2 * m + 1, d.kmax)] = (T)0;
+            }
+        }
+    }
+    // status bits seen by this workgroup's threads
     {
         int st = status;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) st |= __shfl_xor(st, off, 64);
-        if ((tid & 63) == 0 && st) atomicOr(&sh_status, st);
+        if ((tid & 63) == 0 && st)
+            __hip_atomic_fetch_or(&sync[SYNC_STATUS], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __syncthreads();
-    if (tid == 0) {
+    if (lead) {
+        // every workgroup read the robot 3×3 block, pose and savedLineCount at its start
+        wait_all_started(sync, G);
+        y[0] = xp[0];
+        y[1] = xp[1];
+        y[2] = xp[2];
+        p.pose[3 * e + 0] = pose[0];
+        p.pose[3 * e + 1] = pose[1];
+        p.pose[3 * e + 2] = pose[2];
         for (int a = 0; a < 9; a++) Rs[(a / 3) * n + (a % 3)] = R33[a];
-        res[RES_STATUS] = sh_status;
+        res[RES_STATUS] = ((nextra > nadd) ? EKF_ST_CAP : 0);
         res[RES_M] = m;
         res[RES_NEXTRA] = nextra;
         res[RES_SAVED_IN] = s;
@@ -776,24 +863,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         res[RES_KSTEPS] = (sizeof(T) == 4) ? m : (m + 1) / 2;
         p.saved[e] = reset ? 0 : s + nadd;
     }
-    // f64 operands: zero the odd tail column pair of the last 4-wide k-step
-    if (sizeof(T) == 8 && (m & 1)) {
-        for (int lr = tid; lr < M; lr += SCAN_THREADS) {
-            Uop[op_index_f64(lr, 2 * m, d.kmax)] = (T)0;
-            Uop[op_index_f64(lr, 2 * m + 1, d.kmax)] = (T)0;
-            Vop[op_index_f64(lr, 2 * m, d.kmax)] = (T)0;
-            Vop[op_index_f64(lr, 2 * m + 1, d.kmax)] = (T)0;
-        }
-    }
-    if (reset) {   // Robot.cpp:893-904 (the landmark block is zeroed by downdate_kernel)
-        for (int j = tid; j < N; j += SCAN_THREADS) {
-            const int b = 3 + 2 * j;
-            const double2 z = make_double2(0.0, 0.0);
-            *reinterpret_cast<double2*>(y + b) = z;
-            *reinterpret_cast<double2*>(Rs + b) = z;
-            *reinterpret_cast<double2*>(Rs + n + b) = z;
-            *reinterpret_cast<double2*>(Rs + 2 * n + b) = z;
-        }
+    EKF_STAMP(7);
+    if (dbg) {
+        dbg[8] += t_last - t_first;
+        dbg[9] += 1;
     }
 }
 
@@ -1064,12 +1137,21 @@ __global__ void lowrank_kernel(Dims d, const double* __restrict__ diag,
 // ---------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------
+int scan_blocks_per_cu(int precision)
+{
+    int nb = 0;
+    hipError_t err = (precision == 0)
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<double>, SCAN_THREADS, 0)
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<float>, SCAN_THREADS, 0);
+    return err == hipSuccess ? nb : 0;
+}
+
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 {
     if (precision == 0)
-        hipLaunchKernelGGL(scan_kernel<double>, dim3(p.E), dim3(SCAN_THREADS), 0, st, p);
+        hipLaunchKernelGGL(scan_kernel<double>, dim3(p.G, p.E), dim3(SCAN_THREADS), 0, st, p);
     else
-        hipLaunchKernelGGL(scan_kernel<float>, dim3(p.E), dim3(SCAN_THREADS), 0, st, p);
+        hipLaunchKernelGGL(scan_kernel<float>, dim3(p.G, p.E), dim3(SCAN_THREADS), 0, st, p);
     return hipGetLastError();
 }
 

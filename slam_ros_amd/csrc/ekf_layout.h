@@ -31,7 +31,7 @@ namespace ekf {
 
 constexpr int TILE = 32;            // tile edge (both precisions)
 constexpr int TILE_ELEMS = TILE * TILE;
-constexpr int SCAN_THREADS = 512;   // association kernel: one workgroup per instance
+constexpr int SCAN_THREADS = 256;   // association kernel: threads (= owned landmarks) per workgroup
 constexpr int DD_THREADS = 256;     // downdate kernel: 4 waves, one tile per wave
 
 struct Dims {

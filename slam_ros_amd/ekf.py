@@ -31,7 +31,7 @@ EXPORTED = [
     "ekf_set_stream", "ekf_sync", "ekf_reset_instance", "ekf_localize", "ekf_localize_device",
     "ekf_predict", "ekf_update", "ekf_read_results", "ekf_upload_state", "ekf_download_state",
     "ekf_init_lowrank", "ekf_get_pose_cov", "ekf_get_ellipse", "ekf_landmark_block_bytes",
-    "ekf_state_dim", "ekf_profile_enable", "ekf_profile_read",
+    "ekf_state_dim", "ekf_profile_enable", "ekf_profile_read", "ekf_debug_scan_stamps",
 ]
 
 
@@ -103,6 +103,7 @@ def load_library(path: str = LIB_PATH):
         "ekf_state_dim": (ctypes.c_int, [vp]),
         "ekf_profile_enable": (ctypes.c_int, [vp, ctypes.c_int]),
         "ekf_profile_read": (ctypes.c_int, [vp, dp, dp, dp, ip]),
+        "ekf_debug_scan_stamps": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_ulonglong)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -261,6 +262,11 @@ class Ensemble:
         if rc < 0:
             _check(-rc, "ekf_get_ellipse")
         return rc == 1, [axii[0], axii[1]], ang.value
+
+    def scan_stamps(self) -> list[int]:
+        out = (ctypes.c_ulonglong * 16)()
+        _check(self._lib.ekf_debug_scan_stamps(self._h, out), "ekf_debug_scan_stamps")
+        return list(out)
 
     def landmark_block_bytes(self) -> int:
         return int(self._lib.ekf_landmark_block_bytes(self._h))
