@@ -60,9 +60,14 @@ typedef struct ekf_config {
     int32_t max_lines;     /* per-scan line capacity per instance, <= EKF_MAX_LINES */
     int32_t r_mode;        /* EKF_R_* */
     int32_t reset_margin;  /* map wiped when savedLineCount > N - margin (Robot.cpp:893: 10) */
-    int32_t pipeline;      /* 1: double-buffer the landmark block so that a step's association
-                              kernel overlaps the previous step's covariance downdate (applying
-                              it on read, bit-identically); 0: in-place, strictly sequential */
+    int32_t pipeline;      /* 1: double-buffer the landmark block so that association kernels
+                              overlap the covariance downdate of earlier scans (applying it on
+                              read, bit-identically); 0: in-place, strictly sequential */
+    int32_t flush_interval;/* T >= 1: the landmark block is rewritten once per T scans by one
+                              rank-2·Σm MFMA pass; scans in between read it with the pending
+                              downdates applied on read. Bit-identical state for every T (the
+                              MFMA chain is an ordered FMA chain); T = 1: once per scan. <= 16 */
+    int32_t reserved;
     double mahalanobis;    /* MAHALANOBIS gate, Robot.h:15 (0.4) */
     double encoder_noise;  /* ENCODERNOISE, Robot.h:17 (0.024) */
 } ekf_config;

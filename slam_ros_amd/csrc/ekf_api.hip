@@ -2,14 +2,17 @@
 //
 // A context owns E instances' state in HBM and two HIP streams:
 //   S  association/gain kernels (scan_kernel) — all state except the landmark block;
-//   D  landmark-block kernels (downdate_kernel, patch_kernel).
-// The landmark block ping-pongs between X[0] and X[1]: step k's downdate reads X[w_{k-1}] and
-// writes X[w_k] = the other buffer, while step k+1's association already runs on S reading the
-// older buffer plus step k's pending downdate (see ekf_kernels.hip). Per-step scratch (gain
-// operands, patch rows, results) alternates between two slots. Events order the streams:
-//   downdate_k  waits for scan_k           (needs its operands)
-//   scan_{k+1}  waits for downdate_{k-1}   (reads the buffer that downdate wrote; reuses its slot)
-// Any call that reads or replaces the landmark block drains both streams first.
+//   D  the landmark-block flush (downdate kernel).
+// Every update step k writes its downdate operands, augmented rows and result record into slot
+// k mod R of a ring. The landmark block is rewritten by a flush once per group of T =
+// flush_interval steps; association kernels read the last materialised block ("base") with the
+// steps not yet in it applied on read (bit-identical to flushing first, see ekf_kernels.hip).
+//   sequential (pipeline = 0): one buffer, flushed in place; R = T. A scan waits for the last
+//     flush; a flush waits for the last scan of its group.
+//   pipelined  (pipeline = 1): flush f reads X[in] and writes X[out] = the other buffer while the
+//     next group's scans run on S reading X[in] — the output of flush f-1 — with the steps of
+//     groups f and f+1 pending (< 2T); R = 2T.
+// Any call that reads or replaces the landmark block drains (flushes the partial group, syncs).
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -29,10 +32,6 @@ struct EvPair {
     hipEvent_t a, b;
 };
 
-struct SlotBuf {
-    ekf::Slot s;
-};
-
 struct ekf_ctx {
     ekf_config cfg;
     Dims d;
@@ -50,7 +49,9 @@ struct ekf_ctx {
     double* xpre;
     int* saved;
     double* D;
-    SlotBuf slot[2];
+    std::vector<ekf::Slot> ring;   // R per-step slots
+    double* Ust;              // fp64 gain scratch of the running scan
+    double* Vst;
     int2* tile_rc;
     double* d_enc;
     ekf_line* d_lines;
@@ -64,14 +65,17 @@ struct ekf_ctx {
     double* mbox;
     int* sync;
     unsigned long long* dbg;  // association-kernel phase timers (EKF_SCAN_STAMPS=1)
-    // pipeline state
-    int cur;                  // buffer holding the newest landmark block (in stream order)
-    int pending;              // 1: a step was enqueued since the last drain
-    long long step;           // steps enqueued (slot = step & 1)
-    int have_results;
-    hipEvent_t ev_scan[2];    // recorded on S after scan of slot p
-    hipEvent_t ev_dd[2];      // recorded on D after downdate+patch of slot p
-    int ev_dd_valid[2];
+    // flush scheduling (see the top of this file)
+    int T;                    // flush interval
+    long long nsteps;         // update steps enqueued
+    long long unflushed0;     // first step not covered by an enqueued flush
+    long long pend0;          // first step not contained in X[base]
+    int base;                 // buffer the association kernels read
+    int last_out;             // buffer the newest enqueued flush writes (materialised after drain)
+    long long nflush;
+    hipEvent_t ev_scan;       // recorded on S after each update scan
+    hipEvent_t ev_flush[2];   // recorded on D after flush f (f & 1)
+    hipEvent_t ev_base;       // event guarding X[base] and the ring (nullptr: none pending)
     // profiling
     int prof;
     std::vector<EvPair> ev[3];   // scan, downdate, patch
@@ -124,15 +128,13 @@ static void free_all(ekf_ctx* c)
 {
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->pose, c->xpre, c->saved, c->D,
                                c->tile_rc, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->mbox,
-                               c->sync};
-    for (auto& sb : c->slot) {
-        ptrs.push_back(sb.s.Ust);
-        ptrs.push_back(sb.s.Vst);
-        ptrs.push_back(sb.s.Uop);
-        ptrs.push_back(sb.s.Vop);
-        ptrs.push_back(sb.s.patch);
-        ptrs.push_back(sb.s.patch_diag);
-        ptrs.push_back(sb.s.res);
+                               c->sync, c->Ust, c->Vst};
+    for (auto& sl : c->ring) {
+        ptrs.push_back(sl.Uop);
+        ptrs.push_back(sl.Vop);
+        ptrs.push_back(sl.patch);
+        ptrs.push_back(sl.patch_diag);
+        ptrs.push_back(sl.res);
     }
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -141,30 +143,39 @@ static void free_all(ekf_ctx* c)
     for (auto& v : c->ev)
         for (auto& pr : v) { (void)hipEventDestroy(pr.a); (void)hipEventDestroy(pr.b); }
     for (auto& pr : c->pool) { (void)hipEventDestroy(pr.a); (void)hipEventDestroy(pr.b); }
-    for (int k = 0; k < 2; k++) {
-        if (c->ev_scan[k]) (void)hipEventDestroy(c->ev_scan[k]);
-        if (c->ev_dd[k]) (void)hipEventDestroy(c->ev_dd[k]);
-    }
+    if (c->ev_scan) (void)hipEventDestroy(c->ev_scan);
+    for (int k = 0; k < 2; k++)
+        if (c->ev_flush[k]) (void)hipEventDestroy(c->ev_flush[k]);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     if (c->dstream) (void)hipStreamDestroy(c->dstream);
 }
 
-// Wait for everything on both streams; afterwards X[cur] is the materialised landmark block.
+static int enqueue_flush(ekf_ctx* c);
+
+// Flush the partial group and wait for both streams; afterwards X[last_out] is the materialised
+// landmark block and nothing is pending.
 static int drain(ekf_ctx* c)
 {
+    if (c->nsteps > c->unflushed0) {
+        int rc = enqueue_flush(c);
+        if (rc) return rc;
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipStreamSynchronize(c->dstream));
-    c->pending = 0;
-    c->ev_dd_valid[0] = c->ev_dd_valid[1] = 0;
+    c->base = c->last_out;
+    c->pend0 = c->nsteps;
+    c->ev_base = nullptr;
     return EKF_OK;
 }
+
+static inline int cur_buf(const ekf_ctx* c) { return c->last_out; }
 
 static int set_robot_ctor(ekf_ctx* c, int e, double x, double y, double th)
 {
     // Robot::Robot (Robot.cpp:20-35): P_t0[0][0] = P_t0[1][1] = 0.05, P_t0[2][2] = 0, the rest
     // (and y, savedLineCount) zero.
     const Dims& d = c->d;
-    HIP_TRY(hipMemsetAsync((char*)c->X[c->cur] + (size_t)e * c->pll_inst * c->elem, 0,
+    HIP_TRY(hipMemsetAsync((char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem, 0,
                            c->pll_inst * c->elem, c->stream));
     HIP_TRY(hipMemsetAsync(c->Rs + (size_t)e * 3 * d.n, 0, sizeof(double) * 3 * d.n, c->stream));
     HIP_TRY(hipMemsetAsync(c->y + (size_t)e * d.n, 0, sizeof(double) * d.n, c->stream));
@@ -193,7 +204,8 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         cfg->max_lines < 1 ||
         cfg->max_lines > EKF_MAX_LINES ||
         (cfg->precision != EKF_PREC_F64 && cfg->precision != EKF_PREC_F32) ||
-        (cfg->r_mode != EKF_R_INTENDED && cfg->r_mode != EKF_R_AS_WRITTEN))
+        (cfg->r_mode != EKF_R_INTENDED && cfg->r_mode != EKF_R_AS_WRITTEN) ||
+        cfg->flush_interval < 0 || cfg->flush_interval > 16)
         return EKF_EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return EKF_EDEVICE;
@@ -228,14 +240,16 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     ALLOC(c->xpre, sizeof(double) * 3 * E);
     ALLOC(c->saved, sizeof(int) * E);
     ALLOC(c->D, sizeof(double) * 4 * d.N * E);
-    for (auto& sb : c->slot) {
-        ALLOC(sb.s.Ust, sizeof(double) * d.max_lines * d.n * 2 * E);
-        ALLOC(sb.s.Vst, sizeof(double) * d.max_lines * d.n * 2 * E);
-        ALLOC(sb.s.Uop, c->op_inst * c->elem * E);
-        ALLOC(sb.s.Vop, c->op_inst * c->elem * E);
-        ALLOC(sb.s.patch, sizeof(double) * d.max_lines * 2 * d.M * E);
-        ALLOC(sb.s.patch_diag, sizeof(double) * d.max_lines * 4 * E);
-        ALLOC(sb.s.res, sizeof(int) * ekf::RES_STRIDE * E);
+    ALLOC(c->Ust, sizeof(double) * d.max_lines * d.n * 2 * E);
+    ALLOC(c->Vst, sizeof(double) * d.max_lines * d.n * 2 * E);
+    c->T = cfg->flush_interval > 0 ? cfg->flush_interval : 1;
+    c->ring.assign((size_t)c->T * (cfg->pipeline ? 2 : 1), ekf::Slot{});
+    for (auto& sl : c->ring) {
+        ALLOC(sl.Uop, c->op_inst * c->elem * E);
+        ALLOC(sl.Vop, c->op_inst * c->elem * E);
+        ALLOC(sl.patch, sizeof(double) * d.max_lines * 2 * d.M * E);
+        ALLOC(sl.patch_diag, sizeof(double) * d.max_lines * 4 * E);
+        ALLOC(sl.res, sizeof(int) * ekf::RES_STRIDE * E);
     }
     ALLOC(c->tile_rc, sizeof(int2) * d.ntiles);
     ALLOC(c->d_enc, sizeof(double) * 3 * E);
@@ -254,10 +268,9 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) goto fail;
     if (hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking) != hipSuccess) goto fail;
     c->stream = c->own_stream;
-    for (int k = 0; k < 2; k++) {
-        if (hipEventCreateWithFlags(&c->ev_scan[k], hipEventDisableTiming) != hipSuccess) goto fail;
-        if (hipEventCreateWithFlags(&c->ev_dd[k], hipEventDisableTiming) != hipSuccess) goto fail;
-    }
+    if (hipEventCreateWithFlags(&c->ev_scan, hipEventDisableTiming) != hipSuccess) goto fail;
+    for (int k = 0; k < 2; k++)
+        if (hipEventCreateWithFlags(&c->ev_flush[k], hipEventDisableTiming) != hipSuccess) goto fail;
     {
         std::vector<int2> rcv((size_t)d.ntiles);
         for (int bi = 0; bi < d.nb; bi++)
@@ -274,7 +287,10 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) goto fail;
-        c->dd_grid = prop.multiProcessorCount * 8;
+        int dd_per_cu = 8;   // downdate workgroups per CU (4 waves each)
+        if (getenv("EKF_DD_BLOCKS_PER_CU")) dd_per_cu = atoi(getenv("EKF_DD_BLOCKS_PER_CU"));
+        if (dd_per_cu < 1) dd_per_cu = 1;
+        c->dd_grid = prop.multiProcessorCount * dd_per_cu;
         // all G workgroups of an instance must be co-resident (they exchange per line): bound
         // the instances per association launch by the occupancy the hardware admits, less one
         // workgroup per CU of margin (MI355X_MICROARCH.md: the API can over-report by one)
@@ -289,7 +305,7 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         }
         if (c->scan_batch > E) c->scan_batch = E;
     }
-    c->cur = 0;
+    c->base = c->last_out = 0;
     for (int e = 0; e < E; e++)
         if (set_robot_ctor(c, e, 0.0, 0.0, 0.0) != EKF_OK) goto fail;
     *out = c;
@@ -322,9 +338,7 @@ extern "C" int ekf_set_stream(ekf_ctx* c, void* s)
 extern "C" int ekf_sync(ekf_ctx* c)
 {
     if (!c) return EKF_EINVAL;
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipStreamSynchronize(c->dstream));
-    return EKF_OK;
+    return drain(c);
 }
 
 extern "C" int ekf_reset_instance(ekf_ctx* c, int e, double x, double y, double th)
@@ -381,7 +395,6 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.pose = c->pose;
     p.xpre = c->xpre;
     p.saved = c->saved;
-    p.D = c->D;
     p.enc = enc;
     p.lines = lines;
     p.nlines = nlines;
@@ -407,6 +420,49 @@ static hipError_t launch_scans(ekf_ctx* c, ekf::ScanParams sp)
     return err;
 }
 
+static const ekf::Slot& slot_of(const ekf_ctx* c, long long k)
+{
+    return c->ring[(size_t)(k % (long long)c->ring.size())];
+}
+
+// One pass over the landmark block applying steps [unflushed0, nsteps) (stream D).
+static int enqueue_flush(ekf_ctx* c)
+{
+    const int nst = (int)(c->nsteps - c->unflushed0);
+    if (nst <= 0) return EKF_OK;
+    HIP_TRY(hipStreamWaitEvent(c->dstream, c->ev_scan, 0));
+    ekf::DowndateParams dp;
+    memset(&dp, 0, sizeof(dp));
+    dp.d = c->d;
+    dp.E = c->cfg.instances;
+    dp.nsteps = nst;
+    dp.tile_rc = c->tile_rc;
+    for (int q = 0; q < nst; q++) dp.steps[q] = slot_of(c, c->unflushed0 + q);
+    const int in = c->last_out;
+    const int out = c->cfg.pipeline ? 1 - in : in;
+    dp.Pin = c->X[in];
+    dp.Pout = c->X[out];
+    EvPair* pr = prof_begin(c, 1, c->dstream);
+    HIP_TRY(ekf::launch_downdate(dp, c->cfg.precision, c->dd_grid, c->dstream));
+    prof_end(c, pr, c->dstream);
+    hipEvent_t ev = c->ev_flush[c->nflush & 1];
+    HIP_TRY(hipEventRecord(ev, c->dstream));
+    if (c->cfg.pipeline) {
+        // next scans read X[in] (= output of the previous flush) with both groups pending
+        c->base = in;
+        c->ev_base = c->nflush > 0 ? c->ev_flush[(c->nflush - 1) & 1] : nullptr;
+        c->pend0 = c->unflushed0;
+    } else {
+        c->base = in;
+        c->ev_base = ev;
+        c->pend0 = c->nsteps;
+    }
+    c->last_out = out;
+    c->unflushed0 = c->nsteps;
+    c->nflush++;
+    return EKF_OK;
+}
+
 // Enqueue one localize step (or its predict / update half).
 static int enqueue(ekf_ctx* c, int phase, const double* enc, const ekf_line* lines,
                    const int* nlines)
@@ -418,63 +474,22 @@ static int enqueue(ekf_ctx* c, int phase, const double* enc, const ekf_line* lin
         prof_end(c, pr, c->stream);
         return EKF_OK;
     }
-    const int sl = (int)(c->step & 1);
-    int rbuf, wbuf;
-    if (!c->cfg.pipeline) {
-        // sequential: scan_k after downdate_{k-1} (+patch), in-place downdate
-        rbuf = wbuf = c->cur;
-        sp.pending = 0;
-        if (c->ev_dd_valid[1 - sl]) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_dd[1 - sl], 0));
-    } else if (c->pending) {
-        // previous step wrote X[cur] (maybe still running on D): read the other buffer + its
-        // pending downdate, and let this step's downdate write the other buffer again.
-        rbuf = 1 - c->cur;
-        wbuf = 1 - c->cur;
-        sp.pending = 1;
-        sp.prev = c->slot[1 - sl].s;
-    } else {
-        rbuf = c->cur;
-        wbuf = 1 - c->cur;
-        sp.pending = 0;
-    }
-    sp.Pread = c->X[rbuf];
-    sp.cur = c->slot[sl].s;
-    // scan_k reuses slot sl and reads X[rbuf]: both were last used by downdate_{k-2}
-    if (c->ev_dd_valid[sl]) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_dd[sl], 0));
+    // X[base] and the ring slot this step reuses are released by the event guarding base
+    if (c->ev_base) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_base, 0));
+    const int np = (int)(c->nsteps - c->pend0);
+    if (np > ekf::PMAX) return EKF_EINVAL;   // unreachable: T <= 16
+    sp.Pread = c->X[c->base];
+    sp.npend = np;
+    for (int q = 0; q < np; q++) sp.pend[q] = slot_of(c, c->pend0 + q);
+    sp.cur = slot_of(c, c->nsteps);
+    sp.Ust = c->Ust;
+    sp.Vst = c->Vst;
     EvPair* pr = prof_begin(c, 0, c->stream);
     HIP_TRY(launch_scans(c, sp));
     prof_end(c, pr, c->stream);
-    HIP_TRY(hipEventRecord(c->ev_scan[sl], c->stream));
-    HIP_TRY(hipStreamWaitEvent(c->dstream, c->ev_scan[sl], 0));
-
-    ekf::DowndateParams dp;
-    dp.d = c->d;
-    dp.E = c->cfg.instances;
-    dp.Pin = c->X[c->cur];
-    dp.Pout = c->X[wbuf];
-    dp.Uop = c->slot[sl].s.Uop;
-    dp.Vop = c->slot[sl].s.Vop;
-    dp.res = c->slot[sl].s.res;
-    dp.tile_rc = c->tile_rc;
-    pr = prof_begin(c, 1, c->dstream);
-    HIP_TRY(ekf::launch_downdate(dp, c->cfg.precision, c->dd_grid, c->dstream));
-    prof_end(c, pr, c->dstream);
-    ekf::PatchParams pp;
-    pp.d = c->d;
-    pp.E = c->cfg.instances;
-    pp.P = c->X[wbuf];
-    pp.patch = c->slot[sl].s.patch;
-    pp.patch_diag = c->slot[sl].s.patch_diag;
-    pp.res = c->slot[sl].s.res;
-    pr = prof_begin(c, 2, c->dstream);
-    HIP_TRY(ekf::launch_patch(pp, c->cfg.precision, c->dstream));
-    prof_end(c, pr, c->dstream);
-    HIP_TRY(hipEventRecord(c->ev_dd[sl], c->dstream));
-    c->ev_dd_valid[sl] = 1;
-    c->cur = wbuf;
-    c->pending = 1;
-    c->step++;
-    c->have_results = 1;
+    HIP_TRY(hipEventRecord(c->ev_scan, c->stream));
+    c->nsteps++;
+    if (c->nsteps - c->unflushed0 >= c->T) return enqueue_flush(c);
     return EKF_OK;
 }
 
@@ -502,12 +517,11 @@ extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
 {
     if (!c) return EKF_EINVAL;
     const int E = c->cfg.instances;
-    if (!c->have_results) {
+    if (c->nsteps == 0) {
         if (out) memset(out, 0, sizeof(ekf_result) * E);
         return EKF_OK;
     }
-    const int sl = (int)((c->step - 1) & 1);
-    HIP_TRY(hipMemcpyAsync(c->h_res, c->slot[sl].s.res, sizeof(int) * ekf::RES_STRIDE * E,
+    HIP_TRY(hipMemcpyAsync(c->h_res, slot_of(c, c->nsteps - 1).res, sizeof(int) * ekf::RES_STRIDE * E,
                            hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_pose, c->pose, sizeof(double) * 3 * E, hipMemcpyDeviceToHost,
                            c->stream));
@@ -590,7 +604,7 @@ extern "C" int ekf_upload_state(ekf_ctx* c, int e, const double* P, const double
                                         c->stream);
         if (err == hipSuccess)
             err = ekf::launch_pack(d, c->cfg.precision, tmp,
-                                   (char*)c->X[c->cur] + (size_t)e * c->pll_inst * c->elem,
+                                   (char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem,
                                    c->Rs + (size_t)e * 3 * d.n, c->tile_rc, c->stream);
         if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
         (void)hipFree(tmp);
@@ -622,7 +636,7 @@ extern "C" int ekf_download_state(ekf_ctx* c, int e, double* P, double* y, int* 
         double* tmp = nullptr;
         HIP_TRY(hipMalloc((void**)&tmp, sizeof(double) * d.n * d.n));
         hipError_t err = ekf::launch_unpack(d, c->cfg.precision, tmp,
-                                            (const char*)c->X[c->cur] + (size_t)e * c->pll_inst * c->elem,
+                                            (const char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem,
                                             c->Rs + (size_t)e * 3 * d.n, c->stream);
         if (err == hipSuccess)
             err = hipMemcpyAsync(P, tmp, sizeof(double) * d.n * d.n, hipMemcpyDeviceToHost,
@@ -660,7 +674,7 @@ extern "C" int ekf_init_lowrank(ekf_ctx* c, int e, const double* diag, const dou
         err = hipMemcpyAsync(du, U, sizeof(double) * d.n * rank, hipMemcpyHostToDevice, c->stream);
     if (err == hipSuccess)
         err = ekf::launch_lowrank(d, c->cfg.precision, dd, du, rank,
-                                  (char*)c->X[c->cur] + (size_t)e * c->pll_inst * c->elem,
+                                  (char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem,
                                   c->Rs + (size_t)e * 3 * d.n, c->tile_rc, c->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
     (void)hipFree(dd);

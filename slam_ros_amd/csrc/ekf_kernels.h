@@ -33,17 +33,19 @@ enum {
     RES_STRIDE = 16 + 2 * EKF_MAX_LINES,
 };
 
-// Per-step scratch ("slot"): two slots alternate so that step k's association kernel can run
-// while step k-1's downdate still reads its operands.
+// Per-step outputs that outlive the step's association kernel (a ring of slots): the
+// downdate operands, the augmented rows and the result record. They are consumed by the flush
+// (covariance downdate) of the step's group and, until then, by later association kernels
+// that read the landmark block with the pending steps applied on read.
 struct Slot {
-    double* Ust;        // [E][max_lines][n][2]   U_t = K_t·S_t  (fp64)
-    double* Vst;        // [E][max_lines][n][2]   V_t = K_t      (fp64)
     void* Uop;          // [E][nb][64][kmax/2]    -U in MFMA operand order (storage precision)
     void* Vop;          //                         V in MFMA operand order
     double* patch;      // [E][max_lines][2][M]   rows of landmarks added by this step
     double* patch_diag; // [E][max_lines][4]      their 2x2 diagonal blocks
     int* res;           // [E][RES_STRIDE]
 };
+
+constexpr int PMAX = 32;   // pending steps (2 × flush_interval in pipeline mode)
 
 struct ScanParams {
     Dims d;
@@ -56,7 +58,7 @@ struct ScanParams {
     int phase;
     int r_mode;
     int reset_margin;
-    int pending;          // 1: Pread is X_{k-2}; the previous slot's downdate is applied on read
+    int npend;            // steps not yet in Pread, applied on read (in order)
     double gate;
     double enc_noise;
     const void* Pread;    // [E][ntiles][1024] landmark block to read
@@ -65,39 +67,31 @@ struct ScanParams {
     double* pose;         // [E][3]
     double* xpre;         // [E][3]
     int* saved;           // [E]
-    double* D;            // [E][N][4]  landmark 2x2 diagonal blocks (per scan)
+    double* Ust;          // [E][max_lines][n][2] U_t = K_t·S_t of this scan (fp64 scratch)
+    double* Vst;          // [E][max_lines][n][2] V_t = K_t
     Slot cur;             // this step's slot
-    Slot prev;            // previous step's slot (read only, used when pending)
+    Slot pend[PMAX];      // pending steps, oldest first
     const double* enc;    // [E][3]
     const ekf_line* lines;// [E][max_lines]
     const int* nlines;    // [E]
     unsigned long long* dbg;  // optional [E][16] phase timers (s_memrealtime ticks, 100 MHz)
 };
 
+// One pass over the landmark block applying nsteps steps in order (each: reset, or rank-2m
+// downdate then its augmented rows). Pout may equal Pin (in place).
 struct DowndateParams {
     Dims d;
     int E;
-    const void* Pin;      // X_{k-1}
-    void* Pout;           // X_k (may equal Pin: in place)
-    const void* Uop;
-    const void* Vop;
-    const int* res;
+    int nsteps;
+    const void* Pin;
+    void* Pout;
     const int2* tile_rc;  // [ntiles] (bi, bj)
-};
-
-struct PatchParams {
-    Dims d;
-    int E;
-    void* P;              // X_k
-    const double* patch;
-    const double* patch_diag;
-    const int* res;
+    Slot steps[PMAX];
 };
 
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st);
 int scan_blocks_per_cu(int precision);
 hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st);
-hipError_t launch_patch(const PatchParams& p, int precision, hipStream_t st);
 hipError_t launch_pack(const Dims& d, int precision, const double* Pfull, void* Pll, double* Rs,
                        const int2* tile_rc, hipStream_t st);
 hipError_t launch_unpack(const Dims& d, int precision, double* Pfull, const void* Pll,

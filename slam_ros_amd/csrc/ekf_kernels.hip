@@ -17,7 +17,6 @@
 //        X_k = X_{k-1} − Σ_t U_t·V_tᵀ (rank 2m) on MFMA, reading and writing each stored tile
 //        once: the reference's m dense n×n passes (Robot.cpp:560-572) fused into one. Also the
 //        capacity reset of the landmark block (Robot.cpp:893-904).
-//   3. patch_kernel    (stream D): writes the augmented landmark rows into X_k.
 //
 // Cross-scan pipelining: X ping-pongs between two buffers, so scan k can read X_{k-2} while
 // downdate k-1 writes X_{k-1}; scan k then applies step k-1's downdate itself, element by
@@ -87,112 +86,115 @@ __device__ __forceinline__ void ll_store_sym(T* P, int i, int j, int nb, double 
 template <typename T>
 struct PllView {
     const T* X;
-    int nb, kmax, M;
-    int pend_ks;      // k-steps of the pending downdate (0: none)
-    int pend_reset;
-    const T* pU;      // pending operands (this instance)
-    const T* pV;
-    int ps0, pn;      // landmarks added by the previous step
-    const double* patch;
-    const double* pdiag;
+    int nb, kmax, M, max_lines;
+    int e;            // instance
+    size_t opstride;  // operand elements per instance
+    int npend;        // pending steps (oldest first)
+    const Slot* pend;
 };
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
-typedef double f64x2v __attribute__((ext_vector_type(2)));
 
-// 2x2 block (i0, i0+1) × (j0, j0+1) of the landmark block, i0 and j0 even.
+// 2x2 block (i0, i0+1) × (j0, j0+1) of the landmark block, i0 and j0 even, as it will be once
+// the pending steps are flushed: per step (in order) a reset, or the rank-2m downdate as the
+// k-ordered FMA chain the MFMA executes, then the step's augmented rows rounded to storage.
 template <typename T>
 __device__ __forceinline__ void pll_block(const PllView<T>& v, int i0, int j0, double out[4])
 {
-    if (v.pend_reset) {
-        out[0] = out[1] = out[2] = out[3] = 0.0;
-        return;
-    }
-    const int li = i0 >> 1, lj = j0 >> 1;
-    if (v.pn > 0) {
-        const int hi = li > lj ? li : lj;
-        if (hi >= v.ps0 && hi < v.ps0 + v.pn) {
-            // values as patch_kernel stores them (rounded to the storage precision)
-            const int q = hi - v.ps0;
-            double raw[4];
-            if (li == lj) {
-                raw[0] = v.pdiag[q * 4 + 0]; raw[1] = v.pdiag[q * 4 + 1];
-                raw[2] = v.pdiag[q * 4 + 2]; raw[3] = v.pdiag[q * 4 + 3];
-            } else if (li > lj) {
-                const double* r0 = v.patch + (size_t)(q * 2) * v.M;
-                raw[0] = r0[j0]; raw[1] = r0[j0 + 1];
-                raw[2] = r0[v.M + j0]; raw[3] = r0[v.M + j0 + 1];
-            } else {
-                const double* r0 = v.patch + (size_t)(q * 2) * v.M;
-                raw[0] = r0[i0]; raw[1] = r0[v.M + i0];
-                raw[2] = r0[i0 + 1]; raw[3] = r0[v.M + i0 + 1];
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++) out[k] = (double)(T)raw[k];
-            return;
-        }
-    }
-    // stored orientation: rows a0, a0+1 and columns b0, b0+1 of one tile
     const bool swap = (i0 >> 5) > (j0 >> 5);
-    const int a0 = swap ? j0 : i0, b0 = swap ? i0 : j0;
-    double st[4];   // stored (a0+p, b0+c) at st[p*2+c]
-    T x[4];
+    const int a0 = swap ? j0 : i0, b0 = swap ? i0 : j0;   // stored orientation
+    T acc[4];
 #pragma unroll
     for (int p = 0; p < 2; p++)
 #pragma unroll
-        for (int c = 0; c < 2; c++) x[p * 2 + c] = v.X[ll_offset<T>(a0 + p, b0 + c, v.nb)];
-    if (v.pend_ks == 0) {
+        for (int c = 0; c < 2; c++) acc[p * 2 + c] = v.X[ll_offset<T>(a0 + p, b0 + c, v.nb)];
+    for (int q = 0; q < v.npend; q++) {
+        const Slot& sq = v.pend[q];
+        const int* r = sq.res + (size_t)v.e * RES_STRIDE;
+        if (r[RES_RESET]) {
+            acc[0] = acc[1] = acc[2] = acc[3] = (T)0;
+            continue;
+        }
+        const int ks = r[RES_KSTEPS];
+        if (ks > 0) {
+            if constexpr (sizeof(T) == 4) {
+                // v_mfma_f32_32x32x2_f32 = ordered fmaf chain (k0 lanes 0-31, then k1)
+                const int kh = v.kmax / 2;
+                const float* ua = reinterpret_cast<const float*>(sq.Uop) + v.e * v.opstride +
+                                  ((size_t)(a0 >> 5) * 64 + (a0 & 31)) * kh;   // row a0; a0+1 at +kh
+                const float* vb = reinterpret_cast<const float*>(sq.Vop) + v.e * v.opstride +
+                                  ((size_t)(b0 >> 5) * 64 + (b0 & 31)) * kh;
+                for (int s0 = 0; s0 < ks; s0 += 4) {
+                    const f32x4v ae0 = *reinterpret_cast<const f32x4v*>(ua + s0);
+                    const f32x4v ae1 = *reinterpret_cast<const f32x4v*>(ua + kh + s0);
+                    const f32x4v ao0 = *reinterpret_cast<const f32x4v*>(ua + 32 * kh + s0);
+                    const f32x4v ao1 = *reinterpret_cast<const f32x4v*>(ua + 33 * kh + s0);
+                    const f32x4v be0 = *reinterpret_cast<const f32x4v*>(vb + s0);
+                    const f32x4v be1 = *reinterpret_cast<const f32x4v*>(vb + kh + s0);
+                    const f32x4v bo0 = *reinterpret_cast<const f32x4v*>(vb + 32 * kh + s0);
+                    const f32x4v bo1 = *reinterpret_cast<const f32x4v*>(vb + 33 * kh + s0);
 #pragma unroll
-        for (int q = 0; q < 4; q++) st[q] = (double)x[q];
-    } else if constexpr (sizeof(T) == 4) {
-        // v_mfma_f32_32x32x2_f32 is bit-for-bit a k-ordered fmaf chain (k0 lanes 0-31, then k1)
-        const int kh = v.kmax / 2;
-        const float* ua = v.pU + ((size_t)(a0 >> 5) * 64 + (a0 & 31)) * kh;   // row a0; a0+1 at +kh
-        const float* vb = v.pV + ((size_t)(b0 >> 5) * 64 + (b0 & 31)) * kh;
-        float acc[4] = {x[0], x[1], x[2], x[3]};
-        for (int s0 = 0; s0 < v.pend_ks; s0 += 4) {
-            const f32x4v ae0 = *reinterpret_cast<const f32x4v*>(ua + s0);
-            const f32x4v ae1 = *reinterpret_cast<const f32x4v*>(ua + kh + s0);
-            const f32x4v ao0 = *reinterpret_cast<const f32x4v*>(ua + 32 * kh + s0);
-            const f32x4v ao1 = *reinterpret_cast<const f32x4v*>(ua + 33 * kh + s0);
-            const f32x4v be0 = *reinterpret_cast<const f32x4v*>(vb + s0);
-            const f32x4v be1 = *reinterpret_cast<const f32x4v*>(vb + kh + s0);
-            const f32x4v bo0 = *reinterpret_cast<const f32x4v*>(vb + 32 * kh + s0);
-            const f32x4v bo1 = *reinterpret_cast<const f32x4v*>(vb + 33 * kh + s0);
+                    for (int s = 0; s < 4; s++) {
+                        if (s0 + s >= ks) break;
+                        acc[0] = fmaf(ao0[s], bo0[s], fmaf(ae0[s], be0[s], acc[0]));
+                        acc[1] = fmaf(ao0[s], bo1[s], fmaf(ae0[s], be1[s], acc[1]));
+                        acc[2] = fmaf(ao1[s], bo0[s], fmaf(ae1[s], be0[s], acc[2]));
+                        acc[3] = fmaf(ao1[s], bo1[s], fmaf(ae1[s], be1[s], acc[3]));
+                    }
+                }
+            } else {
+                // v_mfma_f64_16x16x4_f64 = ordered fma chain over k = 4s..4s+3
+                const int kq = v.kmax / 4;
+                const double* ua = reinterpret_cast<const double*>(sq.Uop) + v.e * v.opstride +
+                                   ((size_t)(a0 >> 5) * 64 + (a0 & 15)) * (2 * kq) + ((a0 >> 4) & 1) * kq;
+                const double* vb = reinterpret_cast<const double*>(sq.Vop) + v.e * v.opstride +
+                                   ((size_t)(b0 >> 5) * 64 + (b0 & 15)) * (2 * kq) + ((b0 >> 4) & 1) * kq;
+                for (int s = 0; s < ks; s++)
 #pragma unroll
-            for (int s = 0; s < 4; s++) {
-                if (s0 + s >= v.pend_ks) break;
-                acc[0] = fmaf(ao0[s], bo0[s], fmaf(ae0[s], be0[s], acc[0]));
-                acc[1] = fmaf(ao0[s], bo1[s], fmaf(ae0[s], be1[s], acc[1]));
-                acc[2] = fmaf(ao1[s], bo0[s], fmaf(ae1[s], be0[s], acc[2]));
-                acc[3] = fmaf(ao1[s], bo1[s], fmaf(ae1[s], be1[s], acc[3]));
+                    for (int kk = 0; kk < 4; kk++) {
+                        const size_t o = (size_t)16 * kk * 2 * kq + s;
+                        const double x0 = ua[o], x1 = ua[o + 2 * kq];
+                        const double y0 = vb[o], y1 = vb[o + 2 * kq];
+                        acc[0] = fma(x0, y0, (double)acc[0]);
+                        acc[1] = fma(x0, y1, (double)acc[1]);
+                        acc[2] = fma(x1, y0, (double)acc[2]);
+                        acc[3] = fma(x1, y1, (double)acc[3]);
+                    }
             }
         }
-#pragma unroll
-        for (int q = 0; q < 4; q++) st[q] = (double)acc[q];
-    } else {
-        const int kq = v.kmax / 4;
-        const double* ua = v.pU + ((size_t)(a0 >> 5) * 64 + (a0 & 15)) * (2 * kq) + ((a0 >> 4) & 1) * kq;
-        const double* vb = v.pV + ((size_t)(b0 >> 5) * 64 + (b0 & 15)) * (2 * kq) + ((b0 >> 4) & 1) * kq;
-        double acc[4] = {(double)x[0], (double)x[1], (double)x[2], (double)x[3]};
-        for (int s = 0; s < v.pend_ks; s++)
-#pragma unroll
-            for (int kk = 0; kk < 4; kk++) {
-                const size_t o = (size_t)16 * kk * 2 * kq + s;
-                const double a_0 = ua[o], a_1 = ua[o + 2 * kq];
-                const double b_0 = vb[o], b_1 = vb[o + 2 * kq];
-                acc[0] = fma(a_0, b_0, acc[0]);
-                acc[1] = fma(a_0, b_1, acc[1]);
-                acc[2] = fma(a_1, b_0, acc[2]);
-                acc[3] = fma(a_1, b_1, acc[3]);
+        const int nadd = r[RES_NADD];
+        if (nadd > 0) {
+            const int s0 = r[RES_SAVED_IN];
+            const int li = i0 >> 1, lj = j0 >> 1;
+            const int hi = li > lj ? li : lj;
+            if (hi >= s0 && hi < s0 + nadd) {
+                // augmented rows (requested orientation), rounded as they are stored
+                const int qa = hi - s0;
+                const double* pdg = sq.patch_diag + (size_t)v.e * v.max_lines * 4;
+                const double* prw = sq.patch + ((size_t)v.e * v.max_lines + qa) * 2 * v.M;
+                double raw[4];
+                if (li == lj) {
+                    raw[0] = pdg[qa * 4 + 0]; raw[1] = pdg[qa * 4 + 1];
+                    raw[2] = pdg[qa * 4 + 2]; raw[3] = pdg[qa * 4 + 3];
+                } else if (li > lj) {
+                    raw[0] = prw[j0]; raw[1] = prw[j0 + 1];
+                    raw[2] = prw[v.M + j0]; raw[3] = prw[v.M + j0 + 1];
+                } else {
+                    raw[0] = prw[i0]; raw[1] = prw[v.M + i0];
+                    raw[2] = prw[i0 + 1]; raw[3] = prw[v.M + i0 + 1];
+                }
+                if (swap) {
+                    acc[0] = (T)raw[0]; acc[1] = (T)raw[2]; acc[2] = (T)raw[1]; acc[3] = (T)raw[3];
+                } else {
+                    acc[0] = (T)raw[0]; acc[1] = (T)raw[1]; acc[2] = (T)raw[2]; acc[3] = (T)raw[3];
+                }
             }
-#pragma unroll
-        for (int q = 0; q < 4; q++) st[q] = acc[q];
+        }
     }
     if (swap) {
-        out[0] = st[0]; out[1] = st[2]; out[2] = st[1]; out[3] = st[3];
+        out[0] = (double)acc[0]; out[1] = (double)acc[2]; out[2] = (double)acc[1]; out[3] = (double)acc[3];
     } else {
-        out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
+        out[0] = (double)acc[0]; out[1] = (double)acc[1]; out[2] = (double)acc[2]; out[3] = (double)acc[3];
     }
 }
 
@@ -511,8 +513,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
 
     // ---------------- association / update (Robot.cpp:288-904) ----------------
     const size_t opstride = (size_t)d.nb * 64 * (d.kmax / 2);
-    double* Ust = p.cur.Ust + (size_t)e * d.max_lines * n * 2;
-    double* Vst = p.cur.Vst + (size_t)e * d.max_lines * n * 2;
+    double* Ust = p.Ust + (size_t)e * d.max_lines * n * 2;
+    double* Vst = p.Vst + (size_t)e * d.max_lines * n * 2;
     T* Uop = reinterpret_cast<T*>(p.cur.Uop) + (size_t)e * opstride;
     T* Vop = reinterpret_cast<T*>(p.cur.Vop) + (size_t)e * opstride;
     double* patch = p.cur.patch + (size_t)e * d.max_lines * 2 * M;
@@ -524,22 +526,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     pv.nb = d.nb;
     pv.kmax = d.kmax;
     pv.M = M;
-    pv.pend_ks = 0;
-    pv.pend_reset = 0;
-    pv.pU = pv.pV = nullptr;
-    pv.ps0 = pv.pn = 0;
-    pv.patch = pv.pdiag = nullptr;
-    if (p.pending) {
-        const int* pres = p.prev.res + (size_t)e * RES_STRIDE;
-        pv.pend_ks = pres[RES_KSTEPS];
-        pv.pend_reset = pres[RES_RESET];
-        pv.pU = reinterpret_cast<const T*>(p.prev.Uop) + (size_t)e * opstride;
-        pv.pV = reinterpret_cast<const T*>(p.prev.Vop) + (size_t)e * opstride;
-        pv.ps0 = pres[RES_SAVED_IN];
-        pv.pn = pres[RES_NADD];
-        pv.patch = p.prev.patch + (size_t)e * d.max_lines * 2 * M;
-        pv.pdiag = p.prev.patch_diag + (size_t)e * d.max_lines * 4;
-    }
+    pv.max_lines = d.max_lines;
+    pv.e = e;
+    pv.opstride = opstride;
+    pv.npend = p.npend;
+    pv.pend = p.pend;
 
     int L = p.nlines[e];
     L = L < 0 ? 0 : (L > d.max_lines ? d.max_lines : L);
@@ -871,12 +862,29 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
 }
 
 // ---------------------------------------------------------------------------------------
-// 2. packed rank-2m covariance downdate on MFMA (out of place: X_{k-1} → X_k)
+// 2. covariance downdate of the landmark block on MFMA, one pass for a group of steps
 // ---------------------------------------------------------------------------------------
+// For every stored 32×32 tile and every step of the group, in order: the capacity reset
+// (Robot.cpp:893-904), or X ← X − U_t·V_tᵀ summed over the step's matches (rank 2m, the
+// reference's m dense passes of Robot.cpp:560-572) followed by the rows of the landmarks that
+// step appended (Robot.cpp:845-862). The tile stays in the MFMA accumulators for the whole
+// group: one HBM read and one write per tile per group.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// value of landmark-block element (i, j) written by a step's augmentation
+__device__ __forceinline__ double patched_value(const double* prw0, const double* pdg, int M,
+                                                int s0, int i, int j)
+{
+    const int li = i >> 1, lj = j >> 1;
+    const int hi = li > lj ? li : lj;
+    const int qa = hi - s0;
+    if (li == lj) return pdg[qa * 4 + (i & 1) * 2 + (j & 1)];
+    const double* prw = prw0 + (size_t)qa * 2 * M;
+    return (li > lj) ? prw[(size_t)(i & 1) * M + j] : prw[(size_t)(j & 1) * M + i];
+}
 
 __global__ __launch_bounds__(DD_THREADS) void downdate_f32_kernel(DowndateParams p)
 {
@@ -885,60 +893,83 @@ __global__ __launch_bounds__(DD_THREADS) void downdate_f32_kernel(DowndateParams
     const int64_t nwaves = (int64_t)gridDim.x * (DD_THREADS / 64);
     const int64_t total = (int64_t)p.E * d.ntiles;
     const int kh = d.kmax / 2;   // operand floats per lane per row block
+    const size_t opstride = (size_t)d.nb * 64 * kh;
     for (int64_t g = (int64_t)blockIdx.x * (DD_THREADS / 64) + (threadIdx.x >> 6); g < total;
          g += nwaves) {
         const int e = (int)(g / d.ntiles);
         const int64_t t = g - (int64_t)e * d.ntiles;
-        const int* res = p.res + (size_t)e * RES_STRIDE;
-        const int ks = res[RES_KSTEPS];
-        const int reset = res[RES_RESET];
         const size_t toff = ((size_t)e * d.ntiles + t) * TILE_ELEMS;
         const f32x4* src = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.Pin) + toff) + lane;
         f32x4* dst = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.Pout) + toff) + lane;
-        if (reset) {
-            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int q = 0; q < 4; q++) __builtin_nontemporal_store(z, dst + q * 64);
-            continue;
+        // does any step of the group change this tile?
+        const int2 rc = p.tile_rc[t];
+        bool work = false;
+        for (int q = 0; q < p.nsteps; q++) {
+            const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
+            const int nadd = r[RES_NADD], s0 = r[RES_SAVED_IN];
+            work |= r[RES_RESET] || r[RES_KSTEPS] > 0 ||
+                    (nadd > 0 && rc.y * 16 + 15 >= s0 && rc.y * 16 < s0 + nadd);
         }
-        if (ks == 0) {
-            if (p.Pin != p.Pout) {   // no match: X_k = X_{k-1} (P_t0 ← P_pre, Robot.cpp:713)
+        if (!work) {
+            if (p.Pin != p.Pout) {   // unchanged tile of an out-of-place pass
 #pragma unroll
-                for (int q = 0; q < 4; q++)
-                    __builtin_nontemporal_store(__builtin_nontemporal_load(src + q * 64), dst + q * 64);
+                for (int qq = 0; qq < 4; qq++)
+                    __builtin_nontemporal_store(__builtin_nontemporal_load(src + qq * 64), dst + qq * 64);
             }
             continue;
         }
-        const int2 rc = p.tile_rc[t];
         f32x16 acc;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const f32x4 v = __builtin_nontemporal_load(src + q * 64);
-            acc[4 * q + 0] = v[0];
-            acc[4 * q + 1] = v[1];
-            acc[4 * q + 2] = v[2];
-            acc[4 * q + 3] = v[3];
+        for (int qq = 0; qq < 4; qq++) {
+            const f32x4 v = __builtin_nontemporal_load(src + qq * 64);
+            acc[4 * qq + 0] = v[0];
+            acc[4 * qq + 1] = v[1];
+            acc[4 * qq + 2] = v[2];
+            acc[4 * qq + 3] = v[3];
         }
-        const size_t opbase = (size_t)e * d.nb * 64 * kh;
-        const float* A = reinterpret_cast<const float*>(p.Uop) + opbase +
-                         ((size_t)rc.x * 64 + lane) * kh;
-        const float* B = reinterpret_cast<const float*>(p.Vop) + opbase +
-                         ((size_t)rc.y * 64 + lane) * kh;
-        for (int s0 = 0; s0 < ks; s0 += 8) {
-            const f32x4 a0 = *reinterpret_cast<const f32x4*>(A + s0);
-            const f32x4 a1 = *reinterpret_cast<const f32x4*>(A + s0 + 4);
-            const f32x4 b0 = *reinterpret_cast<const f32x4*>(B + s0);
-            const f32x4 b1 = *reinterpret_cast<const f32x4*>(B + s0 + 4);
-            const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-            const float bv[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        for (int q = 0; q < p.nsteps; q++) {
+            const Slot& sq = p.steps[q];
+            const int* r = sq.res + (size_t)e * RES_STRIDE;
+            if (r[RES_RESET]) {
 #pragma unroll
-            for (int s = 0; s < 8; s++)
-                if (s0 + s < ks) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
+                for (int k = 0; k < 16; k++) acc[k] = 0.f;
+                continue;
+            }
+            const int ks = r[RES_KSTEPS];
+            if (ks > 0) {
+                const float* A = reinterpret_cast<const float*>(sq.Uop) + e * opstride +
+                                 ((size_t)rc.x * 64 + lane) * kh;
+                const float* B = reinterpret_cast<const float*>(sq.Vop) + e * opstride +
+                                 ((size_t)rc.y * 64 + lane) * kh;
+                for (int s0 = 0; s0 < ks; s0 += 8) {
+                    const f32x4 a0 = *reinterpret_cast<const f32x4*>(A + s0);
+                    const f32x4 a1 = *reinterpret_cast<const f32x4*>(A + s0 + 4);
+                    const f32x4 b0 = *reinterpret_cast<const f32x4*>(B + s0);
+                    const f32x4 b1 = *reinterpret_cast<const f32x4*>(B + s0 + 4);
+                    const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+                    const float bv[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+                    for (int s = 0; s < 8; s++)
+                        if (s0 + s < ks) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
+                }
+            }
+            const int nadd = r[RES_NADD], s0 = r[RES_SAVED_IN];
+            if (nadd > 0 && rc.y * 16 + 15 >= s0 && rc.y * 16 < s0 + nadd) {
+                const double* prw0 = sq.patch + (size_t)e * d.max_lines * 2 * d.M;
+                const double* pdg = sq.patch_diag + (size_t)e * d.max_lines * 4;
+                const int col = rc.y * 32 + (lane & 31);
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int row = rc.x * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
+                    const int hi = max(row >> 1, col >> 1);
+                    if (hi >= s0 && hi < s0 + nadd) acc[k] = (float)patched_value(prw0, pdg, d.M, s0, row, col);
+                }
+            }
         }
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const f32x4 v = {acc[4 * q + 0], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
-            __builtin_nontemporal_store(v, dst + q * 64);
+        for (int qq = 0; qq < 4; qq++) {
+            const f32x4 v = {acc[4 * qq + 0], acc[4 * qq + 1], acc[4 * qq + 2], acc[4 * qq + 3]};
+            __builtin_nontemporal_store(v, dst + qq * 64);
         }
     }
 }
@@ -951,95 +982,87 @@ __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams
     const int64_t total = (int64_t)p.E * d.ntiles;
     const int kh = d.kmax / 2;   // doubles per lane per row block (2 halves × kmax/4)
     const int kq = d.kmax / 4;
+    const size_t opstride = (size_t)d.nb * 64 * kh;
     for (int64_t g = (int64_t)blockIdx.x * (DD_THREADS / 64) + (threadIdx.x >> 6); g < total;
          g += nwaves) {
         const int e = (int)(g / d.ntiles);
         const int64_t t = g - (int64_t)e * d.ntiles;
-        const int* res = p.res + (size_t)e * RES_STRIDE;
-        const int ks = res[RES_KSTEPS];
-        const int reset = res[RES_RESET];
         const size_t toff = ((size_t)e * d.ntiles + t) * TILE_ELEMS;
         const f64x2* src = reinterpret_cast<const f64x2*>(reinterpret_cast<const double*>(p.Pin) + toff) + 2 * lane;
         f64x2* dst = reinterpret_cast<f64x2*>(reinterpret_cast<double*>(p.Pout) + toff) + 2 * lane;
-        if (reset) {
-            const f64x2 z = {0.0, 0.0};
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                __builtin_nontemporal_store(z, dst + q * 128);
-                __builtin_nontemporal_store(z, dst + q * 128 + 1);
-            }
-            continue;
+        const int2 rc = p.tile_rc[t];
+        bool work = false;
+        for (int q = 0; q < p.nsteps; q++) {
+            const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
+            const int nadd = r[RES_NADD], s0 = r[RES_SAVED_IN];
+            work |= r[RES_RESET] || r[RES_KSTEPS] > 0 ||
+                    (nadd > 0 && rc.y * 16 + 15 >= s0 && rc.y * 16 < s0 + nadd);
         }
-        if (ks == 0) {
+        if (!work) {
             if (p.Pin != p.Pout) {
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    __builtin_nontemporal_store(__builtin_nontemporal_load(src + q * 128), dst + q * 128);
-                    __builtin_nontemporal_store(__builtin_nontemporal_load(src + q * 128 + 1), dst + q * 128 + 1);
+                for (int qq = 0; qq < 4; qq++) {
+                    __builtin_nontemporal_store(__builtin_nontemporal_load(src + qq * 128), dst + qq * 128);
+                    __builtin_nontemporal_store(__builtin_nontemporal_load(src + qq * 128 + 1), dst + qq * 128 + 1);
                 }
             }
             continue;
         }
-        const int2 rc = p.tile_rc[t];
         f64x4 acc[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const f64x2 v0 = __builtin_nontemporal_load(src + q * 128);
-            const f64x2 v1 = __builtin_nontemporal_load(src + q * 128 + 1);
-            acc[q][0] = v0[0];
-            acc[q][1] = v0[1];
-            acc[q][2] = v1[0];
-            acc[q][3] = v1[1];
+        for (int qq = 0; qq < 4; qq++) {
+            const f64x2 v0 = __builtin_nontemporal_load(src + qq * 128);
+            const f64x2 v1 = __builtin_nontemporal_load(src + qq * 128 + 1);
+            acc[qq][0] = v0[0];
+            acc[qq][1] = v0[1];
+            acc[qq][2] = v1[0];
+            acc[qq][3] = v1[1];
         }
-        const size_t opbase = (size_t)e * d.nb * 64 * kh;
-        const double* A = reinterpret_cast<const double*>(p.Uop) + opbase +
-                          ((size_t)rc.x * 64 + lane) * kh;
-        const double* B = reinterpret_cast<const double*>(p.Vop) + opbase +
-                          ((size_t)rc.y * 64 + lane) * kh;
-        for (int s = 0; s < ks; s++) {
-            const double a0 = A[s], a1 = A[kq + s];
-            const double b0 = B[s], b1 = B[kq + s];
-            acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
-            acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1], 0, 0, 0);
-            acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[2], 0, 0, 0);
-            acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[3], 0, 0, 0);
+        for (int q = 0; q < p.nsteps; q++) {
+            const Slot& sq = p.steps[q];
+            const int* r = sq.res + (size_t)e * RES_STRIDE;
+            if (r[RES_RESET]) {
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) acc[qq] = f64x4{0.0, 0.0, 0.0, 0.0};
+                continue;
+            }
+            const int ks = r[RES_KSTEPS];
+            if (ks > 0) {
+                const double* A = reinterpret_cast<const double*>(sq.Uop) + e * opstride +
+                                  ((size_t)rc.x * 64 + lane) * kh;
+                const double* B = reinterpret_cast<const double*>(sq.Vop) + e * opstride +
+                                  ((size_t)rc.y * 64 + lane) * kh;
+                for (int s = 0; s < ks; s++) {
+                    const double a0 = A[s], a1 = A[kq + s];
+                    const double b0 = B[s], b1 = B[kq + s];
+                    acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
+                    acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1], 0, 0, 0);
+                    acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[2], 0, 0, 0);
+                    acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[3], 0, 0, 0);
+                }
+            }
+            const int nadd = r[RES_NADD], s0 = r[RES_SAVED_IN];
+            if (nadd > 0 && rc.y * 16 + 15 >= s0 && rc.y * 16 < s0 + nadd) {
+                const double* prw0 = sq.patch + (size_t)e * d.max_lines * 2 * d.M;
+                const double* pdg = sq.patch_diag + (size_t)e * d.max_lines * 4;
+#pragma unroll
+                for (int blk = 0; blk < 4; blk++)
+#pragma unroll
+                    for (int reg = 0; reg < 4; reg++) {
+                        const int row = rc.x * 32 + (lane >> 4) + 4 * reg + 16 * (blk >> 1);
+                        const int col = rc.y * 32 + (lane & 15) + 16 * (blk & 1);
+                        const int hi = max(row >> 1, col >> 1);
+                        if (hi >= s0 && hi < s0 + nadd)
+                            acc[blk][reg] = patched_value(prw0, pdg, d.M, s0, row, col);
+                    }
+            }
         }
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const f64x2 v0 = {acc[q][0], acc[q][1]};
-            const f64x2 v1 = {acc[q][2], acc[q][3]};
-            __builtin_nontemporal_store(v0, dst + q * 128);
-            __builtin_nontemporal_store(v1, dst + q * 128 + 1);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// 3. augmented landmark rows into X_k (after the downdate, Robot.cpp:845-862)
-// ---------------------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(SCAN_THREADS) void patch_kernel(PatchParams p)
-{
-    const Dims d = p.d;
-    const int e = blockIdx.x;
-    const int* res = p.res + (size_t)e * RES_STRIDE;
-    const int nadd = res[RES_NADD];
-    if (res[RES_RESET] || nadd == 0) return;
-    const int s0 = res[RES_SAVED_IN];
-    T* P = reinterpret_cast<T*>(p.P) + (size_t)e * d.ntiles * TILE_ELEMS;
-    const double* patch = p.patch + (size_t)e * d.max_lines * 2 * d.M;
-    const double* pdiag = p.patch_diag + (size_t)e * d.max_lines * 4;
-    for (int q = 0; q < nadd; q++) {
-        const int i0 = 2 * (s0 + q);
-        for (int c = threadIdx.x; c < i0; c += SCAN_THREADS) {
-            ll_store_sym(P, i0, c, d.nb, patch[(size_t)(q * 2) * d.M + c]);
-            ll_store_sym(P, i0 + 1, c, d.nb, patch[(size_t)(q * 2 + 1) * d.M + c]);
-        }
-        if (threadIdx.x == 0) {
-            P[ll_offset<T>(i0, i0, d.nb)] = (T)pdiag[q * 4 + 0];
-            P[ll_offset<T>(i0, i0 + 1, d.nb)] = (T)pdiag[q * 4 + 1];
-            P[ll_offset<T>(i0 + 1, i0, d.nb)] = (T)pdiag[q * 4 + 2];
-            P[ll_offset<T>(i0 + 1, i0 + 1, d.nb)] = (T)pdiag[q * 4 + 3];
+        for (int qq = 0; qq < 4; qq++) {
+            const f64x2 v0 = {acc[qq][0], acc[qq][1]};
+            const f64x2 v1 = {acc[qq][2], acc[qq][3]};
+            __builtin_nontemporal_store(v0, dst + qq * 128);
+            __builtin_nontemporal_store(v1, dst + qq * 128 + 1);
         }
     }
 }
@@ -1161,15 +1184,6 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
         hipLaunchKernelGGL(downdate_f64_kernel, dim3(grid), dim3(DD_THREADS), 0, st, p);
     else
         hipLaunchKernelGGL(downdate_f32_kernel, dim3(grid), dim3(DD_THREADS), 0, st, p);
-    return hipGetLastError();
-}
-
-hipError_t launch_patch(const PatchParams& p, int precision, hipStream_t st)
-{
-    if (precision == 0)
-        hipLaunchKernelGGL(patch_kernel<double>, dim3(p.E), dim3(SCAN_THREADS), 0, st, p);
-    else
-        hipLaunchKernelGGL(patch_kernel<float>, dim3(p.E), dim3(SCAN_THREADS), 0, st, p);
     return hipGetLastError();
 }
 

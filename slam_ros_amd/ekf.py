@@ -41,6 +41,7 @@ class EkfConfig(ctypes.Structure):
         ("precision", ctypes.c_int32), ("device", ctypes.c_int32),
         ("max_lines", ctypes.c_int32), ("r_mode", ctypes.c_int32),
         ("reset_margin", ctypes.c_int32), ("pipeline", ctypes.c_int32),
+        ("flush_interval", ctypes.c_int32), ("reserved", ctypes.c_int32),
         ("mahalanobis", ctypes.c_double), ("encoder_noise", ctypes.c_double),
     ]
 
@@ -140,7 +141,7 @@ class Ensemble:
     def __init__(self, capacity: int, instances: int = 1, precision: int = PREC_F64,
                  max_lines: int = 20, device: int = -1, r_mode: int = R_INTENDED,
                  reset_margin: int = 10, mahalanobis: float = 0.4, encoder_noise: float = 0.024,
-                 pipeline: bool = False):
+                 pipeline: bool = False, flush_interval: int = 1):
         self._lib = load_library()
         cfg = EkfConfig()
         self._lib.ekf_config_init(ctypes.byref(cfg))
@@ -148,6 +149,7 @@ class Ensemble:
         cfg.device, cfg.max_lines, cfg.r_mode = device, max_lines, r_mode
         cfg.reset_margin, cfg.mahalanobis, cfg.encoder_noise = reset_margin, mahalanobis, encoder_noise
         cfg.pipeline = 1 if pipeline else 0
+        cfg.flush_interval = int(flush_interval)
         h = ctypes.c_void_p()
         _check(self._lib.ekf_create(ctypes.byref(cfg), ctypes.byref(h)), "ekf_create")
         self._h = h

@@ -60,7 +60,7 @@ def test_struct_layouts_match_header():
     # ekf_line is 6 doubles; ekf_result as declared
     from slam_ros_amd import ekf
     assert ctypes.sizeof(ekf.EkfLine) == 48
-    assert ctypes.sizeof(ekf.EkfConfig) == 48
+    assert ctypes.sizeof(ekf.EkfConfig) == 56
     assert ctypes.sizeof(ekf.EkfResult) == 24 + 6 * 4 + 4 * ekf.EKF_MAX_LINES
 
 

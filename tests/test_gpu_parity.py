@@ -139,15 +139,19 @@ def test_trajectory_fp64_with_reset(ekf_mod, oracle_mod):
 
 
 @pytest.mark.parametrize("prec", [0, 1])
-def test_pipelined_equals_drained(ekf_mod, oracle_mod, prec):
-    """Back-to-back steps (step k's association overlaps step k-1's downdate and applies it
-    on read) give bit-identical state to draining after every step; fp64 also vs the oracle.
-    Covers matches, augmentation (patch rows) and the capacity reset across the pipeline."""
+@pytest.mark.parametrize("pipeline,T,drain_at", [(True, 1, ()), (False, 4, ()), (True, 3, (7,)),
+                                                 (False, 16, (5,)), (True, 16, ())])
+def test_deferred_flush_equals_drained(ekf_mod, oracle_mod, prec, pipeline, T, drain_at):
+    """Deferred covariance downdates — the landmark block rewritten once per T scans, the
+    association kernels applying the pending steps on read, optionally overlapped with the
+    next scans (pipeline) — give bit-identical state to one in-place flush per scan drained
+    after every step; fp64 also vs the oracle. Covers matches, augmentation rows, the
+    capacity reset inside a group and partial groups (a drain mid-group, the trajectory end)."""
     N = 64
     w = G.make_world(N, active=N - 14)
     st = G.initial_state(w)
-    a = ekf_mod.Ensemble(N, 2, prec, max_lines=8, pipeline=True)
-    b = ekf_mod.Ensemble(N, 2, prec, max_lines=8, pipeline=True)
+    a = ekf_mod.Ensemble(N, 2, prec, max_lines=8, pipeline=pipeline, flush_interval=T)
+    b = ekf_mod.Ensemble(N, 2, prec, max_lines=8)
     for ens in (a, b):
         for e in range(2):
             ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
@@ -162,9 +166,12 @@ def test_pipelined_equals_drained(ekf_mod, oracle_mod, prec):
         nl = np.full(2, ln.shape[1], dtype=np.int32)
         ra = a.localize(enc, ln, nl)
         rb = b.localize(enc, ln, nl)
-        b.download_state(0, with_P=False)          # drains b's pipeline every step
+        b.download_state(0, with_P=False)          # drains b after every step
+        if step in drain_at:
+            a.download_state(1, with_P=False)      # partial group flushed mid-trajectory
         m = ref.localize(ln[0], enc[0])
         assert ra[0]["match"] == rb[0]["match"] == m, (step, ra[0]["match"], m)
+        assert ra[1]["match"] == rb[1]["match"], step
         resets += ra[0]["reset"]
     assert resets >= 1
     for e in range(2):
@@ -173,9 +180,10 @@ def test_pipelined_equals_drained(ekf_mod, oracle_mod, prec):
         bad = np.argwhere(Pa != Pb)
         assert bad.size == 0, (e, bad[:12].tolist(), rel(Pa, Pb))
         np.testing.assert_array_equal(ya, yb)
+        np.testing.assert_array_equal(pa, pb)
         assert sa == sb
     if prec == 0:
-        check_same(a, ref, 0, where="pipelined fp64 trajectory")
+        check_same(a, ref, 0, where="deferred fp64 trajectory")
 
 
 @pytest.mark.parametrize("prec", [0, 1])
