@@ -9,9 +9,16 @@ RCCL/xGMI; every rank runs its slice of instances (no other collective on the da
 Inputs are resident in HBM before the timed region. `value` = instances × steps (all ranks)
 ÷ max-over-ranks wall time of the K timed steps.
 
-roofline: the dominant kernel is the packed rank-2m covariance downdate. Algorithmic bytes per
-launch = instances_per_gpu × n(n+1) × 4 (read + write of the packed symmetric P once, SURVEY.md
-§8d); its average duration comes from HIP events recorded on the stream it runs on.
+Schedule (defaults): the landmark block is flushed once per T = 4 scans (flush_interval) and the
+flush overlaps the next scans' association (pipeline); both are bit-identical to a per-scan
+in-place update (tests/test_gpu_parity.py::test_deferred_flush_equals_drained). The timed region
+ends with ekf_sync, which flushes the partial group: every step's downdate is in P.
+
+roofline: the dominant kernel is the covariance flush (rank-2m MFMA downdate of every step of the
+group, one read + write of the packed block). Per launch: algorithmic bytes = instances_per_gpu ×
+n(n+1) × 4, algorithmic flops = steps_per_launch × instances_per_gpu × 2m·n(n+1)
+(BASELINE.md §3). `bound` is whichever roof is the longer ideal time; its average duration comes
+from HIP events recorded on the stream the kernel runs on.
 cpu_baseline (rank 0, N=1 only): the CPU restatement (oracle/, fast mode, fp64, 1 thread) on a
 bounded sample of the same scans of instance 0; the same scans also give the per-scan parity
 numbers (‖P−P_ref‖_F/‖P_ref‖_F, state, association) from identical inputs.
@@ -31,22 +38,24 @@ sys.path.insert(0, ROOT)
 
 METRIC = "EKF updates/s at N=4096 landmarks, 1→8 MI355X; ‖P−P_ref‖_F rel-err"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: dense fp32 MFMA (v_mfma_f32_32x32x2_f32)
+MFMA_F64_PEAK_TFS = 78.6    # MI355X_MICROARCH.md: dense fp64 MFMA
 L_LINES = 8
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=48)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--capacity", type=int, default=4096)
     ap.add_argument("--instances", type=int, default=8, help="EKF instances per GPU")
     ap.add_argument("--precision", choices=["f32", "f64"], default="f32")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--pipeline", type=int, default=0,
-                    help="1: overlap step k's association with step k-1's downdate")
-    ap.add_argument("--flush-interval", type=int, default=1,
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="1: overlap the association kernels with the previous group's flush")
+    ap.add_argument("--flush-interval", type=int, default=4,
                     help="T: rewrite the landmark block once per T scans (bit-identical state)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return ap.parse_args()
@@ -151,14 +160,24 @@ def main():
 
     value = E_total * K / elapsed
     dd_ms = prof["downdate_ms"]
+    launches = max(1, prof["launches"])
+    steps_per_launch = K / launches
     alg_bytes = E * n * (n + 1) * bpe   # one read + write of the packed block per flush
-    achieved = alg_bytes / (dd_ms * 1e-3) / 1e9 if dd_ms > 0 else None
+    alg_flops = steps_per_launch * E * 2 * L_LINES * n * (n + 1)
+    mfma_peak = MFMA_F32_PEAK_TFS if prec == ekf.PREC_F32 else MFMA_F64_PEAK_TFS
+    t_hbm = alg_bytes / (HBM_PEAK_GBS * 1e9)
+    t_mfma = alg_flops / (mfma_peak * 1e12)
+    bound = "hbm" if t_hbm >= t_mfma else "mfma"
+    gbs = alg_bytes / (dd_ms * 1e-3) / 1e9 if dd_ms > 0 else None
+    tfs = alg_flops / (dd_ms * 1e-3) / 1e12 if dd_ms > 0 else None
     traffic = None
     traffic_src = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("capacity") == N and tj.get("instances") == E and tj.get("precision") == args.precision:
+            if (tj.get("capacity") == N and tj.get("instances") == E and tj.get("precision") == args.precision
+                    and tj.get("flush_interval") == args.flush_interval
+                    and tj.get("pipeline") == bool(args.pipeline)):
                 traffic = tj.get("hbm_bytes_per_launch")
                 traffic_src = os.path.relpath(args.traffic_json, ROOT)
         except Exception:
@@ -185,17 +204,22 @@ def main():
             "pipeline": bool(args.pipeline), "flush_interval": args.flush_interval,
         },
         "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "bound": bound,
+            "achieved": gbs if bound == "hbm" else tfs,
+            "peak": HBM_PEAK_GBS if bound == "hbm" else mfma_peak,
+            "unit": "GB/s" if bound == "hbm" else "TFLOP/s",
+            "frac": ((gbs / HBM_PEAK_GBS) if bound == "hbm" else (tfs / mfma_peak)) if dd_ms > 0 else None,
             "traffic": traffic,
-            "kernel": "downdate_f32_kernel" if prec == ekf.PREC_F32 else "downdate_f64_kernel",
+            "kernel": "flush_f32_sb_kernel" if prec == ekf.PREC_F32 else "downdate_f64_kernel",
             "alg_bytes_per_launch": alg_bytes,
+            "alg_flops_per_launch": alg_flops,
+            "steps_per_launch": steps_per_launch,
+            "hbm_gbs": gbs, "hbm_frac": (gbs / HBM_PEAK_GBS) if gbs else None,
+            "mfma_tflops": tfs, "mfma_frac": (tfs / mfma_peak) if tfs else None,
+            "ideal_ms": max(t_hbm, t_mfma) * 1e3,
             "traffic_source": traffic_src,
         },
-        "kernel_ms": {"scan": prof["scan_ms"], "downdate": dd_ms, "augment": prof["augment_ms"]},
+        "kernel_ms": {"scan": prof["scan_ms"], "flush": dd_ms, "flush_launches": prof["launches"]},
         "all_lines_matched": all_matched,
         "cpu_baseline": None,
     }

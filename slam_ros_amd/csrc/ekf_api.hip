@@ -53,6 +53,7 @@ struct ekf_ctx {
     double* Ust;              // fp64 gain scratch of the running scan
     double* Vst;
     int2* tile_rc;
+    int2* stile_rc;
     double* d_enc;
     ekf_line* d_lines;
     int* d_nlines;
@@ -127,7 +128,7 @@ int ekf_abi_version(void) { return SLAM_EKF_ABI_VERSION; }
 static void free_all(ekf_ctx* c)
 {
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->pose, c->xpre, c->saved, c->D,
-                               c->tile_rc, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->mbox,
+                               c->tile_rc, c->stile_rc, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->mbox,
                                c->sync, c->Ust, c->Vst};
     for (auto& sl : c->ring) {
         ptrs.push_back(sl.Uop);
@@ -252,6 +253,10 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         ALLOC(sl.res, sizeof(int) * ekf::RES_STRIDE * E);
     }
     ALLOC(c->tile_rc, sizeof(int2) * d.ntiles);
+    {
+        const int nsb = (d.nb + ekf::DD_SB - 1) / ekf::DD_SB;
+        ALLOC(c->stile_rc, sizeof(int2) * (size_t)nsb * (nsb + 1) / 2);
+    }
     ALLOC(c->d_enc, sizeof(double) * 3 * E);
     ALLOC(c->d_lines, sizeof(ekf_line) * d.max_lines * E);
     ALLOC(c->d_nlines, sizeof(int) * E);
@@ -281,6 +286,18 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
                 rcv[(size_t)ekf::tile_index(bi, bj, d.nb)] = v;
             }
         if (hipMemcpy(c->tile_rc, rcv.data(), sizeof(int2) * d.ntiles, hipMemcpyHostToDevice) !=
+            hipSuccess)
+            goto fail;
+        const int nsb = (d.nb + ekf::DD_SB - 1) / ekf::DD_SB;
+        std::vector<int2> srcv;
+        for (int bi = 0; bi < nsb; bi++)
+            for (int bj = bi; bj < nsb; bj++) {
+                int2 v;
+                v.x = bi;
+                v.y = bj;
+                srcv.push_back(v);
+            }
+        if (hipMemcpy(c->stile_rc, srcv.data(), sizeof(int2) * srcv.size(), hipMemcpyHostToDevice) !=
             hipSuccess)
             goto fail;
     }
@@ -437,6 +454,7 @@ static int enqueue_flush(ekf_ctx* c)
     dp.E = c->cfg.instances;
     dp.nsteps = nst;
     dp.tile_rc = c->tile_rc;
+    dp.stile_rc = c->stile_rc;
     for (int q = 0; q < nst; q++) dp.steps[q] = slot_of(c, c->unflushed0 + q);
     const int in = c->last_out;
     const int out = c->cfg.pipeline ? 1 - in : in;

@@ -45,7 +45,8 @@ struct Slot {
     int* res;           // [E][RES_STRIDE]
 };
 
-constexpr int PMAX = 32;   // pending steps (2 × flush_interval in pipeline mode)
+constexpr int PMAX = 32;
+constexpr int DD_SB = 4;   // f32 flush: tiles per super-tile side (one wave per tile row)   // pending steps (2 × flush_interval in pipeline mode)
 
 struct ScanParams {
     Dims d;
@@ -86,6 +87,7 @@ struct DowndateParams {
     const void* Pin;
     void* Pout;
     const int2* tile_rc;  // [ntiles] (bi, bj)
+    const int2* stile_rc; // [nsb(nsb+1)/2] (sbi, sbj) super-tiles of DD_SB × DD_SB tiles, sbi <= sbj
     Slot steps[PMAX];
 };
 

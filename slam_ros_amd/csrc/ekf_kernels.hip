@@ -886,92 +886,221 @@ __device__ __forceinline__ double patched_value(const double* prw0, const double
     return (li > lj) ? prw[(size_t)(i & 1) * M + j] : prw[(size_t)(j & 1) * M + i];
 }
 
-__global__ __launch_bounds__(DD_THREADS) void downdate_f32_kernel(DowndateParams p)
+// f32 flush on super-tiles: a workgroup owns DD_SB × DD_SB tiles (wave w: tile row
+// sbi·DD_SB + w, tile columns sbj·DD_SB + 0..3), keeps their 4 accumulators in registers for
+// the whole group of steps and stages each step's operands for the DD_SB row blocks and DD_SB
+// column blocks through LDS in chunks of 8 MFMA k-steps (double-buffered, one barrier per
+// chunk, next chunk prefetched into registers while the current one runs). Operand traffic
+// per tile and k-step falls from 512 B to 128 B; the MFMA chain per element is unchanged
+// (k-ordered within a step, steps in order), so results are bit-identical to the per-tile form.
+namespace {
+constexpr int SBK = 8;   // MFMA k-steps per staged chunk (2 float4 per lane per block)
+
+struct SbStep {
+    int reset, ks, nadd, s0;
+};
+
+__device__ __forceinline__ SbStep sb_step(const DowndateParams& p, int q, int e)
+{
+    const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
+    SbStep s;
+    s.reset = r[RES_RESET];
+    s.ks = s.reset ? 0 : r[RES_KSTEPS];
+    s.nadd = r[RES_NADD];
+    s.s0 = r[RES_SAVED_IN];
+    return s;
+}
+}  // namespace
+
+__global__ __launch_bounds__(DD_THREADS) void flush_f32_sb_kernel(DowndateParams p)
 {
     const Dims d = p.d;
+    const int nsb = (d.nb + DD_SB - 1) / DD_SB;
+    const int64_t nst = (int64_t)nsb * (nsb + 1) / 2;
+    const int64_t total = (int64_t)p.E * nst;
+    // XCD-aware order: the hardware deals workgroup b to XCD b mod 8; give every XCD a
+    // contiguous range of (instance, super-tile) so that its L2 holds one instance's operands
+    const int64_t per = (total + 7) / 8;
+    const int64_t g = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (g >= total) return;
+    const int e = (int)(g / nst);
+    const int2 sb = p.stile_rc[g - (int64_t)e * nst];
     const int lane = threadIdx.x & 63;
-    const int64_t nwaves = (int64_t)gridDim.x * (DD_THREADS / 64);
-    const int64_t total = (int64_t)p.E * d.ntiles;
-    const int kh = d.kmax / 2;   // operand floats per lane per row block
+    const int w = threadIdx.x >> 6;
+    const int bi = sb.x * DD_SB + w;
+    const int kh = d.kmax / 2;
     const size_t opstride = (size_t)d.nb * 64 * kh;
-    for (int64_t g = (int64_t)blockIdx.x * (DD_THREADS / 64) + (threadIdx.x >> 6); g < total;
-         g += nwaves) {
-        const int e = (int)(g / d.ntiles);
-        const int64_t t = g - (int64_t)e * d.ntiles;
-        const size_t toff = ((size_t)e * d.ntiles + t) * TILE_ELEMS;
-        const f32x4* src = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.Pin) + toff) + lane;
-        f32x4* dst = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.Pout) + toff) + lane;
-        // does any step of the group change this tile?
-        const int2 rc = p.tile_rc[t];
-        bool work = false;
-        for (int q = 0; q < p.nsteps; q++) {
-            const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
-            const int nadd = r[RES_NADD], s0 = r[RES_SAVED_IN];
-            work |= r[RES_RESET] || r[RES_KSTEPS] > 0 ||
-                    (nadd > 0 && rc.y * 16 + 15 >= s0 && rc.y * 16 < s0 + nadd);
-        }
-        if (!work) {
-            if (p.Pin != p.Pout) {   // unchanged tile of an out-of-place pass
+
+    // does any step change this super-tile? (uniform)
+    bool work = false;
+    for (int q = 0; q < p.nsteps; q++) {
+        const SbStep s = sb_step(p, q, e);
+        work |= s.reset || s.ks > 0 ||
+                (s.nadd > 0 && (sb.y + 1) * DD_SB * 16 > s.s0 && sb.y * DD_SB * 16 < s.s0 + s.nadd);
+    }
+    bool valid[DD_SB];
+    size_t toff[DD_SB];
+    int vmask = 0;
 #pragma unroll
-                for (int qq = 0; qq < 4; qq++)
-                    __builtin_nontemporal_store(__builtin_nontemporal_load(src + qq * 64), dst + qq * 64);
-            }
-            continue;
-        }
-        f32x16 acc;
+    for (int c = 0; c < DD_SB; c++) {
+        const int bj = sb.y * DD_SB + c;
+        valid[c] = bi < d.nb && bj < d.nb && bi <= bj;
+        vmask |= valid[c] << c;
+        toff[c] = valid[c] ? ((size_t)e * d.ntiles + tile_index(bi, bj, d.nb)) * TILE_ELEMS : 0;
+    }
+    const float* Pin = reinterpret_cast<const float*>(p.Pin);
+    float* Pout = reinterpret_cast<float*>(p.Pout);
+    if (!work) {
+        if (p.Pin != p.Pout) {
 #pragma unroll
-        for (int qq = 0; qq < 4; qq++) {
-            const f32x4 v = __builtin_nontemporal_load(src + qq * 64);
-            acc[4 * qq + 0] = v[0];
-            acc[4 * qq + 1] = v[1];
-            acc[4 * qq + 2] = v[2];
-            acc[4 * qq + 3] = v[3];
-        }
-        for (int q = 0; q < p.nsteps; q++) {
-            const Slot& sq = p.steps[q];
-            const int* r = sq.res + (size_t)e * RES_STRIDE;
-            if (r[RES_RESET]) {
+            for (int c = 0; c < DD_SB; c++)
+                if (valid[c]) {
+                    const f32x4* src = reinterpret_cast<const f32x4*>(Pin + toff[c]) + lane;
+                    f32x4* dst = reinterpret_cast<f32x4*>(Pout + toff[c]) + lane;
 #pragma unroll
-                for (int k = 0; k < 16; k++) acc[k] = 0.f;
-                continue;
-            }
-            const int ks = r[RES_KSTEPS];
-            if (ks > 0) {
-                const float* A = reinterpret_cast<const float*>(sq.Uop) + e * opstride +
-                                 ((size_t)rc.x * 64 + lane) * kh;
-                const float* B = reinterpret_cast<const float*>(sq.Vop) + e * opstride +
-                                 ((size_t)rc.y * 64 + lane) * kh;
-                for (int s0 = 0; s0 < ks; s0 += 8) {
-                    const f32x4 a0 = *reinterpret_cast<const f32x4*>(A + s0);
-                    const f32x4 a1 = *reinterpret_cast<const f32x4*>(A + s0 + 4);
-                    const f32x4 b0 = *reinterpret_cast<const f32x4*>(B + s0);
-                    const f32x4 b1 = *reinterpret_cast<const f32x4*>(B + s0 + 4);
-                    const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-                    const float bv[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-#pragma unroll
-                    for (int s = 0; s < 8; s++)
-                        if (s0 + s < ks) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
+                    for (int qq = 0; qq < 4; qq++)
+                        __builtin_nontemporal_store(__builtin_nontemporal_load(src + qq * 64), dst + qq * 64);
                 }
-            }
-            const int nadd = r[RES_NADD], s0 = r[RES_SAVED_IN];
-            if (nadd > 0 && rc.y * 16 + 15 >= s0 && rc.y * 16 < s0 + nadd) {
-                const double* prw0 = sq.patch + (size_t)e * d.max_lines * 2 * d.M;
-                const double* pdg = sq.patch_diag + (size_t)e * d.max_lines * 4;
-                const int col = rc.y * 32 + (lane & 31);
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    const int row = rc.x * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
-                    const int hi = max(row >> 1, col >> 1);
-                    if (hi >= s0 && hi < s0 + nadd) acc[k] = (float)patched_value(prw0, pdg, d.M, s0, row, col);
-                }
-            }
         }
+        return;
+    }
+    f32x16 acc[DD_SB];
 #pragma unroll
-        for (int qq = 0; qq < 4; qq++) {
-            const f32x4 v = {acc[4 * qq + 0], acc[4 * qq + 1], acc[4 * qq + 2], acc[4 * qq + 3]};
-            __builtin_nontemporal_store(v, dst + qq * 64);
+    for (int c = 0; c < DD_SB; c++) {
+        if (valid[c]) {
+            const f32x4* src = reinterpret_cast<const f32x4*>(Pin + toff[c]) + lane;
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) {
+                const f32x4 v = __builtin_nontemporal_load(src + qq * 64);
+                acc[c][4 * qq + 0] = v[0];
+                acc[c][4 * qq + 1] = v[1];
+                acc[c][4 * qq + 2] = v[2];
+                acc[c][4 * qq + 3] = v[3];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; k++) acc[c][k] = 0.f;
         }
     }
+
+    // [buf][A/B][block][s4][lane] float4: 2 × 2 × 4 × 2 × 64 × 16 B = 32 KB
+    __shared__ f32x4 lds[2][2][DD_SB][2][64];
+    // staging: thread t moves float4 i = t + 256 j (j < 4): lane, s4, block, A/B
+    auto fetch = [&](int q, int k0, f32x4 reg[4]) {
+        const float* U = reinterpret_cast<const float*>(p.steps[q].Uop) + e * opstride;
+        const float* V = reinterpret_cast<const float*>(p.steps[q].Vop) + e * opstride;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int i = threadIdx.x + 256 * j;
+            const int ln = i & 63, s4 = (i >> 6) & 1, blk = (i >> 7) & 3, ab = i >> 9;
+            const int rb = (ab ? sb.y : sb.x) * DD_SB + blk;
+            if (rb < d.nb) {
+                const float* src = (ab ? V : U) + ((size_t)rb * 64 + ln) * kh + k0 + 4 * s4;
+                reg[j] = *reinterpret_cast<const f32x4*>(src);
+            }
+        }
+    };
+    auto stage = [&](int buf, const f32x4 reg[4]) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int i = threadIdx.x + 256 * j;
+            const int ln = i & 63, s4 = (i >> 6) & 1, blk = (i >> 7) & 3, ab = i >> 9;
+            lds[buf][ab][blk][s4][ln] = reg[j];
+        }
+    };
+    // reset or augmented rows of step q, after its downdate
+    auto post = [&](int q) {
+        const SbStep s = sb_step(p, q, e);
+        if (s.reset) {
+#pragma unroll
+            for (int c = 0; c < DD_SB; c++)
+#pragma unroll
+                for (int k = 0; k < 16; k++) acc[c][k] = 0.f;
+            return;
+        }
+        if (s.nadd <= 0) return;
+        const double* prw0 = p.steps[q].patch + (size_t)e * d.max_lines * 2 * d.M;
+        const double* pdg = p.steps[q].patch_diag + (size_t)e * d.max_lines * 4;
+        // one tile at a time through acc[0], rotating the four accumulators (rare path: keeps
+        // a single copy of the per-element code and its registers)
+#pragma nounroll
+        for (int c = 0; c < DD_SB; c++) {
+            const int bj = sb.y * DD_SB + c;
+            if (((vmask >> c) & 1) && bj * 16 + 15 >= s.s0 && bj * 16 < s.s0 + s.nadd) {
+                const int col = bj * 32 + (lane & 31);
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
+                    const int hi = max(row >> 1, col >> 1);
+                    if (hi >= s.s0 && hi < s.s0 + s.nadd)
+                        acc[0][k] = (float)patched_value(prw0, pdg, d.M, s.s0, row, col);
+                }
+            }
+            const f32x16 t0 = acc[0];
+            acc[0] = acc[1];
+            acc[1] = acc[2];
+            acc[2] = acc[3];
+            acc[3] = t0;
+        }
+    };
+    // first chunk at or after step q (k0 = 0): steps without a downdate are passed through post
+    auto first_mfma = [&](int q) {
+        while (q < p.nsteps && sb_step(p, q, e).ks == 0) q++;
+        return q;
+    };
+
+    int q = first_mfma(0);
+    for (int t = 0; t < q; t++) post(t);
+    int k0 = 0, buf = 0;
+    f32x4 reg[4];
+    if (q < p.nsteps) fetch(q, 0, reg);
+    while (q < p.nsteps) {
+        const int ks = sb_step(p, q, e).ks;
+        const int kc = min(SBK, ks - k0);
+        stage(buf, reg);
+        __syncthreads();
+        // next chunk
+        int qn = q, kn = k0 + SBK;
+        if (kn >= ks) {
+            qn = first_mfma(q + 1);
+            kn = 0;
+        }
+        if (qn < p.nsteps) fetch(qn, kn, reg);
+        const f32x4 a0 = lds[buf][0][w][0][lane];
+        const f32x4 a1 = lds[buf][0][w][1][lane];
+        f32x4 b0[DD_SB], b1[DD_SB];
+#pragma unroll
+        for (int c = 0; c < DD_SB; c++) {
+            b0[c] = lds[buf][1][c][0][lane];
+            b1[c] = lds[buf][1][c][1][lane];
+        }
+        {
+#pragma unroll
+            for (int s = 0; s < SBK; s++)
+                if (s < kc) {
+#pragma unroll
+                    for (int c = 0; c < DD_SB; c++)
+                        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(s < 4 ? a0[s & 3] : a1[s & 3],
+                                                                      s < 4 ? b0[c][s & 3] : b1[c][s & 3],
+                                                                      acc[c], 0, 0, 0);
+                }
+        }
+        if (qn != q)
+            for (int t = q; t < qn && t < p.nsteps; t++) post(t);
+        q = qn;
+        k0 = kn;
+        buf ^= 1;
+    }
+#pragma unroll
+    for (int c = 0; c < DD_SB; c++)
+        if (valid[c]) {
+            f32x4* dst = reinterpret_cast<f32x4*>(Pout + toff[c]) + lane;
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) {
+                const f32x4 v = {acc[c][4 * qq + 0], acc[c][4 * qq + 1], acc[c][4 * qq + 2], acc[c][4 * qq + 3]};
+                __builtin_nontemporal_store(v, dst + qq * 64);
+            }
+        }
 }
 
 __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams p)
@@ -1180,10 +1309,14 @@ hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 
 hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st)
 {
-    if (precision == 0)
+    if (precision == 0) {
         hipLaunchKernelGGL(downdate_f64_kernel, dim3(grid), dim3(DD_THREADS), 0, st, p);
-    else
-        hipLaunchKernelGGL(downdate_f32_kernel, dim3(grid), dim3(DD_THREADS), 0, st, p);
+    } else {
+        const int64_t nsb = (p.d.nb + DD_SB - 1) / DD_SB;
+        const int64_t total = (int64_t)p.E * (nsb * (nsb + 1) / 2);
+        const int64_t sgrid = 8 * ((total + 7) / 8);
+        hipLaunchKernelGGL(flush_f32_sb_kernel, dim3((unsigned)sgrid), dim3(DD_THREADS), 0, st, p);
+    }
     return hipGetLastError();
 }
 
