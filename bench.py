@@ -71,7 +71,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from slam_ros_amd import ekf, scan_gen as G
+    from slam_ros_amd import dist as D, ekf, scan_gen as G
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -85,6 +85,8 @@ def main():
     prec = ekf.PREC_F32 if args.precision == "f32" else ekf.PREC_F64
     bpe = 4 if prec == ekf.PREC_F32 else 8
     E_total = E * world
+    first, count = D.shard(E_total, world, rank)
+    assert count == E
     n = 3 + 2 * N
 
     world_map = G.make_world(N)
@@ -99,14 +101,13 @@ def main():
 
     # ---- pre-generated scan payloads, resident in HBM (rank 0 is the sensor) ----
     steps_total = W + K
-    per_step = E_total * 3 + E_total * L_LINES * 6
+    per_step = D.payload_len(E_total, L_LINES)
     payload = torch.empty((steps_total, per_step), dtype=torch.float64, device=dev)
     if rank == 0:
         host = np.zeros((steps_total, per_step))
         for s in range(steps_total):
             enc, lines, _ = G.make_scan(world_map, s + 1, instances=E_total, lines=L_LINES)
-            host[s, : E_total * 3] = enc.ravel()
-            host[s, E_total * 3:] = lines.ravel()
+            host[s] = D.pack(enc, lines)
         payload.copy_(torch.from_numpy(host))
     recv = payload if world == 1 else torch.empty((2, per_step), dtype=torch.float64, device=dev)
     nlines = torch.full((E,), L_LINES, dtype=torch.int32, device=dev)
@@ -119,10 +120,11 @@ def main():
             buf = recv[s & 1]
             if rank == 0:
                 buf.copy_(payload[s], non_blocking=True)
-            dist.broadcast(buf, src=0)
+            D.broadcast_step(buf, dist, src=0)
         base = buf.data_ptr()
-        enc_ptr = base + (rank * E * 3) * 8
-        lines_ptr = base + (E_total * 3 + rank * E * L_LINES * 6) * 8
+        eo, lo = D.offsets(E_total, L_LINES, first)
+        enc_ptr = base + eo * 8
+        lines_ptr = base + lo * 8
         ens.localize_device(enc_ptr, lines_ptr, nlines.data_ptr())
 
     for s in range(W):

@@ -1,27 +1,26 @@
 // ekf_kernels.hip — gfx950 kernels of the EKF-SLAM update (slam_ros Robot::localize).
 //
 // Per scan (one "step"), all E ensemble instances at once:
-//   1. scan_kernel     (one 1024-thread workgroup per instance, stream S)
+//   1. scan_kernel (⌈N/256⌉ cooperating 256-thread workgroups per instance, stream S)
 //        predict of the robot strip (Robot.cpp:130-286: Fx = I outside rows 0..2), then for
 //        every observed line in order: Mahalanobis gating of all unmatched saved landmarks in
 //        parallel + min-index reduction (== the reference's first passing candidate,
 //        Robot.cpp:313-504); for a match the gain chain in deferred low-rank form
 //        (Robot.cpp:515-602): W_t = P_{t-1}·H_tᵀ, K_t = W_t·S_t⁻¹, U_t = K_t·S_t, y += K_t·v_t.
-//        Thread tid OWNS landmarks j ≡ tid (mod 1024): their gating, their two rows of W/K/U/y,
-//        their robot-strip columns and their 2×2 diagonal block. The robot 3×3 block and the
-//        pose are computed redundantly by every thread. Cross-thread traffic per line is the
-//        winner's candidate (LDS) and the matched landmark's columns (uniform loads), so a line
-//        costs two workgroup barriers. Landmark augmentation (Robot.cpp:776-866) runs at the end
-//        of the same kernel; its rows of the landmark block go to a patch buffer.
-//   2. downdate_kernel (grid-stride over E × packed 32×32 tiles, one tile per wave, stream D)
-//        X_k = X_{k-1} − Σ_t U_t·V_tᵀ (rank 2m) on MFMA, reading and writing each stored tile
-//        once: the reference's m dense n×n passes (Robot.cpp:560-572) fused into one. Also the
-//        capacity reset of the landmark block (Robot.cpp:893-904).
+//        Landmark augmentation (Robot.cpp:776-866) and the capacity reset decision
+//        (Robot.cpp:893-904) run at the end of the same kernel; the new landmarks' rows of the
+//        landmark block go to the step's slot (patch buffers), the rank-2m operands U/V to the
+//        slot's MFMA-ordered operand buffers.
+//   2. flush (stream D): one pass over the packed landmark block applying a group of T steps in
+//        order — per step X ← X − U_t·V_tᵀ (rank 2m on MFMA, the reference's m dense n×n passes
+//        of Robot.cpp:560-572 fused), then that step's augmented rows, or the reset. Each stored
+//        tile is read and written once per group. fp32: flush_f32_sb_kernel (super-tiles, LDS
+//        operands); fp64: downdate_f64_kernel (one tile per wave).
 //
-// Cross-scan pipelining: X ping-pongs between two buffers, so scan k can read X_{k-2} while
-// downdate k-1 writes X_{k-1}; scan k then applies step k-1's downdate itself, element by
-// element, as the same k-ordered fp32/fp64 FMA chain the MFMA executes (bit-identical to the
-// value downdate k-1 stores), plus step k-1's patch and reset.
+// Deferred reads: between flushes the association kernels read the landmark block with the
+// pending steps applied on read (pll_block): per element, the same k-ordered fp32/fp64 FMA chain
+// the MFMA executes, then the patch rounded to storage, so every read sees bit-for-bit the value
+// the flush will store (tests/test_gpu_parity.py::test_deferred_flush_equals_drained).
 #include <hip/hip_runtime.h>
 
 #include "ekf_kernels.h"
@@ -80,8 +79,7 @@ __device__ __forceinline__ void ll_store_sym(T* P, int i, int j, int nb, double 
 }
 
 // ---------------------------------------------------------------------------------------
-// Landmark block as seen by step k: X plus step k-1's pending downdate / patch / reset
-// (pipeline mode; in sequential mode pend_ks = pend_reset = pn = 0 and X is current).
+// Landmark block as seen by a step: X plus the pending (not yet flushed) steps, in order.
 // ---------------------------------------------------------------------------------------
 template <typename T>
 struct PllView {

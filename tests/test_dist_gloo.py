@@ -1,0 +1,104 @@
+"""Multi-rank path on CPU (gloo, world_size 2): the ensemble sharding and the per-step payload
+broadcast of slam_ros_amd/dist.py give every instance exactly the inputs — and therefore, through
+the CPU restatement, exactly the trajectory — of a single-process run. The GPU path of each rank
+is the same C-ABI call on its slice (bench.py); only the transport differs (RCCL vs gloo)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from slam_ros_amd import dist as D, scan_gen as G
+
+N, E_TOTAL, L, STEPS = 24, 5, 4, 4
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_instances(oracle, payloads, first, count):
+    w = G.make_world(N, active=N - 10)
+    st = G.initial_state(w)
+    out = []
+    for e in range(count):
+        ref = oracle.OracleRobot(N)
+        ref.set_state(st.dense_P(), st.y, st.saved, st.pose)
+        matches = []
+        for buf in payloads:
+            enc, lines = D.unpack_slice(buf, E_TOTAL, L, first, count)
+            matches.append(ref.localize(lines[e], enc[e]))
+        out.append(np.concatenate([ref.y, ref.pose, [float(sum(m >= 0 for ms in matches for m in ms))]]))
+    return np.array(out)
+
+
+def payload_stream():
+    w = G.make_world(N, active=N - 10)
+    return [D.pack(*G.make_scan(w, s + 1, instances=E_TOTAL, lines=L)[:2]) for s in range(STEPS)]
+
+
+def worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle
+    plen = D.payload_len(E_TOTAL, L)
+    src = payload_stream() if rank == 0 else None
+    got = []
+    for s in range(STEPS):
+        buf = torch.from_numpy(src[s].copy()) if rank == 0 else torch.empty(plen, dtype=torch.float64)
+        D.broadcast_step(buf, dist, src=0)
+        got.append(buf.numpy().copy())
+    first, count = D.shard(E_TOTAL, world, rank)
+    res = torch.from_numpy(run_instances(oracle, got, first, count))
+    # gather the slices (padded to the largest) on every rank
+    maxc = D.shard(E_TOTAL, world, 0)[1]
+    pad = torch.zeros((maxc, res.shape[1]), dtype=torch.float64)
+    pad[:count] = res
+    parts = [torch.zeros_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    if rank == 0:
+        rows = [parts[r][: D.shard(E_TOTAL, world, r)[1]] for r in range(world)]
+        q.put(torch.cat(rows).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_covers_all_instances():
+    for E in (1, 5, 8, 64):
+        for world in (1, 2, 3, 8):
+            spans = [D.shard(E, world, r) for r in range(world)]
+            assert sum(c for _, c in spans) == E
+            assert all(spans[r][0] + spans[r][1] == spans[r + 1][0] for r in range(world - 1))
+            assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+
+
+def test_payload_roundtrip():
+    w = G.make_world(N, active=N - 10)
+    enc, lines, _ = G.make_scan(w, 3, instances=E_TOTAL, lines=L)
+    buf = D.pack(enc, lines)
+    assert buf.size == D.payload_len(E_TOTAL, L)
+    for first, count in [(0, 2), (2, 3), (4, 1)]:
+        e, l = D.unpack_slice(buf, E_TOTAL, L, first, count)
+        np.testing.assert_array_equal(e, enc[first:first + count])
+        np.testing.assert_array_equal(l, lines[first:first + count])
+
+
+def test_two_rank_broadcast_sharding_matches_single_process(oracle_mod):
+    port = free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    sharded = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    single = run_instances(oracle_mod, payload_stream(), 0, E_TOTAL)
+    np.testing.assert_array_equal(sharded, single)
+    assert single[:, -1].min() > 0     # the instances did associate lines
