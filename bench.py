@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--precision", choices=["f32", "f64"], default="f32")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--pipeline", type=int, default=1,
+    ap.add_argument("--pipeline", type=int, default=0,
                     help="1: overlap the association kernels with the previous group's flush")
     ap.add_argument("--flush-interval", type=int, default=4,
                     help="T: rewrite the landmark block once per T scans (bit-identical state)")

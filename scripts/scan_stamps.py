@@ -4,10 +4,11 @@ os.environ["EKF_SCAN_STAMPS"] = "1"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from slam_ros_amd import ekf, scan_gen as G
 N = int(os.environ.get("N", 4096)); E = 8
-names = ["predict", "diag+barrier", "gating", "reduce-barrier", "winner", "bcast-barrier",
+names = ["predict", "diag", "gating", "mailbox-write", "exchange", "unused",
          "gain-rows", "commit", "total"]
+T = int(os.environ.get("T", 1)); PIPE = int(os.environ.get("PIPE", 0))
 w = G.make_world(N); st = G.initial_state(w)
-ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8)
+ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8, pipeline=bool(PIPE), flush_interval=T)
 for e in range(E):
     ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
 for s in range(1, 11):
@@ -15,4 +16,4 @@ for s in range(1, 11):
     r = ens.localize(enc, lines, nl)
 st_ = ens.scan_stamps()
 launches = st_[9] or 1
-print(json.dumps({k: st_[i] * 10e-3 / launches for i, k in enumerate(names)}))  # µs per launch (per instance)
+print(T, PIPE, json.dumps({k: round(st_[i] * 10e-3 / launches, 2) for i, k in enumerate(names)}))  # µs per launch (per instance)

@@ -60,9 +60,12 @@ struct ekf_ctx {
     int* h_res;
     double* h_pose;
     int dd_grid;
+    int dd_variant;           // f32 flush kernel form (EKF_FLUSH_VARIANT)
+    int ncu;
     int G;                    // association workgroups per instance
     int mbw;                  // mailbox words per workgroup slot
     int scan_batch;           // instances per association launch (co-residency bound)
+    unsigned scan_epoch;      // association launches so far (mailbox tags)
     double* mbox;
     int* sync;
     unsigned long long* dbg;  // association-kernel phase timers (EKF_SCAN_STAMPS=1)
@@ -308,6 +311,8 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         if (getenv("EKF_DD_BLOCKS_PER_CU")) dd_per_cu = atoi(getenv("EKF_DD_BLOCKS_PER_CU"));
         if (dd_per_cu < 1) dd_per_cu = 1;
         c->dd_grid = prop.multiProcessorCount * dd_per_cu;
+        c->ncu = prop.multiProcessorCount;
+        c->dd_variant = getenv("EKF_FLUSH_VARIANT") ? atoi(getenv("EKF_FLUSH_VARIANT")) : 0;
         // all G workgroups of an instance must be co-resident (they exchange per line): bound
         // the instances per association launch by the occupancy the hardware admits, less one
         // workgroup per CU of margin (MI355X_MICROARCH.md: the API can over-report by one)
@@ -428,6 +433,7 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
 static hipError_t launch_scans(ekf_ctx* c, ekf::ScanParams sp)
 {
     const int E = c->cfg.instances;
+    sp.epoch = ++c->scan_epoch;
     hipError_t err = hipMemsetAsync(c->sync, 0, sizeof(int) * ekf::SYNC_WORDS * E, c->stream);
     for (int e0 = 0; err == hipSuccess && e0 < E; e0 += c->scan_batch) {
         sp.e0 = e0;
@@ -453,6 +459,8 @@ static int enqueue_flush(ekf_ctx* c)
     dp.d = c->d;
     dp.E = c->cfg.instances;
     dp.nsteps = nst;
+    dp.variant = c->dd_variant;
+    dp.ncu = c->ncu;
     dp.tile_rc = c->tile_rc;
     dp.stile_rc = c->stile_rc;
     for (int q = 0; q < nst; q++) dp.steps[q] = slot_of(c, c->unflushed0 + q);

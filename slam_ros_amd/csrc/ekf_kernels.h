@@ -13,7 +13,7 @@ enum { EKF_ST_SINGULAR = EKF_ST_SINGULAR_S, EKF_ST_CAP = EKF_ST_CAPACITY, EKF_ST
        EKF_ST_TIMEOUT_BIT = EKF_ST_SYNC_TIMEOUT };
 
 // per-instance synchronisation words of the association kernel (zeroed before every launch)
-enum { SYNC_ARRIVE = 0, SYNC_STATUS = 1, SYNC_START = 2, SYNC_WORDS = 4 };
+enum { SYNC_STATUS = 1, SYNC_START = 2, SYNC_WORDS = 4 };
 constexpr int MAX_GROUPS = 128;   // workgroups per instance (N <= 128 × 256)
 constexpr int MB_WORDS_FIXED = 26; // mailbox words before the V-history (see ekf_kernels.hip)
 
@@ -60,6 +60,7 @@ struct ScanParams {
     int r_mode;
     int reset_margin;
     int npend;            // steps not yet in Pread, applied on read (in order)
+    unsigned epoch;       // launch sequence number: tags the mailbox words of this launch
     double gate;
     double enc_noise;
     const void* Pread;    // [E][ntiles][1024] landmark block to read
@@ -84,6 +85,8 @@ struct DowndateParams {
     Dims d;
     int E;
     int nsteps;
+    int variant;          // f32 flush form: 0 auto (persistent when it applies), 1 16-wave, 2 super-tile
+    int ncu;              // compute units (persistent grid)
     const void* Pin;
     void* Pout;
     const int2* tile_rc;  // [ntiles] (bi, bj)

@@ -89,6 +89,7 @@ struct PllView {
     size_t opstride;  // operand elements per instance
     int npend;        // pending steps (oldest first)
     const Slot* pend;
+    const int4* ctl;  // per pending step {reset, ks, nadd, s0} of instance e (LDS copy)
 };
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
@@ -108,12 +109,12 @@ __device__ __forceinline__ void pll_block(const PllView<T>& v, int i0, int j0, d
         for (int c = 0; c < 2; c++) acc[p * 2 + c] = v.X[ll_offset<T>(a0 + p, b0 + c, v.nb)];
     for (int q = 0; q < v.npend; q++) {
         const Slot& sq = v.pend[q];
-        const int* r = sq.res + (size_t)v.e * RES_STRIDE;
-        if (r[RES_RESET]) {
+        const int4 cw = v.ctl[q];
+        if (cw.x) {
             acc[0] = acc[1] = acc[2] = acc[3] = (T)0;
             continue;
         }
-        const int ks = r[RES_KSTEPS];
+        const int ks = cw.y;
         if (ks > 0) {
             if constexpr (sizeof(T) == 4) {
                 // v_mfma_f32_32x32x2_f32 = ordered fmaf chain (k0 lanes 0-31, then k1)
@@ -160,9 +161,9 @@ __device__ __forceinline__ void pll_block(const PllView<T>& v, int i0, int j0, d
                     }
             }
         }
-        const int nadd = r[RES_NADD];
+        const int nadd = cw.z;
         if (nadd > 0) {
-            const int s0 = r[RES_SAVED_IN];
+            const int s0 = cw.w;
             const int li = i0 >> 1, lj = j0 >> 1;
             const int hi = li > lj ? li : lj;
             if (hi >= s0 && hi < s0 + nadd) {
@@ -421,6 +422,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     __shared__ int sh_red[SCAN_THREADS / 64];
     __shared__ int sh_best[MAX_GROUPS];
     __shared__ int sh_extra[EKF_MAX_LINES];
+    __shared__ int4 sh_ctl[PMAX];
     unsigned long long* dbg = (p.dbg && lead) ? p.dbg + (size_t)e * 16 : nullptr;
     unsigned long long t_last = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const unsigned long long t_first = t_last;
@@ -529,6 +531,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     pv.opstride = opstride;
     pv.npend = p.npend;
     pv.pend = p.pend;
+    pv.ctl = sh_ctl;
+    if (tid < p.npend) {
+        const int* r = p.pend[tid].res + (size_t)e * RES_STRIDE;
+        sh_ctl[tid] = make_int4(r[RES_RESET], r[RES_KSTEPS], r[RES_NADD], r[RES_SAVED_IN]);
+    }
 
     int L = p.nlines[e];
     L = L < 0 ? 0 : (L > d.max_lines ? d.max_lines : L);
@@ -611,27 +618,33 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
                 mb_store(slot + MB_VH + 4 * q + 3, vq.w);
             }
         }
-        if (tid == 0) mb_store(slot + MB_BEST, gbest == 0x7fffffff ? -1.0 : (double)gbest);
+        // the package is drained by its writer and ordered by the barrier before the tagged best
+        // word (data-tagged granule: launch epoch, line, best); every workgroup polls all G words
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        // tag: bits 63..32 launch epoch, 31..24 line + 1, 23..0 best + 1 (0: no candidate)
+        const unsigned long long want = ((unsigned long long)p.epoch << 8) | (unsigned)(i + 1);
+        if (tid == 0)
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(slot + MB_BEST),
+                               (want << 24) | (unsigned)(gbest == 0x7fffffff ? 0 : gbest + 1),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         EKF_STAMP(3);
-        if (tid == 0) {
-            __hip_atomic_fetch_add(&sync[SYNC_ARRIVE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int target = G * (i + 1);
+        for (int k = tid; k < G; k += SCAN_THREADS) {
+            const unsigned long long* tw =
+                reinterpret_cast<const unsigned long long*>(mbox + ((size_t)par * G + k) * p.mbw + MB_BEST);
+            unsigned long long v = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             int polls = 0;
-            while (__hip_atomic_load(&sync[SYNC_ARRIVE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            while ((v >> 24) != want) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++polls > (1 << 24)) {   // ~seconds: a workgroup never arrived
                     __hip_atomic_fetch_or(&sync[SYNC_STATUS], EKF_ST_TIMEOUT_BIT, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
+                v = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-        }
-        __syncthreads();
-        if (tid < G) {
-            const double bv = mb_load(mbox + ((size_t)par * G + tid) * p.mbw + MB_BEST);
-            sh_best[tid] = bv < 0.0 ? 0x7fffffff : (int)bv;
+            const int b = (int)(v & 0xffffffu);
+            sh_best[k] = b == 0 ? 0x7fffffff : b - 1;
         }
         __syncthreads();
         int jstar = 0x7fffffff, gstar = 0;
@@ -1101,6 +1114,363 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_sb_kernel(DowndateParams
         }
 }
 
+// f32 flush, 16-wave form: a 1024-thread workgroup owns the same DD_SB × DD_SB super-tile, one
+// tile per wave (one accumulator, ~64 VGPRs) so that 8 waves per SIMD interleave the HBM
+// streaming of some tiles with the MFMA chains of others. Operand staging as above (one float4
+// per thread per chunk); waves whose tile lies below the diagonal only stage.
+constexpr int SB16_THREADS = 1024;
+
+__global__ __launch_bounds__(SB16_THREADS, 8) void flush_f32_sb16_kernel(DowndateParams p)
+{
+    const Dims d = p.d;
+    const int nsb = (d.nb + DD_SB - 1) / DD_SB;
+    const int64_t nst = (int64_t)nsb * (nsb + 1) / 2;
+    const int64_t total = (int64_t)p.E * nst;
+    const int64_t per = (total + 7) / 8;
+    const int64_t g = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (g >= total) return;
+    const int e = (int)(g / nst);
+    const int2 sb = p.stile_rc[g - (int64_t)e * nst];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int tr = w >> 2, tc = w & 3;
+    const int bi = sb.x * DD_SB + tr, bj = sb.y * DD_SB + tc;
+    const bool valid = bi < d.nb && bj < d.nb && bi <= bj;
+    const int kh = d.kmax / 2;
+    const size_t opstride = (size_t)d.nb * 64 * kh;
+
+    bool work = false;
+    for (int q = 0; q < p.nsteps; q++) {
+        const SbStep s = sb_step(p, q, e);
+        work |= s.reset || s.ks > 0 ||
+                (s.nadd > 0 && (sb.y + 1) * DD_SB * 16 > s.s0 && sb.y * DD_SB * 16 < s.s0 + s.nadd);
+    }
+    const size_t toff = valid ? ((size_t)e * d.ntiles + tile_index(bi, bj, d.nb)) * TILE_ELEMS : 0;
+    const f32x4* src = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.Pin) + toff) + lane;
+    f32x4* dst = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.Pout) + toff) + lane;
+    if (!work) {
+        if (p.Pin != p.Pout && valid) {
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++)
+                __builtin_nontemporal_store(__builtin_nontemporal_load(src + qq * 64), dst + qq * 64);
+        }
+        return;
+    }
+    f32x16 acc;
+#pragma unroll
+    for (int k = 0; k < 16; k++) acc[k] = 0.f;
+    if (valid) {
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) {
+            const f32x4 v = __builtin_nontemporal_load(src + qq * 64);
+            acc[4 * qq + 0] = v[0];
+            acc[4 * qq + 1] = v[1];
+            acc[4 * qq + 2] = v[2];
+            acc[4 * qq + 3] = v[3];
+        }
+    }
+    __shared__ f32x4 lds[2][2][DD_SB][2][64];
+    const int ln = threadIdx.x & 63, s4 = (threadIdx.x >> 6) & 1, blk = (threadIdx.x >> 7) & 3,
+              ab = threadIdx.x >> 9;
+    const int rb = (ab ? sb.y : sb.x) * DD_SB + blk;
+    auto fetch = [&](int q, int k0) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (rb < d.nb) {
+            const float* base = reinterpret_cast<const float*>(ab ? p.steps[q].Vop : p.steps[q].Uop) + e * opstride;
+            v = *reinterpret_cast<const f32x4*>(base + ((size_t)rb * 64 + ln) * kh + k0 + 4 * s4);
+        }
+        return v;
+    };
+    auto post = [&](int q) {
+        const SbStep s = sb_step(p, q, e);
+        if (s.reset) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) acc[k] = 0.f;
+            return;
+        }
+        if (s.nadd <= 0 || !valid || bj * 16 + 15 < s.s0 || bj * 16 >= s.s0 + s.nadd) return;
+        const double* prw0 = p.steps[q].patch + (size_t)e * d.max_lines * 2 * d.M;
+        const double* pdg = p.steps[q].patch_diag + (size_t)e * d.max_lines * 4;
+        const int col = bj * 32 + (lane & 31);
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
+            const int hi = max(row >> 1, col >> 1);
+            if (hi >= s.s0 && hi < s.s0 + s.nadd)
+                acc[k] = (float)patched_value(prw0, pdg, d.M, s.s0, row, col);
+        }
+    };
+    auto first_mfma = [&](int q) {
+        while (q < p.nsteps && sb_step(p, q, e).ks == 0) q++;
+        return q;
+    };
+
+    int q = first_mfma(0);
+    for (int t = 0; t < q; t++) post(t);
+    int k0 = 0, buf = 0;
+    f32x4 reg = {0.f, 0.f, 0.f, 0.f};
+    if (q < p.nsteps) reg = fetch(q, 0);
+    while (q < p.nsteps) {
+        const int ks = sb_step(p, q, e).ks;
+        const int kc = min(SBK, ks - k0);
+        lds[buf][ab][blk][s4][ln] = reg;
+        __syncthreads();
+        int qn = q, kn = k0 + SBK;
+        if (kn >= ks) {
+            qn = first_mfma(q + 1);
+            kn = 0;
+        }
+        if (qn < p.nsteps) reg = fetch(qn, kn);
+        if (valid) {
+            const f32x4 a0 = lds[buf][0][tr][0][lane];
+            const f32x4 a1 = lds[buf][0][tr][1][lane];
+            const f32x4 b0 = lds[buf][1][tc][0][lane];
+            const f32x4 b1 = lds[buf][1][tc][1][lane];
+#pragma unroll
+            for (int s = 0; s < SBK; s++)
+                if (s < kc)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s < 4 ? a0[s & 3] : a1[s & 3],
+                                                               s < 4 ? b0[s & 3] : b1[s & 3], acc, 0, 0, 0);
+        }
+        if (qn != q)
+            for (int t = q; t < qn && t < p.nsteps; t++) post(t);
+        q = qn;
+        k0 = kn;
+        buf ^= 1;
+    }
+    if (valid) {
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) {
+            const f32x4 v = {acc[4 * qq + 0], acc[4 * qq + 1], acc[4 * qq + 2], acc[4 * qq + 3]};
+            __builtin_nontemporal_store(v, dst + qq * 64);
+        }
+    }
+}
+
+// f32 flush, persistent software-pipelined form: one 4-wave workgroup per CU walks a range of
+// super-tiles; while it runs the MFMA chains of super-tile k, the operands and the tiles of
+// super-tile k+1 are already in flight into registers (operands first, tiles second, so that
+// the in-order vmcnt lets the operand wait pass while the tiles still stream). Operands are
+// staged to a double-buffered LDS image once per super-tile (every chunk of the group), one raw
+// barrier per super-tile. All per-super-tile control (instance, super-tile, step records) is
+// wave-uniform and read with scalar loads, so no vector-memory wait sits between issuing the
+// prefetch and the MFMA work. Used when a group has at most PST_MAXC steps and kmax <= 16 (one
+// chunk per step); otherwise flush_f32_sb_kernel runs. Per element the chain is the same as in
+// the other forms: bit-identical results.
+constexpr int PST_MAXC = 4;
+
+// scalar (constant address space) load of a wave-uniform word that no kernel of this launch
+// writes: keeps the control words on lgkmcnt, out of the vmcnt queue the prefetch occupies
+template <typename T>
+__device__ __forceinline__ T sload(const T* ptr)
+{
+    return *(const __attribute__((address_space(4))) T*)(ptr);
+}
+
+struct PstInfo {
+    int e, sbi, sbj;
+    int reset[PST_MAXC], ks[PST_MAXC], nadd[PST_MAXC], s0[PST_MAXC];
+};
+
+__device__ __forceinline__ void pst_info(const DowndateParams& p, int gg, int nst, PstInfo& t)
+{
+    t.e = __builtin_amdgcn_readfirstlane(gg / nst);
+    const int li = __builtin_amdgcn_readfirstlane(gg - t.e * nst);
+    const int* rc = reinterpret_cast<const int*>(p.stile_rc + li);
+    t.sbi = sload(rc);
+    t.sbj = sload(rc + 1);
+#pragma unroll
+    for (int q = 0; q < PST_MAXC; q++) {
+        t.reset[q] = 0;
+        t.ks[q] = 0;
+        t.nadd[q] = 0;
+        t.s0[q] = 0;
+        if (q < p.nsteps) {
+            const int* r = p.steps[q].res + (size_t)t.e * RES_STRIDE;
+            t.reset[q] = sload(r + RES_RESET);
+            t.ks[q] = t.reset[q] ? 0 : sload(r + RES_KSTEPS);
+            t.nadd[q] = sload(r + RES_NADD);
+            t.s0[q] = sload(r + RES_SAVED_IN);
+        }
+    }
+}
+
+__global__ __launch_bounds__(DD_THREADS) void flush_f32_persist_kernel(DowndateParams p)
+{
+    const Dims d = p.d;
+    const int nsb = (d.nb + DD_SB - 1) / DD_SB;
+    const int nst = nsb * (nsb + 1) / 2;
+    const int total = p.E * nst;
+    // XCD-aware ranges: workgroup b runs on XCD b mod 8 and walks that XCD's contiguous range
+    const int per = (total + 7) / 8;
+    const int xcd = blockIdx.x & 7;
+    const int wpx = gridDim.x >> 3;
+    const int g_end = min(total, (xcd + 1) * per);
+    int g = xcd * per + (blockIdx.x >> 3);
+    if (g >= g_end) return;
+
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int kh = d.kmax / 2;
+    const size_t opstride = (size_t)d.nb * 64 * kh;
+    const float* Pin = reinterpret_cast<const float*>(p.Pin);
+    float* Pout = reinterpret_cast<float*>(p.Pout);
+    // this thread's staging slot: float4 i = tid + 256 j of a chunk
+    auto tile_off = [&](const PstInfo& t, int c, bool& valid) {
+        const int bi = t.sbi * DD_SB + w, bj = t.sbj * DD_SB + c;
+        valid = bi < d.nb && bj < d.nb && bi <= bj;
+        return valid ? ((size_t)t.e * d.ntiles + tile_index(bi, bj, d.nb)) * TILE_ELEMS : (size_t)0;
+    };
+    // unconditional loads (absent steps re-read step 0's operands) keep the prefetched values
+    // in the registers the next iteration reads: no copy, so no early vmcnt(0) at the back edge
+    auto fetch = [&](const PstInfo& t, f32x4 opreg[PST_MAXC][4], f32x4 pref[DD_SB][4]) {
+#pragma unroll
+        for (int c = 0; c < PST_MAXC; c++) {
+            const int qc = t.ks[c] > 0 ? c : 0;
+            const float* U = reinterpret_cast<const float*>(p.steps[qc].Uop) + t.e * opstride;
+            const float* V = reinterpret_cast<const float*>(p.steps[qc].Vop) + t.e * opstride;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int i = threadIdx.x + 256 * j;
+                const int ln = i & 63, s4 = (i >> 6) & 1, blk = (i >> 7) & 3, ab = i >> 9;
+                const int rb = min((ab ? t.sbj : t.sbi) * DD_SB + blk, d.nb - 1);   // past the block: unused
+                opreg[c][j] = *reinterpret_cast<const f32x4*>((ab ? V : U) + ((size_t)rb * 64 + ln) * kh + 4 * s4);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < DD_SB; c++) {
+            bool v;
+            const f32x4* src = reinterpret_cast<const f32x4*>(Pin + tile_off(t, c, v)) + lane;
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) pref[c][qq] = __builtin_nontemporal_load(src + qq * 64);
+        }
+    };
+
+    __shared__ f32x4 lds[2][PST_MAXC][2][DD_SB][2][64];   // 128 KB
+
+    PstInfo cur;
+    pst_info(p, g, nst, cur);
+    f32x4 opreg[PST_MAXC][4];
+    f32x4 pref[DD_SB][4];
+    fetch(cur, opreg, pref);
+    int buf = 0;
+    f32x16 acc[DD_SB];
+
+    while (true) {
+#pragma unroll
+        for (int c = 0; c < PST_MAXC; c++) {
+            if (cur.ks[c] > 0) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int i = threadIdx.x + 256 * j;
+                    lds[buf][c][i >> 9][(i >> 7) & 3][(i >> 6) & 1][i & 63] = opreg[c][j];
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+        for (int c = 0; c < DD_SB; c++)
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) {
+                acc[c][4 * qq + 0] = pref[c][qq][0];
+                acc[c][4 * qq + 1] = pref[c][qq][1];
+                acc[c][4 * qq + 2] = pref[c][qq][2];
+                acc[c][4 * qq + 3] = pref[c][qq][3];
+            }
+        const int gn = g + wpx;
+        const bool more = gn < g_end;
+        PstInfo nxt;
+        pst_info(p, more ? gn : g, nst, nxt);   // the last iteration re-reads its own super-tile
+        fetch(nxt, opreg, pref);
+
+        const int e = cur.e;
+        const int bi = cur.sbi * DD_SB + w;
+        int vmask = 0;
+#pragma unroll
+        for (int c = 0; c < DD_SB; c++) {
+            bool v;
+            (void)tile_off(cur, c, v);
+            vmask |= (int)v << c;
+        }
+        auto post = [&](int q) {
+            if (cur.reset[q]) {
+#pragma unroll
+                for (int c = 0; c < DD_SB; c++)
+#pragma unroll
+                    for (int k = 0; k < 16; k++) acc[c][k] = 0.f;
+                return;
+            }
+            const int nadd = cur.nadd[q], s0 = cur.s0[q];
+            if (nadd <= 0 || (cur.sbj + 1) * DD_SB * 16 <= s0 || cur.sbj * DD_SB * 16 >= s0 + nadd) return;
+            const double* prw0 = p.steps[q].patch + (size_t)e * d.max_lines * 2 * d.M;
+            const double* pdg = p.steps[q].patch_diag + (size_t)e * d.max_lines * 4;
+#pragma nounroll
+            for (int c = 0; c < DD_SB; c++) {
+                const int bj = cur.sbj * DD_SB + c;
+                if (((vmask >> c) & 1) && bj * 16 + 15 >= s0 && bj * 16 < s0 + nadd) {
+                    const int col = bj * 32 + (lane & 31);
+#pragma unroll
+                    for (int k = 0; k < 16; k++) {
+                        const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
+                        const int hi = max(row >> 1, col >> 1);
+                        if (hi >= s0 && hi < s0 + nadd)
+                            acc[0][k] = (float)patched_value(prw0, pdg, d.M, s0, row, col);
+                    }
+                }
+                const f32x16 t0 = acc[0];
+                acc[0] = acc[1];
+                acc[1] = acc[2];
+                acc[2] = acc[3];
+                acc[3] = t0;
+            }
+        };
+        // the group's steps in order: a chunk of MFMA k-steps, then the step's rows / reset
+#pragma unroll
+        for (int q = 0; q < PST_MAXC; q++) {
+            if (q >= p.nsteps) break;
+            const int kc = cur.ks[q];
+            if (kc > 0) {
+                const int c = q;
+                const f32x4 a0 = lds[buf][c][0][w][0][lane];
+                const f32x4 a1 = lds[buf][c][0][w][1][lane];
+                f32x4 b0[DD_SB], b1[DD_SB];
+#pragma unroll
+                for (int cc = 0; cc < DD_SB; cc++) {
+                    b0[cc] = lds[buf][c][1][cc][0][lane];
+                    b1[cc] = lds[buf][c][1][cc][1][lane];
+                }
+#pragma unroll
+                for (int s = 0; s < SBK; s++)
+                    if (s < kc) {
+#pragma unroll
+                        for (int cc = 0; cc < DD_SB; cc++)
+                            acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(s < 4 ? a0[s & 3] : a1[s & 3],
+                                                                           s < 4 ? b0[cc][s & 3] : b1[cc][s & 3],
+                                                                           acc[cc], 0, 0, 0);
+                    }
+            }
+            post(q);
+        }
+#pragma unroll
+        for (int c = 0; c < DD_SB; c++) {
+            bool v;
+            const size_t off = tile_off(cur, c, v);
+            if (v) {
+                f32x4* dst = reinterpret_cast<f32x4*>(Pout + off) + lane;
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) {
+                    const f32x4 o = {acc[c][4 * qq + 0], acc[c][4 * qq + 1], acc[c][4 * qq + 2], acc[c][4 * qq + 3]};
+                    __builtin_nontemporal_store(o, dst + qq * 64);
+                }
+            }
+        }
+        if (!more) break;
+        g = gn;
+        cur = nxt;
+        buf ^= 1;
+    }
+}
+
 __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams p)
 {
     const Dims d = p.d;
@@ -1313,7 +1683,15 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
         const int64_t nsb = (p.d.nb + DD_SB - 1) / DD_SB;
         const int64_t total = (int64_t)p.E * (nsb * (nsb + 1) / 2);
         const int64_t sgrid = 8 * ((total + 7) / 8);
-        hipLaunchKernelGGL(flush_f32_sb_kernel, dim3((unsigned)sgrid), dim3(DD_THREADS), 0, st, p);
+        const bool persist_ok = p.nsteps <= PST_MAXC && p.d.kmax <= 16;
+        if (p.variant == 1)
+            hipLaunchKernelGGL(flush_f32_sb16_kernel, dim3((unsigned)sgrid), dim3(SB16_THREADS), 0, st, p);
+        else if (p.variant == 2 || !persist_ok)
+            hipLaunchKernelGGL(flush_f32_sb_kernel, dim3((unsigned)sgrid), dim3(DD_THREADS), 0, st, p);
+        else {
+            const int pgrid = 8 * ((p.ncu + 7) / 8);   // one workgroup per CU (128 KB LDS)
+            hipLaunchKernelGGL(flush_f32_persist_kernel, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+        }
     }
     return hipGetLastError();
 }
