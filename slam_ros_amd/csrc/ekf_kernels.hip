@@ -346,6 +346,8 @@ __device__ __forceinline__ bool certified_reject(const Block5& b, double ma, dou
         }                                                                       \
     } while (0)
 
+constexpr int HIST_LDS = 8;   // matches per scan whose owned U rows stay in LDS
+
 __device__ __forceinline__ int wave_min(int v)
 {
 #pragma unroll
@@ -423,6 +425,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     __shared__ int sh_best[MAX_GROUPS];
     __shared__ int sh_extra[EKF_MAX_LINES];
     __shared__ int4 sh_ctl[PMAX];
+    __shared__ ekf_line sh_lines[EKF_MAX_LINES];
+    // U_q rows of the owned landmark for the first HIST_LDS matches of the scan (the rest in Ust)
+    __shared__ double4 sh_uhist[HIST_LDS][SCAN_THREADS];
     unsigned long long* dbg = (p.dbg && lead) ? p.dbg + (size_t)e * 16 : nullptr;
     unsigned long long t_last = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const unsigned long long t_first = t_last;
@@ -541,6 +546,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     L = L < 0 ? 0 : (L > d.max_lines ? d.max_lines : L);
     const int s = p.saved[e];
     const ekf_line* lines = p.lines + (size_t)e * d.max_lines;
+    for (int k = tid; k < L * 6; k += SCAN_THREADS)
+        reinterpret_cast<double*>(sh_lines)[k] = reinterpret_cast<const double*>(lines)[k];
     // all per-instance inputs that the lead rewrites at the end (robot 3×3, pose, saved) are read
     signal_started(sync, tid);
 
@@ -551,7 +558,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     bool matched = false;
     int m = 0, nextra = 0, status = 0;
     for (int i = 0; i < L; ++i) {
-        const ekf_line ln = lines[i];
+        const ekf_line ln = sh_lines[i];
         double Rm[4] = {0, 0, 0, 0};
         if (p.r_mode == 1) {
             if (i < 4) Rm[i] = ln.R[3];   // Robot.cpp:302-304 as written (zero-initialised stack)
@@ -685,7 +692,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
             double blk[4];
             pll_block(pv, 2 * j, 2 * jstar, blk);
             for (int q = 0; q < t; q++) {   // earlier matches of this scan, in order
-                const double4 uq = *reinterpret_cast<const double4*>(Ust + ((size_t)q * n + b0) * 2);
+                const double4 uq = q < HIST_LDS ? sh_uhist[q][tid]
+                                                : *reinterpret_cast<const double4*>(Ust + ((size_t)q * n + b0) * 2);
                 const double* vh = sh_pkg + MB_VH + 4 * q;
                 blk[0] -= uq.x * vh[0] + uq.y * vh[1];
                 blk[1] -= uq.x * vh[2] + uq.y * vh[3];
@@ -710,7 +718,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
                 const double dyv = k0 * v0 + k1 * v1;   // y += K·v (Robot.cpp:585-589)
                 if (pp) yb.y += dyv; else yb.x += dyv;
             }
-            *reinterpret_cast<double4*>(Ust + ((size_t)t * n + b0) * 2) = make_double4(uu[0], uu[1], uu[2], uu[3]);
+            if (t < HIST_LDS)
+                sh_uhist[t][tid] = make_double4(uu[0], uu[1], uu[2], uu[3]);
+            else
+                *reinterpret_cast<double4*>(Ust + ((size_t)t * n + b0) * 2) = make_double4(uu[0], uu[1], uu[2], uu[3]);
             *reinterpret_cast<double4*>(Vst + ((size_t)t * n + b0) * 2) = make_double4(kk[0], kk[1], kk[2], kk[3]);
 #pragma unroll
             for (int pp = 0; pp < 2; pp++) {
@@ -767,7 +778,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     // ---------------- augmentation (Robot.cpp:776-866) ----------------
     if (!reset) {
         for (int q = 0; q < nadd; q++) {
-            const ekf_line ln = lines[sh_extra[q]];
+            const ekf_line ln = sh_lines[sh_extra[q]];
             const int sq = s + q;
             double alfa = ln.alpha;
             const double r = ln.r + (pose[0] * cos(alfa) + pose[1] * sin(alfa));
