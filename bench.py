@@ -50,7 +50,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--capacity", type=int, default=4096)
     ap.add_argument("--instances", type=int, default=8, help="EKF instances per GPU")
-    ap.add_argument("--precision", choices=["f32", "f64"], default="f32")
+    ap.add_argument("--precision", choices=["f32", "f64", "f16"], default="f32",
+                    help="landmark-block storage (f16: fp32 MFMA accumulation, BASELINE config 5)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pipeline", type=int, default=0,
@@ -82,8 +83,8 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     N, E, K, W = args.capacity, args.instances, args.steps, args.warmup
-    prec = ekf.PREC_F32 if args.precision == "f32" else ekf.PREC_F64
-    bpe = 4 if prec == ekf.PREC_F32 else 8
+    prec = {"f32": ekf.PREC_F32, "f64": ekf.PREC_F64, "f16": ekf.PREC_F16}[args.precision]
+    bpe = {"f32": 4, "f64": 8, "f16": 2}[args.precision]
     E_total = E * world
     first, count = D.shard(E_total, world, rank)
     assert count == E
@@ -166,7 +167,7 @@ def main():
     steps_per_launch = K / launches
     alg_bytes = E * n * (n + 1) * bpe   # one read + write of the packed block per flush
     alg_flops = steps_per_launch * E * 2 * L_LINES * n * (n + 1)
-    mfma_peak = MFMA_F32_PEAK_TFS if prec == ekf.PREC_F32 else MFMA_F64_PEAK_TFS
+    mfma_peak = MFMA_F64_PEAK_TFS if prec == ekf.PREC_F64 else MFMA_F32_PEAK_TFS   # f16 storage: f32 MFMA
     t_hbm = alg_bytes / (HBM_PEAK_GBS * 1e9)
     t_mfma = alg_flops / (mfma_peak * 1e12)
     bound = "hbm" if t_hbm >= t_mfma else "mfma"
@@ -212,7 +213,8 @@ def main():
             "unit": "GB/s" if bound == "hbm" else "TFLOP/s",
             "frac": ((gbs / HBM_PEAK_GBS) if bound == "hbm" else (tfs / mfma_peak)) if dd_ms > 0 else None,
             "traffic": traffic,
-            "kernel": "flush_f32_sb_kernel" if prec == ekf.PREC_F32 else "downdate_f64_kernel",
+            "kernel": ("downdate_f64_kernel" if prec == ekf.PREC_F64 else
+                       "flush_f32_persist_kernel" if args.flush_interval <= 4 else "flush_f32_sb_kernel"),
             "alg_bytes_per_launch": alg_bytes,
             "alg_flops_per_launch": alg_flops,
             "steps_per_launch": steps_per_launch,

@@ -47,8 +47,10 @@ enum {
                                 exchange within the spin bound (results of that call invalid) */
 };
 
-/* storage precision of the landmark-landmark covariance block */
-enum { EKF_PREC_F64 = 0, EKF_PREC_F32 = 1 };
+/* storage precision of the landmark-landmark covariance block (robot rows, mean: always fp64).
+ * F16: fp16 storage, fp32 MFMA accumulation, the block rounded to fp16 after every scan
+ * (BASELINE config 5); the tolerance it meets is stated in tests/test_gpu_parity.py. */
+enum { EKF_PREC_F64 = 0, EKF_PREC_F32 = 1, EKF_PREC_F16 = 2 };
 /* R source inside the association loop (SURVEY.md §8a parity-mode flags) */
 enum { EKF_R_INTENDED = 0, EKF_R_AS_WRITTEN = 1 };
 

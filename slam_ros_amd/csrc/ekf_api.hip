@@ -40,6 +40,7 @@ struct ekf_ctx {
     hipStream_t stream;       // S
     hipStream_t dstream;      // D
     size_t elem;              // bytes per stored landmark-block element
+    size_t op_elem;           // bytes per downdate operand element (fp32 for fp16 storage)
     size_t pll_inst;          // elements per instance
     size_t op_inst;           // operand elements per instance
     void* X[2];
@@ -207,7 +208,8 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         cfg->instances < 1 ||
         cfg->max_lines < 1 ||
         cfg->max_lines > EKF_MAX_LINES ||
-        (cfg->precision != EKF_PREC_F64 && cfg->precision != EKF_PREC_F32) ||
+        (cfg->precision != EKF_PREC_F64 && cfg->precision != EKF_PREC_F32 &&
+         cfg->precision != EKF_PREC_F16) ||
         (cfg->r_mode != EKF_R_INTENDED && cfg->r_mode != EKF_R_AS_WRITTEN) ||
         cfg->flush_interval < 0 || cfg->flush_interval > 16)
         return EKF_EINVAL;
@@ -226,7 +228,8 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     c->d = ekf::make_dims(cfg->capacity, cfg->max_lines);
     const Dims& d = c->d;
     const int E = cfg->instances;
-    c->elem = (cfg->precision == EKF_PREC_F64) ? 8 : 4;
+    c->elem = (cfg->precision == EKF_PREC_F64) ? 8 : (cfg->precision == EKF_PREC_F32) ? 4 : 2;
+    c->op_elem = (cfg->precision == EKF_PREC_F64) ? 8 : 4;   // operands in the compute type
     c->pll_inst = (size_t)d.ntiles * ekf::TILE_ELEMS;
     c->op_inst = (size_t)d.nb * 64 * (d.kmax / 2);
     int rc = EKF_ENOMEM;
@@ -249,8 +252,8 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     c->T = cfg->flush_interval > 0 ? cfg->flush_interval : 1;
     c->ring.assign((size_t)c->T * (cfg->pipeline ? 2 : 1), ekf::Slot{});
     for (auto& sl : c->ring) {
-        ALLOC(sl.Uop, c->op_inst * c->elem * E);
-        ALLOC(sl.Vop, c->op_inst * c->elem * E);
+        ALLOC(sl.Uop, c->op_inst * c->op_elem * E);
+        ALLOC(sl.Vop, c->op_inst * c->op_elem * E);
         ALLOC(sl.patch, sizeof(double) * d.max_lines * 2 * d.M * E);
         ALLOC(sl.patch_diag, sizeof(double) * d.max_lines * 4 * E);
         ALLOC(sl.res, sizeof(int) * ekf::RES_STRIDE * E);

@@ -29,6 +29,59 @@ namespace ekf {
 
 #define EKF_PI 3.14159265358979323846
 
+// Storage type T of the landmark block → compute type C (MFMA / FMA chain) and tile layout L.
+// fp16 storage computes in fp32 on the f32 layout and rounds to fp16 after every step, in the
+// flush and in the on-read replay alike, so the stored value never depends on when it is flushed.
+// It holds 2^10·P (|P| < 64 representable, normal down to 6e-8, no subnormal loss for
+// landmark covariances). The fp16 path computes in that scaled domain throughout: the scan
+// writes the U operand scaled by 2^10 (exact), so flush and on-read replay both run
+// acc = 2^10·X − (2^10·U)·Vᵀ, bit-for-bit 2^10 × the unscaled chain, and round with two
+// conversions per element; values leave the scaled domain only where they are read as P.
+template <typename T> struct Stor {
+    using C = T;
+    using L = T;
+    static constexpr bool half = false;
+    static constexpr float scale = 1.f;
+};
+template <> struct Stor<_Float16> {
+    using C = float;
+    using L = float;
+    static constexpr bool half = true;
+    static constexpr float scale = 1024.f;
+};
+
+template <typename T>
+__device__ __forceinline__ T to_store(typename Stor<T>::C x)
+{
+    return (T)x;
+}
+
+template <typename T>
+__device__ __forceinline__ typename Stor<T>::C from_store(T h)
+{
+    return (typename Stor<T>::C)h;
+}
+
+template <typename T>
+__device__ __forceinline__ typename Stor<T>::C round_step(typename Stor<T>::C x)
+{
+    return (typename Stor<T>::C)(T)x;
+}
+
+// P value (fp64) → scaled compute domain, and back
+template <typename T>
+__device__ __forceinline__ typename Stor<T>::C to_domain(double v)
+{
+    using C = typename Stor<T>::C;
+    return (C)v * (C)Stor<T>::scale;
+}
+
+template <typename T>
+__device__ __forceinline__ double from_domain(typename Stor<T>::C x)
+{
+    return (double)x * (1.0 / (double)Stor<T>::scale);
+}
+
 __device__ __forceinline__ double normalize_radian(double rad)
 {
     // Robot.cpp:62-71
@@ -74,8 +127,9 @@ __device__ __forceinline__ bool lu_invert2(const double S[4], double Si[4])
 template <typename T>
 __device__ __forceinline__ void ll_store_sym(T* P, int i, int j, int nb, double v)
 {
-    P[ll_offset<T>(i, j, nb)] = (T)v;
-    if ((i >> 5) == (j >> 5) && i != j) P[ll_offset<T>(j, i, nb)] = (T)v;
+    using L = typename Stor<T>::L;
+    P[ll_offset<L>(i, j, nb)] = to_store<T>(to_domain<T>(v));
+    if ((i >> 5) == (j >> 5) && i != j) P[ll_offset<L>(j, i, nb)] = to_store<T>(to_domain<T>(v));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -102,21 +156,23 @@ __device__ __forceinline__ void pll_block(const PllView<T>& v, int i0, int j0, d
 {
     const bool swap = (i0 >> 5) > (j0 >> 5);
     const int a0 = swap ? j0 : i0, b0 = swap ? i0 : j0;   // stored orientation
-    T acc[4];
+    using C = typename Stor<T>::C;
+    using L = typename Stor<T>::L;
+    C acc[4];
 #pragma unroll
     for (int p = 0; p < 2; p++)
 #pragma unroll
-        for (int c = 0; c < 2; c++) acc[p * 2 + c] = v.X[ll_offset<T>(a0 + p, b0 + c, v.nb)];
+        for (int c = 0; c < 2; c++) acc[p * 2 + c] = from_store<T>(v.X[ll_offset<L>(a0 + p, b0 + c, v.nb)]);
     for (int q = 0; q < v.npend; q++) {
         const Slot& sq = v.pend[q];
         const int4 cw = v.ctl[q];
         if (cw.x) {
-            acc[0] = acc[1] = acc[2] = acc[3] = (T)0;
+            acc[0] = acc[1] = acc[2] = acc[3] = (C)0;
             continue;
         }
         const int ks = cw.y;
         if (ks > 0) {
-            if constexpr (sizeof(T) == 4) {
+            if constexpr (sizeof(C) == 4) {
                 // v_mfma_f32_32x32x2_f32 = ordered fmaf chain (k0 lanes 0-31, then k1)
                 const int kh = v.kmax / 2;
                 const float* ua = reinterpret_cast<const float*>(sq.Uop) + v.e * v.opstride +
@@ -160,6 +216,8 @@ __device__ __forceinline__ void pll_block(const PllView<T>& v, int i0, int j0, d
                         acc[3] = fma(x1, y1, (double)acc[3]);
                     }
             }
+#pragma unroll
+            for (int k = 0; k < 4; k++) acc[k] = round_step<T>(acc[k]);
         }
         const int nadd = cw.z;
         if (nadd > 0) {
@@ -183,17 +241,21 @@ __device__ __forceinline__ void pll_block(const PllView<T>& v, int i0, int j0, d
                     raw[2] = prw[i0 + 1]; raw[3] = prw[v.M + i0 + 1];
                 }
                 if (swap) {
-                    acc[0] = (T)raw[0]; acc[1] = (T)raw[2]; acc[2] = (T)raw[1]; acc[3] = (T)raw[3];
+                    acc[0] = round_step<T>(to_domain<T>(raw[0])); acc[1] = round_step<T>(to_domain<T>(raw[2]));
+                    acc[2] = round_step<T>(to_domain<T>(raw[1])); acc[3] = round_step<T>(to_domain<T>(raw[3]));
                 } else {
-                    acc[0] = (T)raw[0]; acc[1] = (T)raw[1]; acc[2] = (T)raw[2]; acc[3] = (T)raw[3];
+                    acc[0] = round_step<T>(to_domain<T>(raw[0])); acc[1] = round_step<T>(to_domain<T>(raw[1]));
+                    acc[2] = round_step<T>(to_domain<T>(raw[2])); acc[3] = round_step<T>(to_domain<T>(raw[3]));
                 }
             }
         }
     }
     if (swap) {
-        out[0] = (double)acc[0]; out[1] = (double)acc[2]; out[2] = (double)acc[1]; out[3] = (double)acc[3];
+        out[0] = from_domain<T>(acc[0]); out[1] = from_domain<T>(acc[2]);
+        out[2] = from_domain<T>(acc[1]); out[3] = from_domain<T>(acc[3]);
     } else {
-        out[0] = (double)acc[0]; out[1] = (double)acc[1]; out[2] = (double)acc[2]; out[3] = (double)acc[3];
+        out[0] = from_domain<T>(acc[0]); out[1] = from_domain<T>(acc[1]);
+        out[2] = from_domain<T>(acc[2]); out[3] = from_domain<T>(acc[3]);
     }
 }
 
@@ -520,8 +582,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     const size_t opstride = (size_t)d.nb * 64 * (d.kmax / 2);
     double* Ust = p.Ust + (size_t)e * d.max_lines * n * 2;
     double* Vst = p.Vst + (size_t)e * d.max_lines * n * 2;
-    T* Uop = reinterpret_cast<T*>(p.cur.Uop) + (size_t)e * opstride;
-    T* Vop = reinterpret_cast<T*>(p.cur.Vop) + (size_t)e * opstride;
+    using C = typename Stor<T>::C;   // operand (compute) type
+    C* Uop = reinterpret_cast<C*>(p.cur.Uop) + (size_t)e * opstride;
+    C* Vop = reinterpret_cast<C*>(p.cur.Vop) + (size_t)e * opstride;
     double* patch = p.cur.patch + (size_t)e * d.max_lines * 2 * M;
     double* pdiag = p.cur.patch_diag + (size_t)e * d.max_lines * 4;
     int* res = p.cur.res + (size_t)e * RES_STRIDE;
@@ -726,16 +789,16 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
 #pragma unroll
             for (int pp = 0; pp < 2; pp++) {
                 const int lr = 2 * j + pp;
-                if constexpr (sizeof(T) == 4) {
-                    Uop[op_index_f32(lr, 2 * t, d.kmax)] = (T)(-uu[2 * pp]);
-                    Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (T)(-uu[2 * pp + 1]);
-                    Vop[op_index_f32(lr, 2 * t, d.kmax)] = (T)kk[2 * pp];
-                    Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (T)kk[2 * pp + 1];
+                if constexpr (sizeof(C) == 4) {
+                    Uop[op_index_f32(lr, 2 * t, d.kmax)] = to_domain<T>(-uu[2 * pp]);
+                    Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = to_domain<T>(-uu[2 * pp + 1]);
+                    Vop[op_index_f32(lr, 2 * t, d.kmax)] = (C)kk[2 * pp];
+                    Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (C)kk[2 * pp + 1];
                 } else {
-                    Uop[op_index_f64(lr, 2 * t, d.kmax)] = (T)(-uu[2 * pp]);
-                    Uop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (T)(-uu[2 * pp + 1]);
-                    Vop[op_index_f64(lr, 2 * t, d.kmax)] = (T)kk[2 * pp];
-                    Vop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (T)kk[2 * pp + 1];
+                    Uop[op_index_f64(lr, 2 * t, d.kmax)] = (C)(-uu[2 * pp]);
+                    Uop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (C)(-uu[2 * pp + 1]);
+                    Vop[op_index_f64(lr, 2 * t, d.kmax)] = (C)kk[2 * pp];
+                    Vop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (C)kk[2 * pp + 1];
                 }
             }
             // eager downdate of the owned robot-strip columns and diagonal block (Robot.cpp:568)
@@ -836,14 +899,14 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         *reinterpret_cast<double2*>(Rs + n + b0) = rr1;
         *reinterpret_cast<double2*>(Rs + 2 * n + b0) = rr2;
         *reinterpret_cast<double2*>(y + b0) = yb;
-        if (sizeof(T) == 8 && (m & 1)) {
+        if (sizeof(C) == 8 && (m & 1)) {
             // f64 operands: zero the odd tail column pair of the last 4-wide k-step
 #pragma unroll
             for (int pp = 0; pp < 2; pp++) {
-                Uop[op_index_f64(2 * j + pp, 2 * m, d.kmax)] = (T)0;
-                Uop[op_index_f64(2 * j + pp, 2 * m + 1, d.kmax)] = (T)0;
-                Vop[op_index_f64(2 * j + pp, 2 * m, d.kmax)] = (T)0;
-                Vop[op_index_f64(2 * j + pp, 2 * m + 1, d.kmax)] = (T)0;
+                Uop[op_index_f64(2 * j + pp, 2 * m, d.kmax)] = (C)0;
+                Uop[op_index_f64(2 * j + pp, 2 * m + 1, d.kmax)] = (C)0;
+                Vop[op_index_f64(2 * j + pp, 2 * m, d.kmax)] = (C)0;
+                Vop[op_index_f64(2 * j + pp, 2 * m + 1, d.kmax)] = (C)0;
             }
         }
     }
@@ -873,7 +936,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         res[RES_RESET] = reset;
         res[RES_NADD] = reset ? 0 : nadd;
         res[RES_NLINES] = L;
-        res[RES_KSTEPS] = (sizeof(T) == 4) ? m : (m + 1) / 2;
+        res[RES_KSTEPS] = (sizeof(C) == 4) ? m : (m + 1) / 2;
         p.saved[e] = reset ? 0 : s + nadd;
     }
     EKF_STAMP(7);
@@ -908,6 +971,43 @@ __device__ __forceinline__ double patched_value(const double* prw0, const double
     return (li > lj) ? prw[(size_t)(i & 1) * M + j] : prw[(size_t)(j & 1) * M + i];
 }
 
+// fp32-layout tiles in fp32 or fp16 storage: lane's 4 consecutive elements of accumulator group qq
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+template <typename TS>
+__device__ __forceinline__ f32x4 tile_ld(const TS* tile, int lane, int qq)
+{
+    if constexpr (sizeof(TS) == 4) {
+        return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(tile) + lane + qq * 64);
+    } else {
+        const f16x4 h = __builtin_nontemporal_load(reinterpret_cast<const f16x4*>(tile) + lane + qq * 64);
+        return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+    }
+}
+
+template <typename TS>
+__device__ __forceinline__ void tile_st(TS* tile, int lane, int qq, const f32x16& a)
+{
+    if constexpr (sizeof(TS) == 4) {
+        const f32x4 v = {a[4 * qq + 0], a[4 * qq + 1], a[4 * qq + 2], a[4 * qq + 3]};
+        __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(tile) + lane + qq * 64);
+    } else {
+        const f16x4 v = {(_Float16)a[4 * qq + 0], (_Float16)a[4 * qq + 1], (_Float16)a[4 * qq + 2],
+                         (_Float16)a[4 * qq + 3]};
+        __builtin_nontemporal_store(v, reinterpret_cast<f16x4*>(tile) + lane + qq * 64);
+    }
+}
+
+// fp16 storage: the value a step leaves in the block is its fp16 rounding (see Stor)
+template <typename TS>
+__device__ __forceinline__ void round_acc(f32x16& a)
+{
+    if constexpr (sizeof(TS) == 2) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) a[k] = round_step<_Float16>(a[k]);
+    }
+}
+
 // f32 flush on super-tiles: a workgroup owns DD_SB × DD_SB tiles (wave w: tile row
 // sbi·DD_SB + w, tile columns sbj·DD_SB + 0..3), keeps their 4 accumulators in registers for
 // the whole group of steps and stages each step's operands for the DD_SB row blocks and DD_SB
@@ -934,6 +1034,7 @@ __device__ __forceinline__ SbStep sb_step(const DowndateParams& p, int q, int e)
 }
 }  // namespace
 
+template <typename TS>
 __global__ __launch_bounds__(DD_THREADS) void flush_f32_sb_kernel(DowndateParams p)
 {
     const Dims d = p.d;
@@ -970,18 +1071,21 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_sb_kernel(DowndateParams
         vmask |= valid[c] << c;
         toff[c] = valid[c] ? ((size_t)e * d.ntiles + tile_index(bi, bj, d.nb)) * TILE_ELEMS : 0;
     }
-    const float* Pin = reinterpret_cast<const float*>(p.Pin);
-    float* Pout = reinterpret_cast<float*>(p.Pout);
+    const TS* Pin = reinterpret_cast<const TS*>(p.Pin);
+    TS* Pout = reinterpret_cast<TS*>(p.Pout);
     if (!work) {
         if (p.Pin != p.Pout) {
 #pragma unroll
             for (int c = 0; c < DD_SB; c++)
                 if (valid[c]) {
-                    const f32x4* src = reinterpret_cast<const f32x4*>(Pin + toff[c]) + lane;
-                    f32x4* dst = reinterpret_cast<f32x4*>(Pout + toff[c]) + lane;
+                    f32x16 t;
 #pragma unroll
-                    for (int qq = 0; qq < 4; qq++)
-                        __builtin_nontemporal_store(__builtin_nontemporal_load(src + qq * 64), dst + qq * 64);
+                    for (int qq = 0; qq < 4; qq++) {
+                        const f32x4 v = tile_ld(Pin + toff[c], lane, qq);
+                        t[4 * qq + 0] = v[0]; t[4 * qq + 1] = v[1]; t[4 * qq + 2] = v[2]; t[4 * qq + 3] = v[3];
+                    }
+#pragma unroll
+                    for (int qq = 0; qq < 4; qq++) tile_st(Pout + toff[c], lane, qq, t);
                 }
         }
         return;
@@ -990,10 +1094,9 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_sb_kernel(DowndateParams
 #pragma unroll
     for (int c = 0; c < DD_SB; c++) {
         if (valid[c]) {
-            const f32x4* src = reinterpret_cast<const f32x4*>(Pin + toff[c]) + lane;
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) {
-                const f32x4 v = __builtin_nontemporal_load(src + qq * 64);
+                const f32x4 v = tile_ld(Pin + toff[c], lane, qq);
                 acc[c][4 * qq + 0] = v[0];
                 acc[c][4 * qq + 1] = v[1];
                 acc[c][4 * qq + 2] = v[2];
@@ -1055,7 +1158,7 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_sb_kernel(DowndateParams
                     const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
                     const int hi = max(row >> 1, col >> 1);
                     if (hi >= s.s0 && hi < s.s0 + s.nadd)
-                        acc[0][k] = (float)patched_value(prw0, pdg, d.M, s.s0, row, col);
+                        acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s.s0, row, col)));
                 }
             }
             const f32x16 t0 = acc[0];
@@ -1107,8 +1210,11 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_sb_kernel(DowndateParams
                                                                       acc[c], 0, 0, 0);
                 }
         }
-        if (qn != q)
+        if (qn != q) {
+#pragma unroll
+            for (int c = 0; c < DD_SB; c++) round_acc<TS>(acc[c]);
             for (int t = q; t < qn && t < p.nsteps; t++) post(t);
+        }
         q = qn;
         k0 = kn;
         buf ^= 1;
@@ -1116,146 +1222,9 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_sb_kernel(DowndateParams
 #pragma unroll
     for (int c = 0; c < DD_SB; c++)
         if (valid[c]) {
-            f32x4* dst = reinterpret_cast<f32x4*>(Pout + toff[c]) + lane;
 #pragma unroll
-            for (int qq = 0; qq < 4; qq++) {
-                const f32x4 v = {acc[c][4 * qq + 0], acc[c][4 * qq + 1], acc[c][4 * qq + 2], acc[c][4 * qq + 3]};
-                __builtin_nontemporal_store(v, dst + qq * 64);
-            }
+            for (int qq = 0; qq < 4; qq++) tile_st(Pout + toff[c], lane, qq, acc[c]);
         }
-}
-
-// f32 flush, 16-wave form: a 1024-thread workgroup owns the same DD_SB × DD_SB super-tile, one
-// tile per wave (one accumulator, ~64 VGPRs) so that 8 waves per SIMD interleave the HBM
-// streaming of some tiles with the MFMA chains of others. Operand staging as above (one float4
-// per thread per chunk); waves whose tile lies below the diagonal only stage.
-constexpr int SB16_THREADS = 1024;
-
-__global__ __launch_bounds__(SB16_THREADS, 8) void flush_f32_sb16_kernel(DowndateParams p)
-{
-    const Dims d = p.d;
-    const int nsb = (d.nb + DD_SB - 1) / DD_SB;
-    const int64_t nst = (int64_t)nsb * (nsb + 1) / 2;
-    const int64_t total = (int64_t)p.E * nst;
-    const int64_t per = (total + 7) / 8;
-    const int64_t g = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    if (g >= total) return;
-    const int e = (int)(g / nst);
-    const int2 sb = p.stile_rc[g - (int64_t)e * nst];
-    const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
-    const int tr = w >> 2, tc = w & 3;
-    const int bi = sb.x * DD_SB + tr, bj = sb.y * DD_SB + tc;
-    const bool valid = bi < d.nb && bj < d.nb && bi <= bj;
-    const int kh = d.kmax / 2;
-    const size_t opstride = (size_t)d.nb * 64 * kh;
-
-    bool work = false;
-    for (int q = 0; q < p.nsteps; q++) {
-        const SbStep s = sb_step(p, q, e);
-        work |= s.reset || s.ks > 0 ||
-                (s.nadd > 0 && (sb.y + 1) * DD_SB * 16 > s.s0 && sb.y * DD_SB * 16 < s.s0 + s.nadd);
-    }
-    const size_t toff = valid ? ((size_t)e * d.ntiles + tile_index(bi, bj, d.nb)) * TILE_ELEMS : 0;
-    const f32x4* src = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.Pin) + toff) + lane;
-    f32x4* dst = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.Pout) + toff) + lane;
-    if (!work) {
-        if (p.Pin != p.Pout && valid) {
-#pragma unroll
-            for (int qq = 0; qq < 4; qq++)
-                __builtin_nontemporal_store(__builtin_nontemporal_load(src + qq * 64), dst + qq * 64);
-        }
-        return;
-    }
-    f32x16 acc;
-#pragma unroll
-    for (int k = 0; k < 16; k++) acc[k] = 0.f;
-    if (valid) {
-#pragma unroll
-        for (int qq = 0; qq < 4; qq++) {
-            const f32x4 v = __builtin_nontemporal_load(src + qq * 64);
-            acc[4 * qq + 0] = v[0];
-            acc[4 * qq + 1] = v[1];
-            acc[4 * qq + 2] = v[2];
-            acc[4 * qq + 3] = v[3];
-        }
-    }
-    __shared__ f32x4 lds[2][2][DD_SB][2][64];
-    const int ln = threadIdx.x & 63, s4 = (threadIdx.x >> 6) & 1, blk = (threadIdx.x >> 7) & 3,
-              ab = threadIdx.x >> 9;
-    const int rb = (ab ? sb.y : sb.x) * DD_SB + blk;
-    auto fetch = [&](int q, int k0) {
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (rb < d.nb) {
-            const float* base = reinterpret_cast<const float*>(ab ? p.steps[q].Vop : p.steps[q].Uop) + e * opstride;
-            v = *reinterpret_cast<const f32x4*>(base + ((size_t)rb * 64 + ln) * kh + k0 + 4 * s4);
-        }
-        return v;
-    };
-    auto post = [&](int q) {
-        const SbStep s = sb_step(p, q, e);
-        if (s.reset) {
-#pragma unroll
-            for (int k = 0; k < 16; k++) acc[k] = 0.f;
-            return;
-        }
-        if (s.nadd <= 0 || !valid || bj * 16 + 15 < s.s0 || bj * 16 >= s.s0 + s.nadd) return;
-        const double* prw0 = p.steps[q].patch + (size_t)e * d.max_lines * 2 * d.M;
-        const double* pdg = p.steps[q].patch_diag + (size_t)e * d.max_lines * 4;
-        const int col = bj * 32 + (lane & 31);
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
-            const int hi = max(row >> 1, col >> 1);
-            if (hi >= s.s0 && hi < s.s0 + s.nadd)
-                acc[k] = (float)patched_value(prw0, pdg, d.M, s.s0, row, col);
-        }
-    };
-    auto first_mfma = [&](int q) {
-        while (q < p.nsteps && sb_step(p, q, e).ks == 0) q++;
-        return q;
-    };
-
-    int q = first_mfma(0);
-    for (int t = 0; t < q; t++) post(t);
-    int k0 = 0, buf = 0;
-    f32x4 reg = {0.f, 0.f, 0.f, 0.f};
-    if (q < p.nsteps) reg = fetch(q, 0);
-    while (q < p.nsteps) {
-        const int ks = sb_step(p, q, e).ks;
-        const int kc = min(SBK, ks - k0);
-        lds[buf][ab][blk][s4][ln] = reg;
-        __syncthreads();
-        int qn = q, kn = k0 + SBK;
-        if (kn >= ks) {
-            qn = first_mfma(q + 1);
-            kn = 0;
-        }
-        if (qn < p.nsteps) reg = fetch(qn, kn);
-        if (valid) {
-            const f32x4 a0 = lds[buf][0][tr][0][lane];
-            const f32x4 a1 = lds[buf][0][tr][1][lane];
-            const f32x4 b0 = lds[buf][1][tc][0][lane];
-            const f32x4 b1 = lds[buf][1][tc][1][lane];
-#pragma unroll
-            for (int s = 0; s < SBK; s++)
-                if (s < kc)
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s < 4 ? a0[s & 3] : a1[s & 3],
-                                                               s < 4 ? b0[s & 3] : b1[s & 3], acc, 0, 0, 0);
-        }
-        if (qn != q)
-            for (int t = q; t < qn && t < p.nsteps; t++) post(t);
-        q = qn;
-        k0 = kn;
-        buf ^= 1;
-    }
-    if (valid) {
-#pragma unroll
-        for (int qq = 0; qq < 4; qq++) {
-            const f32x4 v = {acc[4 * qq + 0], acc[4 * qq + 1], acc[4 * qq + 2], acc[4 * qq + 3]};
-            __builtin_nontemporal_store(v, dst + qq * 64);
-        }
-    }
 }
 
 // f32 flush, persistent software-pipelined form: one 4-wave workgroup per CU walks a range of
@@ -1306,6 +1275,7 @@ __device__ __forceinline__ void pst_info(const DowndateParams& p, int gg, int ns
     }
 }
 
+template <typename TS>
 __global__ __launch_bounds__(DD_THREADS) void flush_f32_persist_kernel(DowndateParams p)
 {
     const Dims d = p.d;
@@ -1324,8 +1294,8 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_persist_kernel(DowndateP
     const int w = threadIdx.x >> 6;
     const int kh = d.kmax / 2;
     const size_t opstride = (size_t)d.nb * 64 * kh;
-    const float* Pin = reinterpret_cast<const float*>(p.Pin);
-    float* Pout = reinterpret_cast<float*>(p.Pout);
+    const TS* Pin = reinterpret_cast<const TS*>(p.Pin);
+    TS* Pout = reinterpret_cast<TS*>(p.Pout);
     // this thread's staging slot: float4 i = tid + 256 j of a chunk
     auto tile_off = [&](const PstInfo& t, int c, bool& valid) {
         const int bi = t.sbi * DD_SB + w, bj = t.sbj * DD_SB + c;
@@ -1351,9 +1321,9 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_persist_kernel(DowndateP
 #pragma unroll
         for (int c = 0; c < DD_SB; c++) {
             bool v;
-            const f32x4* src = reinterpret_cast<const f32x4*>(Pin + tile_off(t, c, v)) + lane;
+            const TS* tl = Pin + tile_off(t, c, v);
 #pragma unroll
-            for (int qq = 0; qq < 4; qq++) pref[c][qq] = __builtin_nontemporal_load(src + qq * 64);
+            for (int qq = 0; qq < 4; qq++) pref[c][qq] = tile_ld(tl, lane, qq);
         }
     };
 
@@ -1425,7 +1395,7 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_persist_kernel(DowndateP
                         const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
                         const int hi = max(row >> 1, col >> 1);
                         if (hi >= s0 && hi < s0 + nadd)
-                            acc[0][k] = (float)patched_value(prw0, pdg, d.M, s0, row, col);
+                            acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s0, row, col)));
                     }
                 }
                 const f32x16 t0 = acc[0];
@@ -1459,6 +1429,8 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_persist_kernel(DowndateP
                                                                            s < 4 ? b0[cc][s & 3] : b1[cc][s & 3],
                                                                            acc[cc], 0, 0, 0);
                     }
+#pragma unroll
+                for (int cc = 0; cc < DD_SB; cc++) round_acc<TS>(acc[cc]);
             }
             post(q);
         }
@@ -1467,12 +1439,8 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_persist_kernel(DowndateP
             bool v;
             const size_t off = tile_off(cur, c, v);
             if (v) {
-                f32x4* dst = reinterpret_cast<f32x4*>(Pout + off) + lane;
 #pragma unroll
-                for (int qq = 0; qq < 4; qq++) {
-                    const f32x4 o = {acc[c][4 * qq + 0], acc[c][4 * qq + 1], acc[c][4 * qq + 2], acc[c][4 * qq + 3]};
-                    __builtin_nontemporal_store(o, dst + qq * 64);
-                }
+                for (int qq = 0; qq < 4; qq++) tile_st(Pout + off, lane, qq, acc[c]);
             }
         }
         if (!more) break;
@@ -1581,7 +1549,7 @@ __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams
 template <typename T>
 __device__ __forceinline__ void tile_rc_of(int rem, int& r, int& c)
 {
-    if (sizeof(T) == 4) {
+    if (sizeof(typename Stor<T>::L) == 4) {
         const int q = rem & 3, lane = (rem >> 2) & 63, grp = rem >> 8;
         c = lane & 31;
         r = q + 4 * (lane >> 5) + 8 * grp;
@@ -1606,7 +1574,7 @@ __global__ void pack_kernel(Dims d, const double* __restrict__ Pfull, T* __restr
         const int i = rc.x * TILE + r, j = rc.y * TILE + c;
         double v = 0.0;
         if (i < d.M && j < d.M) v = Pfull[(size_t)(3 + i) * d.n + (3 + j)];
-        Pll[g] = (T)v;
+        Pll[g] = to_store<T>(to_domain<T>(v));
     }
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < 3 * (int64_t)d.n;
          g += (int64_t)gridDim.x * blockDim.x) {
@@ -1626,7 +1594,7 @@ __global__ void unpack_kernel(Dims d, double* __restrict__ Pfull, const T* __res
         double v;
         if (a < 3) v = Rs[(size_t)a * d.n + b];
         else if (b < 3) v = Rs[(size_t)b * d.n + a];
-        else v = (double)Pll[ll_offset<T>(a - 3, b - 3, d.nb)];
+        else v = from_domain<T>(from_store<T>(Pll[ll_offset<typename Stor<T>::L>(a - 3, b - 3, d.nb)]));
         Pfull[g] = v;
     }
 }
@@ -1651,7 +1619,7 @@ __global__ void lowrank_kernel(Dims d, const double* __restrict__ diag,
             for (int k = 0; k < rank; k++) v += ui[k] * uj[k];
             if (i == j) v += diag[3 + i];
         }
-        Pll[g] = (T)v;
+        Pll[g] = to_store<T>(to_domain<T>(v));
     }
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < 3 * (int64_t)d.n;
          g += (int64_t)gridDim.x * blockDim.x) {
@@ -1671,16 +1639,19 @@ __global__ void lowrank_kernel(Dims d, const double* __restrict__ diag,
 int scan_blocks_per_cu(int precision)
 {
     int nb = 0;
-    hipError_t err = (precision == 0)
-        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<double>, SCAN_THREADS, 0)
+    hipError_t err =
+        (precision == EKF_PREC_F64) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<double>, SCAN_THREADS, 0)
+        : (precision == EKF_PREC_F16) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<_Float16>, SCAN_THREADS, 0)
         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<float>, SCAN_THREADS, 0);
     return err == hipSuccess ? nb : 0;
 }
 
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 {
-    if (precision == 0)
+    if (precision == EKF_PREC_F64)
         hipLaunchKernelGGL(scan_kernel<double>, dim3(p.G, p.E), dim3(SCAN_THREADS), 0, st, p);
+    else if (precision == EKF_PREC_F16)
+        hipLaunchKernelGGL(scan_kernel<_Float16>, dim3(p.G, p.E), dim3(SCAN_THREADS), 0, st, p);
     else
         hipLaunchKernelGGL(scan_kernel<float>, dim3(p.G, p.E), dim3(SCAN_THREADS), 0, st, p);
     return hipGetLastError();
@@ -1688,21 +1659,26 @@ hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 
 hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st)
 {
-    if (precision == 0) {
+    if (precision == EKF_PREC_F64) {
         hipLaunchKernelGGL(downdate_f64_kernel, dim3(grid), dim3(DD_THREADS), 0, st, p);
+        return hipGetLastError();
+    }
+    const bool half = precision == EKF_PREC_F16;
+    const bool persist_ok = p.nsteps <= PST_MAXC && p.d.kmax <= 16 && p.variant != 2;
+    if (persist_ok) {
+        const int pgrid = 8 * ((p.ncu + 7) / 8);   // one workgroup per CU (128 KB LDS)
+        if (half)
+            hipLaunchKernelGGL(flush_f32_persist_kernel<_Float16>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+        else
+            hipLaunchKernelGGL(flush_f32_persist_kernel<float>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
     } else {
         const int64_t nsb = (p.d.nb + DD_SB - 1) / DD_SB;
         const int64_t total = (int64_t)p.E * (nsb * (nsb + 1) / 2);
-        const int64_t sgrid = 8 * ((total + 7) / 8);
-        const bool persist_ok = p.nsteps <= PST_MAXC && p.d.kmax <= 16;
-        if (p.variant == 1)
-            hipLaunchKernelGGL(flush_f32_sb16_kernel, dim3((unsigned)sgrid), dim3(SB16_THREADS), 0, st, p);
-        else if (p.variant == 2 || !persist_ok)
-            hipLaunchKernelGGL(flush_f32_sb_kernel, dim3((unsigned)sgrid), dim3(DD_THREADS), 0, st, p);
-        else {
-            const int pgrid = 8 * ((p.ncu + 7) / 8);   // one workgroup per CU (128 KB LDS)
-            hipLaunchKernelGGL(flush_f32_persist_kernel, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
-        }
+        const unsigned sgrid = (unsigned)(8 * ((total + 7) / 8));
+        if (half)
+            hipLaunchKernelGGL(flush_f32_sb_kernel<_Float16>, dim3(sgrid), dim3(DD_THREADS), 0, st, p);
+        else
+            hipLaunchKernelGGL(flush_f32_sb_kernel<float>, dim3(sgrid), dim3(DD_THREADS), 0, st, p);
     }
     return hipGetLastError();
 }
@@ -1719,9 +1695,12 @@ hipError_t launch_pack(const Dims& d, int precision, const double* Pfull, void* 
                        const int2* tile_rc, hipStream_t st)
 {
     const int grid = grid_for(d.ntiles * TILE_ELEMS, 256);
-    if (precision == 0)
+    if (precision == EKF_PREC_F64)
         hipLaunchKernelGGL(pack_kernel<double>, dim3(grid), dim3(256), 0, st, d, Pfull,
                            (double*)Pll, Rs, tile_rc);
+    else if (precision == EKF_PREC_F16)
+        hipLaunchKernelGGL(pack_kernel<_Float16>, dim3(grid), dim3(256), 0, st, d, Pfull,
+                           (_Float16*)Pll, Rs, tile_rc);
     else
         hipLaunchKernelGGL(pack_kernel<float>, dim3(grid), dim3(256), 0, st, d, Pfull,
                            (float*)Pll, Rs, tile_rc);
@@ -1732,9 +1711,12 @@ hipError_t launch_unpack(const Dims& d, int precision, double* Pfull, const void
                          const double* Rs, hipStream_t st)
 {
     const int grid = grid_for((int64_t)d.n * d.n, 256);
-    if (precision == 0)
+    if (precision == EKF_PREC_F64)
         hipLaunchKernelGGL(unpack_kernel<double>, dim3(grid), dim3(256), 0, st, d, Pfull,
                            (const double*)Pll, Rs);
+    else if (precision == EKF_PREC_F16)
+        hipLaunchKernelGGL(unpack_kernel<_Float16>, dim3(grid), dim3(256), 0, st, d, Pfull,
+                           (const _Float16*)Pll, Rs);
     else
         hipLaunchKernelGGL(unpack_kernel<float>, dim3(grid), dim3(256), 0, st, d, Pfull,
                            (const float*)Pll, Rs);
@@ -1745,9 +1727,12 @@ hipError_t launch_lowrank(const Dims& d, int precision, const double* diag, cons
                           int rank, void* Pll, double* Rs, const int2* tile_rc, hipStream_t st)
 {
     const int grid = grid_for(d.ntiles * TILE_ELEMS, 256);
-    if (precision == 0)
+    if (precision == EKF_PREC_F64)
         hipLaunchKernelGGL(lowrank_kernel<double>, dim3(grid), dim3(256), 0, st, d, diag, U,
                            rank, (double*)Pll, Rs, tile_rc);
+    else if (precision == EKF_PREC_F16)
+        hipLaunchKernelGGL(lowrank_kernel<_Float16>, dim3(grid), dim3(256), 0, st, d, diag, U,
+                           rank, (_Float16*)Pll, Rs, tile_rc);
     else
         hipLaunchKernelGGL(lowrank_kernel<float>, dim3(grid), dim3(256), 0, st, d, diag, U,
                            rank, (float*)Pll, Rs, tile_rc);

@@ -19,7 +19,7 @@ import numpy as np
 from . import build as _build
 
 EKF_MAX_LINES = 64
-PREC_F64, PREC_F32 = 0, 1
+PREC_F64, PREC_F32, PREC_F16 = 0, 1, 2
 R_INTENDED, R_AS_WRITTEN = 0, 1
 ST_SINGULAR_S, ST_CAPACITY, ST_NONSYM = 1, 2, 4
 

@@ -1,7 +1,8 @@
 """GPU parity: the HIP path (through the C-ABI) against the CPU restatement (oracle/).
 
 Tolerances (BASELINE.json north_star): per scan from identical inputs,
-‖P − P_ref‖_F / ‖P_ref‖_F ≤ 1e-6 and ‖y − y_ref‖₂ / ‖y_ref‖₂ ≤ 1e-8, association identical.
+‖P − P_ref‖_F / ‖P_ref‖_F ≤ 1e-6 and ‖y − y_ref‖₂ / ‖y_ref‖₂ ≤ 1e-8, association identical
+(fp16 storage: P ≤ 1e-3, see P_TOL).
 fp64 storage is held to 1e-10 over whole trajectories.
 """
 import math
@@ -13,7 +14,10 @@ from slam_ros_amd import scan_gen as G
 
 pytestmark = pytest.mark.gpu
 
-P_TOL = {0: 1e-10, 1: 1e-6}    # precision → per-scan relative Frobenius bound on P
+# precision → per-scan relative Frobenius bound on P. fp16 storage (BASELINE config 5, tolerance
+# re-stated): the block is rounded to fp16 (11-bit significand) after the scan, which alone is
+# ≈3e-4 relative in Frobenius norm; the state vector and the association are still fp64 exact.
+P_TOL = {0: 1e-10, 1: 1e-6, 2: 1e-3}
 Y_TOL = 1e-8
 
 
@@ -47,7 +51,7 @@ def check_same(ens, ref, prec, res=None, mref=None, where=""):
     return P, y, saved, pose
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 @pytest.mark.parametrize("N", [5, 37, 64, 100])
 def test_state_roundtrip(ekf_mod, prec, N):
     n = 3 + 2 * N
@@ -55,6 +59,8 @@ def test_state_roundtrip(ekf_mod, prec, N):
     A = rng.normal(size=(n, n))
     P = A @ A.T
     P = (P + P.T) / 2                           # exactly symmetric (packed storage)
+    if prec == 2:
+        P = P / (2 * n)                         # within the fp16 storage range (|P| < 64)
     y = rng.normal(size=n)
     ens = ekf_mod.Ensemble(N, 1, prec)
     ens.upload_state(0, P, y, N // 2, [1.0, 2.0, 0.3])
@@ -65,10 +71,14 @@ def test_state_roundtrip(ekf_mod, prec, N):
         np.testing.assert_array_equal(Pg, P)
     else:
         np.testing.assert_array_equal(Pg[:3], P[:3])            # robot strip kept in fp64
-        np.testing.assert_allclose(Pg[3:, 3:], P[3:, 3:].astype(np.float32), rtol=0, atol=0)
+        if prec == 1:
+            want = P[3:, 3:].astype(np.float32)
+        else:                                                   # fp16 scaled by 2^10
+            want = (P[3:, 3:].astype(np.float32) * 1024).astype(np.float16).astype(np.float64) / 1024
+        np.testing.assert_allclose(Pg[3:, 3:], want, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 def test_lowrank_init_equals_dense(ekf_mod, prec):
     N = 48
     w = G.make_world(N)
@@ -77,7 +87,7 @@ def test_lowrank_init_equals_dense(ekf_mod, prec):
     a.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
     Pa = a.download_state(0)[0]
     ref = st.dense_P()
-    tol = 1e-14 if prec == 0 else 1e-7
+    tol = {0: 1e-14, 1: 1e-7, 2: 1e-3}[prec]
     assert rel(Pa, ref) <= tol
 
 
@@ -91,7 +101,7 @@ def test_ctor_state_matches_reference(ekf_mod, oracle_mod):
     assert s == 0 and list(pose) == [1.5, -2.0, 0.25]
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 def test_map_from_scratch(ekf_mod, oracle_mod, prec):
     """Robot(0,0,0) → first scan augments every line → later scans match and augment.
     fp64: one trajectory vs the faithful dense restatement. fp32: per scan from identical state."""
@@ -101,8 +111,10 @@ def test_map_from_scratch(ekf_mod, oracle_mod, prec):
     first = G.random_lines(rng, 5)
     res = ens.localize([0.01, 0.0, 0.0], first[None], [5])[0]
     m = ref.localize(first, [0.01, 0.0, 0.0])
-    check_same(ens, ref, prec, res, m, "first")
+    P, yg, s, pose = check_same(ens, ref, prec, res, m, "first")
     assert res["new_landmarks"] == 5 and res["saved"] == 5
+    if prec:
+        ref.set_state(P, yg, s, pose)   # next scan from the stored (rounded) state
     for step in range(15):
         y = ref.y
         lines = []
@@ -115,7 +127,7 @@ def test_map_from_scratch(ekf_mod, oracle_mod, prec):
         res = ens.localize(enc, lines[None], [len(lines)])[0]
         m = ref.localize(lines, enc)
         P, yg, s, pose = check_same(ens, ref, prec, res, m, f"step {step}")
-        if prec == 1:
+        if prec:
             ref.set_state(P, yg, s, pose)
 
 
@@ -138,7 +150,7 @@ def test_trajectory_fp64_with_reset(ekf_mod, oracle_mod):
     assert resets >= 1
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 @pytest.mark.parametrize("pipeline,T,drain_at", [(True, 1, ()), (False, 4, ()), (True, 3, (7,)),
                                                  (False, 16, (5,)), (True, 16, ())])
 def test_deferred_flush_equals_drained(ekf_mod, oracle_mod, prec, pipeline, T, drain_at):
@@ -186,7 +198,7 @@ def test_deferred_flush_equals_drained(ekf_mod, oracle_mod, prec, pipeline, T, d
         check_same(a, ref, 0, where="deferred fp64 trajectory")
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 @pytest.mark.parametrize("N", [64, 256, 1024])
 def test_per_scan_parity(ekf_mod, oracle_mod, prec, N):
     w = G.make_world(N)
@@ -220,7 +232,7 @@ def test_n4096_fp32_scan(ekf_mod, oracle_mod):
     check_same(ens, ref, 1, res, m, "N=4096")
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 def test_predict_then_update_equals_localize(ekf_mod, prec):
     N = 64
     w = G.make_world(N)
@@ -242,7 +254,7 @@ def test_predict_then_update_equals_localize(ekf_mod, prec):
         np.testing.assert_array_equal(pa, pb)
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 def test_ensemble_instances_are_independent(ekf_mod, prec):
     N, E = 64, 3
     w = G.make_world(N)
@@ -287,7 +299,7 @@ def test_as_written_r_mode(ekf_mod, oracle_mod):
     assert res["match"][1] >= 0 and res["status"] & ekf_mod.ST_NONSYM
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 def test_edge_cases(ekf_mod, oracle_mod, prec):
     N = 30
     w = G.make_world(N, active=12)
