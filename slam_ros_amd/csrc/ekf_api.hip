@@ -55,6 +55,8 @@ struct ekf_ctx {
     double* Vst;
     int2* tile_rc;
     int2* stile_rc;
+    int2* stile2_rc;
+    int nstiles2;
     double* d_enc;
     ekf_line* d_lines;
     int* d_nlines;
@@ -69,6 +71,7 @@ struct ekf_ctx {
     unsigned scan_epoch;      // association launches so far (mailbox tags)
     double* mbox;
     int* sync;
+    int sync_stride;
     unsigned long long* dbg;  // association-kernel phase timers (EKF_SCAN_STAMPS=1)
     // flush scheduling (see the top of this file)
     int T;                    // flush interval
@@ -132,7 +135,7 @@ int ekf_abi_version(void) { return SLAM_EKF_ABI_VERSION; }
 static void free_all(ekf_ctx* c)
 {
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->pose, c->xpre, c->saved, c->D,
-                               c->tile_rc, c->stile_rc, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->mbox,
+                               c->tile_rc, c->stile_rc, c->stile2_rc, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->mbox,
                                c->sync, c->Ust, c->Vst};
     for (auto& sl : c->ring) {
         ptrs.push_back(sl.Uop);
@@ -262,6 +265,7 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     {
         const int nsb = (d.nb + ekf::DD_SB - 1) / ekf::DD_SB;
         ALLOC(c->stile_rc, sizeof(int2) * (size_t)nsb * (nsb + 1) / 2);
+        ALLOC(c->stile2_rc, sizeof(int2) * (size_t)nsb * ((d.nb + 1) / 2));
     }
     ALLOC(c->d_enc, sizeof(double) * 3 * E);
     ALLOC(c->d_lines, sizeof(ekf_line) * d.max_lines * E);
@@ -269,7 +273,8 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     c->G = (d.N + ekf::SCAN_THREADS - 1) / ekf::SCAN_THREADS;
     c->mbw = ((ekf::MB_WORDS_FIXED + 4 * d.max_lines + 15) / 16) * 16;   // whole 128-B lines
     ALLOC(c->mbox, sizeof(double) * 2 * c->G * c->mbw * E);
-    ALLOC(c->sync, sizeof(int) * ekf::SYNC_WORDS * E);
+    c->sync_stride = ((ekf::SYNC_WG0 + c->G + 15) / 16) * 16;
+    ALLOC(c->sync, sizeof(int) * c->sync_stride * E);
     if (getenv("EKF_SCAN_STAMPS") && atoi(getenv("EKF_SCAN_STAMPS")))
         ALLOC(c->dbg, sizeof(unsigned long long) * 16 * E);
 #undef ALLOC
@@ -304,6 +309,20 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
                 srcv.push_back(v);
             }
         if (hipMemcpy(c->stile_rc, srcv.data(), sizeof(int2) * srcv.size(), hipMemcpyHostToDevice) !=
+            hipSuccess)
+            goto fail;
+        // 4 × 2 super-tiles holding at least one stored tile (bi <= bj): sbj·2 + 1 >= sbi·4
+        std::vector<int2> s2;
+        for (int si = 0; si < nsb; si++)
+            for (int sj = 0; sj < (d.nb + 1) / 2; sj++)
+                if (sj * 2 + 1 >= si * 4) {
+                    int2 v;
+                    v.x = si;
+                    v.y = sj;
+                    s2.push_back(v);
+                }
+        c->nstiles2 = (int)s2.size();
+        if (hipMemcpy(c->stile2_rc, s2.data(), sizeof(int2) * s2.size(), hipMemcpyHostToDevice) !=
             hipSuccess)
             goto fail;
     }
@@ -428,6 +447,7 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.mbw = c->mbw;
     p.mbox = c->mbox;
     p.sync = c->sync;
+    p.sync_stride = c->sync_stride;
     return p;
 }
 
@@ -437,7 +457,7 @@ static hipError_t launch_scans(ekf_ctx* c, ekf::ScanParams sp)
 {
     const int E = c->cfg.instances;
     sp.epoch = ++c->scan_epoch;
-    hipError_t err = hipMemsetAsync(c->sync, 0, sizeof(int) * ekf::SYNC_WORDS * E, c->stream);
+    hipError_t err = hipSuccess;
     for (int e0 = 0; err == hipSuccess && e0 < E; e0 += c->scan_batch) {
         sp.e0 = e0;
         sp.E = (E - e0 < c->scan_batch) ? E - e0 : c->scan_batch;
@@ -466,6 +486,8 @@ static int enqueue_flush(ekf_ctx* c)
     dp.ncu = c->ncu;
     dp.tile_rc = c->tile_rc;
     dp.stile_rc = c->stile_rc;
+    dp.stile2_rc = c->stile2_rc;
+    dp.nstiles2 = c->nstiles2;
     for (int q = 0; q < nst; q++) dp.steps[q] = slot_of(c, c->unflushed0 + q);
     const int in = c->last_out;
     const int out = c->cfg.pipeline ? 1 - in : in;
@@ -554,12 +576,13 @@ extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
                            hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_pose, c->pose, sizeof(double) * 3 * E, hipMemcpyDeviceToHost,
                            c->stream));
-    std::vector<int> hs((size_t)ekf::SYNC_WORDS * E);
+    std::vector<int> hs((size_t)c->sync_stride * E);
     HIP_TRY(hipMemcpyAsync(hs.data(), c->sync, sizeof(int) * hs.size(), hipMemcpyDeviceToHost,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (int e = 0; e < E; e++)
-        c->h_res[(size_t)e * ekf::RES_STRIDE + ekf::RES_STATUS] |= hs[(size_t)e * ekf::SYNC_WORDS + ekf::SYNC_STATUS];
+        for (int gq = 0; gq < c->G; gq++)
+            c->h_res[(size_t)e * ekf::RES_STRIDE + ekf::RES_STATUS] |= hs[(size_t)e * c->sync_stride + ekf::SYNC_WG0 + gq];
     if (!out) return EKF_OK;
     for (int e = 0; e < E; e++) {
         const int* r = c->h_res + (size_t)e * ekf::RES_STRIDE;

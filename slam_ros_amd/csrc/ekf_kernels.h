@@ -12,8 +12,9 @@ enum { PHASE_PREDICT = 1, PHASE_UPDATE = 2, PHASE_BOTH = 3 };
 enum { EKF_ST_SINGULAR = EKF_ST_SINGULAR_S, EKF_ST_CAP = EKF_ST_CAPACITY, EKF_ST_NSYM = EKF_ST_NONSYM,
        EKF_ST_TIMEOUT_BIT = EKF_ST_SYNC_TIMEOUT };
 
-// per-instance synchronisation words of the association kernel (zeroed before every launch)
-enum { SYNC_STATUS = 1, SYNC_START = 2, SYNC_WORDS = 4 };
+// per-instance synchronisation words of the association kernel (never reset): a monotonic
+// start counter, then one status word per workgroup, rewritten by every launch
+enum { SYNC_START = 0, SYNC_WG0 = 4 };
 constexpr int MAX_GROUPS = 128;   // workgroups per instance (N <= 128 × 256)
 constexpr int MB_WORDS_FIXED = 26; // mailbox words before the V-history (see ekf_kernels.hip)
 
@@ -55,7 +56,8 @@ struct ScanParams {
     int G;                // workgroups per instance (grid.x) = ceil(N / SCAN_THREADS)
     int mbw;              // mailbox words per workgroup slot
     double* mbox;         // [E][2][G][mbw] per-line candidate exchange
-    int* sync;            // [E][SYNC_WORDS]
+    int* sync;            // [E][sync_stride]
+    int sync_stride;      // SYNC_WG0 + G, rounded up
     int phase;
     int r_mode;
     int reset_margin;
@@ -85,12 +87,14 @@ struct DowndateParams {
     Dims d;
     int E;
     int nsteps;
-    int variant;          // f32 flush form: 0 auto (persistent when it applies), 1 16-wave, 2 super-tile
+    int variant;          // f32 flush form: 0 auto, 2 super-tile, 3 persistent 1 WG/CU
     int ncu;              // compute units (persistent grid)
     const void* Pin;
     void* Pout;
     const int2* tile_rc;  // [ntiles] (bi, bj)
     const int2* stile_rc; // [nsb(nsb+1)/2] (sbi, sbj) super-tiles of DD_SB × DD_SB tiles, sbi <= sbj
+    const int2* stile2_rc;// [nstiles2] (sbi, sbj) super-tiles of DD_SB × 2 tiles holding a stored tile
+    int nstiles2;
     Slot steps[PMAX];
 };
 

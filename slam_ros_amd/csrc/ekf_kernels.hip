@@ -451,17 +451,17 @@ __device__ __forceinline__ void signal_started(int* sync, int tid)
         __hip_atomic_fetch_add(&sync[SYNC_START], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ void wait_all_started(int* sync, int G)
+// The start counter is never reset: launch `epoch` is complete once it reaches epoch·G.
+__device__ __forceinline__ int wait_all_started(int* sync, int G, unsigned epoch)
 {
+    const unsigned target = epoch * (unsigned)G;
     int polls = 0;
-    while (__hip_atomic_load(&sync[SYNC_START], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G) {
+    while ((int)((unsigned)__hip_atomic_load(&sync[SYNC_START], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                 target) < 0) {
         __builtin_amdgcn_s_sleep(1);
-        if (++polls > (1 << 24)) {
-            __hip_atomic_fetch_or(&sync[SYNC_STATUS], EKF_ST_TIMEOUT_BIT, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-            break;
-        }
+        if (++polls > (1 << 24)) return EKF_ST_TIMEOUT_BIT;
     }
+    return 0;
 }
 
 template <typename T>
@@ -478,7 +478,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     const int b0 = 3 + 2 * j;                   // its first row of P
     double* Rs = p.Rs + (size_t)e * 3 * n;
     double* y = p.y + (size_t)e * n;
-    int* sync = p.sync + (size_t)e * SYNC_WORDS;
+    int* sync = p.sync + (size_t)e * p.sync_stride;
     double* mbox = p.mbox + (size_t)e * 2 * G * p.mbw;
     const bool lead = (g == 0 && tid == 0);
 
@@ -562,8 +562,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
                 *reinterpret_cast<double2*>(Rs + 2 * n + b0) = rr2;
             }
             signal_started(sync, tid);
+            if (tid == 0 && !lead) sync[SYNC_WG0 + g] = 0;
             if (lead) {
-                wait_all_started(sync, G);
+                const int to = wait_all_started(sync, G, p.epoch);
+                sync[SYNC_WG0 + g] = to;
                 for (int a = 0; a < 9; a++) Rs[(a / 3) * n + (a % 3)] = R33[a];
                 p.xpre[3 * e + 0] = xp[0];
                 p.xpre[3 * e + 1] = xp[1];
@@ -707,8 +709,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
             while ((v >> 24) != want) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++polls > (1 << 24)) {   // ~seconds: a workgroup never arrived
-                    __hip_atomic_fetch_or(&sync[SYNC_STATUS], EKF_ST_TIMEOUT_BIT, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
+                    status |= EKF_ST_TIMEOUT_BIT;
                     break;
                 }
                 v = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -910,17 +911,23 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
             }
         }
     }
-    // status bits seen by this workgroup's threads
+    // status bits seen by this workgroup's threads → its status word (read by ekf_read_results)
+    int wgst = 0;
     {
         int st = status;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) st |= __shfl_xor(st, off, 64);
-        if ((tid & 63) == 0 && st)
-            __hip_atomic_fetch_or(&sync[SYNC_STATUS], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if ((tid & 63) == 0) sh_red[tid >> 6] = st;
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < SCAN_THREADS / 64; w++) wgst |= sh_red[w];
     }
+    if (tid == 0 && !lead) sync[SYNC_WG0 + g] = wgst;
     if (lead) {
         // every workgroup read the robot 3×3 block, pose and savedLineCount at its start
-        wait_all_started(sync, G);
+        wgst |= wait_all_started(sync, G, p.epoch);
+        sync[SYNC_WG0 + g] = wgst;
         y[0] = xp[0];
         y[1] = xp[1];
         y[2] = xp[2];
@@ -1450,6 +1457,205 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_persist_kernel(DowndateP
     }
 }
 
+// f32/f16 flush, persistent 2-workgroups-per-CU form: super-tiles of 4 × 2 tiles (wave w: tile
+// row sbi·4 + w, tile columns sbj·2 + 0..1), two accumulators per wave, single-buffered LDS
+// operands (48 KB: 4 A blocks + 2 B blocks per chunk), two barriers per super-tile. Two
+// independent workgroups per CU (≤ 256 registers per wave) let one workgroup's MFMA chains run
+// while the other stages, waits or streams; prefetch as in flush_f32_persist_kernel.
+constexpr int P2_C = 2;   // tile columns per super-tile
+
+template <typename TS>
+__global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(DowndateParams p)
+{
+    const Dims d = p.d;
+    const int nst = p.nstiles2;
+    const int total = p.E * nst;
+    const int per = (total + 7) / 8;
+    const int xcd = blockIdx.x & 7;
+    const int wpx = gridDim.x >> 3;
+    const int g_end = min(total, (xcd + 1) * per);
+    int g = xcd * per + (blockIdx.x >> 3);
+    if (g >= g_end) return;
+
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int kh = d.kmax / 2;
+    const size_t opstride = (size_t)d.nb * 64 * kh;
+    const TS* Pin = reinterpret_cast<const TS*>(p.Pin);
+    TS* Pout = reinterpret_cast<TS*>(p.Pout);
+    auto info = [&](int gg, PstInfo& t) {
+        t.e = __builtin_amdgcn_readfirstlane(gg / nst);
+        const int li = __builtin_amdgcn_readfirstlane(gg - t.e * nst);
+        const int* rc = reinterpret_cast<const int*>(p.stile2_rc + li);
+        t.sbi = sload(rc);
+        t.sbj = sload(rc + 1);
+#pragma unroll
+        for (int q = 0; q < PST_MAXC; q++) {
+            t.reset[q] = 0;
+            t.ks[q] = 0;
+            t.nadd[q] = 0;
+            t.s0[q] = 0;
+            if (q < p.nsteps) {
+                const int* r = p.steps[q].res + (size_t)t.e * RES_STRIDE;
+                t.reset[q] = sload(r + RES_RESET);
+                t.ks[q] = t.reset[q] ? 0 : sload(r + RES_KSTEPS);
+                t.nadd[q] = sload(r + RES_NADD);
+                t.s0[q] = sload(r + RES_SAVED_IN);
+            }
+        }
+    };
+    auto tile_off = [&](const PstInfo& t, int c, bool& valid) {
+        const int bi = t.sbi * DD_SB + w, bj = t.sbj * P2_C + c;
+        valid = bi < d.nb && bj < d.nb && bi <= bj;
+        return valid ? ((size_t)t.e * d.ntiles + tile_index(bi, bj, d.nb)) * TILE_ELEMS : (size_t)0;
+    };
+    // staging slot j < 3 of a chunk: float4 i = tid + 256 j of [A: 4 blocks × 2 × 64 | B: 2 × 2 × 64]
+    auto fetch = [&](const PstInfo& t, f32x4 opreg[PST_MAXC][3], f32x4 pref[P2_C][4]) {
+#pragma unroll
+        for (int c = 0; c < PST_MAXC; c++) {
+            const int qc = t.ks[c] > 0 ? c : 0;
+            const float* U = reinterpret_cast<const float*>(p.steps[qc].Uop) + t.e * opstride;
+            const float* V = reinterpret_cast<const float*>(p.steps[qc].Vop) + t.e * opstride;
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const int i = threadIdx.x + 256 * j;
+                const int ln = i & 63, s4 = (i >> 6) & 1;
+                const bool isA = i < 512;
+                const int blk = isA ? (i >> 7) : ((i - 512) >> 7);
+                const int rb = min(isA ? t.sbi * DD_SB + blk : t.sbj * P2_C + blk, d.nb - 1);
+                opreg[c][j] = *reinterpret_cast<const f32x4*>((isA ? U : V) + ((size_t)rb * 64 + ln) * kh + 4 * s4);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < P2_C; c++) {
+            bool v;
+            const TS* tl = Pin + tile_off(t, c, v);
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) pref[c][qq] = tile_ld(tl, lane, qq);
+        }
+    };
+
+    __shared__ f32x4 ldsA[PST_MAXC][DD_SB][2][64];   // 32 KB
+    __shared__ f32x4 ldsB[PST_MAXC][P2_C][2][64];    // 16 KB
+
+    PstInfo cur;
+    info(g, cur);
+    f32x4 opreg[PST_MAXC][3];
+    f32x4 pref[P2_C][4];
+    fetch(cur, opreg, pref);
+    f32x16 acc[P2_C];
+
+    while (true) {
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS free
+#pragma unroll
+        for (int c = 0; c < PST_MAXC; c++) {
+            if (cur.ks[c] > 0) {
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    const int i = threadIdx.x + 256 * j;
+                    const int ln = i & 63, s4 = (i >> 6) & 1;
+                    if (i < 512) ldsA[c][i >> 7][s4][ln] = opreg[c][j];
+                    else ldsB[c][(i - 512) >> 7][s4][ln] = opreg[c][j];
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS written
+#pragma unroll
+        for (int c = 0; c < P2_C; c++)
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) {
+                acc[c][4 * qq + 0] = pref[c][qq][0];
+                acc[c][4 * qq + 1] = pref[c][qq][1];
+                acc[c][4 * qq + 2] = pref[c][qq][2];
+                acc[c][4 * qq + 3] = pref[c][qq][3];
+            }
+        const int gn = g + wpx;
+        const bool more = gn < g_end;
+        PstInfo nxt;
+        info(more ? gn : g, nxt);
+        fetch(nxt, opreg, pref);
+
+        const int e = cur.e;
+        const int bi = cur.sbi * DD_SB + w;
+        int vmask = 0;
+#pragma unroll
+        for (int c = 0; c < P2_C; c++) {
+            bool v;
+            (void)tile_off(cur, c, v);
+            vmask |= (int)v << c;
+        }
+        auto post = [&](int q) {
+            if (cur.reset[q]) {
+#pragma unroll
+                for (int c = 0; c < P2_C; c++)
+#pragma unroll
+                    for (int k = 0; k < 16; k++) acc[c][k] = 0.f;
+                return;
+            }
+            const int nadd = cur.nadd[q], s0 = cur.s0[q];
+            if (nadd <= 0 || (cur.sbj + 1) * P2_C * 16 <= s0 || cur.sbj * P2_C * 16 >= s0 + nadd) return;
+            const double* prw0 = p.steps[q].patch + (size_t)e * d.max_lines * 2 * d.M;
+            const double* pdg = p.steps[q].patch_diag + (size_t)e * d.max_lines * 4;
+#pragma nounroll
+            for (int c = 0; c < P2_C; c++) {
+                const int bj = cur.sbj * P2_C + c;
+                if (((vmask >> c) & 1) && bj * 16 + 15 >= s0 && bj * 16 < s0 + nadd) {
+                    const int col = bj * 32 + (lane & 31);
+#pragma unroll
+                    for (int k = 0; k < 16; k++) {
+                        const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
+                        const int hi = max(row >> 1, col >> 1);
+                        if (hi >= s0 && hi < s0 + nadd)
+                            acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s0, row, col)));
+                    }
+                }
+                const f32x16 t0 = acc[0];
+                acc[0] = acc[1];
+                acc[1] = t0;
+            }
+        };
+#pragma unroll
+        for (int q = 0; q < PST_MAXC; q++) {
+            if (q >= p.nsteps) break;
+            const int kc = cur.ks[q];
+            if (kc > 0) {
+                const f32x4 a0 = ldsA[q][w][0][lane];
+                const f32x4 a1 = ldsA[q][w][1][lane];
+                f32x4 b0[P2_C], b1[P2_C];
+#pragma unroll
+                for (int cc = 0; cc < P2_C; cc++) {
+                    b0[cc] = ldsB[q][cc][0][lane];
+                    b1[cc] = ldsB[q][cc][1][lane];
+                }
+#pragma unroll
+                for (int s = 0; s < SBK; s++)
+                    if (s < kc) {
+#pragma unroll
+                        for (int cc = 0; cc < P2_C; cc++)
+                            acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(s < 4 ? a0[s & 3] : a1[s & 3],
+                                                                           s < 4 ? b0[cc][s & 3] : b1[cc][s & 3],
+                                                                           acc[cc], 0, 0, 0);
+                    }
+#pragma unroll
+                for (int cc = 0; cc < P2_C; cc++) round_acc<TS>(acc[cc]);
+            }
+            post(q);
+        }
+#pragma unroll
+        for (int c = 0; c < P2_C; c++) {
+            bool v;
+            const size_t off = tile_off(cur, c, v);
+            if (v) {
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) tile_st(Pout + off, lane, qq, acc[c]);
+            }
+        }
+        if (!more) break;
+        g = gn;
+        cur = nxt;
+    }
+}
+
 __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams p)
 {
     const Dims d = p.d;
@@ -1665,7 +1871,13 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     }
     const bool half = precision == EKF_PREC_F16;
     const bool persist_ok = p.nsteps <= PST_MAXC && p.d.kmax <= 16 && p.variant != 2;
-    if (persist_ok) {
+    if (persist_ok && p.variant != 3) {
+        const int pgrid = 16 * ((p.ncu + 7) / 8);   // two workgroups per CU (48 KB LDS each)
+        if (half)
+            hipLaunchKernelGGL(flush_f32_persist2_kernel<_Float16>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+        else
+            hipLaunchKernelGGL(flush_f32_persist2_kernel<float>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+    } else if (persist_ok) {
         const int pgrid = 8 * ((p.ncu + 7) / 8);   // one workgroup per CU (128 KB LDS)
         if (half)
             hipLaunchKernelGGL(flush_f32_persist_kernel<_Float16>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
