@@ -144,8 +144,9 @@ int ekf_get_ellipse(ekf_ctx* ctx, int e, float axii[2], float* angle);
 /* Introspection for the benchmark's roofline accounting. */
 size_t ekf_landmark_block_bytes(const ekf_ctx* ctx); /* stored bytes of P_ll per instance */
 int ekf_state_dim(const ekf_ctx* ctx);                /* n */
-/* Per-kernel HIP-event timing on the stream each kernel runs on (0 = off). Averages are over
- * the launches recorded since the last enable: scan_ms = association kernel, downdate_ms = the
+/* Per-kernel HIP-event timing on the stream each kernel runs on: enable 0 = off, 1 = the flush
+ * only (2 events per flush), 2 = also every association kernel. Averages are over the launches
+ * recorded since the last enable: scan_ms = association kernel (level 2), downdate_ms = the
  * landmark-block flush, augment_ms = 0 (augmentation is fused into the flush), launches =
  * flushes. */
 int ekf_profile_enable(ekf_ctx* ctx, int enable);

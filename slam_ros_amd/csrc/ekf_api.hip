@@ -401,9 +401,11 @@ extern "C" int ekf_reset_instance(ekf_ctx* c, int e, double x, double y, double 
     return set_robot_ctor(c, e, x, y, th);
 }
 
+// profiling level 1 times the flush only (what the roofline needs, 2 events per group);
+// level 2 also every association kernel
 static EvPair* prof_begin(ekf_ctx* c, int kind, hipStream_t st)
 {
-    if (!c->prof) return nullptr;
+    if (!c->prof || (kind == 0 && c->prof < 2)) return nullptr;
     EvPair pr;
     if (!c->pool.empty()) {
         pr = c->pool.back();
@@ -801,7 +803,7 @@ extern "C" int ekf_profile_enable(ekf_ctx* c, int enable)
         for (auto& pr : v) c->pool.push_back(pr);
         v.clear();
     }
-    c->prof = enable ? 1 : 0;
+    c->prof = enable < 0 ? 0 : (enable > 2 ? 2 : enable);
     return EKF_OK;
 }
 

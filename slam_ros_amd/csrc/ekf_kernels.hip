@@ -490,6 +490,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     __shared__ ekf_line sh_lines[EKF_MAX_LINES];
     // U_q rows of the owned landmark for the first HIST_LDS matches of the scan (the rest in Ust)
     __shared__ double4 sh_uhist[HIST_LDS][SCAN_THREADS];
+    __shared__ double4 sh_vhist[HIST_LDS][SCAN_THREADS];   // V_q rows, for the package
     unsigned long long* dbg = (p.dbg && lead) ? p.dbg + (size_t)e * 16 : nullptr;
     unsigned long long t_last = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const unsigned long long t_first = t_last;
@@ -683,7 +684,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
                 mb_store(slot + MB_UR + 2 * a + 1, k0 * c.S[1] + k1 * c.S[3]);
             }
             for (int q = 0; q < m; q++) {
-                const double4 vq = *reinterpret_cast<const double4*>(Vst + ((size_t)q * n + b0) * 2);
+                const double4 vq = q < HIST_LDS ? sh_vhist[q][tid]
+                                                : *reinterpret_cast<const double4*>(Vst + ((size_t)q * n + b0) * 2);
                 mb_store(slot + MB_VH + 4 * q + 0, vq.x);
                 mb_store(slot + MB_VH + 4 * q + 1, vq.y);
                 mb_store(slot + MB_VH + 4 * q + 2, vq.z);
@@ -735,8 +737,17 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
             continue;
         }
         // ---- match (Robot.cpp:500-641) ----
+        // the winner's package and this thread's block of column jstar are independent: issue both
+        // loads before waiting on either
         const double* ps = mbox + ((size_t)par * G + gstar) * p.mbw;
-        for (int k = tid; k < MB_VH + 4 * m; k += SCAN_THREADS) sh_pkg[k] = mb_load(ps + k);
+        const int npk = MB_VH + 4 * m;
+        double pk0 = 0.0, pk1 = 0.0;
+        if (tid < npk) pk0 = mb_load(ps + tid);
+        if (tid + SCAN_THREADS < npk) pk1 = mb_load(ps + tid + SCAN_THREADS);
+        double blk[4] = {0.0, 0.0, 0.0, 0.0};
+        if (own) pll_block(pv, 2 * j, 2 * jstar, blk);
+        if (tid < npk) sh_pkg[tid] = pk0;
+        if (tid + SCAN_THREADS < npk) sh_pkg[tid + SCAN_THREADS] = pk1;
         __syncthreads();
         const double S0 = sh_pkg[MB_S], S1 = sh_pkg[MB_S + 1], S2 = sh_pkg[MB_S + 2], S3 = sh_pkg[MB_S + 3];
         const double Si0 = sh_pkg[MB_SI], Si1 = sh_pkg[MB_SI + 1], Si2 = sh_pkg[MB_SI + 2], Si3 = sh_pkg[MB_SI + 3];
@@ -753,8 +764,6 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
 
         // owned landmark rows
         if (own) {
-            double blk[4];
-            pll_block(pv, 2 * j, 2 * jstar, blk);
             for (int q = 0; q < t; q++) {   // earlier matches of this scan, in order
                 const double4 uq = q < HIST_LDS ? sh_uhist[q][tid]
                                                 : *reinterpret_cast<const double4*>(Ust + ((size_t)q * n + b0) * 2);
@@ -786,7 +795,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
                 sh_uhist[t][tid] = make_double4(uu[0], uu[1], uu[2], uu[3]);
             else
                 *reinterpret_cast<double4*>(Ust + ((size_t)t * n + b0) * 2) = make_double4(uu[0], uu[1], uu[2], uu[3]);
-            *reinterpret_cast<double4*>(Vst + ((size_t)t * n + b0) * 2) = make_double4(kk[0], kk[1], kk[2], kk[3]);
+            if (t < HIST_LDS)
+                sh_vhist[t][tid] = make_double4(kk[0], kk[1], kk[2], kk[3]);
+            else
+                *reinterpret_cast<double4*>(Vst + ((size_t)t * n + b0) * 2) = make_double4(kk[0], kk[1], kk[2], kk[3]);
 #pragma unroll
             for (int pp = 0; pp < 2; pp++) {
                 const int lr = 2 * j + pp;

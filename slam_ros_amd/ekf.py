@@ -273,8 +273,11 @@ class Ensemble:
     def landmark_block_bytes(self) -> int:
         return int(self._lib.ekf_landmark_block_bytes(self._h))
 
-    def profile(self, enable: bool = True):
-        _check(self._lib.ekf_profile_enable(self._h, int(enable)), "ekf_profile_enable")
+    def profile(self, level: int = 2):
+        """HIP-event timing: 0 off, 1 the flush only, 2 also every association kernel
+        (True = 2)."""
+        level = 2 if level is True else int(level)
+        _check(self._lib.ekf_profile_enable(self._h, level), "ekf_profile_enable")
 
     def profile_read(self):
         s, dd, a = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
