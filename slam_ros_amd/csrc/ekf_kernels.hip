@@ -1473,8 +1473,15 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_persist_kernel(DowndateP
 // row sbi·4 + w, tile columns sbj·2 + 0..1), two accumulators per wave, single-buffered LDS
 // operands (48 KB: 4 A blocks + 2 B blocks per chunk), two barriers per super-tile. Two
 // independent workgroups per CU (≤ 256 registers per wave) let one workgroup's MFMA chains run
-// while the other stages, waits or streams; prefetch as in flush_f32_persist_kernel.
+// while the other stages, waits or streams. Per super-tile the control is four scalar words
+// (instance, super-tile, packed step flags); when every step of the group is a full 8-k-step
+// downdate with nothing else to apply (the steady state) the MFMA block runs without predicates.
 constexpr int P2_C = 2;   // tile columns per super-tile
+
+struct P2Info {
+    int e, sbi, sbj;
+    int flags;   // per step q, byte q: bits 0-3 ks, bit 4 reset, bit 5 augmented rows present
+};
 
 template <typename TS>
 __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(DowndateParams p)
@@ -1495,48 +1502,47 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
     const size_t opstride = (size_t)d.nb * 64 * kh;
     const TS* Pin = reinterpret_cast<const TS*>(p.Pin);
     TS* Pout = reinterpret_cast<TS*>(p.Pout);
-    auto info = [&](int gg, PstInfo& t) {
-        t.e = __builtin_amdgcn_readfirstlane(gg / nst);
-        const int li = __builtin_amdgcn_readfirstlane(gg - t.e * nst);
+    const int nsteps = p.nsteps;
+    // this thread's staging slots j < 3 of a chunk: float4 i = tid + 256 j of
+    // [A: 4 blocks × 2 × 64 | B: 2 blocks × 2 × 64]; offsets inside a block row are invariant
+    const int ln = threadIdx.x & 63, s4 = (threadIdx.x >> 6) & 1, bl = threadIdx.x >> 7;
+    const int in_blk = ln * kh + 4 * s4;
+
+    auto load_flags = [&](P2Info& t) {
+        int f = 0;
+#pragma unroll
+        for (int q = 0; q < PST_MAXC; q++) {
+            if (q < nsteps) {
+                const int* r = p.steps[q].res + (size_t)t.e * RES_STRIDE;
+                const int reset = sload(r + RES_RESET);
+                const int ks = reset ? 0 : sload(r + RES_KSTEPS);
+                const int nadd = sload(r + RES_NADD);
+                f |= ((ks & 15) | (reset ? 16 : 0) | (nadd > 0 ? 32 : 0)) << (8 * q);
+            }
+        }
+        t.flags = f;
+    };
+    auto locate = [&](int li, P2Info& t) {
         const int* rc = reinterpret_cast<const int*>(p.stile2_rc + li);
         t.sbi = sload(rc);
         t.sbj = sload(rc + 1);
-#pragma unroll
-        for (int q = 0; q < PST_MAXC; q++) {
-            t.reset[q] = 0;
-            t.ks[q] = 0;
-            t.nadd[q] = 0;
-            t.s0[q] = 0;
-            if (q < p.nsteps) {
-                const int* r = p.steps[q].res + (size_t)t.e * RES_STRIDE;
-                t.reset[q] = sload(r + RES_RESET);
-                t.ks[q] = t.reset[q] ? 0 : sload(r + RES_KSTEPS);
-                t.nadd[q] = sload(r + RES_NADD);
-                t.s0[q] = sload(r + RES_SAVED_IN);
-            }
-        }
     };
-    auto tile_off = [&](const PstInfo& t, int c, bool& valid) {
+    auto tile_off = [&](const P2Info& t, int c, bool& valid) {
         const int bi = t.sbi * DD_SB + w, bj = t.sbj * P2_C + c;
         valid = bi < d.nb && bj < d.nb && bi <= bj;
         return valid ? ((size_t)t.e * d.ntiles + tile_index(bi, bj, d.nb)) * TILE_ELEMS : (size_t)0;
     };
-    // staging slot j < 3 of a chunk: float4 i = tid + 256 j of [A: 4 blocks × 2 × 64 | B: 2 × 2 × 64]
-    auto fetch = [&](const PstInfo& t, f32x4 opreg[PST_MAXC][3], f32x4 pref[P2_C][4]) {
+    auto fetch = [&](const P2Info& t, f32x4 opreg[PST_MAXC][3], f32x4 pref[P2_C][4]) {
+        const int rA0 = min(t.sbi * DD_SB + bl, d.nb - 1), rA1 = min(t.sbi * DD_SB + 2 + bl, d.nb - 1);
+        const int rB = min(t.sbj * P2_C + bl, d.nb - 1);   // rows past the block: unused
 #pragma unroll
         for (int c = 0; c < PST_MAXC; c++) {
-            const int qc = t.ks[c] > 0 ? c : 0;
+            const int qc = ((t.flags >> (8 * c)) & 15) ? c : 0;   // absent steps re-read step 0
             const float* U = reinterpret_cast<const float*>(p.steps[qc].Uop) + t.e * opstride;
             const float* V = reinterpret_cast<const float*>(p.steps[qc].Vop) + t.e * opstride;
-#pragma unroll
-            for (int j = 0; j < 3; j++) {
-                const int i = threadIdx.x + 256 * j;
-                const int ln = i & 63, s4 = (i >> 6) & 1;
-                const bool isA = i < 512;
-                const int blk = isA ? (i >> 7) : ((i - 512) >> 7);
-                const int rb = min(isA ? t.sbi * DD_SB + blk : t.sbj * P2_C + blk, d.nb - 1);
-                opreg[c][j] = *reinterpret_cast<const f32x4*>((isA ? U : V) + ((size_t)rb * 64 + ln) * kh + 4 * s4);
-            }
+            opreg[c][0] = *reinterpret_cast<const f32x4*>(U + (size_t)rA0 * 64 * kh + in_blk);
+            opreg[c][1] = *reinterpret_cast<const f32x4*>(U + (size_t)rA1 * 64 * kh + in_blk);
+            opreg[c][2] = *reinterpret_cast<const f32x4*>(V + (size_t)rB * 64 * kh + in_blk);
         }
 #pragma unroll
         for (int c = 0; c < P2_C; c++) {
@@ -1550,25 +1556,28 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
     __shared__ f32x4 ldsA[PST_MAXC][DD_SB][2][64];   // 32 KB
     __shared__ f32x4 ldsB[PST_MAXC][P2_C][2][64];    // 16 KB
 
-    PstInfo cur;
-    info(g, cur);
+    P2Info cur;
+    cur.e = __builtin_amdgcn_readfirstlane(g / nst);
+    int li = __builtin_amdgcn_readfirstlane(g - cur.e * nst);
+    locate(li, cur);
+    load_flags(cur);
     f32x4 opreg[PST_MAXC][3];
     f32x4 pref[P2_C][4];
     fetch(cur, opreg, pref);
     f32x16 acc[P2_C];
+    // steady state: every step of the group a full chunk, no reset, no augmented rows
+    int steady = 0;
+#pragma unroll
+    for (int q = 0; q < PST_MAXC; q++) steady |= (q < nsteps ? SBK : 0) << (8 * q);
 
     while (true) {
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS free
 #pragma unroll
         for (int c = 0; c < PST_MAXC; c++) {
-            if (cur.ks[c] > 0) {
-#pragma unroll
-                for (int j = 0; j < 3; j++) {
-                    const int i = threadIdx.x + 256 * j;
-                    const int ln = i & 63, s4 = (i >> 6) & 1;
-                    if (i < 512) ldsA[c][i >> 7][s4][ln] = opreg[c][j];
-                    else ldsB[c][(i - 512) >> 7][s4][ln] = opreg[c][j];
-                }
+            if ((cur.flags >> (8 * c)) & 15) {
+                ldsA[c][bl][s4][ln] = opreg[c][0];
+                ldsA[c][2 + bl][s4][ln] = opreg[c][1];
+                ldsB[c][bl][s4][ln] = opreg[c][2];
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS written
@@ -1581,77 +1590,115 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
                 acc[c][4 * qq + 2] = pref[c][qq][2];
                 acc[c][4 * qq + 3] = pref[c][qq][3];
             }
+        // next super-tile in flight (the last iteration re-reads its own)
         const int gn = g + wpx;
         const bool more = gn < g_end;
-        PstInfo nxt;
-        info(more ? gn : g, nxt);
+        P2Info nxt;
+        nxt.e = cur.e;
+        int lin = li;
+        if (more) {
+            lin += wpx;
+            while (lin >= nst) {
+                lin -= nst;
+                nxt.e++;
+            }
+        }
+        locate(lin, nxt);
+        load_flags(nxt);
         fetch(nxt, opreg, pref);
 
         const int e = cur.e;
         const int bi = cur.sbi * DD_SB + w;
-        int vmask = 0;
+        if (cur.flags == steady) {
 #pragma unroll
-        for (int c = 0; c < P2_C; c++) {
-            bool v;
-            (void)tile_off(cur, c, v);
-            vmask |= (int)v << c;
-        }
-        auto post = [&](int q) {
-            if (cur.reset[q]) {
+            for (int q = 0; q < PST_MAXC; q++) {
+                if (q < nsteps) {
+                    const f32x4 a0 = ldsA[q][w][0][lane];
+                    const f32x4 a1 = ldsA[q][w][1][lane];
+                    const f32x4 b00 = ldsB[q][0][0][lane], b01 = ldsB[q][0][1][lane];
+                    const f32x4 b10 = ldsB[q][1][0][lane], b11 = ldsB[q][1][1][lane];
 #pragma unroll
-                for (int c = 0; c < P2_C; c++)
+                    for (int s = 0; s < 4; s++) {
+                        acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b00[s], acc[0], 0, 0, 0);
+                        acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b10[s], acc[1], 0, 0, 0);
+                    }
 #pragma unroll
-                    for (int k = 0; k < 16; k++) acc[c][k] = 0.f;
-                return;
+                    for (int s = 0; s < 4; s++) {
+                        acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b01[s], acc[0], 0, 0, 0);
+                        acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b11[s], acc[1], 0, 0, 0);
+                    }
+                    round_acc<TS>(acc[0]);
+                    round_acc<TS>(acc[1]);
+                }
             }
-            const int nadd = cur.nadd[q], s0 = cur.s0[q];
-            if (nadd <= 0 || (cur.sbj + 1) * P2_C * 16 <= s0 || cur.sbj * P2_C * 16 >= s0 + nadd) return;
-            const double* prw0 = p.steps[q].patch + (size_t)e * d.max_lines * 2 * d.M;
-            const double* pdg = p.steps[q].patch_diag + (size_t)e * d.max_lines * 4;
-#pragma nounroll
+        } else {
+            int vmask = 0;
+#pragma unroll
             for (int c = 0; c < P2_C; c++) {
-                const int bj = cur.sbj * P2_C + c;
-                if (((vmask >> c) & 1) && bj * 16 + 15 >= s0 && bj * 16 < s0 + nadd) {
-                    const int col = bj * 32 + (lane & 31);
-#pragma unroll
-                    for (int k = 0; k < 16; k++) {
-                        const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
-                        const int hi = max(row >> 1, col >> 1);
-                        if (hi >= s0 && hi < s0 + nadd)
-                            acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s0, row, col)));
-                    }
-                }
-                const f32x16 t0 = acc[0];
-                acc[0] = acc[1];
-                acc[1] = t0;
+                bool v;
+                (void)tile_off(cur, c, v);
+                vmask |= (int)v << c;
             }
-        };
+            auto post = [&](int q) {
+                const int fq = (cur.flags >> (8 * q)) & 255;
+                if (fq & 16) {
 #pragma unroll
-        for (int q = 0; q < PST_MAXC; q++) {
-            if (q >= p.nsteps) break;
-            const int kc = cur.ks[q];
-            if (kc > 0) {
-                const f32x4 a0 = ldsA[q][w][0][lane];
-                const f32x4 a1 = ldsA[q][w][1][lane];
-                f32x4 b0[P2_C], b1[P2_C];
+                    for (int c = 0; c < P2_C; c++)
 #pragma unroll
-                for (int cc = 0; cc < P2_C; cc++) {
-                    b0[cc] = ldsB[q][cc][0][lane];
-                    b1[cc] = ldsB[q][cc][1][lane];
+                        for (int k = 0; k < 16; k++) acc[c][k] = 0.f;
+                    return;
                 }
+                if (!(fq & 32)) return;
+                const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
+                const int nadd = sload(r + RES_NADD), s0 = sload(r + RES_SAVED_IN);
+                if ((cur.sbj + 1) * P2_C * 16 <= s0 || cur.sbj * P2_C * 16 >= s0 + nadd) return;
+                const double* prw0 = p.steps[q].patch + (size_t)e * d.max_lines * 2 * d.M;
+                const double* pdg = p.steps[q].patch_diag + (size_t)e * d.max_lines * 4;
+#pragma nounroll
+                for (int c = 0; c < P2_C; c++) {
+                    const int bj = cur.sbj * P2_C + c;
+                    if (((vmask >> c) & 1) && bj * 16 + 15 >= s0 && bj * 16 < s0 + nadd) {
+                        const int col = bj * 32 + (lane & 31);
 #pragma unroll
-                for (int s = 0; s < SBK; s++)
-                    if (s < kc) {
+                        for (int k = 0; k < 16; k++) {
+                            const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
+                            const int hi = max(row >> 1, col >> 1);
+                            if (hi >= s0 && hi < s0 + nadd)
+                                acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s0, row, col)));
+                        }
+                    }
+                    const f32x16 t0 = acc[0];
+                    acc[0] = acc[1];
+                    acc[1] = t0;
+                }
+            };
 #pragma unroll
-                        for (int cc = 0; cc < P2_C; cc++)
-                            acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(s < 4 ? a0[s & 3] : a1[s & 3],
-                                                                           s < 4 ? b0[cc][s & 3] : b1[cc][s & 3],
-                                                                           acc[cc], 0, 0, 0);
+            for (int q = 0; q < PST_MAXC; q++) {
+                if (q >= nsteps) break;
+                const int kc = (cur.flags >> (8 * q)) & 15;
+                if (kc > 0) {
+                    const f32x4 a0 = ldsA[q][w][0][lane];
+                    const f32x4 a1 = ldsA[q][w][1][lane];
+                    f32x4 b0[P2_C], b1[P2_C];
+#pragma unroll
+                    for (int cc = 0; cc < P2_C; cc++) {
+                        b0[cc] = ldsB[q][cc][0][lane];
+                        b1[cc] = ldsB[q][cc][1][lane];
                     }
 #pragma unroll
-                for (int cc = 0; cc < P2_C; cc++) round_acc<TS>(acc[cc]);
+                    for (int s = 0; s < SBK; s++)
+                        if (s < kc) {
+#pragma unroll
+                            for (int cc = 0; cc < P2_C; cc++)
+                                acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(s < 4 ? a0[s & 3] : a1[s & 3],
+                                                                               s < 4 ? b0[cc][s & 3] : b1[cc][s & 3],
+                                                                               acc[cc], 0, 0, 0);
+                        }
+#pragma unroll
+                    for (int cc = 0; cc < P2_C; cc++) round_acc<TS>(acc[cc]);
+                }
+                post(q);
             }
-            post(q);
         }
 #pragma unroll
         for (int c = 0; c < P2_C; c++) {
@@ -1664,6 +1711,7 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
         }
         if (!more) break;
         g = gn;
+        li = lin;
         cur = nxt;
     }
 }
