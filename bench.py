@@ -9,10 +9,12 @@ RCCL/xGMI; every rank runs its slice of instances (no other collective on the da
 Inputs are resident in HBM before the timed region. `value` = instances × steps (all ranks)
 ÷ max-over-ranks wall time of the K timed steps.
 
-Schedule (defaults): the landmark block is flushed once per T = 4 scans (flush_interval) and the
-flush overlaps the next scans' association (pipeline); both are bit-identical to a per-scan
-in-place update (tests/test_gpu_parity.py::test_deferred_flush_equals_drained). The timed region
-ends with ekf_sync, which flushes the partial group: every step's downdate is in P.
+Schedule (defaults): the landmark block is flushed once per T = 4 scans (flush_interval), in
+place, between association kernels (--pipeline 1 overlaps them instead); every schedule is
+bit-identical to a per-scan in-place update (tests/test_gpu_parity.py::
+test_deferred_flush_equals_drained). The timed region ends with ekf_sync, which flushes the
+partial group: every step's downdate is in P. HIP events in the timed region bracket the flush
+kernel only; the association-kernel time is measured on extra steps after it.
 
 roofline: the dominant kernel is the covariance flush (rank-2m MFMA downdate of every step of the
 group, one read + write of the packed block). Per launch: algorithmic bytes = instances_per_gpu ×
@@ -222,7 +224,7 @@ def main():
             "frac": ((gbs / HBM_PEAK_GBS) if bound == "hbm" else (tfs / mfma_peak)) if dd_ms > 0 else None,
             "traffic": traffic,
             "kernel": ("downdate_f64_kernel" if prec == ekf.PREC_F64 else
-                       "flush_f32_persist_kernel" if args.flush_interval <= 4 else "flush_f32_sb_kernel"),
+                       "flush_f32_persist2_kernel" if args.flush_interval <= 4 else "flush_f32_sb_kernel"),
             "alg_bytes_per_launch": alg_bytes,
             "alg_flops_per_launch": alg_flops,
             "steps_per_launch": steps_per_launch,
