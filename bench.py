@@ -60,6 +60,11 @@ def parse():
                     help="1: overlap the association kernels with the previous group's flush")
     ap.add_argument("--flush-interval", type=int, default=4,
                     help="T: rewrite the landmark block once per T scans (bit-identical state)")
+    ap.add_argument("--bcast-every", type=int, default=0,
+                    help="scans per broadcast (default: the flush interval); broadcasts run one "
+                         "group ahead of the scans that use them")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL on ROCm); gloo only to rehearse ranks on one GPU")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return ap.parse_args()
 
@@ -79,10 +84,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("BENCH_SAME_DEVICE") == "1":   # rehearsal: every rank on device 0
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     N, E, K, W = args.capacity, args.instances, args.steps, args.warmup
     prec = {"f32": ekf.PREC_F32, "f64": ekf.PREC_F64, "f16": ekf.PREC_F16}[args.precision]
@@ -112,18 +122,48 @@ def main():
             enc, lines, _ = G.make_scan(world_map, s + 1, instances=E_total, lines=L_LINES)
             host[s] = D.pack(enc, lines)
         payload.copy_(torch.from_numpy(host))
-    recv = payload if world == 1 else torch.empty((2, per_step), dtype=torch.float64, device=dev)
     nlines = torch.full((E,), L_LINES, dtype=torch.int32, device=dev)
+    # N > 1: rank 0 broadcasts B scans (all instances) per collective, one group ahead of the
+    # scans that use them; double-buffered receive groups
+    B = max(1, args.bcast_every or args.flush_interval)
+    recv = torch.empty((2, B, per_step), dtype=torch.float64, device=dev) if world > 1 else None
+    inflight = {}
+
+    host_coll = world > 1 and args.dist_backend != "nccl"   # rehearsal: collectives on host tensors
+
+    class _Done:
+        def wait(self):
+            pass
+
+    def issue(gi):
+        if world == 1 or gi * B >= steps_total:
+            return
+        buf = recv[gi & 1]
+        cnt = min(B, steps_total - gi * B)
+        if host_coll:
+            torch.cuda.synchronize(dev)   # the group's previous user of this buffer is done
+            hb = (payload[gi * B: gi * B + cnt].cpu() if rank == 0
+                  else torch.empty((cnt, per_step), dtype=torch.float64))
+            D.broadcast_step(hb, dist, src=0)
+            buf[:cnt].copy_(hb[:cnt].to(dev))
+            inflight[gi] = _Done()
+            return
+        if rank == 0:
+            buf[:cnt].copy_(payload[gi * B: gi * B + cnt], non_blocking=True)
+        inflight[gi] = D.broadcast_async(buf, dist, src=0)
+
+    issue(0)
     torch.cuda.synchronize(dev)
 
     def step(s):
         if world == 1:
             buf = payload[s]
         else:
-            buf = recv[s & 1]
-            if rank == 0:
-                buf.copy_(payload[s], non_blocking=True)
-            D.broadcast_step(buf, dist, src=0)
+            gi, k = divmod(s, B)
+            if k == 0:
+                inflight.pop(gi).wait()   # the current stream waits for this group's scans
+                issue(gi + 1)             # the next group's broadcast overlaps these steps
+            buf = recv[gi & 1][k]
         base = buf.data_ptr()
         eo, lo = D.offsets(E_total, L_LINES, first)
         enc_ptr = base + eo * 8
@@ -159,7 +199,7 @@ def main():
     scan_ms = ens.profile_read()["scan_ms"]
     ens.profile(0)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if host_coll else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -167,7 +207,7 @@ def main():
     all_matched = all(r["matches"] == L_LINES and r["saved"] == st.saved and not r["reset"]
                       for r in res)
     if world > 1:
-        ok = torch.tensor([1 if all_matched else 0], dtype=torch.int32, device=dev)
+        ok = torch.tensor([1 if all_matched else 0], dtype=torch.int32, device="cpu" if host_coll else dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         all_matched = bool(ok.item())
 
@@ -213,7 +253,9 @@ def main():
             "workload": f"N={N} landmarks (n={n}), {E} EKF instances/GPU, L=m={L_LINES} matched "
                         f"lines/scan, s=N-10 active, {args.precision} covariance storage",
             "capacity": N, "instances_per_gpu": E, "global_batch": E_total,
-            "lines_per_scan": L_LINES, "parallelism": f"ensemble x{world} (RCCL broadcast of scans)",
+            "lines_per_scan": L_LINES,
+            "parallelism": (f"ensemble x{world} ({'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} "
+                            f"broadcast of {B} scans per collective)") if world > 1 else "ensemble x1",
             "pipeline": bool(args.pipeline), "flush_interval": args.flush_interval,
         },
         "roofline": {

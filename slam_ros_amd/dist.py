@@ -56,3 +56,9 @@ def unpack_slice(buf, E_total: int, L: int, first: int, count: int):
 def broadcast_step(buf, dist, src: int = 0) -> None:
     """The one exchange of a step: the sensor rank's payload to every rank (in place)."""
     dist.broadcast(buf, src=src)
+
+
+def broadcast_async(buf, dist, src: int = 0):
+    """Same for a group of steps, asynchronously; `.wait()` on the returned work orders the
+    caller's current stream after it (NCCL/RCCL) or blocks until it is done (gloo)."""
+    return dist.broadcast(buf, src=src, async_op=True)
