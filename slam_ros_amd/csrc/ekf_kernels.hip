@@ -658,19 +658,19 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         for (int w = 1; w < SCAN_THREADS / 64; w++) gbest = min(gbest, sh_red[w]);
         const int par = i & 1;
         double* slot = mbox + ((size_t)par * G + g) * p.mbw;
+        const int npk = MB_VH + 4 * m;
         if (best != 0x7fffffff && best == gbest) {
             // this workgroup's candidate: the uniform gain package of the robot rows
             // (Robot.cpp:522-602 for rows 0..2) and the V rows of the candidate for the
-            // earlier matches of this scan (Robot.cpp:560-568 corrections)
+            // earlier matches of this scan (Robot.cpp:560-568 corrections), staged in LDS
             const double RL0[3] = {rr0.x, rr1.x, rr2.x};
             const double RL1[3] = {rr0.y, rr1.y, rr2.y};
-            mb_store(slot + MB_S + 0, c.S[0]); mb_store(slot + MB_S + 1, c.S[1]);
-            mb_store(slot + MB_S + 2, c.S[2]); mb_store(slot + MB_S + 3, c.S[3]);
-            mb_store(slot + MB_SI + 0, c.Si[0]); mb_store(slot + MB_SI + 1, c.Si[1]);
-            mb_store(slot + MB_SI + 2, c.Si[2]); mb_store(slot + MB_SI + 3, c.Si[3]);
-            mb_store(slot + MB_V + 0, c.v[0]); mb_store(slot + MB_V + 1, c.v[1]);
-            mb_store(slot + MB_H + 0, c.h10); mb_store(slot + MB_H + 1, c.h11);
-            mb_store(slot + MB_H + 2, c.h1l);
+            sh_pkg[MB_S + 0] = c.S[0]; sh_pkg[MB_S + 1] = c.S[1];
+            sh_pkg[MB_S + 2] = c.S[2]; sh_pkg[MB_S + 3] = c.S[3];
+            sh_pkg[MB_SI + 0] = c.Si[0]; sh_pkg[MB_SI + 1] = c.Si[1];
+            sh_pkg[MB_SI + 2] = c.Si[2]; sh_pkg[MB_SI + 3] = c.Si[3];
+            sh_pkg[MB_V + 0] = c.v[0]; sh_pkg[MB_V + 1] = c.v[1];
+            sh_pkg[MB_H + 0] = c.h10; sh_pkg[MB_H + 1] = c.h11; sh_pkg[MB_H + 2] = c.h1l;
 #pragma unroll
             for (int a = 0; a < 3; a++) {
                 // W = P·Hᵀ (Robot.cpp:522), K = W·S⁻¹ (:526), U = K·S (:560)
@@ -678,52 +678,61 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
                 const double w1 = c.h10 * R33[a * 3 + 0] + c.h11 * R33[a * 3 + 1] + c.h1l * RL0[a] + RL1[a];
                 const double k0 = w0 * c.Si[0] + w1 * c.Si[2];
                 const double k1 = w0 * c.Si[1] + w1 * c.Si[3];
-                mb_store(slot + MB_KR + 2 * a, k0);
-                mb_store(slot + MB_KR + 2 * a + 1, k1);
-                mb_store(slot + MB_UR + 2 * a, k0 * c.S[0] + k1 * c.S[2]);
-                mb_store(slot + MB_UR + 2 * a + 1, k0 * c.S[1] + k1 * c.S[3]);
+                sh_pkg[MB_KR + 2 * a] = k0;
+                sh_pkg[MB_KR + 2 * a + 1] = k1;
+                sh_pkg[MB_UR + 2 * a] = k0 * c.S[0] + k1 * c.S[2];
+                sh_pkg[MB_UR + 2 * a + 1] = k0 * c.S[1] + k1 * c.S[3];
             }
             for (int q = 0; q < m; q++) {
                 const double4 vq = q < HIST_LDS ? sh_vhist[q][tid]
                                                 : *reinterpret_cast<const double4*>(Vst + ((size_t)q * n + b0) * 2);
-                mb_store(slot + MB_VH + 4 * q + 0, vq.x);
-                mb_store(slot + MB_VH + 4 * q + 1, vq.y);
-                mb_store(slot + MB_VH + 4 * q + 2, vq.z);
-                mb_store(slot + MB_VH + 4 * q + 3, vq.w);
+                sh_pkg[MB_VH + 4 * q + 0] = vq.x;
+                sh_pkg[MB_VH + 4 * q + 1] = vq.y;
+                sh_pkg[MB_VH + 4 * q + 2] = vq.z;
+                sh_pkg[MB_VH + 4 * q + 3] = vq.w;
             }
         }
-        // the package is drained by its writer and ordered by the barrier before the tagged best
-        // word (data-tagged granule: launch epoch, line, best); every workgroup polls all G words
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        // tag: bits 63..32 launch epoch, 31..24 line + 1, 23..0 best + 1 (0: no candidate)
-        const unsigned long long want = ((unsigned long long)p.epoch << 8) | (unsigned)(i + 1);
-        if (tid == 0)
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(slot + MB_BEST),
-                               (want << 24) | (unsigned)(gbest == 0x7fffffff ? 0 : gbest + 1),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        EKF_STAMP(3);
-        for (int k = tid; k < G; k += SCAN_THREADS) {
-            const unsigned long long* tw =
-                reinterpret_cast<const unsigned long long*>(mbox + ((size_t)par * G + k) * p.mbw + MB_BEST);
-            unsigned long long v = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int polls = 0;
-            while ((v >> 24) != want) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++polls > (1 << 24)) {   // ~seconds: a workgroup never arrived
-                    status |= EKF_ST_TIMEOUT_BIT;
-                    break;
+        __syncthreads();   // the staged package
+        int jstar = gbest, gstar = 0;
+        if (G > 1) {
+            // to the mailbox, one word per lane; drained and ordered by the barrier before the
+            // tagged best word (data-tagged granule: launch epoch, line, best); every workgroup
+            // polls all G words
+            if (gbest != 0x7fffffff)
+                for (int k = tid; k < npk; k += SCAN_THREADS) mb_store(slot + k, sh_pkg[k]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            // tag: bits 63..32 launch epoch, 31..24 line + 1, 23..0 best + 1 (0: no candidate)
+            const unsigned long long want = ((unsigned long long)p.epoch << 8) | (unsigned)(i + 1);
+            if (tid == 0)
+                __hip_atomic_store(reinterpret_cast<unsigned long long*>(slot + MB_BEST),
+                                   (want << 24) | (unsigned)(gbest == 0x7fffffff ? 0 : gbest + 1),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            EKF_STAMP(3);
+            for (int k = tid; k < G; k += SCAN_THREADS) {
+                const unsigned long long* tw =
+                    reinterpret_cast<const unsigned long long*>(mbox + ((size_t)par * G + k) * p.mbw + MB_BEST);
+                unsigned long long v = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                int polls = 0;
+                while ((v >> 24) != want) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++polls > (1 << 24)) {   // ~seconds: a workgroup never arrived
+                        status |= EKF_ST_TIMEOUT_BIT;
+                        break;
+                    }
+                    v = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
-                v = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int bq = (int)(v & 0xffffffu);
+                sh_best[k] = bq == 0 ? 0x7fffffff : bq - 1;
             }
-            const int b = (int)(v & 0xffffffu);
-            sh_best[k] = b == 0 ? 0x7fffffff : b - 1;
-        }
-        __syncthreads();
-        int jstar = 0x7fffffff, gstar = 0;
-        for (int k = 0; k < G; k++) {
-            const int v = sh_best[k];
-            if (v < jstar) { jstar = v; gstar = k; }
+            __syncthreads();
+            jstar = 0x7fffffff;
+            for (int k = 0; k < G; k++) {
+                const int v = sh_best[k];
+                if (v < jstar) { jstar = v; gstar = k; }
+            }
+        } else {
+            EKF_STAMP(3);   // one workgroup: the package never leaves LDS
         }
         EKF_STAMP(4);
         if (jstar == 0x7fffffff) {
@@ -738,17 +747,22 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         }
         // ---- match (Robot.cpp:500-641) ----
         // the winner's package and this thread's block of column jstar are independent: issue both
-        // loads before waiting on either
-        const double* ps = mbox + ((size_t)par * G + gstar) * p.mbw;
-        const int npk = MB_VH + 4 * m;
-        double pk0 = 0.0, pk1 = 0.0;
-        if (tid < npk) pk0 = mb_load(ps + tid);
-        if (tid + SCAN_THREADS < npk) pk1 = mb_load(ps + tid + SCAN_THREADS);
+        // loads before waiting on either (another workgroup's winner: every workgroup reloads, its
+        // own staged candidate included)
         double blk[4] = {0.0, 0.0, 0.0, 0.0};
-        if (own) pll_block(pv, 2 * j, 2 * jstar, blk);
-        if (tid < npk) sh_pkg[tid] = pk0;
-        if (tid + SCAN_THREADS < npk) sh_pkg[tid + SCAN_THREADS] = pk1;
-        __syncthreads();
+        if (G > 1) {
+            // (every thread passed the poll barrier after its mailbox stores read sh_pkg)
+            const double* ps = mbox + ((size_t)par * G + gstar) * p.mbw;
+            double pk0 = 0.0, pk1 = 0.0;
+            if (tid < npk) pk0 = mb_load(ps + tid);
+            if (tid + SCAN_THREADS < npk) pk1 = mb_load(ps + tid + SCAN_THREADS);
+            if (own) pll_block(pv, 2 * j, 2 * jstar, blk);
+            if (tid < npk) sh_pkg[tid] = pk0;
+            if (tid + SCAN_THREADS < npk) sh_pkg[tid + SCAN_THREADS] = pk1;
+            __syncthreads();
+        } else if (own) {
+            pll_block(pv, 2 * j, 2 * jstar, blk);
+        }
         const double S0 = sh_pkg[MB_S], S1 = sh_pkg[MB_S + 1], S2 = sh_pkg[MB_S + 2], S3 = sh_pkg[MB_S + 3];
         const double Si0 = sh_pkg[MB_SI], Si1 = sh_pkg[MB_SI + 1], Si2 = sh_pkg[MB_SI + 2], Si3 = sh_pkg[MB_SI + 3];
         const double v0 = sh_pkg[MB_V], v1 = sh_pkg[MB_V + 1];
