@@ -1624,6 +1624,7 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
         const int e = cur.e;
         const int bi = cur.sbi * DD_SB + w;
         if (cur.flags == steady) {
+            __builtin_amdgcn_s_setprio(1);   // this MFMA cluster ahead of the partner's staging
 #pragma unroll
             for (int q = 0; q < PST_MAXC; q++) {
                 if (q < nsteps) {
@@ -1645,6 +1646,7 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
                     round_acc<TS>(acc[1]);
                 }
             }
+            __builtin_amdgcn_s_setprio(0);
         } else {
             int vmask = 0;
 #pragma unroll
