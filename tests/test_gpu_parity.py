@@ -346,3 +346,48 @@ def test_ellipse_matches_eigen(ekf_mod):
     want = math.atan2(v[0], v[1])
     d = (angle - want) % math.pi
     assert min(d, math.pi - d) < 1e-5          # GSL eigenvector sign: parity modulo π
+
+
+def test_large_capacity_multi_workgroup_exchange(ekf_mod, oracle_mod):
+    """N=8192 (32 cooperating workgroups per instance, two instances per launch) with the
+    benchmark's deferred flush: 4 scans vs the restatement, association identical."""
+    N = 8192
+    w = G.make_world(N)
+    st = G.initial_state(w)
+    ens = ekf_mod.Ensemble(N, 2, 1, max_lines=8, flush_interval=4)
+    for e in range(2):
+        ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+    P0, y0, s0, pose0 = ens.download_state(1)
+    ref = oracle_mod.OracleRobot(N)
+    ref.set_state(P0, y0, s0, pose0)
+    del P0
+    for step in range(1, 5):
+        enc, lines, nl = G.make_scan(w, step, instances=2)
+        res = ens.localize(enc, lines, nl)
+        m = ref.localize(lines[1], enc[1])
+        assert res[1]["match"] == m and res[1]["matches"] == 8, (step, res[1]["match"], m)
+    P, y, s, pose = ens.download_state(1)
+    assert rel(P, ref.P_t0) <= 1e-5 and rel(y, ref.y) <= 1e-8
+
+
+@pytest.mark.parametrize("T", [1, 4])
+def test_many_lines_per_scan(ekf_mod, oracle_mod, T):
+    """max_lines = EKF_MAX_LINES (kmax = 128: the general flush path) with 40 lines per scan, most
+    of them matches (rank-80 downdates), some new; per scan vs the restatement."""
+    N = 512
+    w = G.make_world(N, active=N - 40)   # room for the new landmarks below the reset threshold
+    st = G.initial_state(w)
+    ens = ekf_mod.Ensemble(N, 1, 1, max_lines=ekf_mod.EKF_MAX_LINES, flush_interval=T)
+    ens.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
+    ref = oracle_mod.OracleRobot(N)
+    ref.set_state(*ens.download_state(0))
+    rng = np.random.default_rng(5)
+    for step in range(1, 4):
+        enc, lines, _ = G.make_scan(w, step, lines=36)
+        ln = np.concatenate([lines[0], G.random_lines(rng, 4)])
+        res = ens.localize(enc, ln[None], [len(ln)])[0]
+        m = ref.localize(ln, enc[0])
+        assert res["match"] == m, (step, res["match"], m)
+        assert res["matches"] >= 30
+    P, y, s, pose = ens.download_state(0)
+    assert rel(P, ref.P_t0) <= 1e-5 and rel(y, ref.y) <= 1e-8
