@@ -67,6 +67,7 @@ struct ekf_ctx {
     int ncu;
     int G;                    // association workgroups per instance
     int mbw;                  // mailbox words per workgroup slot
+    int spec;                 // speculative association (EKF_SPECULATE)
     int scan_batch;           // instances per association launch (co-residency bound)
     unsigned scan_epoch;      // association launches so far (mailbox tags)
     double* mbox;
@@ -271,7 +272,12 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     ALLOC(c->d_lines, sizeof(ekf_line) * d.max_lines * E);
     ALLOC(c->d_nlines, sizeof(int) * E);
     c->G = (d.N + ekf::SCAN_THREADS - 1) / ekf::SCAN_THREADS;
-    c->mbw = ((ekf::MB_WORDS_FIXED + 4 * d.max_lines + 15) / 16) * 16;   // whole 128-B lines
+    {
+        int words = ekf::MB_WORDS_FIXED + 4 * d.max_lines;
+        if (words < ekf::MB_WORDS_SPEC) words = ekf::MB_WORDS_SPEC;
+        c->mbw = ((words + 15) / 16) * 16;   // whole 128-B lines
+    }
+    c->spec = getenv("EKF_SPECULATE") ? atoi(getenv("EKF_SPECULATE")) : 0;
     ALLOC(c->mbox, sizeof(double) * 2 * c->G * c->mbw * E);
     c->sync_stride = ((ekf::SYNC_WG0 + c->G + 15) / 16) * 16;
     ALLOC(c->sync, sizeof(int) * c->sync_stride * E);
@@ -447,6 +453,7 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.dbg = c->dbg;
     p.G = c->G;
     p.mbw = c->mbw;
+    p.spec = c->spec;
     p.mbox = c->mbox;
     p.sync = c->sync;
     p.sync_stride = c->sync_stride;

@@ -17,6 +17,7 @@ enum { EKF_ST_SINGULAR = EKF_ST_SINGULAR_S, EKF_ST_CAP = EKF_ST_CAPACITY, EKF_ST
 enum { SYNC_START = 0, SYNC_WG0 = 4 };
 constexpr int MAX_GROUPS = 128;   // workgroups per instance (N <= 128 × 256)
 constexpr int MB_WORDS_FIXED = 26; // mailbox words before the V-history (see ekf_kernels.hip)
+constexpr int MB_WORDS_SPEC = 1 + 8 * (12 + 4 * 7);   // speculative association: winner records
 
 // per-instance result record in device memory (ints)
 enum {
@@ -62,6 +63,7 @@ struct ScanParams {
     int r_mode;
     int reset_margin;
     int npend;            // steps not yet in Pread, applied on read (in order)
+    int spec;             // speculative association: 0 off, 1 on, 2 test hook (wrong guesses)
     unsigned epoch;       // launch sequence number: tags the mailbox words of this launch
     double gate;
     double enc_noise;

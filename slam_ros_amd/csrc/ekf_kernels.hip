@@ -259,6 +259,11 @@ __device__ __forceinline__ void pll_block(const PllView<T>& v, int i0, int j0, d
     }
 }
 
+// The association arithmetic contracts a·b + c only within one source expression, so a
+// function inlined into different kernels or phases rounds identically everywhere (the
+// speculative and sequential association paths must agree bit for bit).
+#pragma clang fp contract(on)
+
 // Uniform per-line package published by the matching thread (LDS).
 enum {
     C_S = 0, C_SI = 4, C_V = 8, C_H = 10, C_KR = 13, C_UR = 19, C_WORDS = 25,
@@ -423,11 +428,11 @@ __device__ __forceinline__ int wave_min(int v)
 // Thread (g, tid) of instance e OWNS landmark j = 256·g + tid: its gating candidate, its two
 // rows of W/K/U/y, its robot-strip columns and its 2×2 diagonal block, all kept in registers
 // for the whole scan. The robot 3×3 block and x_pre are uniform and recomputed identically by
-// every thread. Per observed line the instance's workgroups exchange one mailbox slot each
-// (their best passing candidate and, from its owner, the uniform gain package), written with
-// 8-byte agent-scope atomic stores (sc1) and read after an arrival counter reaches G·(line+1)
-// (MI355X_MICROARCH.md "Valid forms": sc1 stores drained by s_waitcnt before the counter add,
-// sc1 poll, workgroup barrier, sc1 loads). Every spin is bounded; a timeout sets a status bit.
+// every thread. The instance's workgroups exchange words through a mailbox (one slot per
+// workgroup and parity), written with 8-byte agent-scope atomic stores, drained by s_waitcnt
+// and a workgroup barrier before a data-tagged word (launch epoch, phase code, payload) that
+// the readers poll (MI355X_MICROARCH.md "Valid forms"). Every spin is bounded; a timeout sets a
+// status bit.
 __device__ __forceinline__ void mb_store(double* p, double v)
 {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -438,8 +443,40 @@ __device__ __forceinline__ double mb_load(const double* p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// mailbox slot words
+// mailbox slot words (the package words double as the LDS package layout)
 enum { MB_BEST = 0, MB_S = 1, MB_SI = 5, MB_V = 9, MB_H = 11, MB_KR = 14, MB_UR = 20, MB_VH = 26 };
+
+// tag word: bits 63..32 launch epoch, 31..24 phase code, 23..0 payload. Codes 1..64 are the
+// lines of the sequential association; the speculative exchanges use their own codes.
+enum { TAG_SPEC_LISTS = 0x81, TAG_SPEC_WINNERS = 0x82, TAG_SPEC_VERDICT = 0x83 };
+
+__device__ __forceinline__ void mb_tag(double* slot, unsigned epoch, unsigned code, unsigned payload)
+{
+    const unsigned long long want = ((unsigned long long)epoch << 8) | code;
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(slot + MB_BEST), (want << 24) | payload,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Thread k < G polls workgroup k's tag of the given parity until it carries (epoch, code);
+// returns its payload (-1 on timeout, with the status bit set).
+__device__ __forceinline__ int mb_poll(const double* mbox, int par, int G, int k, int mbw,
+                                       unsigned epoch, unsigned code, int& status)
+{
+    const unsigned long long want = ((unsigned long long)epoch << 8) | code;
+    const unsigned long long* tw =
+        reinterpret_cast<const unsigned long long*>(mbox + ((size_t)par * G + k) * mbw + MB_BEST);
+    unsigned long long v = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int polls = 0;
+    while ((v >> 24) != want) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++polls > (1 << 24)) {   // ~seconds: a workgroup never arrived
+            status |= EKF_ST_TIMEOUT_BIT;
+            return -1;
+        }
+        v = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return (int)(v & 0xffffffu);
+}
 
 // Each workgroup announces that it has read the instance's shared inputs (after its loads
 // returned); the lead waits for all G before overwriting them. Bounded spin.
@@ -463,6 +500,167 @@ __device__ __forceinline__ int wait_all_started(int* sync, int G, unsigned epoch
     }
     return 0;
 }
+
+// R of a line (Robot.cpp:302-304): r_mode 1 reproduces the reference as written (only the
+// first four lines' R[3] lands in a zero-initialised 2×2)
+__device__ __forceinline__ void line_R(const ekf_line& ln, int i, int r_mode, double Rm[4])
+{
+    if (r_mode == 1) {
+        Rm[0] = i == 0 ? ln.R[3] : 0.0;
+        Rm[1] = i == 1 ? ln.R[3] : 0.0;
+        Rm[2] = i == 2 ? ln.R[3] : 0.0;
+        Rm[3] = i == 3 ? ln.R[3] : 0.0;
+    } else {
+        Rm[0] = ln.R[0]; Rm[1] = ln.R[1]; Rm[2] = ln.R[2]; Rm[3] = ln.R[3];
+    }
+}
+
+__device__ __forceinline__ void fill_block5(Block5& b5, const double R33[9], double2 rr0, double2 rr1,
+                                            double2 rr2, const double Dj[4])
+{
+    b5.p00 = R33[0]; b5.p01 = R33[1]; b5.p02 = R33[2];
+    b5.p10 = R33[3]; b5.p11 = R33[4]; b5.p12 = R33[5];
+    b5.p20 = R33[6]; b5.p21 = R33[7]; b5.p22 = R33[8];
+    b5.p0a = rr0.x; b5.p0b = rr0.y;
+    b5.p1a = rr1.x; b5.p1b = rr1.y;
+    b5.p2a = rr2.x; b5.p2b = rr2.y;
+    b5.daa = Dj[0]; b5.dab = Dj[1]; b5.dba = Dj[2]; b5.dbb = Dj[3];
+}
+
+// The uniform gain package of a match from the matching landmark's state: S, S⁻¹, v, H row 1
+// and the robot rows of K = W·S⁻¹ and U = K·S (Robot.cpp:522-602 for rows 0..2).
+__device__ __forceinline__ void build_package(const Cand& c, const double R33[9], double2 rr0,
+                                              double2 rr1, double2 rr2, double* pk)
+{
+    const double RL0[3] = {rr0.x, rr1.x, rr2.x};
+    const double RL1[3] = {rr0.y, rr1.y, rr2.y};
+    pk[MB_S + 0] = c.S[0]; pk[MB_S + 1] = c.S[1];
+    pk[MB_S + 2] = c.S[2]; pk[MB_S + 3] = c.S[3];
+    pk[MB_SI + 0] = c.Si[0]; pk[MB_SI + 1] = c.Si[1];
+    pk[MB_SI + 2] = c.Si[2]; pk[MB_SI + 3] = c.Si[3];
+    pk[MB_V + 0] = c.v[0]; pk[MB_V + 1] = c.v[1];
+    pk[MB_H + 0] = c.h10; pk[MB_H + 1] = c.h11; pk[MB_H + 2] = c.h1l;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        // W = P·Hᵀ (Robot.cpp:522), K = W·S⁻¹ (:526), U = K·S (:560)
+        const double w0 = -R33[a * 3 + 2] + RL0[a];
+        const double w1 = c.h10 * R33[a * 3 + 0] + c.h11 * R33[a * 3 + 1] + c.h1l * RL0[a] + RL1[a];
+        const double k0 = w0 * c.Si[0] + w1 * c.Si[2];
+        const double k1 = w0 * c.Si[1] + w1 * c.Si[3];
+        pk[MB_KR + 2 * a] = k0;
+        pk[MB_KR + 2 * a + 1] = k1;
+        pk[MB_UR + 2 * a] = k0 * c.S[0] + k1 * c.S[2];
+        pk[MB_UR + 2 * a + 1] = k0 * c.S[1] + k1 * c.S[3];
+    }
+}
+
+// The two rows of one landmark for a match: its block of column jstar with the earlier matches
+// of the scan applied (Robot.cpp:560-568, in order), W = P·Hᵀ, K = W·S⁻¹, U = K·S, y += K·v
+// (Robot.cpp:522-589), and the eager downdate of its robot-strip columns and diagonal block.
+// `uq_of(q)` returns the landmark's U rows of the scan's match q; the package holds jstar's V rows.
+template <typename UQ>
+__device__ __forceinline__ void gain_rows(const double* pk, int t, UQ uq_of, double blk[4],
+                                          double2& rr0, double2& rr1, double2& rr2, double2& yb,
+                                          double Dj[4], double kk[4], double uu[4])
+{
+    for (int q = 0; q < t; q++) {   // earlier matches of this scan, in order
+        const double4 uq = uq_of(q);
+        const double* vh = pk + MB_VH + 4 * q;
+        blk[0] -= uq.x * vh[0] + uq.y * vh[1];
+        blk[1] -= uq.x * vh[2] + uq.y * vh[3];
+        blk[2] -= uq.z * vh[0] + uq.w * vh[1];
+        blk[3] -= uq.z * vh[2] + uq.w * vh[3];
+    }
+    const double S0 = pk[MB_S], S1 = pk[MB_S + 1], S2 = pk[MB_S + 2], S3 = pk[MB_S + 3];
+    const double Si0 = pk[MB_SI], Si1 = pk[MB_SI + 1], Si2 = pk[MB_SI + 2], Si3 = pk[MB_SI + 3];
+    const double v0 = pk[MB_V], v1 = pk[MB_V + 1];
+    const double h10 = pk[MB_H], h11 = pk[MB_H + 1], h1l = pk[MB_H + 2];
+#pragma unroll
+    for (int pp = 0; pp < 2; pp++) {
+        const double pb0 = pp ? rr0.y : rr0.x;
+        const double pb1 = pp ? rr1.y : rr1.x;
+        const double pb2 = pp ? rr2.y : rr2.x;
+        const double pba = blk[pp * 2 + 0], pbb = blk[pp * 2 + 1];
+        const double w0 = -pb2 + pba;
+        const double w1 = h10 * pb0 + h11 * pb1 + h1l * pba + pbb;
+        const double k0 = w0 * Si0 + w1 * Si2;
+        const double k1 = w0 * Si1 + w1 * Si3;
+        kk[2 * pp] = k0;
+        kk[2 * pp + 1] = k1;
+        uu[2 * pp] = k0 * S0 + k1 * S2;
+        uu[2 * pp + 1] = k0 * S1 + k1 * S3;
+        const double dyv = k0 * v0 + k1 * v1;   // y += K·v (Robot.cpp:585-589)
+        if (pp) yb.y += dyv; else yb.x += dyv;
+    }
+    double Ur[6];
+#pragma unroll
+    for (int q = 0; q < 6; q++) Ur[q] = pk[MB_UR + q];
+    // eager downdate of the robot-strip columns and the diagonal block (Robot.cpp:568)
+    rr0.x -= Ur[0] * kk[0] + Ur[1] * kk[1];
+    rr0.y -= Ur[0] * kk[2] + Ur[1] * kk[3];
+    rr1.x -= Ur[2] * kk[0] + Ur[3] * kk[1];
+    rr1.y -= Ur[2] * kk[2] + Ur[3] * kk[3];
+    rr2.x -= Ur[4] * kk[0] + Ur[5] * kk[1];
+    rr2.y -= Ur[4] * kk[2] + Ur[5] * kk[3];
+    Dj[0] -= uu[0] * kk[0] + uu[1] * kk[1];
+    Dj[1] -= uu[0] * kk[2] + uu[1] * kk[3];
+    Dj[2] -= uu[2] * kk[0] + uu[3] * kk[1];
+    Dj[3] -= uu[2] * kk[2] + uu[3] * kk[3];
+}
+
+// uniform: robot 3×3 block and x_pre = y[0..2] after a match (Robot.cpp:568, 579-602)
+__device__ __forceinline__ void robot_update(double R33[9], double xp[3], const double* pk)
+{
+    double Kr[6], Ur[6];
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        Kr[q] = pk[MB_KR + q];
+        Ur[q] = pk[MB_UR + q];
+    }
+    const double v0 = pk[MB_V], v1 = pk[MB_V + 1];
+    double yn[3];
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        yn[a] = xp[a] + (Kr[2 * a] * v0 + Kr[2 * a + 1] * v1);
+#pragma unroll
+        for (int cc = 0; cc < 3; cc++)
+            R33[a * 3 + cc] -= Ur[2 * a] * Kr[2 * cc] + Ur[2 * a + 1] * Kr[2 * cc + 1];
+    }
+    xp[0] = yn[0];
+    xp[1] = yn[1];
+    xp[2] = normalize_radian(yn[2]);   // Robot.cpp:596
+}
+
+// Cheap guess of the exact gate (fp32 sine/cosine, no error bounds). It only steers the
+// speculative association; every decision it feeds is re-checked exactly.
+__device__ __forceinline__ bool guess_pass(const Block5& b, double ma, double mr, const double xp[3],
+                                           double za, double zr, const double Rm[4], double gate)
+{
+    float sf, cf;
+    sincosf((float)ma, &sf, &cf);
+    const double sn = sf, cs = cf;
+    const double h10 = -cs, h11 = -sn, h1l = xp[0] * sn - xp[1] * cs;
+    double S[4], hp0[5], hp1[5];
+    innovation_cov(b, h10, h11, h1l, Rm, S, hp0, hp1);
+    const double v0 = innovation_angle(za, ma, xp[2]);
+    const double v1 = zr - (mr - (xp[0] * cs + xp[1] * sn));
+    const double q = v0 * v0 * S[3] - v0 * v1 * (S[1] + S[2]) + v1 * v1 * S[0];
+    const double det = S[0] * S[3] - S[1] * S[2];
+    return !(det > 0.0) || q <= gate * gate * det;
+}
+
+// Speculative association (lines <= SPEC_L, G <= SPEC_GMAX): every line's winner is guessed
+// from the pre-update state, the guesses' mutual data are exchanged once, every workgroup
+// replays the winners' part of the sequential chain to get all gain packages, then every thread
+// runs the sequential gating and gain rows against those packages locally and flags any line
+// whose exact first passing candidate differs from the guess. Three exchanges per scan instead
+// of one per line; on a flag the scan restarts on the sequential path (identical results).
+constexpr int SPEC_L = HIST_LDS;                    // lines
+constexpr int SPEC_K = 6;                           // guessed candidates per line per workgroup
+constexpr int SPEC_GMAX = 32;                       // workgroups per instance
+constexpr int SPEC_WD = 12 + 4 * (SPEC_L - 1);      // winner record: rr, Dj, y, column blocks
+constexpr int PKW = MB_VH + 4 * SPEC_L;             // package words (speculative lines)
+static_assert(1 + SPEC_L * SPEC_WD <= MB_WORDS_SPEC, "mailbox slot too small");
 
 template <typename T>
 __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
@@ -490,94 +688,111 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     __shared__ ekf_line sh_lines[EKF_MAX_LINES];
     // U_q rows of the owned landmark for the first HIST_LDS matches of the scan (the rest in Ust)
     __shared__ double4 sh_uhist[HIST_LDS][SCAN_THREADS];
-    __shared__ double4 sh_vhist[HIST_LDS][SCAN_THREADS];   // V_q rows, for the package
+    // V_q rows (sequential path, for the package); owned blocks of the guessed columns
+    // (speculative path)
+    __shared__ double4 sh_vhist[HIST_LDS][SCAN_THREADS];
+    // speculative association
+    __shared__ unsigned long long sh_wl[SPEC_L][SCAN_THREADS / 64];
+    __shared__ unsigned long long sh_lists[SPEC_GMAX * SPEC_L];
+    __shared__ int sh_glist[SPEC_L][SPEC_K + 1];
+    __shared__ int sh_spec[SPEC_L];
+    __shared__ int sh_flag;
+    __shared__ double sh_wd[SPEC_L * SPEC_WD];
+    __shared__ double4 sh_wh[SPEC_L][SPEC_L][2];
+    __shared__ double sh_pk[SPEC_L][PKW];
     unsigned long long* dbg = (p.dbg && lead) ? p.dbg + (size_t)e * 16 : nullptr;
     unsigned long long t_last = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const unsigned long long t_first = t_last;
 
     // owned state, in registers for the whole scan
-    double2 rr0 = make_double2(0, 0), rr1 = rr0, rr2 = rr0, yb = rr0;
-    if (own) {
-        rr0 = *reinterpret_cast<const double2*>(Rs + b0);
-        rr1 = *reinterpret_cast<const double2*>(Rs + n + b0);
-        rr2 = *reinterpret_cast<const double2*>(Rs + 2 * n + b0);
-        yb = *reinterpret_cast<const double2*>(y + b0);
-    }
+    double2 rr0, rr1, rr2, yb;
     double R33[9], xp[3];
+    // (re)load the owned state and apply the predict (Robot.cpp:130-286, SIMULATIONOFF == true:
+    // `rot` unused); the inputs stay untouched until the commit, so a restart is exact
+    auto init_state = [&]() {
+        rr0 = make_double2(0, 0); rr1 = rr0; rr2 = rr0; yb = rr0;
+        if (own) {
+            rr0 = *reinterpret_cast<const double2*>(Rs + b0);
+            rr1 = *reinterpret_cast<const double2*>(Rs + n + b0);
+            rr2 = *reinterpret_cast<const double2*>(Rs + 2 * n + b0);
+            yb = *reinterpret_cast<const double2*>(y + b0);
+        }
 #pragma unroll
-    for (int a = 0; a < 9; a++) R33[a] = Rs[(a / 3) * n + (a % 3)];
+        for (int a = 0; a < 9; a++) R33[a] = Rs[(a / 3) * n + (a % 3)];
+        if (p.phase & PHASE_PREDICT) {
+            const double x0 = p.pose[3 * e + 0], y0 = p.pose[3 * e + 1], t0 = p.pose[3 * e + 2];
+            const double* enc = p.enc + 3 * e;
+            const double u2 = t0 - enc[2];
+            const double dx = x0 - enc[0], dy = y0 - enc[1];
+            const double u0 = sqrt(dx * dx + dy * dy);
+            const double c = u2 / 2.0 + t0;
+            double sc, cc;
+            sincos(c, &sc, &cc);
+            const double F3[9] = {1, 0, -u0 * sc, 0, 1, u0 * cc, 0, 0, 1};
+            xp[0] = x0 + u0 * cos(t0 + u2 / 2.0);
+            xp[1] = y0 + u0 * sin(t0 + u2 / 2.0);
+            xp[2] = t0 + u2;
+            // rows 0..2 of Fx·P for the owned landmark columns (Robot.cpp:242)
+            {
+                const double2 a0 = rr0, a1 = rr1, a2 = rr2;
+                rr0.x = F3[0] * a0.x + F3[1] * a1.x + F3[2] * a2.x;
+                rr0.y = F3[0] * a0.y + F3[1] * a1.y + F3[2] * a2.y;
+                rr1.x = F3[3] * a0.x + F3[4] * a1.x + F3[5] * a2.x;
+                rr1.y = F3[3] * a0.y + F3[4] * a1.y + F3[5] * a2.y;
+                rr2.x = F3[6] * a0.x + F3[7] * a1.x + F3[8] * a2.x;
+                rr2.y = F3[6] * a0.y + F3[7] * a1.y + F3[8] * a2.y;
+            }
+            // 3×3 block: F3·P33·F3ᵀ + Fu3·Q·Fu3ᵀ (Robot.cpp:178-258)
+            const double Fu3[9] = {cc, 0, -u0 * sc / 2.0, sc, 1, u0 * cc / 2.0, 0, 0, 1};
+            const double qs = (-1.0 / (1 + fabs(u0)) + 1);
+            const double Q[9] = {p.enc_noise * qs, 0, 0, 0, 2 * p.enc_noise * qs, 0, 0, 0,
+                                 p.enc_noise * qs};
+            double FP[9], FuQ[9];
+            for (int a = 0; a < 3; a++)
+                for (int b = 0; b < 3; b++) {
+                    double s = 0.0, t = 0.0;
+                    for (int k = 0; k < 3; k++) {
+                        s += F3[a * 3 + k] * R33[k * 3 + b];
+                        t += Fu3[a * 3 + k] * Q[k * 3 + b];
+                    }
+                    FP[a * 3 + b] = s;
+                    FuQ[a * 3 + b] = t;
+                }
+            for (int a = 0; a < 3; a++)
+                for (int b = 0; b < 3; b++) {
+                    double s = 0.0, t = 0.0;
+                    for (int k = 0; k < 3; k++) {
+                        s += FP[a * 3 + k] * F3[b * 3 + k];
+                        t += FuQ[a * 3 + k] * Fu3[b * 3 + k];
+                    }
+                    R33[a * 3 + b] = s + t;
+                }
+        } else {
+            xp[0] = p.xpre[3 * e + 0];
+            xp[1] = p.xpre[3 * e + 1];
+            xp[2] = p.xpre[3 * e + 2];
+        }
+    };
+    init_state();
 
-    if (p.phase & PHASE_PREDICT) {
-        // Robot.cpp:130-148 (SIMULATIONOFF == true: `rot` unused)
-        const double x0 = p.pose[3 * e + 0], y0 = p.pose[3 * e + 1], t0 = p.pose[3 * e + 2];
-        const double* enc = p.enc + 3 * e;
-        const double u2 = t0 - enc[2];
-        const double dx = x0 - enc[0], dy = y0 - enc[1];
-        const double u0 = sqrt(dx * dx + dy * dy);
-        const double c = u2 / 2.0 + t0;
-        double sc, cc;
-        sincos(c, &sc, &cc);
-        const double F3[9] = {1, 0, -u0 * sc, 0, 1, u0 * cc, 0, 0, 1};
-        xp[0] = x0 + u0 * cos(t0 + u2 / 2.0);
-        xp[1] = y0 + u0 * sin(t0 + u2 / 2.0);
-        xp[2] = t0 + u2;
-        // rows 0..2 of Fx·P for the owned landmark columns (Robot.cpp:242)
-        {
-            const double2 a0 = rr0, a1 = rr1, a2 = rr2;
-            rr0.x = F3[0] * a0.x + F3[1] * a1.x + F3[2] * a2.x;
-            rr0.y = F3[0] * a0.y + F3[1] * a1.y + F3[2] * a2.y;
-            rr1.x = F3[3] * a0.x + F3[4] * a1.x + F3[5] * a2.x;
-            rr1.y = F3[3] * a0.y + F3[4] * a1.y + F3[5] * a2.y;
-            rr2.x = F3[6] * a0.x + F3[7] * a1.x + F3[8] * a2.x;
-            rr2.y = F3[6] * a0.y + F3[7] * a1.y + F3[8] * a2.y;
+    if (!(p.phase & PHASE_UPDATE)) {
+        // predict only: write the predicted robot strip, 3×3 block and x_pre
+        if (own) {
+            *reinterpret_cast<double2*>(Rs + b0) = rr0;
+            *reinterpret_cast<double2*>(Rs + n + b0) = rr1;
+            *reinterpret_cast<double2*>(Rs + 2 * n + b0) = rr2;
         }
-        // 3×3 block: F3·P33·F3ᵀ + Fu3·Q·Fu3ᵀ (Robot.cpp:178-258)
-        const double Fu3[9] = {cc, 0, -u0 * sc / 2.0, sc, 1, u0 * cc / 2.0, 0, 0, 1};
-        const double qs = (-1.0 / (1 + fabs(u0)) + 1);
-        const double Q[9] = {p.enc_noise * qs, 0, 0, 0, 2 * p.enc_noise * qs, 0, 0, 0,
-                             p.enc_noise * qs};
-        double FP[9], FuQ[9];
-        for (int a = 0; a < 3; a++)
-            for (int b = 0; b < 3; b++) {
-                double s = 0.0, t = 0.0;
-                for (int k = 0; k < 3; k++) {
-                    s += F3[a * 3 + k] * R33[k * 3 + b];
-                    t += Fu3[a * 3 + k] * Q[k * 3 + b];
-                }
-                FP[a * 3 + b] = s;
-                FuQ[a * 3 + b] = t;
-            }
-        for (int a = 0; a < 3; a++)
-            for (int b = 0; b < 3; b++) {
-                double s = 0.0, t = 0.0;
-                for (int k = 0; k < 3; k++) {
-                    s += FP[a * 3 + k] * F3[b * 3 + k];
-                    t += FuQ[a * 3 + k] * Fu3[b * 3 + k];
-                }
-                R33[a * 3 + b] = s + t;
-            }
-        if (!(p.phase & PHASE_UPDATE)) {
-            if (own) {
-                *reinterpret_cast<double2*>(Rs + b0) = rr0;
-                *reinterpret_cast<double2*>(Rs + n + b0) = rr1;
-                *reinterpret_cast<double2*>(Rs + 2 * n + b0) = rr2;
-            }
-            signal_started(sync, tid);
-            if (tid == 0 && !lead) sync[SYNC_WG0 + g] = 0;
-            if (lead) {
-                const int to = wait_all_started(sync, G, p.epoch);
-                sync[SYNC_WG0 + g] = to;
-                for (int a = 0; a < 9; a++) Rs[(a / 3) * n + (a % 3)] = R33[a];
-                p.xpre[3 * e + 0] = xp[0];
-                p.xpre[3 * e + 1] = xp[1];
-                p.xpre[3 * e + 2] = xp[2];
-            }
-            return;
+        signal_started(sync, tid);
+        if (tid == 0 && !lead) sync[SYNC_WG0 + g] = 0;
+        if (lead) {
+            const int to = wait_all_started(sync, G, p.epoch);
+            sync[SYNC_WG0 + g] = to;
+            for (int a = 0; a < 9; a++) Rs[(a / 3) * n + (a % 3)] = R33[a];
+            p.xpre[3 * e + 0] = xp[0];
+            p.xpre[3 * e + 1] = xp[1];
+            p.xpre[3 * e + 2] = xp[2];
         }
-    } else {
-        xp[0] = p.xpre[3 * e + 0];
-        xp[1] = p.xpre[3 * e + 1];
-        xp[2] = p.xpre[3 * e + 2];
+        return;
     }
     EKF_STAMP(0);
 
@@ -621,28 +836,325 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     if (own && j < s) pll_block(pv, 2 * j, 2 * j, Dj);
     EKF_STAMP(1);
 
-    bool matched = false;
-    int m = 0, nextra = 0, status = 0;
-    for (int i = 0; i < L; ++i) {
-        const ekf_line ln = sh_lines[i];
-        double Rm[4] = {0, 0, 0, 0};
-        if (p.r_mode == 1) {
-            if (i < 4) Rm[i] = ln.R[3];   // Robot.cpp:302-304 as written (zero-initialised stack)
-        } else {
-            Rm[0] = ln.R[0]; Rm[1] = ln.R[1]; Rm[2] = ln.R[2]; Rm[3] = ln.R[3];
+    // writes a match's owned rows: U/V history and the MFMA downdate operands
+    auto store_rows = [&](int t, const double kk[4], const double uu[4], bool vhist) {
+        if (t < HIST_LDS)
+            sh_uhist[t][tid] = make_double4(uu[0], uu[1], uu[2], uu[3]);
+        else
+            *reinterpret_cast<double4*>(Ust + ((size_t)t * n + b0) * 2) = make_double4(uu[0], uu[1], uu[2], uu[3]);
+        if (vhist) {
+            if (t < HIST_LDS)
+                sh_vhist[t][tid] = make_double4(kk[0], kk[1], kk[2], kk[3]);
+            else
+                *reinterpret_cast<double4*>(Vst + ((size_t)t * n + b0) * 2) = make_double4(kk[0], kk[1], kk[2], kk[3]);
         }
+#pragma unroll
+        for (int pp = 0; pp < 2; pp++) {
+            const int lr = 2 * j + pp;
+            if constexpr (sizeof(C) == 4) {
+                Uop[op_index_f32(lr, 2 * t, d.kmax)] = to_domain<T>(-uu[2 * pp]);
+                Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = to_domain<T>(-uu[2 * pp + 1]);
+                Vop[op_index_f32(lr, 2 * t, d.kmax)] = (C)kk[2 * pp];
+                Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (C)kk[2 * pp + 1];
+            } else {
+                Uop[op_index_f64(lr, 2 * t, d.kmax)] = (C)(-uu[2 * pp]);
+                Uop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (C)(-uu[2 * pp + 1]);
+                Vop[op_index_f64(lr, 2 * t, d.kmax)] = (C)kk[2 * pp];
+                Vop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (C)kk[2 * pp + 1];
+            }
+        }
+    };
+    auto uq_owned = [&](int q) -> double4 {
+        return q < HIST_LDS ? sh_uhist[q][tid] : *reinterpret_cast<const double4*>(Ust + ((size_t)q * n + b0) * 2);
+    };
+
+    bool matched = false;
+    int m = 0, nextra = 0, status = 0, tstatus = 0;
+    int par0 = 0;   // mailbox parity of line 0 on the sequential path
+    bool sequential = true;
+
+    if (p.spec && L > 0 && L <= SPEC_L && s > 0 && G <= SPEC_GMAX) {
+        // ---- (a) guesses: per line, does the owned landmark pass under the predicted state ----
+        unsigned gp = 0;
+        if (own && j < s) {
+            Block5 b5;
+            fill_block5(b5, R33, rr0, rr1, rr2, Dj);
+            for (int t = 0; t < L; t++) {
+                const ekf_line ln = sh_lines[t];
+                double Rm[4];
+                line_R(ln, t, p.r_mode, Rm);
+                if (guess_pass(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate)) gp |= 1u << t;
+            }
+            if (p.spec == 2 && L > 1)   // test hook: every guess taken from the next line
+                gp = ((gp >> 1) | (gp << (L - 1))) & ((1u << L) - 1u);
+        }
+        // per wave and line the guessed candidates (ballot), then the workgroup's first SPEC_K
+        // in landmark order: word = 8-bit local indices | count << 48 | more << 52
+        for (int t = 0; t < L; t++) {
+            const unsigned long long mk = __ballot((gp >> t) & 1u);
+            if ((tid & 63) == 0) sh_wl[t][tid >> 6] = mk;
+        }
+        __syncthreads();
+        if (tid < L) {
+            unsigned long long word = 0;
+            int cnt = 0, more = 0;
+            for (int w = 0; w < SCAN_THREADS / 64 && !more; w++) {
+                unsigned long long mk = sh_wl[tid][w];
+                while (mk) {
+                    if (cnt == SPEC_K) { more = 1; break; }
+                    const int b = __builtin_ctzll(mk);
+                    mk &= mk - 1;
+                    word |= (unsigned long long)(w * 64 + b) << (8 * cnt);
+                    cnt++;
+                }
+            }
+            word |= ((unsigned long long)cnt << 48) | ((unsigned long long)more << 52);
+            sh_lists[g * SPEC_L + tid] = word;
+        }
+        __syncthreads();
+        // ---- (b) exchange 1 (parity 0): every workgroup's lists ----
+        if (G > 1) {
+            double* slot = mbox + (size_t)g * p.mbw;
+            if (tid < L) mb_store(slot + 1 + tid, __longlong_as_double((long long)sh_lists[g * SPEC_L + tid]));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) mb_tag(slot, p.epoch, TAG_SPEC_LISTS, 0);
+            if (tid < G) (void)mb_poll(mbox, 0, G, tid, p.mbw, p.epoch, TAG_SPEC_LISTS, tstatus);
+            __syncthreads();
+            for (int k = tid; k < G * L; k += SCAN_THREADS) {
+                const int gq = k / L, t = k - gq * L;
+                if (gq != g)
+                    sh_lists[gq * SPEC_L + t] =
+                        (unsigned long long)__double_as_longlong(mb_load(mbox + (size_t)gq * p.mbw + 1 + t));
+            }
+            __syncthreads();
+        }
+        // ---- (c) guessed winners: per line the first SPEC_K guessed candidates of the instance
+        // (workgroups are in landmark order), then in line order the first one not already taken
+        // by an earlier line (every workgroup computes the same) ----
+        if (tid < L) {
+            int cnt = 0, more = 0;
+            for (int gq = 0; gq < G; gq++) {
+                const unsigned long long w = sh_lists[gq * SPEC_L + tid];
+                const int c = (int)((w >> 48) & 15);
+                for (int k = 0; k < c; k++) {
+                    if (cnt < SPEC_K) sh_glist[tid][cnt++] = gq * SCAN_THREADS + (int)((w >> (8 * k)) & 255);
+                    else more = 1;
+                }
+                if ((w >> 52) & 1) more = 1;
+            }
+            sh_glist[tid][SPEC_K] = cnt | (more << 8);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int unresolved = 0;
+            for (int t = 0; t < L; t++) {
+                const int info = sh_glist[t][SPEC_K];
+                const int cnt = info & 255;
+                int w = -1;
+                for (int k = 0; k < cnt && w < 0; k++) {
+                    const int cand = sh_glist[t][k];
+                    bool taken = false;
+                    for (int q = 0; q < t; q++) taken |= (sh_spec[q] == cand);
+                    if (!taken) w = cand;
+                }
+                if (w < 0 && (info >> 8)) unresolved = 1;
+                sh_spec[t] = w;
+            }
+            sh_flag = unresolved;
+        }
+        __syncthreads();
+        if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[10] += _t - t_last; t_last = _t; }
+
+        if (!sh_flag) {
+            sequential = false;
+            // ---- (d) owned blocks of the guessed columns (Robot.cpp:560 operands) ----
+            if (own)
+                for (int t = 0; t < L; t++) {
+                    const int w = sh_spec[t];
+                    if (w >= 0) {
+                        double bk[4];
+                        pll_block(pv, 2 * j, 2 * w, bk);
+                        sh_vhist[t][tid] = make_double4(bk[0], bk[1], bk[2], bk[3]);
+                    }
+                }
+            // the owner of each guessed winner u writes its record: robot-strip columns,
+            // diagonal block, mean, and its blocks of the earlier winners' columns
+            if (own)
+                for (int u = 0; u < L; u++)
+                    if (sh_spec[u] == j) {
+                        double* r = sh_wd + u * SPEC_WD;
+                        r[0] = rr0.x; r[1] = rr0.y; r[2] = rr1.x; r[3] = rr1.y; r[4] = rr2.x; r[5] = rr2.y;
+                        r[6] = Dj[0]; r[7] = Dj[1]; r[8] = Dj[2]; r[9] = Dj[3];
+                        r[10] = yb.x; r[11] = yb.y;
+                        for (int t = 0; t < u; t++) {
+                            const double4 bk = sh_vhist[t][tid];
+                            r[12 + 4 * t] = bk.x; r[13 + 4 * t] = bk.y;
+                            r[14 + 4 * t] = bk.z; r[15 + 4 * t] = bk.w;
+                        }
+                    }
+            __syncthreads();
+            // ---- (e) exchange 2 (parity 1): the winner records ----
+            if (G > 1) {
+                double* slot = mbox + ((size_t)G + g) * p.mbw;
+                for (int k = tid; k < L * SPEC_WD; k += SCAN_THREADS) {
+                    const int u = k / SPEC_WD, w = sh_spec[u];
+                    if (w >= 0 && w / SCAN_THREADS == g && k - u * SPEC_WD < 12 + 4 * u)
+                        mb_store(slot + 1 + k, sh_wd[k]);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) mb_tag(slot, p.epoch, TAG_SPEC_WINNERS, 0);
+                if (tid < G) (void)mb_poll(mbox, 1, G, tid, p.mbw, p.epoch, TAG_SPEC_WINNERS, tstatus);
+                __syncthreads();
+                for (int k = tid; k < L * SPEC_WD; k += SCAN_THREADS) {
+                    const int u = k / SPEC_WD, w = sh_spec[u];
+                    if (w >= 0 && w / SCAN_THREADS != g && k - u * SPEC_WD < 12 + 4 * u)
+                        sh_wd[k] = mb_load(mbox + ((size_t)G + w / SCAN_THREADS) * p.mbw + 1 + k);
+                }
+                __syncthreads();
+            }
+            if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[11] += _t - t_last; t_last = _t; }
+            // ---- (f) the winners' part of the sequential chain (one thread, every workgroup):
+            // each line's package from its winner's state, then the later winners' rows ----
+            if (tid == 0) {
+                double R33l[9], xpl[3];
+#pragma unroll
+                for (int a = 0; a < 9; a++) R33l[a] = R33[a];
+                xpl[0] = xp[0]; xpl[1] = xp[1]; xpl[2] = xp[2];
+                int ml = 0, bad = 0;
+                for (int t = 0; t < L && !bad; t++) {
+                    if (sh_spec[t] < 0) continue;
+                    const ekf_line ln = sh_lines[t];
+                    double Rm[4];
+                    line_R(ln, t, p.r_mode, Rm);
+                    double* r = sh_wd + t * SPEC_WD;
+                    double2 w0 = make_double2(r[0], r[1]), w1 = make_double2(r[2], r[3]);
+                    double2 w2 = make_double2(r[4], r[5]);
+                    const double wD[4] = {r[6], r[7], r[8], r[9]};
+                    Block5 b5;
+                    fill_block5(b5, R33l, w0, w1, w2, wD);
+                    Cand c;
+                    eval_candidate(b5, r[10], r[11], xpl, ln.alpha, ln.r, Rm, p.gate, c);
+                    if (!c.pass) { bad = 1; break; }
+                    double* pk = sh_pk[t];
+                    build_package(c, R33l, w0, w1, w2, pk);
+                    for (int q = 0; q < ml; q++) {
+                        const double4 vq = sh_wh[t][q][1];
+                        pk[MB_VH + 4 * q + 0] = vq.x; pk[MB_VH + 4 * q + 1] = vq.y;
+                        pk[MB_VH + 4 * q + 2] = vq.z; pk[MB_VH + 4 * q + 3] = vq.w;
+                    }
+                    for (int u = t + 1; u < L; u++) {
+                        if (sh_spec[u] < 0) continue;
+                        double* ru = sh_wd + u * SPEC_WD;
+                        double2 q0 = make_double2(ru[0], ru[1]), q1 = make_double2(ru[2], ru[3]);
+                        double2 q2 = make_double2(ru[4], ru[5]), qy = make_double2(ru[10], ru[11]);
+                        double qD[4] = {ru[6], ru[7], ru[8], ru[9]};
+                        double blk[4] = {ru[12 + 4 * t], ru[13 + 4 * t], ru[14 + 4 * t], ru[15 + 4 * t]};
+                        double kk[4], uu[4];
+                        gain_rows(pk, ml, [&](int q) { return sh_wh[u][q][0]; }, blk, q0, q1, q2, qy, qD, kk, uu);
+                        ru[0] = q0.x; ru[1] = q0.y; ru[2] = q1.x; ru[3] = q1.y; ru[4] = q2.x; ru[5] = q2.y;
+                        ru[6] = qD[0]; ru[7] = qD[1]; ru[8] = qD[2]; ru[9] = qD[3];
+                        ru[10] = qy.x; ru[11] = qy.y;
+                        sh_wh[u][ml][0] = make_double4(uu[0], uu[1], uu[2], uu[3]);
+                        sh_wh[u][ml][1] = make_double4(kk[0], kk[1], kk[2], kk[3]);
+                    }
+                    robot_update(R33l, xpl, pk);
+                    ml++;
+                }
+                sh_flag = bad;
+            }
+            __syncthreads();
+            if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[12] += _t - t_last; t_last = _t; }
+            // ---- (g) every thread: the sequential gating and gain rows against the packages ----
+            int viol = sh_flag;
+            for (int i = 0; i < L && !viol; ++i) {
+                const ekf_line ln = sh_lines[i];
+                double Rm[4];
+                line_R(ln, i, p.r_mode, Rm);
+                const int w = sh_spec[i];
+                if (own && j < s && !matched) {
+                    Block5 b5;
+                    fill_block5(b5, R33, rr0, rr1, rr2, Dj);
+                    bool pass = false;
+                    if (!certified_reject(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate)) {
+                        Cand c;
+                        eval_candidate(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate, c);
+                        status |= c.singular ? EKF_ST_SINGULAR : 0;
+                        pass = c.pass;
+                    }
+                    // the guess must be the first passing unmatched landmark
+                    if (pass ? (w < 0 || j < w) : (j == w)) viol = 1;
+                }
+                if (w < 0) {
+                    // no match: the line goes to extraLines (Robot.cpp:308-310, 492-496)
+                    if (lead) {
+                        res[RES_MATCH + i] = -1;
+                        res[RES_EXTRA + nextra] = i;
+                    }
+                    if (tid == 0) sh_extra[nextra] = i;
+                    nextra++;
+                    continue;
+                }
+                const double* pk = sh_pk[i];
+                if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
+                if (own) {
+                    const double4 bk = sh_vhist[i][tid];
+                    double blk[4] = {bk.x, bk.y, bk.z, bk.w};
+                    double kk[4], uu[4];
+                    gain_rows(pk, m, uq_owned, blk, rr0, rr1, rr2, yb, Dj, kk, uu);
+                    store_rows(m, kk, uu, false);
+                }
+                robot_update(R33, xp, pk);
+                if (j == w) matched = true;
+                if (lead) res[RES_MATCH + i] = w;
+                m++;
+            }
+            if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[13] += _t - t_last; t_last = _t; }
+            // ---- (h) verdict (exchange 3, parity 0): any flag restarts on the sequential path ----
+            const int wv = __any(viol) ? 1 : 0;
+            __syncthreads();
+            if ((tid & 63) == 0) sh_red[tid >> 6] = wv;
+            __syncthreads();
+            int any = 0;
+#pragma unroll
+            for (int w = 0; w < SCAN_THREADS / 64; w++) any |= sh_red[w];
+            if (G > 1) {
+                if (tid == 0) mb_tag(mbox + (size_t)g * p.mbw, p.epoch, TAG_SPEC_VERDICT, (unsigned)any);
+                if (tid < G) {
+                    const int v = mb_poll(mbox, 0, G, tid, p.mbw, p.epoch, TAG_SPEC_VERDICT, tstatus);
+                    sh_best[tid] = v != 0;
+                }
+                __syncthreads();
+                for (int k = 0; k < G; k++) any |= sh_best[k];
+            }
+            if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[14] += _t - t_last; t_last = _t; }
+            if (any) {
+                if (dbg) dbg[15] += 1;
+                sequential = true;
+                par0 = 1;
+                init_state();
+                Dj[0] = Dj[1] = Dj[2] = Dj[3] = 0.0;
+                if (own && j < s) pll_block(pv, 2 * j, 2 * j, Dj);
+                matched = false;
+                m = nextra = status = 0;
+                __syncthreads();   // sh_extra, sh_vhist reuse
+            }
+        } else {
+            par0 = 1;   // the lists' parity-0 words may still be read
+        }
+    }
+
+    for (int i = 0; sequential && i < L; ++i) {
+        const ekf_line ln = sh_lines[i];
+        double Rm[4];
+        line_R(ln, i, p.r_mode, Rm);
         // gating of the owned candidate (Robot.cpp:313-498); the first passing unmatched j wins
         int best = 0x7fffffff;
         Cand c;
-        Block5 b5;
         if (own && j < s && !matched) {
-            b5.p00 = R33[0]; b5.p01 = R33[1]; b5.p02 = R33[2];
-            b5.p10 = R33[3]; b5.p11 = R33[4]; b5.p12 = R33[5];
-            b5.p20 = R33[6]; b5.p21 = R33[7]; b5.p22 = R33[8];
-            b5.p0a = rr0.x; b5.p0b = rr0.y;
-            b5.p1a = rr1.x; b5.p1b = rr1.y;
-            b5.p2a = rr2.x; b5.p2b = rr2.y;
-            b5.daa = Dj[0]; b5.dab = Dj[1]; b5.dba = Dj[2]; b5.dbb = Dj[3];
+            Block5 b5;
+            fill_block5(b5, R33, rr0, rr1, rr2, Dj);
             if (!certified_reject(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate)) {
                 eval_candidate(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate, c);
                 status |= c.singular ? EKF_ST_SINGULAR : 0;
@@ -656,33 +1168,14 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         int gbest = sh_red[0];
 #pragma unroll
         for (int w = 1; w < SCAN_THREADS / 64; w++) gbest = min(gbest, sh_red[w]);
-        const int par = i & 1;
+        const int par = (i + par0) & 1;
         double* slot = mbox + ((size_t)par * G + g) * p.mbw;
         const int npk = MB_VH + 4 * m;
         if (best != 0x7fffffff && best == gbest) {
-            // this workgroup's candidate: the uniform gain package of the robot rows
-            // (Robot.cpp:522-602 for rows 0..2) and the V rows of the candidate for the
-            // earlier matches of this scan (Robot.cpp:560-568 corrections), staged in LDS
-            const double RL0[3] = {rr0.x, rr1.x, rr2.x};
-            const double RL1[3] = {rr0.y, rr1.y, rr2.y};
-            sh_pkg[MB_S + 0] = c.S[0]; sh_pkg[MB_S + 1] = c.S[1];
-            sh_pkg[MB_S + 2] = c.S[2]; sh_pkg[MB_S + 3] = c.S[3];
-            sh_pkg[MB_SI + 0] = c.Si[0]; sh_pkg[MB_SI + 1] = c.Si[1];
-            sh_pkg[MB_SI + 2] = c.Si[2]; sh_pkg[MB_SI + 3] = c.Si[3];
-            sh_pkg[MB_V + 0] = c.v[0]; sh_pkg[MB_V + 1] = c.v[1];
-            sh_pkg[MB_H + 0] = c.h10; sh_pkg[MB_H + 1] = c.h11; sh_pkg[MB_H + 2] = c.h1l;
-#pragma unroll
-            for (int a = 0; a < 3; a++) {
-                // W = P·Hᵀ (Robot.cpp:522), K = W·S⁻¹ (:526), U = K·S (:560)
-                const double w0 = -R33[a * 3 + 2] + RL0[a];
-                const double w1 = c.h10 * R33[a * 3 + 0] + c.h11 * R33[a * 3 + 1] + c.h1l * RL0[a] + RL1[a];
-                const double k0 = w0 * c.Si[0] + w1 * c.Si[2];
-                const double k1 = w0 * c.Si[1] + w1 * c.Si[3];
-                sh_pkg[MB_KR + 2 * a] = k0;
-                sh_pkg[MB_KR + 2 * a + 1] = k1;
-                sh_pkg[MB_UR + 2 * a] = k0 * c.S[0] + k1 * c.S[2];
-                sh_pkg[MB_UR + 2 * a + 1] = k0 * c.S[1] + k1 * c.S[3];
-            }
+            // this workgroup's candidate: the uniform gain package and the V rows of the
+            // candidate for the earlier matches of this scan (Robot.cpp:560-568 corrections),
+            // staged in LDS
+            build_package(c, R33, rr0, rr1, rr2, sh_pkg);
             for (int q = 0; q < m; q++) {
                 const double4 vq = q < HIST_LDS ? sh_vhist[q][tid]
                                                 : *reinterpret_cast<const double4*>(Vst + ((size_t)q * n + b0) * 2);
@@ -696,34 +1189,16 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         int jstar = gbest, gstar = 0;
         if (G > 1) {
             // to the mailbox, one word per lane; drained and ordered by the barrier before the
-            // tagged best word (data-tagged granule: launch epoch, line, best); every workgroup
-            // polls all G words
+            // tagged best word (payload best + 1, 0: no candidate); every workgroup polls all G
             if (gbest != 0x7fffffff)
-                for (int k = tid; k < npk; k += SCAN_THREADS) mb_store(slot + k, sh_pkg[k]);
+                for (int k = 1 + tid; k < npk; k += SCAN_THREADS) mb_store(slot + k, sh_pkg[k]);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            // tag: bits 63..32 launch epoch, 31..24 line + 1, 23..0 best + 1 (0: no candidate)
-            const unsigned long long want = ((unsigned long long)p.epoch << 8) | (unsigned)(i + 1);
-            if (tid == 0)
-                __hip_atomic_store(reinterpret_cast<unsigned long long*>(slot + MB_BEST),
-                                   (want << 24) | (unsigned)(gbest == 0x7fffffff ? 0 : gbest + 1),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0) mb_tag(slot, p.epoch, (unsigned)(i + 1), (unsigned)(gbest == 0x7fffffff ? 0 : gbest + 1));
             EKF_STAMP(3);
             for (int k = tid; k < G; k += SCAN_THREADS) {
-                const unsigned long long* tw =
-                    reinterpret_cast<const unsigned long long*>(mbox + ((size_t)par * G + k) * p.mbw + MB_BEST);
-                unsigned long long v = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                int polls = 0;
-                while ((v >> 24) != want) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++polls > (1 << 24)) {   // ~seconds: a workgroup never arrived
-                        status |= EKF_ST_TIMEOUT_BIT;
-                        break;
-                    }
-                    v = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                const int bq = (int)(v & 0xffffffu);
-                sh_best[k] = bq == 0 ? 0x7fffffff : bq - 1;
+                const int bq = mb_poll(mbox, par, G, k, p.mbw, p.epoch, (unsigned)(i + 1), tstatus);
+                sh_best[k] = bq <= 0 ? 0x7fffffff : bq - 1;
             }
             __syncthreads();
             jstar = 0x7fffffff;
@@ -763,100 +1238,19 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         } else if (own) {
             pll_block(pv, 2 * j, 2 * jstar, blk);
         }
-        const double S0 = sh_pkg[MB_S], S1 = sh_pkg[MB_S + 1], S2 = sh_pkg[MB_S + 2], S3 = sh_pkg[MB_S + 3];
-        const double Si0 = sh_pkg[MB_SI], Si1 = sh_pkg[MB_SI + 1], Si2 = sh_pkg[MB_SI + 2], Si3 = sh_pkg[MB_SI + 3];
-        const double v0 = sh_pkg[MB_V], v1 = sh_pkg[MB_V + 1];
-        const double h10 = sh_pkg[MB_H], h11 = sh_pkg[MB_H + 1], h1l = sh_pkg[MB_H + 2];
-        double Kr[6], Ur[6];
-#pragma unroll
-        for (int q = 0; q < 6; q++) {
-            Kr[q] = sh_pkg[MB_KR + q];
-            Ur[q] = sh_pkg[MB_UR + q];
-        }
-        const int t = m;
         if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
-
-        // owned landmark rows
         if (own) {
-            for (int q = 0; q < t; q++) {   // earlier matches of this scan, in order
-                const double4 uq = q < HIST_LDS ? sh_uhist[q][tid]
-                                                : *reinterpret_cast<const double4*>(Ust + ((size_t)q * n + b0) * 2);
-                const double* vh = sh_pkg + MB_VH + 4 * q;
-                blk[0] -= uq.x * vh[0] + uq.y * vh[1];
-                blk[1] -= uq.x * vh[2] + uq.y * vh[3];
-                blk[2] -= uq.z * vh[0] + uq.w * vh[1];
-                blk[3] -= uq.z * vh[2] + uq.w * vh[3];
-            }
             double kk[4], uu[4];
-#pragma unroll
-            for (int pp = 0; pp < 2; pp++) {
-                const double pb0 = pp ? rr0.y : rr0.x;
-                const double pb1 = pp ? rr1.y : rr1.x;
-                const double pb2 = pp ? rr2.y : rr2.x;
-                const double pba = blk[pp * 2 + 0], pbb = blk[pp * 2 + 1];
-                const double w0 = -pb2 + pba;
-                const double w1 = h10 * pb0 + h11 * pb1 + h1l * pba + pbb;
-                const double k0 = w0 * Si0 + w1 * Si2;
-                const double k1 = w0 * Si1 + w1 * Si3;
-                kk[2 * pp] = k0;
-                kk[2 * pp + 1] = k1;
-                uu[2 * pp] = k0 * S0 + k1 * S2;
-                uu[2 * pp + 1] = k0 * S1 + k1 * S3;
-                const double dyv = k0 * v0 + k1 * v1;   // y += K·v (Robot.cpp:585-589)
-                if (pp) yb.y += dyv; else yb.x += dyv;
-            }
-            if (t < HIST_LDS)
-                sh_uhist[t][tid] = make_double4(uu[0], uu[1], uu[2], uu[3]);
-            else
-                *reinterpret_cast<double4*>(Ust + ((size_t)t * n + b0) * 2) = make_double4(uu[0], uu[1], uu[2], uu[3]);
-            if (t < HIST_LDS)
-                sh_vhist[t][tid] = make_double4(kk[0], kk[1], kk[2], kk[3]);
-            else
-                *reinterpret_cast<double4*>(Vst + ((size_t)t * n + b0) * 2) = make_double4(kk[0], kk[1], kk[2], kk[3]);
-#pragma unroll
-            for (int pp = 0; pp < 2; pp++) {
-                const int lr = 2 * j + pp;
-                if constexpr (sizeof(C) == 4) {
-                    Uop[op_index_f32(lr, 2 * t, d.kmax)] = to_domain<T>(-uu[2 * pp]);
-                    Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = to_domain<T>(-uu[2 * pp + 1]);
-                    Vop[op_index_f32(lr, 2 * t, d.kmax)] = (C)kk[2 * pp];
-                    Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (C)kk[2 * pp + 1];
-                } else {
-                    Uop[op_index_f64(lr, 2 * t, d.kmax)] = (C)(-uu[2 * pp]);
-                    Uop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (C)(-uu[2 * pp + 1]);
-                    Vop[op_index_f64(lr, 2 * t, d.kmax)] = (C)kk[2 * pp];
-                    Vop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (C)kk[2 * pp + 1];
-                }
-            }
-            // eager downdate of the owned robot-strip columns and diagonal block (Robot.cpp:568)
-            rr0.x -= Ur[0] * kk[0] + Ur[1] * kk[1];
-            rr0.y -= Ur[0] * kk[2] + Ur[1] * kk[3];
-            rr1.x -= Ur[2] * kk[0] + Ur[3] * kk[1];
-            rr1.y -= Ur[2] * kk[2] + Ur[3] * kk[3];
-            rr2.x -= Ur[4] * kk[0] + Ur[5] * kk[1];
-            rr2.y -= Ur[4] * kk[2] + Ur[5] * kk[3];
-            Dj[0] -= uu[0] * kk[0] + uu[1] * kk[1];
-            Dj[1] -= uu[0] * kk[2] + uu[1] * kk[3];
-            Dj[2] -= uu[2] * kk[0] + uu[3] * kk[1];
-            Dj[3] -= uu[2] * kk[2] + uu[3] * kk[3];
+            gain_rows(sh_pkg, m, uq_owned, blk, rr0, rr1, rr2, yb, Dj, kk, uu);
+            store_rows(m, kk, uu, true);
         }
-        // uniform: robot 3×3 block and x_pre = y[0..2] (Robot.cpp:568, 579-602)
-        double yn[3];
-#pragma unroll
-        for (int a = 0; a < 3; a++) {
-            yn[a] = xp[a] + (Kr[2 * a] * v0 + Kr[2 * a + 1] * v1);
-#pragma unroll
-            for (int cc = 0; cc < 3; cc++)
-                R33[a * 3 + cc] -= Ur[2 * a] * Kr[2 * cc] + Ur[2 * a + 1] * Kr[2 * cc + 1];
-        }
-        xp[0] = yn[0];
-        xp[1] = yn[1];
-        xp[2] = normalize_radian(yn[2]);   // Robot.cpp:596
+        robot_update(R33, xp, sh_pkg);
         if (j == jstar) matched = true;
         if (lead) res[RES_MATCH + i] = jstar;
         m++;
         EKF_STAMP(6);
     }
+    status |= tstatus;
 
     // ---------------- commit (Robot.cpp:702-716) ----------------
     __syncthreads();   // sh_extra
@@ -978,6 +1372,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         dbg[9] += 1;
     }
 }
+
+#pragma clang fp contract(fast)
 
 // ---------------------------------------------------------------------------------------
 // 2. covariance downdate of the landmark block on MFMA, one pass for a group of steps

@@ -391,3 +391,63 @@ def test_many_lines_per_scan(ekf_mod, oracle_mod, T):
         assert res["matches"] >= 30
     P, y, s, pose = ens.download_state(0)
     assert rel(P, ref.P_t0) <= 1e-5 and rel(y, ref.y) <= 1e-8
+
+
+def _spec_scans(w, rng, steps, L=8):
+    """Scans that stress the speculative association: ordinary scans, a landmark observed twice
+    in one scan, lines that match nothing (appended), and a mix."""
+    out = []
+    for step in range(1, steps + 1):
+        enc, lines, _ = G.make_scan(w, step, lines=L)
+        ln = lines[0].copy()
+        kind = step % 4
+        if kind == 1:
+            ln[3] = ln[1]                                   # the same landmark twice
+        elif kind == 2:
+            ln[5:] = G.random_lines(rng, L - 5)             # unmatched → new landmarks
+        elif kind == 3:
+            ln[[0, 6]] = ln[[6, 0]]
+            ln[2, 1] += 0.02                                # near-miss observation
+        out.append((enc, ln))
+    return out
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("N", [64, 1024, 4096])
+def test_speculative_association_identical(ekf_mod, oracle_mod, monkeypatch, prec, N):
+    """The speculative association (guessed winners, three exchanges per scan, exact local
+    re-check) gives bit-identical state and results to the per-line sequential exchange, also
+    when every guess is wrong (EKF_SPECULATE=2: every scan falls back); association vs the
+    restatement."""
+    w = G.make_world(N, active=N - 30)
+    st = G.initial_state(w)
+    scans = _spec_scans(w, np.random.default_rng(3), 8)
+    runs = {}
+    monkeypatch.setenv("EKF_SCAN_STAMPS", "1")
+    for mode in (0, 1, 2):
+        monkeypatch.setenv("EKF_SPECULATE", str(mode))
+        ens = ekf_mod.Ensemble(N, 1, prec, max_lines=8, flush_interval=4)
+        ens.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
+        if mode == 1:
+            ref = oracle_mod.OracleRobot(N)
+            ref.set_state(*ens.download_state(0))
+        results = []
+        for enc, ln in scans:
+            r = ens.localize(enc, ln[None], [len(ln)])[0]
+            results.append((r["match"], r["matches"], r["new_landmarks"], r["status"]))
+            if mode == 1:
+                assert r["match"] == ref.localize(ln, enc[0]), r["match"]
+        stamps = ens.scan_stamps()
+        runs[mode] = (results, ens.download_state(0), stamps[15])
+        ens.close()
+    assert runs[1][2] == 0, "speculation fell back on ordinary scans"
+    assert runs[2][2] >= 4, "wrong guesses did not fall back"
+    for mode in (1, 2):
+        assert runs[mode][0] == runs[0][0], mode
+        P, y, s, pose = runs[mode][1]
+        P0, y0, s0, pose0 = runs[0][1]
+        bad = np.argwhere(P != P0)
+        assert bad.size == 0, (mode, bad[:8].tolist(), rel(P, P0))
+        np.testing.assert_array_equal(y, y0)
+        np.testing.assert_array_equal(pose, pose0)
+        assert s == s0
