@@ -277,7 +277,7 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         if (words < ekf::MB_WORDS_SPEC) words = ekf::MB_WORDS_SPEC;
         c->mbw = ((words + 15) / 16) * 16;   // whole 128-B lines
     }
-    c->spec = getenv("EKF_SPECULATE") ? atoi(getenv("EKF_SPECULATE")) : 0;
+    c->spec = getenv("EKF_SPECULATE") ? atoi(getenv("EKF_SPECULATE")) : 1;
     ALLOC(c->mbox, sizeof(double) * 2 * c->G * c->mbw * E);
     c->sync_stride = ((ekf::SYNC_WG0 + c->G + 15) / 16) * 16;
     ALLOC(c->sync, sizeof(int) * c->sync_stride * E);

@@ -148,26 +148,35 @@ struct PllView {
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
-// 2x2 block (i0, i0+1) × (j0, j0+1) of the landmark block, i0 and j0 even, as it will be once
-// the pending steps are flushed: per step (in order) a reset, or the rank-2m downdate as the
-// k-ordered FMA chain the MFMA executes, then the step's augmented rows rounded to storage.
-template <typename T>
-__device__ __forceinline__ void pll_block(const PllView<T>& v, int i0, int j0, double out[4])
+// 2x2 blocks (i0, i0+1) × (j0[b], j0[b]+1), b < B, of the landmark block (i0, j0[b] even) as
+// they will be once the pending steps are flushed: per step (in order) a reset, or the rank-2m
+// downdate as the k-ordered FMA chain the MFMA executes, then the step's augmented rows rounded
+// to storage. The B blocks share one pass over the pending steps so that their loads overlap.
+template <typename T, int B>
+__device__ __forceinline__ void pll_blocks(const PllView<T>& v, int i0, const int (&j0)[B], double (&out)[B][4])
 {
-    const bool swap = (i0 >> 5) > (j0 >> 5);
-    const int a0 = swap ? j0 : i0, b0 = swap ? i0 : j0;   // stored orientation
     using C = typename Stor<T>::C;
     using L = typename Stor<T>::L;
-    C acc[4];
+    bool swap[B];
+    int a0[B], b0[B];
+    C acc[B][4];
 #pragma unroll
-    for (int p = 0; p < 2; p++)
+    for (int b = 0; b < B; b++) {
+        swap[b] = (i0 >> 5) > (j0[b] >> 5);
+        a0[b] = swap[b] ? j0[b] : i0;   // stored orientation
+        b0[b] = swap[b] ? i0 : j0[b];
 #pragma unroll
-        for (int c = 0; c < 2; c++) acc[p * 2 + c] = from_store<T>(v.X[ll_offset<L>(a0 + p, b0 + c, v.nb)]);
+        for (int p = 0; p < 2; p++)
+#pragma unroll
+            for (int c = 0; c < 2; c++)
+                acc[b][p * 2 + c] = from_store<T>(v.X[ll_offset<L>(a0[b] + p, b0[b] + c, v.nb)]);
+    }
     for (int q = 0; q < v.npend; q++) {
         const Slot& sq = v.pend[q];
         const int4 cw = v.ctl[q];
         if (cw.x) {
-            acc[0] = acc[1] = acc[2] = acc[3] = (C)0;
+#pragma unroll
+            for (int b = 0; b < B; b++) acc[b][0] = acc[b][1] = acc[b][2] = acc[b][3] = (C)0;
             continue;
         }
         const int ks = cw.y;
@@ -175,88 +184,125 @@ __device__ __forceinline__ void pll_block(const PllView<T>& v, int i0, int j0, d
             if constexpr (sizeof(C) == 4) {
                 // v_mfma_f32_32x32x2_f32 = ordered fmaf chain (k0 lanes 0-31, then k1)
                 const int kh = v.kmax / 2;
-                const float* ua = reinterpret_cast<const float*>(sq.Uop) + v.e * v.opstride +
-                                  ((size_t)(a0 >> 5) * 64 + (a0 & 31)) * kh;   // row a0; a0+1 at +kh
-                const float* vb = reinterpret_cast<const float*>(sq.Vop) + v.e * v.opstride +
-                                  ((size_t)(b0 >> 5) * 64 + (b0 & 31)) * kh;
+                const float* ua[B];
+                const float* vb[B];
+#pragma unroll
+                for (int b = 0; b < B; b++) {
+                    ua[b] = reinterpret_cast<const float*>(sq.Uop) + v.e * v.opstride +
+                            ((size_t)(a0[b] >> 5) * 64 + (a0[b] & 31)) * kh;   // row a0; a0+1 at +kh
+                    vb[b] = reinterpret_cast<const float*>(sq.Vop) + v.e * v.opstride +
+                            ((size_t)(b0[b] >> 5) * 64 + (b0[b] & 31)) * kh;
+                }
                 for (int s0 = 0; s0 < ks; s0 += 4) {
-                    const f32x4v ae0 = *reinterpret_cast<const f32x4v*>(ua + s0);
-                    const f32x4v ae1 = *reinterpret_cast<const f32x4v*>(ua + kh + s0);
-                    const f32x4v ao0 = *reinterpret_cast<const f32x4v*>(ua + 32 * kh + s0);
-                    const f32x4v ao1 = *reinterpret_cast<const f32x4v*>(ua + 33 * kh + s0);
-                    const f32x4v be0 = *reinterpret_cast<const f32x4v*>(vb + s0);
-                    const f32x4v be1 = *reinterpret_cast<const f32x4v*>(vb + kh + s0);
-                    const f32x4v bo0 = *reinterpret_cast<const f32x4v*>(vb + 32 * kh + s0);
-                    const f32x4v bo1 = *reinterpret_cast<const f32x4v*>(vb + 33 * kh + s0);
+                    f32x4v ae0[B], ae1[B], ao0[B], ao1[B], be0[B], be1[B], bo0[B], bo1[B];
+#pragma unroll
+                    for (int b = 0; b < B; b++) {
+                        ae0[b] = *reinterpret_cast<const f32x4v*>(ua[b] + s0);
+                        ae1[b] = *reinterpret_cast<const f32x4v*>(ua[b] + kh + s0);
+                        ao0[b] = *reinterpret_cast<const f32x4v*>(ua[b] + 32 * kh + s0);
+                        ao1[b] = *reinterpret_cast<const f32x4v*>(ua[b] + 33 * kh + s0);
+                        be0[b] = *reinterpret_cast<const f32x4v*>(vb[b] + s0);
+                        be1[b] = *reinterpret_cast<const f32x4v*>(vb[b] + kh + s0);
+                        bo0[b] = *reinterpret_cast<const f32x4v*>(vb[b] + 32 * kh + s0);
+                        bo1[b] = *reinterpret_cast<const f32x4v*>(vb[b] + 33 * kh + s0);
+                    }
 #pragma unroll
                     for (int s = 0; s < 4; s++) {
                         if (s0 + s >= ks) break;
-                        acc[0] = fmaf(ao0[s], bo0[s], fmaf(ae0[s], be0[s], acc[0]));
-                        acc[1] = fmaf(ao0[s], bo1[s], fmaf(ae0[s], be1[s], acc[1]));
-                        acc[2] = fmaf(ao1[s], bo0[s], fmaf(ae1[s], be0[s], acc[2]));
-                        acc[3] = fmaf(ao1[s], bo1[s], fmaf(ae1[s], be1[s], acc[3]));
+#pragma unroll
+                        for (int b = 0; b < B; b++) {
+                            acc[b][0] = fmaf(ao0[b][s], bo0[b][s], fmaf(ae0[b][s], be0[b][s], acc[b][0]));
+                            acc[b][1] = fmaf(ao0[b][s], bo1[b][s], fmaf(ae0[b][s], be1[b][s], acc[b][1]));
+                            acc[b][2] = fmaf(ao1[b][s], bo0[b][s], fmaf(ae1[b][s], be0[b][s], acc[b][2]));
+                            acc[b][3] = fmaf(ao1[b][s], bo1[b][s], fmaf(ae1[b][s], be1[b][s], acc[b][3]));
+                        }
                     }
                 }
             } else {
                 // v_mfma_f64_16x16x4_f64 = ordered fma chain over k = 4s..4s+3
                 const int kq = v.kmax / 4;
-                const double* ua = reinterpret_cast<const double*>(sq.Uop) + v.e * v.opstride +
-                                   ((size_t)(a0 >> 5) * 64 + (a0 & 15)) * (2 * kq) + ((a0 >> 4) & 1) * kq;
-                const double* vb = reinterpret_cast<const double*>(sq.Vop) + v.e * v.opstride +
-                                   ((size_t)(b0 >> 5) * 64 + (b0 & 15)) * (2 * kq) + ((b0 >> 4) & 1) * kq;
+                const double* ua[B];
+                const double* vb[B];
+#pragma unroll
+                for (int b = 0; b < B; b++) {
+                    ua[b] = reinterpret_cast<const double*>(sq.Uop) + v.e * v.opstride +
+                            ((size_t)(a0[b] >> 5) * 64 + (a0[b] & 15)) * (2 * kq) + ((a0[b] >> 4) & 1) * kq;
+                    vb[b] = reinterpret_cast<const double*>(sq.Vop) + v.e * v.opstride +
+                            ((size_t)(b0[b] >> 5) * 64 + (b0[b] & 15)) * (2 * kq) + ((b0[b] >> 4) & 1) * kq;
+                }
                 for (int s = 0; s < ks; s++)
 #pragma unroll
                     for (int kk = 0; kk < 4; kk++) {
                         const size_t o = (size_t)16 * kk * 2 * kq + s;
-                        const double x0 = ua[o], x1 = ua[o + 2 * kq];
-                        const double y0 = vb[o], y1 = vb[o + 2 * kq];
-                        acc[0] = fma(x0, y0, (double)acc[0]);
-                        acc[1] = fma(x0, y1, (double)acc[1]);
-                        acc[2] = fma(x1, y0, (double)acc[2]);
-                        acc[3] = fma(x1, y1, (double)acc[3]);
+#pragma unroll
+                        for (int b = 0; b < B; b++) {
+                            const double x0 = ua[b][o], x1 = ua[b][o + 2 * kq];
+                            const double y0 = vb[b][o], y1 = vb[b][o + 2 * kq];
+                            acc[b][0] = fma(x0, y0, (double)acc[b][0]);
+                            acc[b][1] = fma(x0, y1, (double)acc[b][1]);
+                            acc[b][2] = fma(x1, y0, (double)acc[b][2]);
+                            acc[b][3] = fma(x1, y1, (double)acc[b][3]);
+                        }
                     }
             }
 #pragma unroll
-            for (int k = 0; k < 4; k++) acc[k] = round_step<T>(acc[k]);
+            for (int b = 0; b < B; b++)
+#pragma unroll
+                for (int k = 0; k < 4; k++) acc[b][k] = round_step<T>(acc[b][k]);
         }
         const int nadd = cw.z;
         if (nadd > 0) {
             const int s0 = cw.w;
-            const int li = i0 >> 1, lj = j0 >> 1;
-            const int hi = li > lj ? li : lj;
-            if (hi >= s0 && hi < s0 + nadd) {
-                // augmented rows (requested orientation), rounded as they are stored
-                const int qa = hi - s0;
-                const double* pdg = sq.patch_diag + (size_t)v.e * v.max_lines * 4;
-                const double* prw = sq.patch + ((size_t)v.e * v.max_lines + qa) * 2 * v.M;
-                double raw[4];
-                if (li == lj) {
-                    raw[0] = pdg[qa * 4 + 0]; raw[1] = pdg[qa * 4 + 1];
-                    raw[2] = pdg[qa * 4 + 2]; raw[3] = pdg[qa * 4 + 3];
-                } else if (li > lj) {
-                    raw[0] = prw[j0]; raw[1] = prw[j0 + 1];
-                    raw[2] = prw[v.M + j0]; raw[3] = prw[v.M + j0 + 1];
-                } else {
-                    raw[0] = prw[i0]; raw[1] = prw[v.M + i0];
-                    raw[2] = prw[i0 + 1]; raw[3] = prw[v.M + i0 + 1];
-                }
-                if (swap) {
-                    acc[0] = round_step<T>(to_domain<T>(raw[0])); acc[1] = round_step<T>(to_domain<T>(raw[2]));
-                    acc[2] = round_step<T>(to_domain<T>(raw[1])); acc[3] = round_step<T>(to_domain<T>(raw[3]));
-                } else {
-                    acc[0] = round_step<T>(to_domain<T>(raw[0])); acc[1] = round_step<T>(to_domain<T>(raw[1]));
-                    acc[2] = round_step<T>(to_domain<T>(raw[2])); acc[3] = round_step<T>(to_domain<T>(raw[3]));
+#pragma unroll
+            for (int b = 0; b < B; b++) {
+                const int li = i0 >> 1, lj = j0[b] >> 1;
+                const int hi = li > lj ? li : lj;
+                if (hi >= s0 && hi < s0 + nadd) {
+                    // augmented rows (requested orientation), rounded as they are stored
+                    const int qa = hi - s0;
+                    const double* pdg = sq.patch_diag + (size_t)v.e * v.max_lines * 4;
+                    const double* prw = sq.patch + ((size_t)v.e * v.max_lines + qa) * 2 * v.M;
+                    double raw[4];
+                    if (li == lj) {
+                        raw[0] = pdg[qa * 4 + 0]; raw[1] = pdg[qa * 4 + 1];
+                        raw[2] = pdg[qa * 4 + 2]; raw[3] = pdg[qa * 4 + 3];
+                    } else if (li > lj) {
+                        raw[0] = prw[j0[b]]; raw[1] = prw[j0[b] + 1];
+                        raw[2] = prw[v.M + j0[b]]; raw[3] = prw[v.M + j0[b] + 1];
+                    } else {
+                        raw[0] = prw[i0]; raw[1] = prw[v.M + i0];
+                        raw[2] = prw[i0 + 1]; raw[3] = prw[v.M + i0 + 1];
+                    }
+                    if (swap[b]) {
+                        acc[b][0] = round_step<T>(to_domain<T>(raw[0])); acc[b][1] = round_step<T>(to_domain<T>(raw[2]));
+                        acc[b][2] = round_step<T>(to_domain<T>(raw[1])); acc[b][3] = round_step<T>(to_domain<T>(raw[3]));
+                    } else {
+                        acc[b][0] = round_step<T>(to_domain<T>(raw[0])); acc[b][1] = round_step<T>(to_domain<T>(raw[1]));
+                        acc[b][2] = round_step<T>(to_domain<T>(raw[2])); acc[b][3] = round_step<T>(to_domain<T>(raw[3]));
+                    }
                 }
             }
         }
     }
-    if (swap) {
-        out[0] = from_domain<T>(acc[0]); out[1] = from_domain<T>(acc[2]);
-        out[2] = from_domain<T>(acc[1]); out[3] = from_domain<T>(acc[3]);
-    } else {
-        out[0] = from_domain<T>(acc[0]); out[1] = from_domain<T>(acc[1]);
-        out[2] = from_domain<T>(acc[2]); out[3] = from_domain<T>(acc[3]);
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+        if (swap[b]) {
+            out[b][0] = from_domain<T>(acc[b][0]); out[b][1] = from_domain<T>(acc[b][2]);
+            out[b][2] = from_domain<T>(acc[b][1]); out[b][3] = from_domain<T>(acc[b][3]);
+        } else {
+            out[b][0] = from_domain<T>(acc[b][0]); out[b][1] = from_domain<T>(acc[b][1]);
+            out[b][2] = from_domain<T>(acc[b][2]); out[b][3] = from_domain<T>(acc[b][3]);
+        }
     }
+}
+
+template <typename T>
+__device__ __forceinline__ void pll_block(const PllView<T>& v, int i0, int j0, double out[4])
+{
+    const int js[1] = {j0};
+    double o[1][4];
+    pll_blocks<T, 1>(v, i0, js, o);
+    out[0] = o[0][0]; out[1] = o[0][1]; out[2] = o[0][2]; out[3] = o[0][3];
 }
 
 // The association arithmetic contracts a·b + c only within one source expression, so a
@@ -501,6 +547,18 @@ __device__ __forceinline__ int wait_all_started(int* sync, int G, unsigned epoch
     return 0;
 }
 
+// rows 0..2 of Fx·P for one landmark's robot-strip columns (Robot.cpp:242)
+__device__ __forceinline__ void predict_cols(const double F3[9], double2& rr0, double2& rr1, double2& rr2)
+{
+    const double2 a0 = rr0, a1 = rr1, a2 = rr2;
+    rr0.x = F3[0] * a0.x + F3[1] * a1.x + F3[2] * a2.x;
+    rr0.y = F3[0] * a0.y + F3[1] * a1.y + F3[2] * a2.y;
+    rr1.x = F3[3] * a0.x + F3[4] * a1.x + F3[5] * a2.x;
+    rr1.y = F3[3] * a0.y + F3[4] * a1.y + F3[5] * a2.y;
+    rr2.x = F3[6] * a0.x + F3[7] * a1.x + F3[8] * a2.x;
+    rr2.y = F3[6] * a0.y + F3[7] * a1.y + F3[8] * a2.y;
+}
+
 // R of a line (Robot.cpp:302-304): r_mode 1 reproduces the reference as written (only the
 // first four lines' R[3] lands in a zero-initialised 2×2)
 __device__ __forceinline__ void line_R(const ekf_line& ln, int i, int r_mode, double Rm[4])
@@ -632,20 +690,36 @@ __device__ __forceinline__ void robot_update(double R33[9], double xp[3], const 
 }
 
 // Cheap guess of the exact gate (fp32 sine/cosine, no error bounds). It only steers the
-// speculative association; every decision it feeds is re-checked exactly.
-__device__ __forceinline__ bool guess_pass(const Block5& b, double ma, double mr, const double xp[3],
-                                           double za, double zr, const double Rm[4], double gate)
+// speculative association; every decision it feeds is re-checked exactly. The landmark's part
+// (predicted measurement, H·P·Hᵀ) does not depend on the line and is computed once.
+struct Guess {
+    double h0, h1, S[4];
+};
+
+__device__ __forceinline__ void guess_prep(const Block5& b, double ma, double mr, const double xp[3],
+                                           Guess& gs)
 {
     float sf, cf;
     sincosf((float)ma, &sf, &cf);
     const double sn = sf, cs = cf;
     const double h10 = -cs, h11 = -sn, h1l = xp[0] * sn - xp[1] * cs;
-    double S[4], hp0[5], hp1[5];
-    innovation_cov(b, h10, h11, h1l, Rm, S, hp0, hp1);
-    const double v0 = innovation_angle(za, ma, xp[2]);
-    const double v1 = zr - (mr - (xp[0] * cs + xp[1] * sn));
-    const double q = v0 * v0 * S[3] - v0 * v1 * (S[1] + S[2]) + v1 * v1 * S[0];
-    const double det = S[0] * S[3] - S[1] * S[2];
+    const double R0[4] = {0.0, 0.0, 0.0, 0.0};
+    double hp0[5], hp1[5];
+    innovation_cov(b, h10, h11, h1l, R0, gs.S, hp0, hp1);
+    gs.h0 = normalize_radian(ma - xp[2]);
+    gs.h1 = mr - (xp[0] * cs + xp[1] * sn);
+}
+
+__device__ __forceinline__ bool guess_pass(const Guess& gs, double za, double zr, const double Rm[4],
+                                           double gate)
+{
+    double v0 = za - gs.h0;
+    if (fabs(v0 - 2.0 * EKF_PI) < fabs(v0)) v0 -= 2.0 * EKF_PI;
+    else if (fabs(v0 + 2.0 * EKF_PI) < fabs(v0)) v0 += 2.0 * EKF_PI;
+    const double v1 = zr - gs.h1;
+    const double S0 = gs.S[0] + Rm[0], S1 = gs.S[1] + Rm[1], S2 = gs.S[2] + Rm[2], S3 = gs.S[3] + Rm[3];
+    const double q = v0 * v0 * S3 - v0 * v1 * (S1 + S2) + v1 * v1 * S0;
+    const double det = S0 * S3 - S1 * S2;
     return !(det > 0.0) || q <= gate * gate * det;
 }
 
@@ -657,21 +731,24 @@ __device__ __forceinline__ bool guess_pass(const Block5& b, double ma, double mr
 // of one per line; on a flag the scan restarts on the sequential path (identical results).
 constexpr int SPEC_L = HIST_LDS;                    // lines
 constexpr int SPEC_K = 6;                           // guessed candidates per line per workgroup
+constexpr int SPEC_PB = 2;                          // guessed columns per pass over the pending steps
 constexpr int SPEC_GMAX = 32;                       // workgroups per instance
 constexpr int SPEC_WD = 12 + 4 * (SPEC_L - 1);      // winner record: rr, Dj, y, column blocks
 constexpr int PKW = MB_VH + 4 * SPEC_L;             // package words (speculative lines)
 static_assert(1 + SPEC_L * SPEC_WD <= MB_WORDS_SPEC, "mailbox slot too small");
 
 template <typename T>
-__global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
+__global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
 {
     const Dims d = p.d;
     const int g = blockIdx.x;
     const int e = p.e0 + blockIdx.y;
     const int G = p.G;
     const int tid = threadIdx.x;
-    const int j = g * SCAN_THREADS + tid;      // owned landmark
-    const bool own = j < d.N;
+    // threads < SCAN_THREADS own landmark j; the last wave (no landmark) replays the guessed
+    // winners' chain in the speculative association
+    const int j = tid < SCAN_THREADS ? g * SCAN_THREADS + tid : -1 - tid;
+    const bool own = tid < SCAN_THREADS && j < d.N;
     const int n = d.n, N = d.N, M = d.M;
     const int b0 = 3 + 2 * j;                   // its first row of P
     double* Rs = p.Rs + (size_t)e * 3 * n;
@@ -697,6 +774,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     __shared__ int sh_glist[SPEC_L][SPEC_K + 1];
     __shared__ int sh_spec[SPEC_L];
     __shared__ int sh_flag;
+    __shared__ int sh_ready;
     __shared__ double sh_wd[SPEC_L * SPEC_WD];
     __shared__ double4 sh_wh[SPEC_L][SPEC_L][2];
     __shared__ double sh_pk[SPEC_L][PKW];
@@ -707,6 +785,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     // owned state, in registers for the whole scan
     double2 rr0, rr1, rr2, yb;
     double R33[9], xp[3];
+    double F3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
     // (re)load the owned state and apply the predict (Robot.cpp:130-286, SIMULATIONOFF == true:
     // `rot` unused); the inputs stay untouched until the commit, so a restart is exact
     auto init_state = [&]() {
@@ -728,20 +807,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
             const double c = u2 / 2.0 + t0;
             double sc, cc;
             sincos(c, &sc, &cc);
-            const double F3[9] = {1, 0, -u0 * sc, 0, 1, u0 * cc, 0, 0, 1};
+            F3[2] = -u0 * sc;
+            F3[5] = u0 * cc;
             xp[0] = x0 + u0 * cos(t0 + u2 / 2.0);
             xp[1] = y0 + u0 * sin(t0 + u2 / 2.0);
             xp[2] = t0 + u2;
-            // rows 0..2 of Fx·P for the owned landmark columns (Robot.cpp:242)
-            {
-                const double2 a0 = rr0, a1 = rr1, a2 = rr2;
-                rr0.x = F3[0] * a0.x + F3[1] * a1.x + F3[2] * a2.x;
-                rr0.y = F3[0] * a0.y + F3[1] * a1.y + F3[2] * a2.y;
-                rr1.x = F3[3] * a0.x + F3[4] * a1.x + F3[5] * a2.x;
-                rr1.y = F3[3] * a0.y + F3[4] * a1.y + F3[5] * a2.y;
-                rr2.x = F3[6] * a0.x + F3[7] * a1.x + F3[8] * a2.x;
-                rr2.y = F3[6] * a0.y + F3[7] * a1.y + F3[8] * a2.y;
-            }
+            predict_cols(F3, rr0, rr1, rr2);
             // 3×3 block: F3·P33·F3ᵀ + Fu3·Q·Fu3ᵀ (Robot.cpp:178-258)
             const double Fu3[9] = {cc, 0, -u0 * sc / 2.0, sc, 1, u0 * cc / 2.0, 0, 0, 1};
             const double qs = (-1.0 / (1 + fabs(u0)) + 1);
@@ -827,7 +898,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
     L = L < 0 ? 0 : (L > d.max_lines ? d.max_lines : L);
     const int s = p.saved[e];
     const ekf_line* lines = p.lines + (size_t)e * d.max_lines;
-    for (int k = tid; k < L * 6; k += SCAN_THREADS)
+    for (int k = tid; k < L * 6; k += SCAN_BLOCK)
         reinterpret_cast<double*>(sh_lines)[k] = reinterpret_cast<const double*>(lines)[k];
     // all per-instance inputs that the lead rewrites at the end (robot 3×3, pose, saved) are read
     signal_started(sync, tid);
@@ -879,11 +950,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         if (own && j < s) {
             Block5 b5;
             fill_block5(b5, R33, rr0, rr1, rr2, Dj);
-            for (int t = 0; t < L; t++) {
+            Guess gs;
+            guess_prep(b5, yb.x, yb.y, xp, gs);
+#pragma unroll
+            for (int t = 0; t < SPEC_L; t++) {
+                if (t >= L) break;
                 const ekf_line ln = sh_lines[t];
                 double Rm[4];
                 line_R(ln, t, p.r_mode, Rm);
-                if (guess_pass(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate)) gp |= 1u << t;
+                if (guess_pass(gs, ln.alpha, ln.r, Rm, p.gate)) gp |= 1u << t;
             }
             if (p.spec == 2 && L > 1)   // test hook: every guess taken from the next line
                 gp = ((gp >> 1) | (gp << (L - 1))) & ((1u << L) - 1u);
@@ -892,7 +967,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         // in landmark order: word = 8-bit local indices | count << 48 | more << 52
         for (int t = 0; t < L; t++) {
             const unsigned long long mk = __ballot((gp >> t) & 1u);
-            if ((tid & 63) == 0) sh_wl[t][tid >> 6] = mk;
+            if ((tid & 63) == 0 && tid < SCAN_THREADS) sh_wl[t][tid >> 6] = mk;
         }
         __syncthreads();
         if (tid < L) {
@@ -912,6 +987,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
             sh_lists[g * SPEC_L + tid] = word;
         }
         __syncthreads();
+        if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[5] += _t - t_last; t_last = _t; }
         // ---- (b) exchange 1 (parity 0): every workgroup's lists ----
         if (G > 1) {
             double* slot = mbox + (size_t)g * p.mbw;
@@ -921,7 +997,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
             if (tid == 0) mb_tag(slot, p.epoch, TAG_SPEC_LISTS, 0);
             if (tid < G) (void)mb_poll(mbox, 0, G, tid, p.mbw, p.epoch, TAG_SPEC_LISTS, tstatus);
             __syncthreads();
-            for (int k = tid; k < G * L; k += SCAN_THREADS) {
+            for (int k = tid; k < G * L; k += SCAN_BLOCK) {
                 const int gq = k / L, t = k - gq * L;
                 if (gq != g)
                     sh_lists[gq * SPEC_L + t] =
@@ -947,20 +1023,29 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         }
         __syncthreads();
         if (tid == 0) {
+            int spec[SPEC_L];
             int unresolved = 0;
-            for (int t = 0; t < L; t++) {
-                const int info = sh_glist[t][SPEC_K];
-                const int cnt = info & 255;
-                int w = -1;
-                for (int k = 0; k < cnt && w < 0; k++) {
-                    const int cand = sh_glist[t][k];
-                    bool taken = false;
-                    for (int q = 0; q < t; q++) taken |= (sh_spec[q] == cand);
-                    if (!taken) w = cand;
+#pragma unroll
+            for (int t = 0; t < SPEC_L; t++) {
+                spec[t] = -1;
+                if (t < L) {
+                    const int info = sh_glist[t][SPEC_K];
+                    const int cnt = info & 255;
+                    int w = -1;
+#pragma unroll
+                    for (int k = 0; k < SPEC_K; k++) {
+                        const int cand = sh_glist[t][k];
+                        bool taken = false;
+#pragma unroll
+                        for (int q = 0; q < t; q++) taken |= (spec[q] == cand);
+                        if (k < cnt && w < 0 && !taken) w = cand;
+                    }
+                    if (w < 0 && (info >> 8)) unresolved = 1;
+                    spec[t] = w;
                 }
-                if (w < 0 && (info >> 8)) unresolved = 1;
-                sh_spec[t] = w;
             }
+#pragma unroll
+            for (int t = 0; t < SPEC_L; t++) sh_spec[t] = spec[t];
             sh_flag = unresolved;
         }
         __syncthreads();
@@ -970,151 +1055,171 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
             sequential = false;
             // ---- (d) owned blocks of the guessed columns (Robot.cpp:560 operands) ----
             if (own)
-                for (int t = 0; t < L; t++) {
-                    const int w = sh_spec[t];
-                    if (w >= 0) {
-                        double bk[4];
-                        pll_block(pv, 2 * j, 2 * w, bk);
-                        sh_vhist[t][tid] = make_double4(bk[0], bk[1], bk[2], bk[3]);
+                for (int t0 = 0; t0 < L; t0 += SPEC_PB) {
+                    int cols[SPEC_PB];
+                    double bk[SPEC_PB][4];
+#pragma unroll
+                    for (int b = 0; b < SPEC_PB; b++) {
+                        const int w = (t0 + b < L) ? sh_spec[t0 + b] : -1;
+                        cols[b] = 2 * (w >= 0 ? w : j);
                     }
+                    pll_blocks<T, SPEC_PB>(pv, 2 * j, cols, bk);
+#pragma unroll
+                    for (int b = 0; b < SPEC_PB; b++)
+                        if (t0 + b < L && sh_spec[t0 + b] >= 0)
+                            sh_vhist[t0 + b][tid] = make_double4(bk[b][0], bk[b][1], bk[b][2], bk[b][3]);
                 }
-            // the owner of each guessed winner u writes its record: robot-strip columns,
-            // diagonal block, mean, and its blocks of the earlier winners' columns
-            if (own)
-                for (int u = 0; u < L; u++)
-                    if (sh_spec[u] == j) {
-                        double* r = sh_wd + u * SPEC_WD;
-                        r[0] = rr0.x; r[1] = rr0.y; r[2] = rr1.x; r[3] = rr1.y; r[4] = rr2.x; r[5] = rr2.y;
-                        r[6] = Dj[0]; r[7] = Dj[1]; r[8] = Dj[2]; r[9] = Dj[3];
-                        r[10] = yb.x; r[11] = yb.y;
-                        for (int t = 0; t < u; t++) {
-                            const double4 bk = sh_vhist[t][tid];
-                            r[12 + 4 * t] = bk.x; r[13 + 4 * t] = bk.y;
-                            r[14 + 4 * t] = bk.z; r[15 + 4 * t] = bk.w;
-                        }
-                    }
-            __syncthreads();
-            // ---- (e) exchange 2 (parity 1): the winner records ----
-            if (G > 1) {
-                double* slot = mbox + ((size_t)G + g) * p.mbw;
-                for (int k = tid; k < L * SPEC_WD; k += SCAN_THREADS) {
-                    const int u = k / SPEC_WD, w = sh_spec[u];
-                    if (w >= 0 && w / SCAN_THREADS == g && k - u * SPEC_WD < 12 + 4 * u)
-                        mb_store(slot + 1 + k, sh_wd[k]);
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (tid == 0) mb_tag(slot, p.epoch, TAG_SPEC_WINNERS, 0);
-                if (tid < G) (void)mb_poll(mbox, 1, G, tid, p.mbw, p.epoch, TAG_SPEC_WINNERS, tstatus);
-                __syncthreads();
-                for (int k = tid; k < L * SPEC_WD; k += SCAN_THREADS) {
-                    const int u = k / SPEC_WD, w = sh_spec[u];
-                    if (w >= 0 && w / SCAN_THREADS != g && k - u * SPEC_WD < 12 + 4 * u)
-                        sh_wd[k] = mb_load(mbox + ((size_t)G + w / SCAN_THREADS) * p.mbw + 1 + k);
-                }
-                __syncthreads();
-            }
             if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[11] += _t - t_last; t_last = _t; }
-            // ---- (f) the winners' part of the sequential chain (one thread, every workgroup):
-            // each line's package from its winner's state, then the later winners' rows ----
-            if (tid == 0) {
+            // the winners' records straight from memory, as their owners hold them: predicted
+            // robot-strip columns and mean, diagonal block, blocks of the earlier winners' columns
+            if (tid == SCAN_BLOCK - 1) sh_ready = 0;
+            if (tid < L * (L + 1) / 2) {
+                int u = 0, t = tid;
+                while (t > u) { t -= u + 1; u++; }
+                const int wu = sh_spec[u], wt = sh_spec[t];
+                if (wu >= 0 && wt >= 0) {
+                    double bk[4];
+                    pll_block(pv, 2 * wu, 2 * wt, bk);
+                    double* r = sh_wd + u * SPEC_WD + (t == u ? 6 : 12 + 4 * t);
+                    r[0] = bk[0]; r[1] = bk[1]; r[2] = bk[2]; r[3] = bk[3];
+                }
+            } else if (tid >= 128 && tid < 128 + L) {
+                const int u = tid - 128, wu = sh_spec[u];
+                if (wu >= 0) {
+                    const int bw = 3 + 2 * wu;
+                    double2 q0 = *reinterpret_cast<const double2*>(Rs + bw);
+                    double2 q1 = *reinterpret_cast<const double2*>(Rs + n + bw);
+                    double2 q2 = *reinterpret_cast<const double2*>(Rs + 2 * n + bw);
+                    const double2 qy = *reinterpret_cast<const double2*>(y + bw);
+                    if (p.phase & PHASE_PREDICT) predict_cols(F3, q0, q1, q2);
+                    double* r = sh_wd + u * SPEC_WD;
+                    r[0] = q0.x; r[1] = q0.y; r[2] = q1.x; r[3] = q1.y; r[4] = q2.x; r[5] = q2.y;
+                    r[10] = qy.x; r[11] = qy.y;
+                }
+            }
+            __syncthreads();
+            if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[12] += _t - t_last; t_last = _t; }
+            // ---- (f) the winners' part of the sequential chain, in the last wave (lane u carries
+            // winner u's rows): per line the winner's lane evaluates it and writes the package,
+            // then the later winners' lanes apply their gain rows. Meanwhile (g) the landmark
+            // waves run every line as soon as its package is published (sh_ready). ----
+            int viol = 0;
+            if (tid >= SCAN_THREADS) {
+                const int u = tid - SCAN_THREADS;
+                const unsigned long long t_l0 = __builtin_amdgcn_s_memrealtime();
+                const bool act = u < L && sh_spec[u] >= 0;
                 double R33l[9], xpl[3];
 #pragma unroll
                 for (int a = 0; a < 9; a++) R33l[a] = R33[a];
                 xpl[0] = xp[0]; xpl[1] = xp[1]; xpl[2] = xp[2];
+                double2 w0 = make_double2(0, 0), w1 = w0, w2 = w0, wy = w0;
+                double wD[4] = {0, 0, 0, 0};
+                if (act) {
+                    const double* r = sh_wd + u * SPEC_WD;
+                    w0 = make_double2(r[0], r[1]); w1 = make_double2(r[2], r[3]);
+                    w2 = make_double2(r[4], r[5]); wy = make_double2(r[10], r[11]);
+                    wD[0] = r[6]; wD[1] = r[7]; wD[2] = r[8]; wD[3] = r[9];
+                }
                 int ml = 0, bad = 0;
-                for (int t = 0; t < L && !bad; t++) {
+                for (int t = 0; t < L; t++) {
                     if (sh_spec[t] < 0) continue;
-                    const ekf_line ln = sh_lines[t];
-                    double Rm[4];
-                    line_R(ln, t, p.r_mode, Rm);
-                    double* r = sh_wd + t * SPEC_WD;
-                    double2 w0 = make_double2(r[0], r[1]), w1 = make_double2(r[2], r[3]);
-                    double2 w2 = make_double2(r[4], r[5]);
-                    const double wD[4] = {r[6], r[7], r[8], r[9]};
-                    Block5 b5;
-                    fill_block5(b5, R33l, w0, w1, w2, wD);
-                    Cand c;
-                    eval_candidate(b5, r[10], r[11], xpl, ln.alpha, ln.r, Rm, p.gate, c);
-                    if (!c.pass) { bad = 1; break; }
                     double* pk = sh_pk[t];
-                    build_package(c, R33l, w0, w1, w2, pk);
-                    for (int q = 0; q < ml; q++) {
-                        const double4 vq = sh_wh[t][q][1];
-                        pk[MB_VH + 4 * q + 0] = vq.x; pk[MB_VH + 4 * q + 1] = vq.y;
-                        pk[MB_VH + 4 * q + 2] = vq.z; pk[MB_VH + 4 * q + 3] = vq.w;
+                    if (u == t) {
+                        const ekf_line ln = sh_lines[t];
+                        double Rm[4];
+                        line_R(ln, t, p.r_mode, Rm);
+                        Block5 b5;
+                        fill_block5(b5, R33l, w0, w1, w2, wD);
+                        Cand c;
+                        eval_candidate(b5, wy.x, wy.y, xpl, ln.alpha, ln.r, Rm, p.gate, c);
+                        bad |= c.pass ? 0 : 1;
+                        build_package(c, R33l, w0, w1, w2, pk);
+                        for (int q = 0; q < ml; q++) {
+                            const double4 vq = sh_wh[u][q][1];
+                            pk[MB_VH + 4 * q + 0] = vq.x; pk[MB_VH + 4 * q + 1] = vq.y;
+                            pk[MB_VH + 4 * q + 2] = vq.z; pk[MB_VH + 4 * q + 3] = vq.w;
+                        }
                     }
-                    for (int u = t + 1; u < L; u++) {
-                        if (sh_spec[u] < 0) continue;
-                        double* ru = sh_wd + u * SPEC_WD;
-                        double2 q0 = make_double2(ru[0], ru[1]), q1 = make_double2(ru[2], ru[3]);
-                        double2 q2 = make_double2(ru[4], ru[5]), qy = make_double2(ru[10], ru[11]);
-                        double qD[4] = {ru[6], ru[7], ru[8], ru[9]};
-                        double blk[4] = {ru[12 + 4 * t], ru[13 + 4 * t], ru[14 + 4 * t], ru[15 + 4 * t]};
+                    // the package is complete: to the other lanes of this wave, and to the
+                    // landmark waves (release of all lanes' LDS writes, then the line counter)
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                    if (u == 0) __hip_atomic_store(&sh_ready, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if (act && u > t) {
+                        const double* r = sh_wd + u * SPEC_WD + 12 + 4 * t;
+                        double blk[4] = {r[0], r[1], r[2], r[3]};
                         double kk[4], uu[4];
-                        gain_rows(pk, ml, [&](int q) { return sh_wh[u][q][0]; }, blk, q0, q1, q2, qy, qD, kk, uu);
-                        ru[0] = q0.x; ru[1] = q0.y; ru[2] = q1.x; ru[3] = q1.y; ru[4] = q2.x; ru[5] = q2.y;
-                        ru[6] = qD[0]; ru[7] = qD[1]; ru[8] = qD[2]; ru[9] = qD[3];
-                        ru[10] = qy.x; ru[11] = qy.y;
+                        gain_rows(pk, ml, [&](int q) { return sh_wh[u][q][0]; }, blk, w0, w1, w2, wy, wD, kk, uu);
                         sh_wh[u][ml][0] = make_double4(uu[0], uu[1], uu[2], uu[3]);
                         sh_wh[u][ml][1] = make_double4(kk[0], kk[1], kk[2], kk[3]);
                     }
                     robot_update(R33l, xpl, pk);
                     ml++;
                 }
-                sh_flag = bad;
+                bad = __any(bad) ? 1 : 0;
+                if (u == 0) {
+                    sh_flag = bad;
+                    if (p.dbg && g == 0) p.dbg[(size_t)e * 16 + 13] += __builtin_amdgcn_s_memrealtime() - t_l0;
+                }
+            } else {
+                // ---- (g) the landmark waves: the sequential gating and gain rows against the
+                // packages ----
+                for (int i = 0; i < L && !viol; ++i) {
+                    const ekf_line ln = sh_lines[i];
+                    double Rm[4];
+                    line_R(ln, i, p.r_mode, Rm);
+                    const int w = sh_spec[i];
+                    if (own && j < s && !matched) {
+                        Block5 b5;
+                        fill_block5(b5, R33, rr0, rr1, rr2, Dj);
+                        bool pass = false;
+                        if (!certified_reject(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate)) {
+                            Cand c;
+                            eval_candidate(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate, c);
+                            status |= c.singular ? EKF_ST_SINGULAR : 0;
+                            pass = c.pass;
+                        }
+                        // the guess must be the first passing unmatched landmark
+                        if (pass ? (w < 0 || j < w) : (j == w)) viol = 1;
+                    }
+                    if (w < 0) {
+                        // no match: the line goes to extraLines (Robot.cpp:308-310, 492-496)
+                        if (lead) {
+                            res[RES_MATCH + i] = -1;
+                            res[RES_EXTRA + nextra] = i;
+                        }
+                        if (tid == 0) sh_extra[nextra] = i;
+                        nextra++;
+                        continue;
+                    }
+                    int polls = 0;
+                    while (__hip_atomic_load(&sh_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= i) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++polls > (1 << 24)) { tstatus |= EKF_ST_TIMEOUT_BIT; viol = 1; break; }
+                    }
+                    const double* pk = sh_pk[i];
+                    if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
+                    if (own) {
+                        const double4 bk = sh_vhist[i][tid];
+                        double blk[4] = {bk.x, bk.y, bk.z, bk.w};
+                        double kk[4], uu[4];
+                        gain_rows(pk, m, uq_owned, blk, rr0, rr1, rr2, yb, Dj, kk, uu);
+                        store_rows(m, kk, uu, false);
+                    }
+                    robot_update(R33, xp, pk);
+                    if (j == w) matched = true;
+                    if (lead) res[RES_MATCH + i] = w;
+                    m++;
+                }
             }
             __syncthreads();
-            if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[12] += _t - t_last; t_last = _t; }
-            // ---- (g) every thread: the sequential gating and gain rows against the packages ----
-            int viol = sh_flag;
-            for (int i = 0; i < L && !viol; ++i) {
-                const ekf_line ln = sh_lines[i];
-                double Rm[4];
-                line_R(ln, i, p.r_mode, Rm);
-                const int w = sh_spec[i];
-                if (own && j < s && !matched) {
-                    Block5 b5;
-                    fill_block5(b5, R33, rr0, rr1, rr2, Dj);
-                    bool pass = false;
-                    if (!certified_reject(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate)) {
-                        Cand c;
-                        eval_candidate(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate, c);
-                        status |= c.singular ? EKF_ST_SINGULAR : 0;
-                        pass = c.pass;
-                    }
-                    // the guess must be the first passing unmatched landmark
-                    if (pass ? (w < 0 || j < w) : (j == w)) viol = 1;
-                }
-                if (w < 0) {
-                    // no match: the line goes to extraLines (Robot.cpp:308-310, 492-496)
-                    if (lead) {
-                        res[RES_MATCH + i] = -1;
-                        res[RES_EXTRA + nextra] = i;
-                    }
-                    if (tid == 0) sh_extra[nextra] = i;
-                    nextra++;
-                    continue;
-                }
-                const double* pk = sh_pk[i];
-                if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
-                if (own) {
-                    const double4 bk = sh_vhist[i][tid];
-                    double blk[4] = {bk.x, bk.y, bk.z, bk.w};
-                    double kk[4], uu[4];
-                    gain_rows(pk, m, uq_owned, blk, rr0, rr1, rr2, yb, Dj, kk, uu);
-                    store_rows(m, kk, uu, false);
-                }
-                robot_update(R33, xp, pk);
-                if (j == w) matched = true;
-                if (lead) res[RES_MATCH + i] = w;
-                m++;
-            }
-            if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[13] += _t - t_last; t_last = _t; }
+            viol |= sh_flag;
+            if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[14] += _t - t_last; t_last = _t; }
             // ---- (h) verdict (exchange 3, parity 0): any flag restarts on the sequential path ----
             const int wv = __any(viol) ? 1 : 0;
             __syncthreads();
-            if ((tid & 63) == 0) sh_red[tid >> 6] = wv;
+            if ((tid & 63) == 0 && tid < SCAN_THREADS) sh_red[tid >> 6] = wv;
             __syncthreads();
             int any = 0;
 #pragma unroll
@@ -1128,7 +1233,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
                 __syncthreads();
                 for (int k = 0; k < G; k++) any |= sh_best[k];
             }
-            if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[14] += _t - t_last; t_last = _t; }
+            if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[6] += _t - t_last; t_last = _t; }
             if (any) {
                 if (dbg) dbg[15] += 1;
                 sequential = true;
@@ -1163,7 +1268,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
         }
         EKF_STAMP(2);
         const int wbest = wave_min(best);
-        if ((tid & 63) == 0) sh_red[tid >> 6] = wbest;
+        if ((tid & 63) == 0 && tid < SCAN_THREADS) sh_red[tid >> 6] = wbest;
         __syncthreads();
         int gbest = sh_red[0];
 #pragma unroll
@@ -1191,12 +1296,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
             // to the mailbox, one word per lane; drained and ordered by the barrier before the
             // tagged best word (payload best + 1, 0: no candidate); every workgroup polls all G
             if (gbest != 0x7fffffff)
-                for (int k = 1 + tid; k < npk; k += SCAN_THREADS) mb_store(slot + k, sh_pkg[k]);
+                for (int k = 1 + tid; k < npk; k += SCAN_BLOCK) mb_store(slot + k, sh_pkg[k]);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid == 0) mb_tag(slot, p.epoch, (unsigned)(i + 1), (unsigned)(gbest == 0x7fffffff ? 0 : gbest + 1));
             EKF_STAMP(3);
-            for (int k = tid; k < G; k += SCAN_THREADS) {
+            for (int k = tid; k < G; k += SCAN_BLOCK) {
                 const int bq = mb_poll(mbox, par, G, k, p.mbw, p.epoch, (unsigned)(i + 1), tstatus);
                 sh_best[k] = bq <= 0 ? 0x7fffffff : bq - 1;
             }
@@ -1230,10 +1335,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
             const double* ps = mbox + ((size_t)par * G + gstar) * p.mbw;
             double pk0 = 0.0, pk1 = 0.0;
             if (tid < npk) pk0 = mb_load(ps + tid);
-            if (tid + SCAN_THREADS < npk) pk1 = mb_load(ps + tid + SCAN_THREADS);
+            if (tid + SCAN_BLOCK < npk) pk1 = mb_load(ps + tid + SCAN_BLOCK);
             if (own) pll_block(pv, 2 * j, 2 * jstar, blk);
             if (tid < npk) sh_pkg[tid] = pk0;
-            if (tid + SCAN_THREADS < npk) sh_pkg[tid + SCAN_THREADS] = pk1;
+            if (tid + SCAN_BLOCK < npk) sh_pkg[tid + SCAN_BLOCK] = pk1;
             __syncthreads();
         } else if (own) {
             pll_block(pv, 2 * j, 2 * jstar, blk);
@@ -1338,7 +1443,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanParams p)
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) st |= __shfl_xor(st, off, 64);
         __syncthreads();
-        if ((tid & 63) == 0) sh_red[tid >> 6] = st;
+        if ((tid & 63) == 0 && tid < SCAN_THREADS) sh_red[tid >> 6] = st;
         __syncthreads();
 #pragma unroll
         for (int w = 0; w < SCAN_THREADS / 64; w++) wgst |= sh_red[w];
@@ -2318,20 +2423,20 @@ int scan_blocks_per_cu(int precision)
 {
     int nb = 0;
     hipError_t err =
-        (precision == EKF_PREC_F64) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<double>, SCAN_THREADS, 0)
-        : (precision == EKF_PREC_F16) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<_Float16>, SCAN_THREADS, 0)
-        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<float>, SCAN_THREADS, 0);
+        (precision == EKF_PREC_F64) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<double>, SCAN_BLOCK, 0)
+        : (precision == EKF_PREC_F16) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<_Float16>, SCAN_BLOCK, 0)
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<float>, SCAN_BLOCK, 0);
     return err == hipSuccess ? nb : 0;
 }
 
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 {
     if (precision == EKF_PREC_F64)
-        hipLaunchKernelGGL(scan_kernel<double>, dim3(p.G, p.E), dim3(SCAN_THREADS), 0, st, p);
+        hipLaunchKernelGGL(scan_kernel<double>, dim3(p.G, p.E), dim3(SCAN_BLOCK), 0, st, p);
     else if (precision == EKF_PREC_F16)
-        hipLaunchKernelGGL(scan_kernel<_Float16>, dim3(p.G, p.E), dim3(SCAN_THREADS), 0, st, p);
+        hipLaunchKernelGGL(scan_kernel<_Float16>, dim3(p.G, p.E), dim3(SCAN_BLOCK), 0, st, p);
     else
-        hipLaunchKernelGGL(scan_kernel<float>, dim3(p.G, p.E), dim3(SCAN_THREADS), 0, st, p);
+        hipLaunchKernelGGL(scan_kernel<float>, dim3(p.G, p.E), dim3(SCAN_BLOCK), 0, st, p);
     return hipGetLastError();
 }
 
