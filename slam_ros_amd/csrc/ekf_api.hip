@@ -208,7 +208,7 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     *out = nullptr;
     // capacity bound: one association thread per landmark, at most MAX_GROUPS workgroups of
     // SCAN_THREADS per instance (N <= 32768, i.e. n <= 65539)
-    if (cfg->capacity < 1 || cfg->capacity > ekf::MAX_GROUPS * ekf::SCAN_THREADS ||
+    if (cfg->capacity < 1 || cfg->capacity > ekf::MAX_CAPACITY ||
         cfg->instances < 1 ||
         cfg->max_lines < 1 ||
         cfg->max_lines > EKF_MAX_LINES ||

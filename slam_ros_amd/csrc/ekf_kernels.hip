@@ -148,6 +148,69 @@ struct PllView {
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
+// Stored 2×2 block at rows a0, a0+1 and columns b0, b0+1 (a0, b0 even, a0's tile <= b0's):
+// acc = {(a0,b0), (a0,b0+1), (a0+1,b0), (a0+1,b0+1)}. In the f32 tile layout the two rows of a
+// column are adjacent and the two columns are 4 elements apart: two paired loads.
+template <typename T>
+__device__ __forceinline__ void load_block(const PllView<T>& v, int a0, int b0, typename Stor<T>::C (&acc)[4])
+{
+    using L = typename Stor<T>::L;
+    if constexpr (sizeof(L) == 4) {
+        const T* x = v.X + ll_offset<L>(a0, b0, v.nb);
+        if constexpr (sizeof(T) == 4) {
+            const float2 c0 = *reinterpret_cast<const float2*>(x);
+            const float2 c1 = *reinterpret_cast<const float2*>(x + 4);
+            acc[0] = from_store<T>(c0.x); acc[2] = from_store<T>(c0.y);
+            acc[1] = from_store<T>(c1.x); acc[3] = from_store<T>(c1.y);
+        } else {
+            typedef T t2 __attribute__((ext_vector_type(2)));
+            const t2 c0 = *reinterpret_cast<const t2*>(x);
+            const t2 c1 = *reinterpret_cast<const t2*>(x + 4);
+            acc[0] = from_store<T>(c0.x); acc[2] = from_store<T>(c0.y);
+            acc[1] = from_store<T>(c1.x); acc[3] = from_store<T>(c1.y);
+        }
+    } else {
+#pragma unroll
+        for (int p = 0; p < 2; p++)
+#pragma unroll
+            for (int c = 0; c < 2; c++) acc[p * 2 + c] = from_store<T>(v.X[ll_offset<L>(a0 + p, b0 + c, v.nb)]);
+    }
+}
+
+// The rows a step appended (Robot.cpp:845-862) replace block (i0, j0) if it lies in them:
+// requested orientation, rounded as they are stored.
+template <typename T>
+__device__ __forceinline__ void patch_block(const PllView<T>& v, const Slot& sq, int4 cw, int i0, int j0,
+                                            bool swap, typename Stor<T>::C (&acc)[4])
+{
+    const int nadd = cw.z, s0 = cw.w;
+    const int li = i0 >> 1, lj = j0 >> 1;
+    const int hi = li > lj ? li : lj;
+    if (hi >= s0 && hi < s0 + nadd) {
+        const int qa = hi - s0;
+        const double* pdg = sq.patch_diag + (size_t)v.e * v.max_lines * 4;
+        const double* prw = sq.patch + ((size_t)v.e * v.max_lines + qa) * 2 * v.M;
+        double raw[4];
+        if (li == lj) {
+            raw[0] = pdg[qa * 4 + 0]; raw[1] = pdg[qa * 4 + 1];
+            raw[2] = pdg[qa * 4 + 2]; raw[3] = pdg[qa * 4 + 3];
+        } else if (li > lj) {
+            raw[0] = prw[j0]; raw[1] = prw[j0 + 1];
+            raw[2] = prw[v.M + j0]; raw[3] = prw[v.M + j0 + 1];
+        } else {
+            raw[0] = prw[i0]; raw[1] = prw[v.M + i0];
+            raw[2] = prw[i0 + 1]; raw[3] = prw[v.M + i0 + 1];
+        }
+        if (swap) {
+            acc[0] = round_step<T>(to_domain<T>(raw[0])); acc[1] = round_step<T>(to_domain<T>(raw[2]));
+            acc[2] = round_step<T>(to_domain<T>(raw[1])); acc[3] = round_step<T>(to_domain<T>(raw[3]));
+        } else {
+            acc[0] = round_step<T>(to_domain<T>(raw[0])); acc[1] = round_step<T>(to_domain<T>(raw[1]));
+            acc[2] = round_step<T>(to_domain<T>(raw[2])); acc[3] = round_step<T>(to_domain<T>(raw[3]));
+        }
+    }
+}
+
 // 2x2 blocks (i0, i0+1) × (j0[b], j0[b]+1), b < B, of the landmark block (i0, j0[b] even) as
 // they will be once the pending steps are flushed: per step (in order) a reset, or the rank-2m
 // downdate as the k-ordered FMA chain the MFMA executes, then the step's augmented rows rounded
@@ -156,7 +219,6 @@ template <typename T, int B>
 __device__ __forceinline__ void pll_blocks(const PllView<T>& v, int i0, const int (&j0)[B], double (&out)[B][4])
 {
     using C = typename Stor<T>::C;
-    using L = typename Stor<T>::L;
     bool swap[B];
     int a0[B], b0[B];
     C acc[B][4];
@@ -165,11 +227,7 @@ __device__ __forceinline__ void pll_blocks(const PllView<T>& v, int i0, const in
         swap[b] = (i0 >> 5) > (j0[b] >> 5);
         a0[b] = swap[b] ? j0[b] : i0;   // stored orientation
         b0[b] = swap[b] ? i0 : j0[b];
-#pragma unroll
-        for (int p = 0; p < 2; p++)
-#pragma unroll
-            for (int c = 0; c < 2; c++)
-                acc[b][p * 2 + c] = from_store<T>(v.X[ll_offset<L>(a0[b] + p, b0[b] + c, v.nb)]);
+        load_block<T>(v, a0[b], b0[b], acc[b]);
     }
     for (int q = 0; q < v.npend; q++) {
         const Slot& sq = v.pend[q];
@@ -250,38 +308,9 @@ __device__ __forceinline__ void pll_blocks(const PllView<T>& v, int i0, const in
 #pragma unroll
                 for (int k = 0; k < 4; k++) acc[b][k] = round_step<T>(acc[b][k]);
         }
-        const int nadd = cw.z;
-        if (nadd > 0) {
-            const int s0 = cw.w;
+        if (cw.z > 0) {
 #pragma unroll
-            for (int b = 0; b < B; b++) {
-                const int li = i0 >> 1, lj = j0[b] >> 1;
-                const int hi = li > lj ? li : lj;
-                if (hi >= s0 && hi < s0 + nadd) {
-                    // augmented rows (requested orientation), rounded as they are stored
-                    const int qa = hi - s0;
-                    const double* pdg = sq.patch_diag + (size_t)v.e * v.max_lines * 4;
-                    const double* prw = sq.patch + ((size_t)v.e * v.max_lines + qa) * 2 * v.M;
-                    double raw[4];
-                    if (li == lj) {
-                        raw[0] = pdg[qa * 4 + 0]; raw[1] = pdg[qa * 4 + 1];
-                        raw[2] = pdg[qa * 4 + 2]; raw[3] = pdg[qa * 4 + 3];
-                    } else if (li > lj) {
-                        raw[0] = prw[j0[b]]; raw[1] = prw[j0[b] + 1];
-                        raw[2] = prw[v.M + j0[b]]; raw[3] = prw[v.M + j0[b] + 1];
-                    } else {
-                        raw[0] = prw[i0]; raw[1] = prw[v.M + i0];
-                        raw[2] = prw[i0 + 1]; raw[3] = prw[v.M + i0 + 1];
-                    }
-                    if (swap[b]) {
-                        acc[b][0] = round_step<T>(to_domain<T>(raw[0])); acc[b][1] = round_step<T>(to_domain<T>(raw[2]));
-                        acc[b][2] = round_step<T>(to_domain<T>(raw[1])); acc[b][3] = round_step<T>(to_domain<T>(raw[3]));
-                    } else {
-                        acc[b][0] = round_step<T>(to_domain<T>(raw[0])); acc[b][1] = round_step<T>(to_domain<T>(raw[1]));
-                        acc[b][2] = round_step<T>(to_domain<T>(raw[2])); acc[b][3] = round_step<T>(to_domain<T>(raw[3]));
-                    }
-                }
-            }
+            for (int b = 0; b < B; b++) patch_block<T>(v, sq, cw, i0, j0[b], swap[b], acc[b]);
         }
     }
 #pragma unroll
@@ -454,7 +483,7 @@ __device__ __forceinline__ bool certified_reject(const Block5& b, double ma, dou
     do {                                                                        \
         if (dbg) {                                                              \
             const unsigned long long _t = __builtin_amdgcn_s_memrealtime();     \
-            dbg[k] += _t - t_last;                                              \
+            sh_stamp[k] += _t - t_last;                                         \
             t_last = _t;                                                        \
         }                                                                       \
     } while (0)
@@ -723,19 +752,120 @@ __device__ __forceinline__ bool guess_pass(const Guess& gs, double za, double zr
     return !(det > 0.0) || q <= gate * gate * det;
 }
 
+constexpr int SPEC_L = HIST_LDS;                    // lines
+constexpr int SPEC_K = 6;                           // guessed candidates per line per workgroup
+constexpr int SPEC_PB = 2;                          // guessed columns per pass over the pending steps
+constexpr int SPEC_QMAX = 4;                        // pending steps staged in LDS
+constexpr int SPEC_GMAX = 64;                       // workgroups per instance (<= one wave)
+constexpr int SPEC_WD = 12 + 4 * (SPEC_L - 1);      // winner record: rr, Dj, y, column blocks
+constexpr int PKW = MB_VH + 4 * SPEC_L;             // package words (speculative lines)
+static_assert(1 + SPEC_L * SPEC_WD <= MB_WORDS_SPEC, "mailbox slot too small");
+
+// Blocks (j, cols[t]) for t < SPEC_L and (j, j) (last; only if `diag`) of the landmark block
+// with the pending steps applied, fp32 operands, every pending step with ks <= 8: the guessed
+// columns' operand rows come from LDS (stg[t][q][U|V][row half][8], staged by the workgroup),
+// the owned rows are loaded once per step. Per element the same chain as pll_blocks.
+template <typename T>
+__device__ __forceinline__ void staged_blocks(const PllView<T>& v, int j, const int (&cols)[8],
+                                              const float* stg, bool diag, double (&out)[9][4])
+{
+    using C = typename Stor<T>::C;
+    constexpr int NB = 9;
+    const int i0 = 2 * j;
+    bool swap[NB];
+    int jb[NB];
+    C acc[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        jb[b] = 2 * (b < 8 ? cols[b] : j);
+        swap[b] = (i0 >> 5) > (jb[b] >> 5);
+        const int a0 = swap[b] ? jb[b] : i0, b0 = swap[b] ? i0 : jb[b];
+        load_block<T>(v, a0, b0, acc[b]);
+    }
+    const int kh = v.kmax / 2;
+    for (int q = 0; q < v.npend; q++) {
+        const Slot& sq = v.pend[q];
+        const int4 cw = v.ctl[q];
+        if (cw.x) {
+#pragma unroll
+            for (int b = 0; b < NB; b++) acc[b][0] = acc[b][1] = acc[b][2] = acc[b][3] = (C)0;
+            continue;
+        }
+        const int ks = cw.y;
+        if (ks > 0) {
+            // owned rows i0, i0+1 of U_q and V_q: [row half][2 × 4 k]
+            const float* ou = reinterpret_cast<const float*>(sq.Uop) + v.e * v.opstride +
+                              ((size_t)(i0 >> 5) * 64 + (i0 & 31)) * kh;
+            const float* ov = reinterpret_cast<const float*>(sq.Vop) + v.e * v.opstride +
+                              ((size_t)(i0 >> 5) * 64 + (i0 & 31)) * kh;
+            f32x4v U[4][2], V[4][2];
+#pragma unroll
+            for (int rh = 0; rh < 4; rh++) {
+                const int roff = (rh & 1) * kh + (rh >> 1) * 32 * kh;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    U[rh][h] = *reinterpret_cast<const f32x4v*>(ou + roff + 4 * h);
+                    V[rh][h] = *reinterpret_cast<const f32x4v*>(ov + roff + 4 * h);
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+                // a side: owned U rows, or the column's U rows when the block is stored transposed;
+                // b side: the column's V rows, or the owned V rows
+                const float* cu = stg + (((b * SPEC_QMAX + q) * 2 + 0) * 4) * 8;
+                const float* cv = stg + (((b * SPEC_QMAX + q) * 2 + 1) * 4) * 8;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    f32x4v A[4], Bv[4];
+#pragma unroll
+                    for (int rh = 0; rh < 4; rh++) {
+                        if (b < 8) {
+                            const f32x4v su = *reinterpret_cast<const f32x4v*>(cu + rh * 8 + 4 * h);
+                            const f32x4v sv = *reinterpret_cast<const f32x4v*>(cv + rh * 8 + 4 * h);
+                            A[rh] = swap[b] ? su : U[rh][h];
+                            Bv[rh] = swap[b] ? V[rh][h] : sv;
+                        } else {
+                            A[rh] = U[rh][h];
+                            Bv[rh] = V[rh][h];
+                        }
+                    }
+                    // rows: 0 = a0 even k, 1 = a0+1 even, 2 = a0 odd, 3 = a0+1 odd
+#pragma unroll
+                    for (int s = 0; s < 4; s++) {
+                        if (4 * h + s >= ks) break;
+                        acc[b][0] = fmaf(A[2][s], Bv[2][s], fmaf(A[0][s], Bv[0][s], acc[b][0]));
+                        acc[b][1] = fmaf(A[2][s], Bv[3][s], fmaf(A[0][s], Bv[1][s], acc[b][1]));
+                        acc[b][2] = fmaf(A[3][s], Bv[2][s], fmaf(A[1][s], Bv[0][s], acc[b][2]));
+                        acc[b][3] = fmaf(A[3][s], Bv[3][s], fmaf(A[1][s], Bv[1][s], acc[b][3]));
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) acc[b][k] = round_step<T>(acc[b][k]);
+            }
+        }
+        if (cw.z > 0) {
+#pragma unroll
+            for (int b = 0; b < NB; b++) patch_block<T>(v, sq, cw, i0, jb[b], swap[b], acc[b]);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        if (swap[b]) {
+            out[b][0] = from_domain<T>(acc[b][0]); out[b][1] = from_domain<T>(acc[b][2]);
+            out[b][2] = from_domain<T>(acc[b][1]); out[b][3] = from_domain<T>(acc[b][3]);
+        } else {
+            out[b][0] = from_domain<T>(acc[b][0]); out[b][1] = from_domain<T>(acc[b][1]);
+            out[b][2] = from_domain<T>(acc[b][2]); out[b][3] = from_domain<T>(acc[b][3]);
+        }
+    }
+}
+
 // Speculative association (lines <= SPEC_L, G <= SPEC_GMAX): every line's winner is guessed
 // from the pre-update state, the guesses' mutual data are exchanged once, every workgroup
 // replays the winners' part of the sequential chain to get all gain packages, then every thread
 // runs the sequential gating and gain rows against those packages locally and flags any line
 // whose exact first passing candidate differs from the guess. Three exchanges per scan instead
 // of one per line; on a flag the scan restarts on the sequential path (identical results).
-constexpr int SPEC_L = HIST_LDS;                    // lines
-constexpr int SPEC_K = 6;                           // guessed candidates per line per workgroup
-constexpr int SPEC_PB = 2;                          // guessed columns per pass over the pending steps
-constexpr int SPEC_GMAX = 32;                       // workgroups per instance
-constexpr int SPEC_WD = 12 + 4 * (SPEC_L - 1);      // winner record: rr, Dj, y, column blocks
-constexpr int PKW = MB_VH + 4 * SPEC_L;             // package words (speculative lines)
-static_assert(1 + SPEC_L * SPEC_WD <= MB_WORDS_SPEC, "mailbox slot too small");
 
 template <typename T>
 __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
@@ -778,7 +908,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     __shared__ double sh_wd[SPEC_L * SPEC_WD];
     __shared__ double4 sh_wh[SPEC_L][SPEC_L][2];
     __shared__ double sh_pk[SPEC_L][PKW];
+    __shared__ float sh_stg[SPEC_L * SPEC_QMAX * 2 * 4 * 8];   // staged pending-step rows
+    __shared__ unsigned long long sh_stamp[16];
     unsigned long long* dbg = (p.dbg && lead) ? p.dbg + (size_t)e * 16 : nullptr;
+    if (p.dbg && tid < 16) sh_stamp[tid] = 0;
     unsigned long long t_last = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const unsigned long long t_first = t_last;
 
@@ -809,8 +942,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             sincos(c, &sc, &cc);
             F3[2] = -u0 * sc;
             F3[5] = u0 * cc;
-            xp[0] = x0 + u0 * cos(t0 + u2 / 2.0);
-            xp[1] = y0 + u0 * sin(t0 + u2 / 2.0);
+            // cos/sin(t0 + u2/2) of Robot.cpp:150-151: the same angle as c (addition commutes)
+            xp[0] = x0 + u0 * cc;
+            xp[1] = y0 + u0 * sc;
             xp[2] = t0 + u2;
             predict_cols(F3, rr0, rr1, rr2);
             // 3×3 block: F3·P33·F3ᵀ + Fu3·Q·Fu3ᵀ (Robot.cpp:178-258)
@@ -903,8 +1037,28 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // all per-instance inputs that the lead rewrites at the end (robot 3×3, pose, saved) are read
     signal_started(sync, tid);
 
+    const bool spec_ok = p.spec && L > 0 && L <= SPEC_L && s > 0 && G <= SPEC_GMAX;
+    // speculative path with fp32 operands and few pending steps: the pending steps' rows of the
+    // guessed columns are staged in LDS and one pass per step updates all owned blocks
+    bool staged = false;
+    if (spec_ok && sizeof(typename Stor<T>::C) == 4 && p.npend <= SPEC_QMAX && d.kmax / 2 >= 8) {
+        __syncthreads();   // sh_ctl
+        staged = true;
+        for (int q = 0; q < p.npend; q++) staged &= sh_ctl[q].y <= 8;
+    }
     double Dj[4] = {0, 0, 0, 0};   // owned diagonal block
-    if (own && j < s) pll_block(pv, 2 * j, 2 * j, Dj);
+    if (own && j < s) {
+        if (staged) {
+            // the guess only needs it approximately: the last flushed value (exact one below)
+            const T* X = pv.X;
+            using Lq = typename Stor<T>::L;
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+                Dj[a] = from_domain<T>(from_store<T>(X[ll_offset<Lq>(2 * j + (a >> 1), 2 * j + (a & 1), d.nb)]));
+        } else {
+            pll_block(pv, 2 * j, 2 * j, Dj);
+        }
+    }
     EKF_STAMP(1);
 
     // writes a match's owned rows: U/V history and the MFMA downdate operands
@@ -944,7 +1098,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     int par0 = 0;   // mailbox parity of line 0 on the sequential path
     bool sequential = true;
 
-    if (p.spec && L > 0 && L <= SPEC_L && s > 0 && G <= SPEC_GMAX) {
+    if (spec_ok) {
         // ---- (a) guesses: per line, does the owned landmark pass under the predicted state ----
         unsigned gp = 0;
         if (own && j < s) {
@@ -987,7 +1141,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             sh_lists[g * SPEC_L + tid] = word;
         }
         __syncthreads();
-        if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[5] += _t - t_last; t_last = _t; }
+        EKF_STAMP(5);
         // ---- (b) exchange 1 (parity 0): every workgroup's lists ----
         if (G > 1) {
             double* slot = mbox + (size_t)g * p.mbw;
@@ -1005,74 +1159,86 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             }
             __syncthreads();
         }
-        // ---- (c) guessed winners: per line the first SPEC_K guessed candidates of the instance
-        // (workgroups are in landmark order), then in line order the first one not already taken
-        // by an earlier line (every workgroup computes the same) ----
-        if (tid < L) {
-            int cnt = 0, more = 0;
-            for (int gq = 0; gq < G; gq++) {
-                const unsigned long long w = sh_lists[gq * SPEC_L + tid];
-                const int c = (int)((w >> 48) & 15);
-                for (int k = 0; k < c; k++) {
-                    if (cnt < SPEC_K) sh_glist[tid][cnt++] = gq * SCAN_THREADS + (int)((w >> (8 * k)) & 255);
-                    else more = 1;
-                }
-                if ((w >> 52) & 1) more = 1;
-            }
-            sh_glist[tid][SPEC_K] = cnt | (more << 8);
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int spec[SPEC_L];
-            int unresolved = 0;
+        EKF_STAMP(2);
+        // ---- (c) guessed winners (every workgroup computes the same). Fast form: per line the
+        // instance's first guessed candidate (workgroups are in landmark order); if those are
+        // distinct they are the winners. Otherwise, per line the first SPEC_K guessed candidates,
+        // and in line order the first one not taken by an earlier line. ----
+        if (tid < 64) {
+            int first[SPEC_L];
 #pragma unroll
             for (int t = 0; t < SPEC_L; t++) {
-                spec[t] = -1;
-                if (t < L) {
-                    const int info = sh_glist[t][SPEC_K];
-                    const int cnt = info & 255;
-                    int w = -1;
-#pragma unroll
-                    for (int k = 0; k < SPEC_K; k++) {
-                        const int cand = sh_glist[t][k];
-                        bool taken = false;
-#pragma unroll
-                        for (int q = 0; q < t; q++) taken |= (spec[q] == cand);
-                        if (k < cnt && w < 0 && !taken) w = cand;
-                    }
-                    if (w < 0 && (info >> 8)) unresolved = 1;
-                    spec[t] = w;
+                int c = 0x7fffffff;
+                if (t < L && tid < G) {
+                    const unsigned long long w = sh_lists[tid * SPEC_L + t];
+                    if ((w >> 48) & 15) c = tid * SCAN_THREADS + (int)(w & 255);
                 }
+                first[t] = wave_min(c);
             }
+            if (tid == 0) {
+                bool distinct = true;
 #pragma unroll
-            for (int t = 0; t < SPEC_L; t++) sh_spec[t] = spec[t];
-            sh_flag = unresolved;
+                for (int t = 0; t < SPEC_L; t++)
+#pragma unroll
+                    for (int q = 0; q < t; q++)
+                        distinct &= !(t < L && first[t] != 0x7fffffff && first[t] == first[q]);
+#pragma unroll
+                for (int t = 0; t < SPEC_L; t++) sh_spec[t] = first[t] == 0x7fffffff ? -1 : first[t];
+                sh_flag = distinct ? 0 : 2;
+            }
         }
         __syncthreads();
-        if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[10] += _t - t_last; t_last = _t; }
+        if (sh_flag == 2) {
+            if (tid < L) {
+                int cnt = 0, more = 0;
+                for (int gq = 0; gq < G; gq++) {
+                    const unsigned long long w = sh_lists[gq * SPEC_L + tid];
+                    const int c = (int)((w >> 48) & 15);
+                    for (int k = 0; k < c; k++) {
+                        if (cnt < SPEC_K) sh_glist[tid][cnt++] = gq * SCAN_THREADS + (int)((w >> (8 * k)) & 255);
+                        else more = 1;
+                    }
+                    if ((w >> 52) & 1) more = 1;
+                }
+                sh_glist[tid][SPEC_K] = cnt | (more << 8);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int spec[SPEC_L];
+                int unresolved = 0;
+    #pragma unroll
+                for (int t = 0; t < SPEC_L; t++) {
+                    spec[t] = -1;
+                    if (t < L) {
+                        const int info = sh_glist[t][SPEC_K];
+                        const int cnt = info & 255;
+                        int w = -1;
+    #pragma unroll
+                        for (int k = 0; k < SPEC_K; k++) {
+                            const int cand = sh_glist[t][k];
+                            bool taken = false;
+    #pragma unroll
+                            for (int q = 0; q < t; q++) taken |= (spec[q] == cand);
+                            if (k < cnt && w < 0 && !taken) w = cand;
+                        }
+                        if (w < 0 && (info >> 8)) unresolved = 1;
+                        spec[t] = w;
+                    }
+                }
+    #pragma unroll
+                for (int t = 0; t < SPEC_L; t++) sh_spec[t] = spec[t];
+                sh_flag = unresolved;
+            }
+            __syncthreads();
+        }
+        EKF_STAMP(10);
 
         if (!sh_flag) {
             sequential = false;
-            // ---- (d) owned blocks of the guessed columns (Robot.cpp:560 operands) ----
-            if (own)
-                for (int t0 = 0; t0 < L; t0 += SPEC_PB) {
-                    int cols[SPEC_PB];
-                    double bk[SPEC_PB][4];
-#pragma unroll
-                    for (int b = 0; b < SPEC_PB; b++) {
-                        const int w = (t0 + b < L) ? sh_spec[t0 + b] : -1;
-                        cols[b] = 2 * (w >= 0 ? w : j);
-                    }
-                    pll_blocks<T, SPEC_PB>(pv, 2 * j, cols, bk);
-#pragma unroll
-                    for (int b = 0; b < SPEC_PB; b++)
-                        if (t0 + b < L && sh_spec[t0 + b] >= 0)
-                            sh_vhist[t0 + b][tid] = make_double4(bk[b][0], bk[b][1], bk[b][2], bk[b][3]);
-                }
-            if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[11] += _t - t_last; t_last = _t; }
-            // the winners' records straight from memory, as their owners hold them: predicted
-            // robot-strip columns and mean, diagonal block, blocks of the earlier winners' columns
-            if (tid == SCAN_BLOCK - 1) sh_ready = 0;
+            // ---- (d) the winners' records straight from memory, as their owners hold them:
+            // predicted robot-strip columns and mean, diagonal block, blocks of the earlier
+            // winners' columns; and (staged replay) the guessed columns' rows of the pending
+            // steps' operands ----
             if (tid < L * (L + 1) / 2) {
                 int u = 0, t = tid;
                 while (t > u) { t -= u + 1; u++; }
@@ -1083,8 +1249,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     double* r = sh_wd + u * SPEC_WD + (t == u ? 6 : 12 + 4 * t);
                     r[0] = bk[0]; r[1] = bk[1]; r[2] = bk[2]; r[3] = bk[3];
                 }
-            } else if (tid >= 128 && tid < 128 + L) {
-                const int u = tid - 128, wu = sh_spec[u];
+            } else if (tid >= SCAN_THREADS && tid < SCAN_THREADS + L) {
+                const int u = tid - SCAN_THREADS, wu = sh_spec[u];
                 if (wu >= 0) {
                     const int bw = 3 + 2 * wu;
                     double2 q0 = *reinterpret_cast<const double2*>(Rs + bw);
@@ -1097,8 +1263,26 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     r[10] = qy.x; r[11] = qy.y;
                 }
             }
+            if (staged) {
+                // rows 2w, 2w+1 of U_q and V_q of every guessed column w, pending step q
+                // (4 row halves × 8 k each)
+                const int kh = d.kmax / 2;
+                const int nld = L * p.npend * 2 * 4 * 2;
+                for (int k = tid; k < nld; k += SCAN_BLOCK) {
+                    const int half = k & 1, rh = (k >> 1) & 3, side = (k >> 3) & 1;
+                    const int tq = k >> 4, q = tq % p.npend, t = tq / p.npend;
+                    const int w = sh_spec[t];
+                    if (w < 0) continue;
+                    const float* base = reinterpret_cast<const float*>(side ? p.pend[q].Vop : p.pend[q].Uop) +
+                                        e * opstride + ((size_t)((2 * w) >> 5) * 64 + ((2 * w) & 31)) * kh;
+                    const int roff = (rh & 1) * kh + (rh >> 1) * 32 * kh;
+                    *reinterpret_cast<f32x4v*>(sh_stg + ((((t * SPEC_QMAX + q) * 2 + side) * 4 + rh) * 8) + half * 4) =
+                        *reinterpret_cast<const f32x4v*>(base + roff + half * 4);
+                }
+            }
+            if (tid == SCAN_BLOCK - 1) sh_ready = 0;
             __syncthreads();
-            if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[12] += _t - t_last; t_last = _t; }
+            EKF_STAMP(12);
             // ---- (f) the winners' part of the sequential chain, in the last wave (lane u carries
             // winner u's rows): per line the winner's lane evaluates it and writes the package,
             // then the later winners' lanes apply their gain rows. Meanwhile (g) the landmark
@@ -1160,9 +1344,47 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 bad = __any(bad) ? 1 : 0;
                 if (u == 0) {
                     sh_flag = bad;
-                    if (p.dbg && g == 0) p.dbg[(size_t)e * 16 + 13] += __builtin_amdgcn_s_memrealtime() - t_l0;
+                    if (p.dbg && g == 0) sh_stamp[13] += __builtin_amdgcn_s_memrealtime() - t_l0;
                 }
             } else {
+                // ---- (e) owned blocks of the guessed columns (Robot.cpp:560 operands), while the
+                // last wave runs (f) ----
+                if (own) {
+                    if (staged) {
+                        int cols[SPEC_L];
+#pragma unroll
+                        for (int t = 0; t < SPEC_L; t++) {
+                            const int w = t < L ? sh_spec[t] : -1;
+                            cols[t] = w >= 0 ? w : j;
+                        }
+                        double blk[SPEC_L + 1][4];
+                        staged_blocks<T>(pv, j, cols, sh_stg, j < s, blk);
+#pragma unroll
+                        for (int t = 0; t < SPEC_L; t++)
+                            if (t < L && sh_spec[t] >= 0)
+                                sh_vhist[t][tid] = make_double4(blk[t][0], blk[t][1], blk[t][2], blk[t][3]);
+                        if (j < s) {
+                            Dj[0] = blk[SPEC_L][0]; Dj[1] = blk[SPEC_L][1];
+                            Dj[2] = blk[SPEC_L][2]; Dj[3] = blk[SPEC_L][3];
+                        }
+                    } else {
+                        for (int t0 = 0; t0 < L; t0 += SPEC_PB) {
+                            int cols[SPEC_PB];
+                            double bk[SPEC_PB][4];
+#pragma unroll
+                            for (int b = 0; b < SPEC_PB; b++) {
+                                const int w = (t0 + b < L) ? sh_spec[t0 + b] : -1;
+                                cols[b] = 2 * (w >= 0 ? w : j);
+                            }
+                            pll_blocks<T, SPEC_PB>(pv, 2 * j, cols, bk);
+#pragma unroll
+                            for (int b = 0; b < SPEC_PB; b++)
+                                if (t0 + b < L && sh_spec[t0 + b] >= 0)
+                                    sh_vhist[t0 + b][tid] = make_double4(bk[b][0], bk[b][1], bk[b][2], bk[b][3]);
+                        }
+                    }
+                }
+                EKF_STAMP(11);
                 // ---- (g) the landmark waves: the sequential gating and gain rows against the
                 // packages ----
                 for (int i = 0; i < L && !viol; ++i) {
@@ -1215,7 +1437,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             }
             __syncthreads();
             viol |= sh_flag;
-            if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[14] += _t - t_last; t_last = _t; }
+            EKF_STAMP(14);
             // ---- (h) verdict (exchange 3, parity 0): any flag restarts on the sequential path ----
             const int wv = __any(viol) ? 1 : 0;
             __syncthreads();
@@ -1233,9 +1455,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 __syncthreads();
                 for (int k = 0; k < G; k++) any |= sh_best[k];
             }
-            if (dbg) { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); dbg[6] += _t - t_last; t_last = _t; }
+            EKF_STAMP(6);
             if (any) {
-                if (dbg) dbg[15] += 1;
+                if (dbg) sh_stamp[15] += 1;
                 sequential = true;
                 par0 = 1;
                 init_state();
@@ -1473,6 +1695,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     }
     EKF_STAMP(7);
     if (dbg) {
+        // (phase times accumulate in LDS: a global read-modify-write per stamp would add a
+        // memory round trip to every phase it measures)
+        for (int k = 0; k < 16; k++) dbg[k] += sh_stamp[k];
         dbg[8] += t_last - t_first;
         dbg[9] += 1;
     }
