@@ -1,14 +1,15 @@
 // ekf_api.hip — C-ABI (include/slam_ekf.h) over the gfx950 kernels in ekf_kernels.hip.
 //
 // A context owns E instances' state in HBM and two HIP streams:
-//   S  association/gain kernels (scan_kernel) — all state except the landmark block;
-//   D  the landmark-block flush (downdate kernel).
+//   S  association/gain kernels (scan_kernel) — all state except the landmark block — and, on
+//      the sequential schedule, the flushes too (stream order is the only dependency);
+//   D  the landmark-block flush of the pipelined schedule.
 // Every update step k writes its downdate operands, augmented rows and result record into slot
 // k mod R of a ring. The landmark block is rewritten by a flush once per group of T =
 // flush_interval steps; association kernels read the last materialised block ("base") with the
 // steps not yet in it applied on read (bit-identical to flushing first, see ekf_kernels.hip).
-//   sequential (pipeline = 0): one buffer, flushed in place; R = T. A scan waits for the last
-//     flush; a flush waits for the last scan of its group.
+//   sequential (pipeline = 0): one buffer, flushed in place on S after the group's last scan;
+//     R = T.
 //   pipelined  (pipeline = 1): flush f reads X[in] and writes X[out] = the other buffer while the
 //     next group's scans run on S reading X[in] — the output of flush f-1 — with the steps of
 //     groups f and f+1 pending (< 2T); R = 2T.
@@ -485,7 +486,10 @@ static int enqueue_flush(ekf_ctx* c)
 {
     const int nst = (int)(c->nsteps - c->unflushed0);
     if (nst <= 0) return EKF_OK;
-    HIP_TRY(hipStreamWaitEvent(c->dstream, c->ev_scan, 0));
+    // sequential schedule: the flush follows the scans on S (no cross-stream events); pipelined:
+    // on D after the group's last scan
+    hipStream_t fs = c->cfg.pipeline ? c->dstream : c->stream;
+    if (c->cfg.pipeline) HIP_TRY(hipStreamWaitEvent(c->dstream, c->ev_scan, 0));
     ekf::DowndateParams dp;
     memset(&dp, 0, sizeof(dp));
     dp.d = c->d;
@@ -502,11 +506,11 @@ static int enqueue_flush(ekf_ctx* c)
     const int out = c->cfg.pipeline ? 1 - in : in;
     dp.Pin = c->X[in];
     dp.Pout = c->X[out];
-    EvPair* pr = prof_begin(c, 1, c->dstream);
-    HIP_TRY(ekf::launch_downdate(dp, c->cfg.precision, c->dd_grid, c->dstream));
-    prof_end(c, pr, c->dstream);
+    EvPair* pr = prof_begin(c, 1, fs);
+    HIP_TRY(ekf::launch_downdate(dp, c->cfg.precision, c->dd_grid, fs));
+    prof_end(c, pr, fs);
     hipEvent_t ev = c->ev_flush[c->nflush & 1];
-    HIP_TRY(hipEventRecord(ev, c->dstream));
+    if (c->cfg.pipeline) HIP_TRY(hipEventRecord(ev, fs));
     if (c->cfg.pipeline) {
         // next scans read X[in] (= output of the previous flush) with both groups pending
         c->base = in;
@@ -514,7 +518,7 @@ static int enqueue_flush(ekf_ctx* c)
         c->pend0 = c->unflushed0;
     } else {
         c->base = in;
-        c->ev_base = ev;
+        c->ev_base = nullptr;   // same stream
         c->pend0 = c->nsteps;
     }
     c->last_out = out;
@@ -547,7 +551,7 @@ static int enqueue(ekf_ctx* c, int phase, const double* enc, const ekf_line* lin
     EvPair* pr = prof_begin(c, 0, c->stream);
     HIP_TRY(launch_scans(c, sp));
     prof_end(c, pr, c->stream);
-    HIP_TRY(hipEventRecord(c->ev_scan, c->stream));
+    if (c->cfg.pipeline) HIP_TRY(hipEventRecord(c->ev_scan, c->stream));
     c->nsteps++;
     if (c->nsteps - c->unflushed0 >= c->T) return enqueue_flush(c);
     return EKF_OK;
