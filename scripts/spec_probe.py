@@ -19,7 +19,7 @@ for mode in (0, 1, 2):
     stp = ens.scan_stamps()
     n = stp[9] or 1
     us = [round(v * 10e-3 / n, 2) for v in stp[:15]]
-    names = {0: "predict", 1: "diag", 2: "seq-gating|spec-ex1-xchg", 3: "seq-mbox|spec-stage", 4: "seq-exch", 6: "seq-gain/spec-verdict",
+    names = {0: "predict", 1: "diag", 2: "seq-gating|spec-ex1-xchg", 3: "seq-mbox|leader-eval", 4: "seq-exch|leader-gain", 6: "seq-gain/spec-verdict",
              5: "spec-guess", 10: "spec-resolve", 11: "spec-prefetch(wave0)", 12: "spec-records+stage", 13: "spec-leader",
              14: "spec-local", 7: "commit", 8: "total"}
     print(mode, ms, json.dumps({names[k]: us[k] for k in sorted(names) if us[k]}), "fallbacks", stp[15])

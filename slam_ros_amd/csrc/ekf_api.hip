@@ -273,11 +273,7 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     ALLOC(c->d_lines, sizeof(ekf_line) * d.max_lines * E);
     ALLOC(c->d_nlines, sizeof(int) * E);
     c->G = (d.N + ekf::SCAN_THREADS - 1) / ekf::SCAN_THREADS;
-    {
-        int words = ekf::MB_WORDS_FIXED + 4 * d.max_lines;
-        if (words < ekf::MB_WORDS_SPEC) words = ekf::MB_WORDS_SPEC;
-        c->mbw = ((words + 15) / 16) * 16;   // whole 128-B lines
-    }
+    c->mbw = ((ekf::MB_WORDS_FIXED + 4 * d.max_lines + 15) / 16) * 16;   // whole 128-B lines
     c->spec = getenv("EKF_SPECULATE") ? atoi(getenv("EKF_SPECULATE")) : 1;
     ALLOC(c->mbox, sizeof(double) * 2 * c->G * c->mbw * E);
     c->sync_stride = ((ekf::SYNC_WG0 + c->G + 15) / 16) * 16;

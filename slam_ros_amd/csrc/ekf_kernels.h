@@ -17,7 +17,6 @@ enum { EKF_ST_SINGULAR = EKF_ST_SINGULAR_S, EKF_ST_CAP = EKF_ST_CAPACITY, EKF_ST
 enum { SYNC_START = 0, SYNC_WG0 = 4 };
 constexpr int MAX_GROUPS = (MAX_CAPACITY + SCAN_THREADS - 1) / SCAN_THREADS;   // workgroups per instance
 constexpr int MB_WORDS_FIXED = 26; // mailbox words before the V-history (see ekf_kernels.hip)
-constexpr int MB_WORDS_SPEC = 1 + 8 * (12 + 4 * 7);   // speculative association: winner records
 
 // per-instance result record in device memory (ints)
 enum {

@@ -406,13 +406,30 @@ __device__ __forceinline__ double innovation_angle(double za, double ma, double 
     return v0;
 }
 
+// sin/cos of a landmark angle from those of its value at the start of the scan: the angle
+// moves by small Kalman corrections within a scan, so sin/cos(ma0 + δ) by the addition formula
+// with Taylor series in δ (|δ| <= 1/64: truncation below 1e-19), and the full fp64 sincos
+// otherwise. Every path that evaluates a candidate uses this form, so they agree bit for bit.
+__device__ __forceinline__ void sincos_near(double ma, double ma0, double s0, double c0, double& sn,
+                                            double& cs)
+{
+    const double dl = ma - ma0;
+    if (fabs(dl) <= 0.015625) {
+        const double d2 = dl * dl;
+        const double sd = dl * (1.0 - d2 * (1.0 / 6.0) * (1.0 - d2 * (1.0 / 20.0) * (1.0 - d2 * (1.0 / 42.0))));
+        const double cm = d2 * 0.5 * (1.0 - d2 * (1.0 / 12.0) * (1.0 - d2 * (1.0 / 30.0) * (1.0 - d2 * (1.0 / 56.0))));
+        sn = s0 - (s0 * cm - c0 * sd);   // s0·cos δ + c0·sin δ, cos δ = 1 − cm
+        cs = c0 - (c0 * cm + s0 * sd);   // c0·cos δ − s0·sin δ
+    } else {
+        sincos(ma, &sn, &cs);
+    }
+}
+
 // Exact candidate evaluation in fp64 (Robot.cpp:367-489).
-__device__ __forceinline__ void eval_candidate(const Block5& b, double ma, double mr,
-                                               const double xp[3], double za, double zr,
+__device__ __forceinline__ void eval_candidate(const Block5& b, double ma, double mr, double sn,
+                                               double cs, const double xp[3], double za, double zr,
                                                const double Rm[4], double gate, Cand& c)
 {
-    double sn, cs;
-    sincos(ma, &sn, &cs);
     c.h10 = -cs;
     c.h11 = -sn;
     c.h1l = xp[0] * sn - xp[1] * cs;
@@ -432,20 +449,17 @@ __device__ __forceinline__ void eval_candidate(const Block5& b, double ma, doubl
     c.pass = !(sqrt(fabs(d2)) > gate);
 }
 
-// Certified rejection without fp64 transcendentals: true only if the exact evaluation is
-// guaranteed to fail the gate. cos/sin come from fp32 sincosf (|error| <= EPS for |ma| <= 8);
+// Certified rejection: true only if the exact evaluation is guaranteed to fail the gate. It
+// accepts sin/cos with |error| <= EPS (here the exact ones of sincos_near);
 // the resulting error in S and v is bounded explicitly and d² = q/det is bounded from below by
 // interval arithmetic. Requires a symmetric R and a determinant that is not tiny relative to
 // |S00·S11| + |S01·S10| (so that the reference's LU-based d² is within 1e-9 of q/det).
-__device__ __forceinline__ bool certified_reject(const Block5& b, double ma, double mr,
-                                                 const double xp[3], double za, double zr,
+__device__ __forceinline__ bool certified_reject(const Block5& b, double ma, double mr, double sn,
+                                                 double cs, const double xp[3], double za, double zr,
                                                  const double Rm[4], double gate)
 {
     if (!(fabs(ma) <= 8.0) || Rm[1] != Rm[2]) return false;
     const double EPS = 1e-5;
-    float sf, cf;
-    sincosf((float)ma, &sf, &cf);
-    const double sn = sf, cs = cf;
     const double h10 = -cs, h11 = -sn, h1l = xp[0] * sn - xp[1] * cs;
     double S[4], hp0[5], hp1[5];
     innovation_cov(b, h10, h11, h1l, Rm, S, hp0, hp1);
@@ -757,9 +771,8 @@ constexpr int SPEC_K = 6;                           // guessed candidates per li
 constexpr int SPEC_PB = 2;                          // guessed columns per pass over the pending steps
 constexpr int SPEC_QMAX = 4;                        // pending steps staged in LDS
 constexpr int SPEC_GMAX = 64;                       // workgroups per instance (<= one wave)
-constexpr int SPEC_WD = 12 + 4 * (SPEC_L - 1);      // winner record: rr, Dj, y, column blocks
+constexpr int SPEC_WD = 14 + 4 * (SPEC_L - 1);      // winner record: rr, Dj, y, sin/cos, column blocks
 constexpr int PKW = MB_VH + 4 * SPEC_L;             // package words (speculative lines)
-static_assert(1 + SPEC_L * SPEC_WD <= MB_WORDS_SPEC, "mailbox slot too small");
 
 // Blocks (j, cols[t]) for t < SPEC_L and (j, j) (last; only if `diag`) of the landmark block
 // with the pending steps applied, fp32 operands, every pending step with ks <= 8: the guessed
@@ -979,6 +992,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         }
     };
     init_state();
+    // the owned landmark's angle at the start of the scan and its sin/cos (sincos_near)
+    double ma0 = yb.x, s0j = 0.0, c0j = 1.0;
+    if (own && (p.phase & PHASE_UPDATE)) sincos(ma0, &s0j, &c0j);
 
     if (!(p.phase & PHASE_UPDATE)) {
         // predict only: write the predicted robot strip, 3×3 block and x_pre
@@ -1246,7 +1262,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 if (wu >= 0 && wt >= 0) {
                     double bk[4];
                     pll_block(pv, 2 * wu, 2 * wt, bk);
-                    double* r = sh_wd + u * SPEC_WD + (t == u ? 6 : 12 + 4 * t);
+                    double* r = sh_wd + u * SPEC_WD + (t == u ? 6 : 14 + 4 * t);
                     r[0] = bk[0]; r[1] = bk[1]; r[2] = bk[2]; r[3] = bk[3];
                 }
             } else if (tid >= SCAN_THREADS && tid < SCAN_THREADS + L) {
@@ -1261,6 +1277,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     double* r = sh_wd + u * SPEC_WD;
                     r[0] = q0.x; r[1] = q0.y; r[2] = q1.x; r[3] = q1.y; r[4] = q2.x; r[5] = q2.y;
                     r[10] = qy.x; r[11] = qy.y;
+                    sincos(qy.x, &r[12], &r[13]);
                 }
             }
             if (staged) {
@@ -1298,13 +1315,17 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 xpl[0] = xp[0]; xpl[1] = xp[1]; xpl[2] = xp[2];
                 double2 w0 = make_double2(0, 0), w1 = w0, w2 = w0, wy = w0;
                 double wD[4] = {0, 0, 0, 0};
+                double wma0 = 0.0, ws0 = 0.0, wc0 = 1.0;
                 if (act) {
                     const double* r = sh_wd + u * SPEC_WD;
                     w0 = make_double2(r[0], r[1]); w1 = make_double2(r[2], r[3]);
                     w2 = make_double2(r[4], r[5]); wy = make_double2(r[10], r[11]);
                     wD[0] = r[6]; wD[1] = r[7]; wD[2] = r[8]; wD[3] = r[9];
+                    wma0 = r[10]; ws0 = r[12]; wc0 = r[13];
                 }
                 int ml = 0, bad = 0;
+                const bool lst = p.dbg && g == 0 && u == 0;
+                unsigned long long tl = lst ? __builtin_amdgcn_s_memrealtime() : 0ull;
                 for (int t = 0; t < L; t++) {
                     if (sh_spec[t] < 0) continue;
                     double* pk = sh_pk[t];
@@ -1315,7 +1336,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         Block5 b5;
                         fill_block5(b5, R33l, w0, w1, w2, wD);
                         Cand c;
-                        eval_candidate(b5, wy.x, wy.y, xpl, ln.alpha, ln.r, Rm, p.gate, c);
+                        double sn, cs;
+                        sincos_near(wy.x, wma0, ws0, wc0, sn, cs);
+                        eval_candidate(b5, wy.x, wy.y, sn, cs, xpl, ln.alpha, ln.r, Rm, p.gate, c);
                         bad |= c.pass ? 0 : 1;
                         build_package(c, R33l, w0, w1, w2, pk);
                         for (int q = 0; q < ml; q++) {
@@ -1330,8 +1353,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     __builtin_amdgcn_wave_barrier();
                     if (u == 0) __hip_atomic_store(&sh_ready, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if (lst) { const unsigned long long t2 = __builtin_amdgcn_s_memrealtime(); sh_stamp[3] += t2 - tl; tl = t2; }
                     if (act && u > t) {
-                        const double* r = sh_wd + u * SPEC_WD + 12 + 4 * t;
+                        const double* r = sh_wd + u * SPEC_WD + 14 + 4 * t;
                         double blk[4] = {r[0], r[1], r[2], r[3]};
                         double kk[4], uu[4];
                         gain_rows(pk, ml, [&](int q) { return sh_wh[u][q][0]; }, blk, w0, w1, w2, wy, wD, kk, uu);
@@ -1340,6 +1364,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     }
                     robot_update(R33l, xpl, pk);
                     ml++;
+                    if (lst) { const unsigned long long t2 = __builtin_amdgcn_s_memrealtime(); sh_stamp[4] += t2 - tl; tl = t2; }
                 }
                 bad = __any(bad) ? 1 : 0;
                 if (u == 0) {
@@ -1396,9 +1421,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         Block5 b5;
                         fill_block5(b5, R33, rr0, rr1, rr2, Dj);
                         bool pass = false;
-                        if (!certified_reject(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate)) {
+                        double sn, cs;
+                        sincos_near(yb.x, ma0, s0j, c0j, sn, cs);
+                        if (!certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate)) {
                             Cand c;
-                            eval_candidate(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate, c);
+                            eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, c);
                             status |= c.singular ? EKF_ST_SINGULAR : 0;
                             pass = c.pass;
                         }
@@ -1482,8 +1509,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         if (own && j < s && !matched) {
             Block5 b5;
             fill_block5(b5, R33, rr0, rr1, rr2, Dj);
-            if (!certified_reject(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate)) {
-                eval_candidate(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate, c);
+            double sn, cs;
+            sincos_near(yb.x, ma0, s0j, c0j, sn, cs);
+            if (!certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate)) {
+                eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, c);
                 status |= c.singular ? EKF_ST_SINGULAR : 0;
                 if (c.pass) best = j;
             }
