@@ -8,7 +8,8 @@
 //   (true poses; the encoder reports them, as realRoboPose does in simulation, main.cpp:84-89)
 // stdout per pose: "pose k L" then L × "line alfa r C00 C01 C10 C11 a0 r0 a1 r1" (robot frame,
 //   interval end points as SetEndPoints leaves them); slam mode adds
-//   "est k x y theta matches" and "match j0 j1 …". Exit 3 if the GPU path fails.
+//   "est k x y theta matches", "match j0 j1 …" and the cycle's published messages (ros_output.hpp):
+//   "pub ok tx ty tz rx ry rz rw nfloats floats…". Exit 3 if the GPU path fails.
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
@@ -16,6 +17,7 @@
 
 #include "line_extraction.hpp"
 #include "robot_ekf.hpp"
+#include "ros_output.hpp"
 
 namespace lx = slam_ekf::lx;
 
@@ -78,7 +80,14 @@ int main(int argc, char** argv)
                             rover->matchesNum());
                 for (size_t i = 0; i < lines.size(); i++) std::printf(" %d", rover->lastResult().match[i]);
                 std::printf("\n");
-                rover->lineIntervals.data.clear();   // main.cpp:174
+                slam_ekf::TransformMsg msg;                 // main.cpp:150-174
+                std::vector<float> pub_lines;
+                const bool ok = slam_ekf::publish_cycle(*rover, msg, pub_lines);
+                std::printf("pub %d %.17g %.17g %.17g %.9g %.9g %.9g %.9g %zu", ok ? 1 : 0, msg.translation.x,
+                            msg.translation.y, msg.translation.z, msg.rotation.x, msg.rotation.y, msg.rotation.z,
+                            msg.rotation.w, pub_lines.size());
+                for (float v : pub_lines) std::printf(" %.9g", v);
+                std::printf("\n");
             }
         }
         delete rover;

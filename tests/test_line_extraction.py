@@ -1,7 +1,7 @@
-"""§8f rank 1: the caller side of the path — 360-beam ray-cast scans of a room (config 1),
+"""§8f ranks 1 and 3: the caller side of the path — 360-beam ray-cast scans of a room (config 1),
 line extraction (slam_ros_amd/host/line_extraction.hpp, the GSL-free restatement of
 lineFitting.cpp / simplifyPath.cpp / main.cpp:37-61) and, on the GPU, the drop-in Robot fed with
-the extracted lines.
+the extracted lines, with the messages main.cpp publishes each cycle (ros_output.hpp).
 
 Parity: the reference's extraction cannot be built here (GSL and ROS are absent)
 and its tests hold no extraction fixtures, so this stage is parity unpinned. It is checked
@@ -62,6 +62,9 @@ def parse(text):
             scans[-1]["est"] = [float(x) for x in f[2:5]] + [int(f[5])]
         elif f[0] == "match":
             scans[-1]["match"] = [int(x) for x in f[1:]]
+        elif f[0] == "pub":
+            scans[-1]["pub"] = {"ok": int(f[1]), "msg": [float(x) for x in f[2:9]],
+                                "lines": [float(x) for x in f[10:10 + int(f[9])]]}
     return scans
 
 
@@ -169,7 +172,7 @@ def test_config1_end_to_end(tmp_path, ekf_mod, oracle_mod):
     assert out.returncode == 0, out.stderr
     scans = parse(out.stdout)
     ref = oracle_mod.OracleRobot(64, mode=oracle_mod.FAITHFUL)
-    matched = 0
+    matched = angles = 0
     for k, (pose, sc) in enumerate(zip(poses, scans)):
         lines = np.array([[l[0], l[1], l[2], l[3], l[4], l[5]] for l in sc["lines"]])
         m = ref.localize(lines, list(pose))
@@ -180,4 +183,20 @@ def test_config1_end_to_end(tmp_path, ekf_mod, oracle_mod):
         # written) lets the heading wander between corrections
         assert abs(x - pose[0]) < 0.1 and abs(y - pose[1]) < 0.1, (k, (x, y), pose)
         matched += sum(1 for j in m if j >= 0)
-    assert matched >= 2 * len(poses)
+        # robotPosition (main.cpp:150-168): translation = pose, rotation = (major, minor, angle)
+        # of the pose ellipse (Robot.cpp:73-124) from the restatement's P
+        pub = sc["pub"]
+        assert pub["ok"] == 1
+        tx, ty, tz, rx, ry, rz, rw = pub["msg"]
+        assert (tx, ty, tz) == (x, y, th) and rw == 0.0
+        lam, vec = np.linalg.eigh(ref.P_t0[:2, :2])
+        ax = 2 * np.sqrt(5.991 * np.abs(lam))
+        np.testing.assert_allclose([rx, ry], [ax[1], ax[0]], rtol=1e-5)
+        if lam[1] - lam[0] > 1e-3 * lam[1]:    # the angle is defined (not a circle)
+            want = math.atan2(vec[0, 1], vec[1, 1])
+            dd = (rz - want) % math.pi
+            assert min(dd, math.pi - dd) < 1e-4, (k, rz, want)
+            angles += 1
+        # lines (main.cpp:171-174): the end points of this cycle's new landmarks, 4 floats each
+        assert len(pub["lines"]) == 4 * sum(1 for j in m if j < 0)
+    assert matched >= 2 * len(poses) and angles >= len(poses) // 2
