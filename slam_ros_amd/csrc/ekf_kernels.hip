@@ -2252,8 +2252,10 @@ struct P2Info {
     int flags;   // per step q, byte q: bits 0-3 ks, bit 4 reset, bit 5 augmented rows present
 };
 
-template <typename TS>
-__global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(DowndateParams p)
+// GLDS: the operands go global → LDS by LDS-DMA (global_load_lds_dwordx4) right after the
+// super-tile's MFMA block, no register staging (48 fewer VGPRs: MINB = 3 workgroups per CU fit)
+template <typename TS, int MINB, bool GLDS>
+__global__ __launch_bounds__(DD_THREADS, MINB) void flush_f32_persist2_kernel(DowndateParams p)
 {
     const Dims d = p.d;
     const int nst = p.nstiles2;
@@ -2321,18 +2323,50 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
             for (int qq = 0; qq < 4; qq++) pref[c][qq] = tile_ld(tl, lane, qq);
         }
     };
+    auto fetch_tiles = [&](const P2Info& t, f32x4 pref[P2_C][4]) {
+#pragma unroll
+        for (int c = 0; c < P2_C; c++) {
+            bool v;
+            const TS* tl = Pin + tile_off(t, c, v);
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) pref[c][qq] = tile_ld(tl, lane, qq);
+        }
+    };
 
     __shared__ f32x4 ldsA[PST_MAXC][DD_SB][2][64];   // 32 KB
     __shared__ f32x4 ldsB[PST_MAXC][P2_C][2][64];    // 16 KB
+    // LDS-DMA of a super-tile's operands: per step 3 wave-instructions (A rows rA0, rA1; B row rB)
+    // of 64 lanes × 16 B, each a contiguous 1 KB of the LDS image
+    auto stage = [&](const P2Info& t) {
+        const int rA0 = min(t.sbi * DD_SB + bl, d.nb - 1), rA1 = min(t.sbi * DD_SB + 2 + bl, d.nb - 1);
+        const int rB = min(t.sbj * P2_C + bl, d.nb - 1);
+#pragma unroll
+        for (int c = 0; c < PST_MAXC; c++) {
+            const int qc = ((t.flags >> (8 * c)) & 15) ? c : 0;
+            const float* U = reinterpret_cast<const float*>(p.steps[qc].Uop) + t.e * opstride;
+            const float* V = reinterpret_cast<const float*>(p.steps[qc].Vop) + t.e * opstride;
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(U + (size_t)rA0 * 64 * kh + in_blk),
+                                             (__attribute__((address_space(3))) void*)&ldsA[c][bl][s4][0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(U + (size_t)rA1 * 64 * kh + in_blk),
+                                             (__attribute__((address_space(3))) void*)&ldsA[c][2 + bl][s4][0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(V + (size_t)rB * 64 * kh + in_blk),
+                                             (__attribute__((address_space(3))) void*)&ldsB[c][bl][s4][0], 16, 0, 0);
+        }
+    };
 
     P2Info cur;
     cur.e = __builtin_amdgcn_readfirstlane(g / nst);
     int li = __builtin_amdgcn_readfirstlane(g - cur.e * nst);
     locate(li, cur);
     load_flags(cur);
-    f32x4 opreg[PST_MAXC][3];
+    f32x4 opreg[GLDS ? 1 : PST_MAXC][3];
     f32x4 pref[P2_C][4];
-    fetch(cur, opreg, pref);
+    if constexpr (GLDS) {
+        stage(cur);
+        fetch_tiles(cur, pref);
+    } else {
+        fetch(cur, opreg, pref);
+    }
     f32x16 acc[P2_C];
     // steady state: every step of the group a full chunk, no reset, no augmented rows
     int steady = 0;
@@ -2340,16 +2374,21 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
     for (int q = 0; q < PST_MAXC; q++) steady |= (q < nsteps ? SBK : 0) << (8 * q);
 
     while (true) {
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS free
+        if constexpr (GLDS) {
+            // this wave's DMAs (and tiles) have landed; after the barrier, every wave's
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS free
 #pragma unroll
-        for (int c = 0; c < PST_MAXC; c++) {
-            if ((cur.flags >> (8 * c)) & 15) {
-                ldsA[c][bl][s4][ln] = opreg[c][0];
-                ldsA[c][2 + bl][s4][ln] = opreg[c][1];
-                ldsB[c][bl][s4][ln] = opreg[c][2];
+            for (int c = 0; c < PST_MAXC; c++) {
+                if ((cur.flags >> (8 * c)) & 15) {
+                    ldsA[c][bl][s4][ln] = opreg[c][0];
+                    ldsA[c][2 + bl][s4][ln] = opreg[c][1];
+                    ldsB[c][bl][s4][ln] = opreg[c][2];
+                }
             }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS written
         }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS written
 #pragma unroll
         for (int c = 0; c < P2_C; c++)
 #pragma unroll
@@ -2374,7 +2413,8 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
         }
         locate(lin, nxt);
         load_flags(nxt);
-        fetch(nxt, opreg, pref);
+        if constexpr (GLDS) fetch_tiles(nxt, pref);
+        else fetch(nxt, opreg, pref);
 
         const int e = cur.e;
         const int bi = cur.sbi * DD_SB + w;
@@ -2470,6 +2510,11 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
                 }
                 post(q);
             }
+        }
+        if constexpr (GLDS) {
+            // every wave is done reading the operands: the next super-tile's DMAs may land
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (more) stage(nxt);
         }
 #pragma unroll
         for (int c = 0; c < P2_C; c++) {
@@ -2702,12 +2747,24 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     }
     const bool half = precision == EKF_PREC_F16;
     const bool persist_ok = p.nsteps <= PST_MAXC && p.d.kmax <= 16 && p.variant != 2;
-    if (persist_ok && p.variant != 3) {
+    if (persist_ok && p.variant == 4) {
+        const int pgrid = 24 * ((p.ncu + 7) / 8);   // three workgroups per CU, operands by LDS-DMA
+        if (half)
+            hipLaunchKernelGGL((flush_f32_persist2_kernel<_Float16, 3, true>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+        else
+            hipLaunchKernelGGL((flush_f32_persist2_kernel<float, 3, true>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+    } else if (persist_ok && p.variant == 5) {
+        const int pgrid = 16 * ((p.ncu + 7) / 8);   // two workgroups per CU, operands by LDS-DMA
+        if (half)
+            hipLaunchKernelGGL((flush_f32_persist2_kernel<_Float16, 2, true>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+        else
+            hipLaunchKernelGGL((flush_f32_persist2_kernel<float, 2, true>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+    } else if (persist_ok && p.variant != 3) {
         const int pgrid = 16 * ((p.ncu + 7) / 8);   // two workgroups per CU (48 KB LDS each)
         if (half)
-            hipLaunchKernelGGL(flush_f32_persist2_kernel<_Float16>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+            hipLaunchKernelGGL((flush_f32_persist2_kernel<_Float16, 2, false>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
         else
-            hipLaunchKernelGGL(flush_f32_persist2_kernel<float>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+            hipLaunchKernelGGL((flush_f32_persist2_kernel<float, 2, false>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
     } else if (persist_ok) {
         const int pgrid = 8 * ((p.ncu + 7) / 8);   // one workgroup per CU (128 KB LDS)
         if (half)
