@@ -503,6 +503,7 @@ __device__ __forceinline__ bool certified_reject(const Block5& b, double ma, dou
     } while (0)
 
 constexpr int HIST_LDS = 8;   // matches per scan whose owned U rows stay in LDS
+constexpr int HIST_V = 4;     // ... and whose V rows do (sequential path; the rest in Vst)
 
 __device__ __forceinline__ int wave_min(int v)
 {
@@ -658,19 +659,27 @@ __device__ __forceinline__ void build_package(const Cand& c, const double R33[9]
 // The two rows of one landmark for a match: its block of column jstar with the earlier matches
 // of the scan applied (Robot.cpp:560-568, in order), W = P·Hᵀ, K = W·S⁻¹, U = K·S, y += K·v
 // (Robot.cpp:522-589), and the eager downdate of its robot-strip columns and diagonal block.
-// `uq_of(q)` returns the landmark's U rows of the scan's match q; the package holds jstar's V rows.
-template <typename UQ>
-__device__ __forceinline__ void gain_rows(const double* pk, int t, UQ uq_of, double blk[4],
+// `uq_of(q)` / `vq_of(q)` return the landmark's U rows and jstar's V rows of the scan's match q.
+// MAXQ > 0: at most MAXQ earlier matches, the loop unrolled (its loads issued together).
+template <int MAXQ, typename UQ, typename VQ>
+__device__ __forceinline__ void gain_rows(const double* pk, int t, UQ uq_of, VQ vq_of, double blk[4],
                                           double2& rr0, double2& rr1, double2& rr2, double2& yb,
                                           double Dj[4], double kk[4], double uu[4])
 {
-    for (int q = 0; q < t; q++) {   // earlier matches of this scan, in order
+    auto correct = [&](int q) {   // earlier matches of this scan, in order
         const double4 uq = uq_of(q);
-        const double* vh = pk + MB_VH + 4 * q;
-        blk[0] -= uq.x * vh[0] + uq.y * vh[1];
-        blk[1] -= uq.x * vh[2] + uq.y * vh[3];
-        blk[2] -= uq.z * vh[0] + uq.w * vh[1];
-        blk[3] -= uq.z * vh[2] + uq.w * vh[3];
+        const double4 vh = vq_of(q);
+        blk[0] -= uq.x * vh.x + uq.y * vh.y;
+        blk[1] -= uq.x * vh.z + uq.y * vh.w;
+        blk[2] -= uq.z * vh.x + uq.w * vh.y;
+        blk[3] -= uq.z * vh.z + uq.w * vh.w;
+    };
+    if constexpr (MAXQ > 0) {
+#pragma unroll
+        for (int q = 0; q < MAXQ; q++)
+            if (q < t) correct(q);
+    } else {
+        for (int q = 0; q < t; q++) correct(q);
     }
     const double S0 = pk[MB_S], S1 = pk[MB_S + 1], S2 = pk[MB_S + 2], S3 = pk[MB_S + 3];
     const double Si0 = pk[MB_SI], Si1 = pk[MB_SI + 1], Si2 = pk[MB_SI + 2], Si3 = pk[MB_SI + 3];
@@ -769,10 +778,10 @@ __device__ __forceinline__ bool guess_pass(const Guess& gs, double za, double zr
 constexpr int SPEC_L = HIST_LDS;                    // lines
 constexpr int SPEC_K = 6;                           // guessed candidates per line per workgroup
 constexpr int SPEC_PB = 2;                          // guessed columns per pass over the pending steps
-constexpr int SPEC_QMAX = 4;                        // pending steps staged in LDS
+constexpr int SPEC_QMAX = 8;                        // pending steps staged in LDS (pipelined T = 4: up to 7)
 constexpr int SPEC_GMAX = 64;                       // workgroups per instance (<= one wave)
 constexpr int SPEC_WD = 14 + 4 * (SPEC_L - 1);      // winner record: rr, Dj, y, sin/cos, column blocks
-constexpr int PKW = MB_VH + 4 * SPEC_L;             // package words (speculative lines)
+constexpr int PKW = MB_VH;                          // package words (speculative lines; V rows in sh_wh)
 
 // Blocks (j, cols[t]) for t < SPEC_L and (j, j) (last; only if `diag`) of the landmark block
 // with the pending steps applied, fp32 operands, every pending step with ks <= 8: the guessed
@@ -908,9 +917,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     __shared__ ekf_line sh_lines[EKF_MAX_LINES];
     // U_q rows of the owned landmark for the first HIST_LDS matches of the scan (the rest in Ust)
     __shared__ double4 sh_uhist[HIST_LDS][SCAN_THREADS];
-    // V_q rows (sequential path, for the package); owned blocks of the guessed columns
-    // (speculative path)
-    __shared__ double4 sh_vhist[HIST_LDS][SCAN_THREADS];
+    // V_q rows (sequential path, for the package); owned blocks of the guessed columns as fp32
+    // (speculative path with fp32 operands: the values are fp32 numbers)
+    __shared__ double4 sh_vhist[HIST_V][SCAN_THREADS];
+    static_assert(sizeof(float4) * SPEC_L == sizeof(double4) * HIST_V, "block buffer aliases sh_vhist");
+    float4 (*sh_blk)[SCAN_THREADS] = reinterpret_cast<float4 (*)[SCAN_THREADS]>(&sh_vhist[0][0]);
     // speculative association
     __shared__ unsigned long long sh_wl[SPEC_L][SCAN_THREADS / 64];
     __shared__ unsigned long long sh_lists[SPEC_GMAX * SPEC_L];
@@ -1084,7 +1095,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         else
             *reinterpret_cast<double4*>(Ust + ((size_t)t * n + b0) * 2) = make_double4(uu[0], uu[1], uu[2], uu[3]);
         if (vhist) {
-            if (t < HIST_LDS)
+            if (t < HIST_V)
                 sh_vhist[t][tid] = make_double4(kk[0], kk[1], kk[2], kk[3]);
             else
                 *reinterpret_cast<double4*>(Vst + ((size_t)t * n + b0) * 2) = make_double4(kk[0], kk[1], kk[2], kk[3]);
@@ -1340,12 +1351,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         sincos_near(wy.x, wma0, ws0, wc0, sn, cs);
                         eval_candidate(b5, wy.x, wy.y, sn, cs, xpl, ln.alpha, ln.r, Rm, p.gate, c);
                         bad |= c.pass ? 0 : 1;
-                        build_package(c, R33l, w0, w1, w2, pk);
-                        for (int q = 0; q < ml; q++) {
-                            const double4 vq = sh_wh[u][q][1];
-                            pk[MB_VH + 4 * q + 0] = vq.x; pk[MB_VH + 4 * q + 1] = vq.y;
-                            pk[MB_VH + 4 * q + 2] = vq.z; pk[MB_VH + 4 * q + 3] = vq.w;
-                        }
+                        build_package(c, R33l, w0, w1, w2, pk);   // its V rows stay in sh_wh[t]
                     }
                     // the package is complete: to the other lanes of this wave, and to the
                     // landmark waves (release of all lanes' LDS writes, then the line counter)
@@ -1358,7 +1364,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         const double* r = sh_wd + u * SPEC_WD + 14 + 4 * t;
                         double blk[4] = {r[0], r[1], r[2], r[3]};
                         double kk[4], uu[4];
-                        gain_rows(pk, ml, [&](int q) { return sh_wh[u][q][0]; }, blk, w0, w1, w2, wy, wD, kk, uu);
+                        gain_rows<SPEC_L>(pk, ml, [&](int q) { return sh_wh[u][q][0]; },
+                                          [&](int q) { return sh_wh[t][q][1]; }, blk, w0, w1, w2, wy, wD, kk, uu);
                         sh_wh[u][ml][0] = make_double4(uu[0], uu[1], uu[2], uu[3]);
                         sh_wh[u][ml][1] = make_double4(kk[0], kk[1], kk[2], kk[3]);
                     }
@@ -1387,12 +1394,12 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
 #pragma unroll
                         for (int t = 0; t < SPEC_L; t++)
                             if (t < L && sh_spec[t] >= 0)
-                                sh_vhist[t][tid] = make_double4(blk[t][0], blk[t][1], blk[t][2], blk[t][3]);
+                                sh_blk[t][tid] = make_float4((float)blk[t][0], (float)blk[t][1], (float)blk[t][2], (float)blk[t][3]);
                         if (j < s) {
                             Dj[0] = blk[SPEC_L][0]; Dj[1] = blk[SPEC_L][1];
                             Dj[2] = blk[SPEC_L][2]; Dj[3] = blk[SPEC_L][3];
                         }
-                    } else {
+                    } else if constexpr (sizeof(typename Stor<T>::C) == 4) {
                         for (int t0 = 0; t0 < L; t0 += SPEC_PB) {
                             int cols[SPEC_PB];
                             double bk[SPEC_PB][4];
@@ -1405,7 +1412,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
 #pragma unroll
                             for (int b = 0; b < SPEC_PB; b++)
                                 if (t0 + b < L && sh_spec[t0 + b] >= 0)
-                                    sh_vhist[t0 + b][tid] = make_double4(bk[b][0], bk[b][1], bk[b][2], bk[b][3]);
+                                    sh_blk[t0 + b][tid] = make_float4((float)bk[b][0], (float)bk[b][1], (float)bk[b][2], (float)bk[b][3]);
                         }
                     }
                 }
@@ -1450,10 +1457,16 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     const double* pk = sh_pk[i];
                     if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
                     if (own) {
-                        const double4 bk = sh_vhist[i][tid];
-                        double blk[4] = {bk.x, bk.y, bk.z, bk.w};
+                        double blk[4];
+                        if constexpr (sizeof(typename Stor<T>::C) == 4) {
+                            const float4 bk = sh_blk[i][tid];
+                            blk[0] = bk.x; blk[1] = bk.y; blk[2] = bk.z; blk[3] = bk.w;
+                        } else {
+                            pll_block(pv, 2 * j, 2 * w, blk);   // fp64 operands: read in the loop
+                        }
                         double kk[4], uu[4];
-                        gain_rows(pk, m, uq_owned, blk, rr0, rr1, rr2, yb, Dj, kk, uu);
+                        gain_rows<SPEC_L>(pk, m, uq_owned, [&](int q) { return sh_wh[i][q][1]; }, blk, rr0, rr1,
+                                          rr2, yb, Dj, kk, uu);
                         store_rows(m, kk, uu, false);
                     }
                     robot_update(R33, xp, pk);
@@ -1533,7 +1546,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             // staged in LDS
             build_package(c, R33, rr0, rr1, rr2, sh_pkg);
             for (int q = 0; q < m; q++) {
-                const double4 vq = q < HIST_LDS ? sh_vhist[q][tid]
+                const double4 vq = q < HIST_V ? sh_vhist[q][tid]
                                                 : *reinterpret_cast<const double4*>(Vst + ((size_t)q * n + b0) * 2);
                 sh_pkg[MB_VH + 4 * q + 0] = vq.x;
                 sh_pkg[MB_VH + 4 * q + 1] = vq.y;
@@ -1597,7 +1610,12 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
         if (own) {
             double kk[4], uu[4];
-            gain_rows(sh_pkg, m, uq_owned, blk, rr0, rr1, rr2, yb, Dj, kk, uu);
+            gain_rows<0>(sh_pkg, m, uq_owned,
+                         [&](int q) {
+                             const double* vh = sh_pkg + MB_VH + 4 * q;
+                             return make_double4(vh[0], vh[1], vh[2], vh[3]);
+                         },
+                         blk, rr0, rr1, rr2, yb, Dj, kk, uu);
             store_rows(m, kk, uu, true);
         }
         robot_update(R33, xp, sh_pkg);
@@ -2759,6 +2777,18 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
             hipLaunchKernelGGL((flush_f32_persist2_kernel<_Float16, 2, true>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
         else
             hipLaunchKernelGGL((flush_f32_persist2_kernel<float, 2, true>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+    } else if (persist_ok && p.variant == 6) {
+        const int pgrid = 8 * ((p.ncu + 7) / 8);   // one workgroup per CU, operands by LDS-DMA
+        if (half)
+            hipLaunchKernelGGL((flush_f32_persist2_kernel<_Float16, 2, true>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+        else
+            hipLaunchKernelGGL((flush_f32_persist2_kernel<float, 2, true>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+    } else if (persist_ok && p.variant == 7) {
+        const int pgrid = 8 * ((p.ncu + 7) / 8);   // one workgroup per CU
+        if (half)
+            hipLaunchKernelGGL((flush_f32_persist2_kernel<_Float16, 2, false>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+        else
+            hipLaunchKernelGGL((flush_f32_persist2_kernel<float, 2, false>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
     } else if (persist_ok && p.variant != 3) {
         const int pgrid = 16 * ((p.ncu + 7) / 8);   // two workgroups per CU (48 KB LDS each)
         if (half)
