@@ -21,6 +21,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <new>
 #include <vector>
 
@@ -58,6 +59,8 @@ struct ekf_ctx {
     int2* stile_rc;
     int2* stile2_rc;
     int nstiles2;
+    ekf::WtEntry* wt;
+    int nwt;
     double* d_enc;
     ekf_line* d_lines;
     int* d_nlines;
@@ -137,7 +140,7 @@ int ekf_abi_version(void) { return SLAM_EKF_ABI_VERSION; }
 static void free_all(ekf_ctx* c)
 {
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->pose, c->xpre, c->saved, c->D,
-                               c->tile_rc, c->stile_rc, c->stile2_rc, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->mbox,
+                               c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->mbox,
                                c->sync, c->Ust, c->Vst};
     for (auto& sl : c->ring) {
         ptrs.push_back(sl.Uop);
@@ -328,6 +331,39 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         if (hipMemcpy(c->stile2_rc, s2.data(), sizeof(int2) * s2.size(), hipMemcpyHostToDevice) !=
             hipSuccess)
             goto fail;
+        // WT_R × WT_C wave-tiles holding a stored tile (wc·WT_C + WT_C − 1 >= wr·WT_R), in panels
+        // of 16 wave-tile columns walked row by row (the wave-tiles an XCD has in flight share
+        // operand rows); each entry carries its tile indices and operand row blocks
+        const int nwr = (d.nb + ekf::WT_R - 1) / ekf::WT_R, nwc = (d.nb + ekf::WT_C - 1) / ekf::WT_C;
+        std::vector<ekf::WtEntry> wt;
+        for (int pc = 0; pc < nwc; pc += 16)
+            for (int wr = 0; wr < nwr; wr++)
+                for (int wc = pc; wc < pc + 16 && wc < nwc; wc++) {
+                    if (wc * ekf::WT_C + ekf::WT_C - 1 < wr * ekf::WT_R) continue;
+                    ekf::WtEntry v;
+                    memset(&v, 0, sizeof(v));
+                    // a stored tile of this wave-tile (its first row, last column in the block)
+                    const int fbi = wr * ekf::WT_R, fbj = std::min(wc * ekf::WT_C + ekf::WT_C - 1, d.nb - 1);
+                    for (int r = 0; r < ekf::WT_R; r++)
+                        for (int cc = 0; cc < ekf::WT_C; cc++) {
+                            const int i = r * ekf::WT_C + cc;
+                            const int bi = wr * ekf::WT_R + r, bj = wc * ekf::WT_C + cc;
+                            const bool ok = bi < d.nb && bj < d.nb && bi <= bj;
+                            v.tile[i] = (int)(ok ? ekf::tile_index(bi, bj, d.nb) : ekf::tile_index(fbi, fbj, d.nb));
+                            v.valid |= (ok ? 1 : 0) << i;
+                        }
+                    for (int r = 0; r < ekf::WT_R; r++)
+                        v.rows[0] |= std::min(wr * ekf::WT_R + r, d.nb - 1) << (16 * r);
+                    for (int cc = 0; cc < ekf::WT_C; cc++)
+                        v.rows[1] |= std::min(wc * ekf::WT_C + cc, d.nb - 1) << (16 * cc);
+                    v.rc = wr | (wc << 16);
+                    wt.push_back(v);
+                }
+        c->nwt = (int)wt.size();
+        if (hipMalloc((void**)&c->wt, sizeof(ekf::WtEntry) * wt.size()) != hipSuccess) goto fail;
+        if (hipMemcpy(c->wt, wt.data(), sizeof(ekf::WtEntry) * wt.size(), hipMemcpyHostToDevice) !=
+            hipSuccess)
+            goto fail;
     }
     {
         hipDeviceProp_t prop;
@@ -497,6 +533,8 @@ static int enqueue_flush(ekf_ctx* c)
     dp.stile_rc = c->stile_rc;
     dp.stile2_rc = c->stile2_rc;
     dp.nstiles2 = c->nstiles2;
+    dp.wt = c->wt;
+    dp.nwt = c->nwt;
     for (int q = 0; q < nst; q++) dp.steps[q] = slot_of(c, c->unflushed0 + q);
     const int in = c->last_out;
     const int out = c->cfg.pipeline ? 1 - in : in;

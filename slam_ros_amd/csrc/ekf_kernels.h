@@ -47,6 +47,18 @@ struct Slot {
 };
 
 constexpr int PMAX = 32;
+constexpr int WT_R = 2, WT_C = 2, WT_N = WT_R * WT_C;   // f32 wave flush: tiles per wave-tile
+
+// one wave-tile of the wave flush (host-built table, read with scalar loads): the linear indices
+// of its WT_N tiles (positions below the diagonal or past the block point at a stored tile of
+// the same wave-tile and are not written back), their validity, the operand row blocks of its
+// WT_R tile rows and WT_C tile columns (16 bits each, clamped to the block) and (wr, wc)
+struct alignas(32) WtEntry {
+    int tile[WT_N];
+    int valid;      // bit i: tile i is stored
+    int rows[2];    // [0]: A row blocks (WT_R × 16 bits), [1]: B row blocks (WT_C × 16 bits)
+    int rc;         // wr | wc << 16
+};
 constexpr int DD_SB = 4;   // f32 flush: tiles per super-tile side (one wave per tile row)   // pending steps (2 × flush_interval in pipeline mode)
 
 struct ScanParams {
@@ -96,6 +108,8 @@ struct DowndateParams {
     const int2* stile_rc; // [nsb(nsb+1)/2] (sbi, sbj) super-tiles of DD_SB × DD_SB tiles, sbi <= sbj
     const int2* stile2_rc;// [nstiles2] (sbi, sbj) super-tiles of DD_SB × 2 tiles holding a stored tile
     int nstiles2;
+    const WtEntry* wt;    // [nwt] wave-tiles of WT_R × WT_C tiles holding a stored tile, panel order
+    int nwt;
     Slot steps[PMAX];
 };
 

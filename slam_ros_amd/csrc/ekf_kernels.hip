@@ -23,6 +23,8 @@
 // the flush will store (tests/test_gpu_parity.py::test_deferred_flush_equals_drained).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "ekf_kernels.h"
 
 namespace ekf {
@@ -2550,6 +2552,277 @@ __global__ __launch_bounds__(DD_THREADS, MINB) void flush_f32_persist2_kernel(Do
     }
 }
 
+// f32/f16 flush, barrier-free per-wave form for groups of an even number of steps NS (2..8,
+// kmax <= 16). One wave per SIMD, each working alone (no LDS, no barriers) through a sequence of
+// wave-tiles of WT_R × WT_C tiles (four 32×32 accumulators). Software pipeline, one wave-tile
+// deep: while wave-tile k runs its NS·32 MFMAs, the tiles of wave-tile k+1 (issued first) and its
+// operand rows (step q's issued right after step q's MFMAs free their registers) stream into
+// registers, so every wait of a wave-tile covers only loads issued during the one before it. The
+// host table wt (WtEntry) gives each wave-tile's tile indices, operand row blocks and validity;
+// the entry of wave-tile k+2 is read (scalar loads) during wave-tile k. The wave-tiles of an
+// instance are walked in panels and each XCD takes a contiguous range of (instance, wave-tile),
+// so the wave-tiles an XCD has in flight share their operand rows in its L2. This pipelined loop
+// serves the groups in which no step of the wave's instances resets the map or adds landmarks
+// (partial downdates are predicated); otherwise the wave runs a plain per-wave-tile loop. Per
+// element the chain is the one every other form runs (k-ordered MFMA steps, fp16 rounding per
+// step, then the step's rows or the reset): bit-identical results.
+template <typename TS, int NS>
+__global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateParams p)
+{
+    static_assert(NS >= 2 && NS % 2 == 0 && NS <= PMAX, "even step count");
+    constexpr bool HALF = sizeof(TS) == 2;
+    const Dims d = p.d;
+    const int nwt = p.nwt;
+    const int total = p.E * nwt;
+    const int per = (total + 7) / 8;
+    const int xcd = blockIdx.x & 7;
+    const int K = (int)(gridDim.x >> 3) * (DD_THREADS / 64);     // waves per XCD
+    const int g_end = min(total, (xcd + 1) * per);
+    const int g0 = __builtin_amdgcn_readfirstlane(
+        xcd * per + (int)(blockIdx.x >> 3) * (DD_THREADS / 64) + (int)(threadIdx.x >> 6));
+    if (g0 >= g_end) return;
+
+    const int lane = threadIdx.x & 63;
+    const int kh = d.kmax / 2;   // 8
+    const size_t opstride = (size_t)d.nb * 64 * kh;
+    const size_t inst_elems = (size_t)d.ntiles * TILE_ELEMS;
+    const TS* Pin = reinterpret_cast<const TS*>(p.Pin);
+    TS* Pout = reinterpret_cast<TS*>(p.Pout);
+    const int lofs = lane * kh;
+
+    // the pipelined loop needs every step of every instance this wave visits to be a plain
+    // downdate (no reset, no new rows)
+    bool fast = true;
+    {
+        const int e_lo = g0 / nwt, e_hi = (g_end - 1) / nwt;
+        for (int e = e_lo; e <= e_hi; e++)
+#pragma unroll
+            for (int q = 0; q < NS; q++) {
+                const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
+                fast = fast && !sload(r + RES_RESET) && sload(r + RES_NADD) == 0;
+            }
+    }
+
+    // a wave-tile: instance, table entry (scalar registers)
+    struct Item {
+        int e, li;
+        WtEntry w;
+    };
+    typedef int i32x8 __attribute__((ext_vector_type(8)));
+    static_assert(sizeof(WtEntry) == sizeof(i32x8), "one scalar dwordx8 per entry");
+    auto load_entry = [&](int li, WtEntry& w) __attribute__((always_inline)) {
+        const i32x8 v = sload(reinterpret_cast<const i32x8*>(p.wt + li));
+#pragma unroll
+        for (int i = 0; i < WT_N; i++) w.tile[i] = v[i];
+        w.valid = v[WT_N];
+        w.rows[0] = v[WT_N + 1];
+        w.rows[1] = v[WT_N + 2];
+        w.rc = v[WT_N + 3];
+    };
+    // the wave's k-th wave-tile follows from the (k−1)-th by adding K to the flat index
+    auto first_item = [&](Item& t) __attribute__((always_inline)) {
+        t.e = g0 / nwt;
+        const int li = g0 - t.e * nwt;
+        load_entry(li, t.w);
+        t.li = li;
+    };
+    auto next_item = [&](const Item& c, Item& t) __attribute__((always_inline)) {
+        int li = c.li + K, e = c.e;
+        while (li >= nwt) {
+            li -= nwt;
+            e++;
+        }
+        t.e = e;
+        load_entry(e < p.E ? li : 0, t.w);
+        t.li = li;
+    };
+    auto tile_ptr = [&](const Item& t, int i) __attribute__((always_inline)) {
+        return (size_t)t.e * inst_elems + (size_t)t.w.tile[i] * TILE_ELEMS;
+    };
+    auto store_tiles = [&](const Item& t, const f32x16 (&acc)[WT_N]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < WT_N; i++)
+            if ((t.w.valid >> i) & 1) {
+                TS* tl = Pout + tile_ptr(t, i);
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) tile_st(tl, lane, qq, acc[i]);
+            }
+    };
+    auto op_row = [&](const Item& t, int side, int k) __attribute__((always_inline)) {
+        return (t.w.rows[side] >> (16 * k)) & 0xffff;
+    };
+
+    if (fast) {
+        // raw tile words in flight (fp16 storage: converted when the wave-tile starts)
+        using Raw = typename std::conditional<HALF, f16x4, f32x4>::type;
+        Raw pref[WT_N][4];
+        f32x4 opA[NS][WT_R][2], opB[NS][WT_C][2];
+        f32x16 acc[WT_N];
+        auto load_ops = [&](int slot, const Item& t, int q) __attribute__((always_inline)) {
+            const float* U = reinterpret_cast<const float*>(p.steps[q].Uop) + t.e * opstride + lofs;
+            const float* V = reinterpret_cast<const float*>(p.steps[q].Vop) + t.e * opstride + lofs;
+#pragma unroll
+            for (int r = 0; r < WT_R; r++) {
+                const float* src = U + (size_t)op_row(t, 0, r) * 64 * kh;
+                opA[slot][r][0] = *reinterpret_cast<const f32x4*>(src);
+                opA[slot][r][1] = *reinterpret_cast<const f32x4*>(src + 4);
+            }
+#pragma unroll
+            for (int c = 0; c < WT_C; c++) {
+                const float* src = V + (size_t)op_row(t, 1, c) * 64 * kh;
+                opB[slot][c][0] = *reinterpret_cast<const f32x4*>(src);
+                opB[slot][c][1] = *reinterpret_cast<const f32x4*>(src + 4);
+            }
+        };
+        auto load_tiles = [&](const Item& t) __attribute__((always_inline)) {
+#pragma unroll
+            for (int i = 0; i < WT_N; i++) {
+                const Raw* tl = reinterpret_cast<const Raw*>(Pin + tile_ptr(t, i));
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) pref[i][qq] = __builtin_nontemporal_load(tl + lane + qq * 64);
+            }
+        };
+        Item cur, nxt, nxt2;
+        first_item(cur);
+        next_item(cur, nxt);
+        load_tiles(cur);
+#pragma unroll
+        for (int q = 0; q < NS; q++) load_ops(q, cur, q);
+        int g = g0;
+        while (true) {
+            const bool more = g + K < g_end;
+            next_item(nxt, nxt2);   // read now, used by the next wave-tile
+#pragma unroll
+            for (int i = 0; i < WT_N; i++)
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = (float)pref[i][qq][j];
+            // the next wave-tile's tiles first: they have the whole wave-tile to land
+            if (more) load_tiles(nxt);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < NS; q++) {
+                // k-steps past the step's matches are skipped (uniform branches, in-place chains)
+                const int kc = sload(p.steps[q].res + (size_t)cur.e * RES_STRIDE + RES_KSTEPS);
+#pragma unroll
+                for (int s = 0; s < SBK; s++)
+                    if (s < kc) {
+#pragma unroll
+                        for (int r = 0; r < WT_R; r++)
+#pragma unroll
+                            for (int c = 0; c < WT_C; c++)
+                                acc[r * WT_C + c] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                                    opA[q][r][s >> 2][s & 3], opB[q][c][s >> 2][s & 3], acc[r * WT_C + c], 0, 0, 0);
+                    }
+                if (kc > 0) {
+#pragma unroll
+                    for (int i = 0; i < WT_N; i++) round_acc<TS>(acc[i]);
+                }
+                // step q's operand registers are free: the next wave-tile's step q
+                if (more) load_ops(q, nxt, q);
+                // keep the issue order (the scheduler would hoist the loads)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            store_tiles(cur, acc);
+            if (!more) break;
+            g += K;
+            cur = nxt;
+            nxt = nxt2;
+        }
+        return;
+    }
+
+    // general loop: per wave-tile, every step in order with its operands loaded in place, then
+    // the step's reset or rows (one tile at a time through acc[0], rotating the accumulators)
+    f32x16 acc[WT_N];
+    Item t;
+    first_item(t);
+    for (int g = g0; g < g_end; g += K) {
+        if (g != g0) {
+            Item n;
+            next_item(t, n);
+            t = n;
+        }
+#pragma unroll
+        for (int i = 0; i < WT_N; i++) {
+            const TS* tl = Pin + tile_ptr(t, i);
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) {
+                const f32x4 v = tile_ld(tl, lane, qq);
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = v[j];
+            }
+        }
+        const int wr = t.w.rc & 0xffff, wc = t.w.rc >> 16;
+#pragma unroll
+        for (int q = 0; q < NS; q++) {
+            const int* r = p.steps[q].res + (size_t)t.e * RES_STRIDE;
+            const int reset = sload(r + RES_RESET);
+            const int kc = reset ? 0 : sload(r + RES_KSTEPS);
+            if (kc > 0) {
+                const float* U = reinterpret_cast<const float*>(p.steps[q].Uop) + t.e * opstride + lofs;
+                const float* V = reinterpret_cast<const float*>(p.steps[q].Vop) + t.e * opstride + lofs;
+                f32x4 a[WT_R][2], b[WT_C][2];
+#pragma unroll
+                for (int rr = 0; rr < WT_R; rr++) {
+                    const float* src = U + (size_t)op_row(t, 0, rr) * 64 * kh;
+                    a[rr][0] = *reinterpret_cast<const f32x4*>(src);
+                    a[rr][1] = *reinterpret_cast<const f32x4*>(src + 4);
+                }
+#pragma unroll
+                for (int c = 0; c < WT_C; c++) {
+                    const float* src = V + (size_t)op_row(t, 1, c) * 64 * kh;
+                    b[c][0] = *reinterpret_cast<const f32x4*>(src);
+                    b[c][1] = *reinterpret_cast<const f32x4*>(src + 4);
+                }
+#pragma unroll
+                for (int s = 0; s < SBK; s++)
+                    if (s < kc) {
+#pragma unroll
+                        for (int rr = 0; rr < WT_R; rr++)
+#pragma unroll
+                            for (int c = 0; c < WT_C; c++)
+                                acc[rr * WT_C + c] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                                    a[rr][s >> 2][s & 3], b[c][s >> 2][s & 3], acc[rr * WT_C + c], 0, 0, 0);
+                    }
+#pragma unroll
+                for (int i = 0; i < WT_N; i++) round_acc<TS>(acc[i]);
+            }
+            if (reset) {
+#pragma unroll
+                for (int i = 0; i < WT_N; i++)
+#pragma unroll
+                    for (int k = 0; k < 16; k++) acc[i][k] = 0.f;
+                continue;
+            }
+            const int nadd = sload(r + RES_NADD), s0 = sload(r + RES_SAVED_IN);
+            if (nadd <= 0 || (wc + 1) * WT_C * 16 <= s0 || wc * WT_C * 16 >= s0 + nadd) continue;
+            const double* prw0 = p.steps[q].patch + (size_t)t.e * d.max_lines * 2 * d.M;
+            const double* pdg = p.steps[q].patch_diag + (size_t)t.e * d.max_lines * 4;
+#pragma nounroll
+            for (int i = 0; i < WT_N; i++) {
+                const int bi = wr * WT_R + i / WT_C, bj = wc * WT_C + i % WT_C;
+                if (((t.w.valid >> i) & 1) && bj * 16 + 15 >= s0 && bj * 16 < s0 + nadd) {
+                    const int col = bj * 32 + (lane & 31);
+#pragma unroll
+                    for (int k = 0; k < 16; k++) {
+                        const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
+                        const int hi = max(row >> 1, col >> 1);
+                        if (hi >= s0 && hi < s0 + nadd)
+                            acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s0, row, col)));
+                    }
+                }
+                const f32x16 t0 = acc[0];
+#pragma unroll
+                for (int j = 0; j < WT_N - 1; j++) acc[j] = acc[j + 1];
+                acc[WT_N - 1] = t0;
+            }
+        }
+        store_tiles(t, acc);
+    }
+}
+
 __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams p)
 {
     const Dims d = p.d;
@@ -2764,6 +3037,24 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
         return hipGetLastError();
     }
     const bool half = precision == EKF_PREC_F16;
+    const bool wave_ok = p.variant == 8 && p.nsteps >= 2 && p.nsteps <= 8 && p.nsteps % 2 == 0 &&
+                         p.d.kmax <= 16 && p.nwt > 0 && p.wt != nullptr;
+    if (wave_ok) {
+        const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
+#define EKF_WAVE_CASE(NSV)                                                                              \
+    case NSV:                                                                                           \
+        if (half) hipLaunchKernelGGL((flush_f32_wave_kernel<_Float16, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, p); \
+        else hipLaunchKernelGGL((flush_f32_wave_kernel<float, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, p);         \
+        break;
+        switch (p.nsteps) {
+            EKF_WAVE_CASE(2)
+            EKF_WAVE_CASE(4)
+            EKF_WAVE_CASE(6)
+            EKF_WAVE_CASE(8)
+        }
+#undef EKF_WAVE_CASE
+        return hipGetLastError();
+    }
     const bool persist_ok = p.nsteps <= PST_MAXC && p.d.kmax <= 16 && p.variant != 2;
     if (persist_ok && p.variant == 4) {
         const int pgrid = 24 * ((p.ncu + 7) / 8);   // three workgroups per CU, operands by LDS-DMA

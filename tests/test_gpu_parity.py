@@ -451,3 +451,43 @@ def test_speculative_association_identical(ekf_mod, oracle_mod, monkeypatch, pre
         np.testing.assert_array_equal(y, y0)
         np.testing.assert_array_equal(pose, pose0)
         assert s == s0
+
+
+@pytest.mark.parametrize("prec", [1, 2])
+@pytest.mark.parametrize("N,T,lines,extra_every", [(80, 8, 6, 3), (80, 2, 8, 0), (64, 6, 6, 4),
+                                                  (1024, 8, 8, 0), (1024, 4, 6, 5)])
+def test_wave_flush_equals_drained(ekf_mod, monkeypatch, prec, N, T, lines, extra_every):
+    """The barrier-free per-wave flush (2 × 2-tile wave-tiles, software-pipelined operand ring;
+    forced with EKF_FLUSH_VARIANT=8) gives bit-identical state to one in-place flush per scan:
+    full groups in its pipelined loop (8 matches, or partial downdates predicated), groups with
+    augmentation rows or the capacity reset in its general loop, odd tile counts (N = 80: 5 tile
+    rows, a wave-tile column past the block) and several instances per XCD range."""
+    monkeypatch.setenv("EKF_FLUSH_VARIANT", "8")
+    E = 3
+    w = G.make_world(N, active=N - 14 if extra_every else N - 10)
+    st = G.initial_state(w)
+    a = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T)
+    monkeypatch.delenv("EKF_FLUSH_VARIANT")
+    b = ekf_mod.Ensemble(N, E, prec, max_lines=8)
+    for ens in (a, b):
+        for e in range(E):
+            ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+    rng = np.random.default_rng(5)
+    for step in range(1, 3 * T + 1):
+        enc, ln, nl = G.make_scan(w, step, instances=E, lines=lines)
+        if extra_every and step % extra_every == 0:
+            ex = G.random_lines(rng, 2)[None].repeat(E, axis=0)
+            ln = np.concatenate([ln, ex], axis=1)
+            nl = np.full(E, ln.shape[1], dtype=np.int32)
+        ra = a.localize(enc, ln, nl)
+        rb = b.localize(enc, ln, nl)
+        b.download_state(0, with_P=False)
+        for e in range(E):
+            assert ra[e]["match"] == rb[e]["match"], (step, e)
+    for e in range(E):
+        Pa, ya, sa, pa = a.download_state(e)
+        Pb, yb, sb, pb = b.download_state(e)
+        bad = np.argwhere(Pa != Pb)
+        assert bad.size == 0, (e, bad[:12].tolist(), rel(Pa, Pb))
+        np.testing.assert_array_equal(ya, yb)
+        assert sa == sb
