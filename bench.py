@@ -10,7 +10,7 @@ Inputs are resident in HBM before the timed region. `value` = instances × steps
 ÷ max-over-ranks wall time of the K timed steps. The default warm-up (200 steps, ≈35 ms) lets
 the GPU reach its steady clocks first: with 8 warm-up steps the same build reads ≈12 % lower.
 
-Schedule (defaults): the landmark block is flushed once per T = 4 scans (flush_interval), in
+Schedule (defaults): the landmark block is flushed once per T = 8 scans (flush_interval), in
 place, between association kernels (--pipeline 1 overlaps them instead); every schedule is
 bit-identical to a per-scan in-place update (tests/test_gpu_parity.py::
 test_deferred_flush_equals_drained). The timed region ends with ekf_sync, which flushes the
@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="1: overlap the association kernels with the previous group's flush")
-    ap.add_argument("--flush-interval", type=int, default=4,
+    ap.add_argument("--flush-interval", type=int, default=8,
                     help="T: rewrite the landmark block once per T scans (bit-identical state)")
     ap.add_argument("--bcast-every", type=int, default=0,
                     help="scans per broadcast (default: the flush interval); broadcasts run one "
@@ -70,6 +70,18 @@ def parse():
                     help="nccl (= RCCL on ROCm); gloo only to rehearse ranks on one GPU")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return ap.parse_args()
+
+
+def flush_kernel_name(prec, T):
+    """The flush form launch_downdate (slam_ros_amd/csrc/ekf_kernels.hip) picks for full groups of
+    T steps at kmax = 16 (8 lines per scan), honouring EKF_FLUSH_VARIANT."""
+    from slam_ros_amd import ekf
+    v = int(os.environ.get("EKF_FLUSH_VARIANT", "0"))
+    if prec == ekf.PREC_F64:
+        return "downdate_f64_kernel"
+    if T % 2 == 0 and 2 <= T <= 8 and ((v == 0 and T >= 4) or v in (8, 81, 82)):
+        return "flush_f32_wave_kernel"
+    return "flush_f32_persist2_kernel" if T <= 4 and v != 2 else "flush_f32_sb_kernel"
 
 
 def rel(a, b):
@@ -268,8 +280,7 @@ def main():
             "unit": "GB/s" if bound == "hbm" else "TFLOP/s",
             "frac": ((gbs / HBM_PEAK_GBS) if bound == "hbm" else (tfs / mfma_peak)) if dd_ms > 0 else None,
             "traffic": traffic,
-            "kernel": ("downdate_f64_kernel" if prec == ekf.PREC_F64 else
-                       "flush_f32_persist2_kernel" if args.flush_interval <= 4 else "flush_f32_sb_kernel"),
+            "kernel": flush_kernel_name(prec, args.flush_interval),
             "alg_bytes_per_launch": alg_bytes,
             "alg_flops_per_launch": alg_flops,
             "steps_per_launch": steps_per_launch,

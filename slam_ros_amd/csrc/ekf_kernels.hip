@@ -67,7 +67,16 @@ __device__ __forceinline__ typename Stor<T>::C from_store(T h)
 template <typename T>
 __device__ __forceinline__ typename Stor<T>::C round_step(typename Stor<T>::C x)
 {
-    return (typename Stor<T>::C)(T)x;
+    if constexpr (Stor<T>::half) {
+        // the same instruction on every path: the compiler may otherwise pair two roundings into
+        // v_cvt_pk_f16_f32 at some call sites, which does not round fp16 subnormals like
+        // v_cvt_f16_f32 (the flush and the on-read replay must round bit-identically)
+        float r;
+        asm("v_cvt_f16_f32 %0, %1\n\tv_cvt_f32_f16 %0, %0" : "=v"(r) : "v"(x));
+        return r;
+    } else {
+        return (typename Stor<T>::C)(T)x;
+    }
 }
 
 // P value (fp64) → scaled compute domain, and back
@@ -788,7 +797,13 @@ constexpr int PKW = MB_VH;                          // package words (speculativ
 // Blocks (j, cols[t]) for t < SPEC_L and (j, j) (last; only if `diag`) of the landmark block
 // with the pending steps applied, fp32 operands, every pending step with ks <= 8: the guessed
 // columns' operand rows come from LDS (stg[t][q][U|V][row half][8], staged by the workgroup),
-// the owned rows are loaded once per step. Per element the same chain as pll_blocks.
+// the owned rows are loaded once per step (the next step's while this one runs). Per element
+// the same chain as pll_blocks, kept in the requested orientation: a block stored transposed
+// (its column's tile row first) evolves as fma(X_col·V_own) terms, which equal the owned-first
+// products bit for bit (fma(a, b, c) == fma(b, a, c)), so every block runs one pattern on
+// O = owned U (or owned V when transposed) and X = staged V (or staged U). Every k-step runs:
+// past a step's matches the operands hold −0 (U) and +0 (V), whose products leave a chain as it
+// is (x + (−0) == x).
 template <typename T>
 __device__ __forceinline__ void staged_blocks(const PllView<T>& v, int j, const int (&cols)[8],
                                               const float* stg, bool diag, double (&out)[9][4])
@@ -798,89 +813,154 @@ __device__ __forceinline__ void staged_blocks(const PllView<T>& v, int j, const 
     const int i0 = 2 * j;
     bool swap[NB];
     int jb[NB];
-    C acc[NB][4];
+    C r[NB][4];   // (i0, jb), (i0, jb+1), (i0+1, jb), (i0+1, jb+1)
 #pragma unroll
     for (int b = 0; b < NB; b++) {
         jb[b] = 2 * (b < 8 ? cols[b] : j);
         swap[b] = (i0 >> 5) > (jb[b] >> 5);
-        const int a0 = swap[b] ? jb[b] : i0, b0 = swap[b] ? i0 : jb[b];
-        load_block<T>(v, a0, b0, acc[b]);
+        C a[4];
+        load_block<T>(v, swap[b] ? jb[b] : i0, swap[b] ? i0 : jb[b], a);
+        r[b][0] = a[0]; r[b][1] = swap[b] ? a[2] : a[1];
+        r[b][2] = swap[b] ? a[1] : a[2]; r[b][3] = a[3];
     }
+    (void)diag;
     const int kh = v.kmax / 2;
+    // owned rows i0, i0+1 of U_q and V_q: [row half][2 × 4 k]
+    auto load_rows = [&](int q, f32x4v (&Ux)[4][2], f32x4v (&Vx)[4][2]) {
+        const Slot& sq = v.pend[q];
+        const float* ou = reinterpret_cast<const float*>(sq.Uop) + v.e * v.opstride +
+                          ((size_t)(i0 >> 5) * 64 + (i0 & 31)) * kh;
+        const float* ov = reinterpret_cast<const float*>(sq.Vop) + v.e * v.opstride +
+                          ((size_t)(i0 >> 5) * 64 + (i0 & 31)) * kh;
+#pragma unroll
+        for (int rh = 0; rh < 4; rh++) {
+            const int roff = (rh & 1) * kh + (rh >> 1) * 32 * kh;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                Ux[rh][h] = *reinterpret_cast<const f32x4v*>(ou + roff + 4 * h);
+                Vx[rh][h] = *reinterpret_cast<const f32x4v*>(ov + roff + 4 * h);
+            }
+        }
+    };
+    f32x4v U[4][2], V[4][2];
+    if (v.npend > 0) load_rows(0, U, V);
     for (int q = 0; q < v.npend; q++) {
+        f32x4v Un[4][2], Vn[4][2];
+        const bool pre = q + 1 < v.npend;
+        if (pre) load_rows(q + 1, Un, Vn);
         const Slot& sq = v.pend[q];
         const int4 cw = v.ctl[q];
         if (cw.x) {
 #pragma unroll
-            for (int b = 0; b < NB; b++) acc[b][0] = acc[b][1] = acc[b][2] = acc[b][3] = (C)0;
-            continue;
-        }
-        const int ks = cw.y;
-        if (ks > 0) {
-            // owned rows i0, i0+1 of U_q and V_q: [row half][2 × 4 k]
-            const float* ou = reinterpret_cast<const float*>(sq.Uop) + v.e * v.opstride +
-                              ((size_t)(i0 >> 5) * 64 + (i0 & 31)) * kh;
-            const float* ov = reinterpret_cast<const float*>(sq.Vop) + v.e * v.opstride +
-                              ((size_t)(i0 >> 5) * 64 + (i0 & 31)) * kh;
-            f32x4v U[4][2], V[4][2];
-#pragma unroll
-            for (int rh = 0; rh < 4; rh++) {
-                const int roff = (rh & 1) * kh + (rh >> 1) * 32 * kh;
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    U[rh][h] = *reinterpret_cast<const f32x4v*>(ou + roff + 4 * h);
-                    V[rh][h] = *reinterpret_cast<const f32x4v*>(ov + roff + 4 * h);
-                }
-            }
+            for (int b = 0; b < NB; b++) r[b][0] = r[b][1] = r[b][2] = r[b][3] = (C)0;
+        } else {
 #pragma unroll
             for (int b = 0; b < NB; b++) {
-                // a side: owned U rows, or the column's U rows when the block is stored transposed;
-                // b side: the column's V rows, or the owned V rows
-                const float* cu = stg + (((b * SPEC_QMAX + q) * 2 + 0) * 4) * 8;
-                const float* cv = stg + (((b * SPEC_QMAX + q) * 2 + 1) * 4) * 8;
+                // staged rows of the column: its V rows, or its U rows when the block is stored
+                // transposed
+                const float* xs = stg + (((b * SPEC_QMAX + q) * 2 + (swap[b] ? 0 : 1)) * 4) * 8;
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
-                    f32x4v A[4], Bv[4];
+                    f32x4v O[4], X[4];
 #pragma unroll
                     for (int rh = 0; rh < 4; rh++) {
                         if (b < 8) {
-                            const f32x4v su = *reinterpret_cast<const f32x4v*>(cu + rh * 8 + 4 * h);
-                            const f32x4v sv = *reinterpret_cast<const f32x4v*>(cv + rh * 8 + 4 * h);
-                            A[rh] = swap[b] ? su : U[rh][h];
-                            Bv[rh] = swap[b] ? V[rh][h] : sv;
+                            X[rh] = *reinterpret_cast<const f32x4v*>(xs + rh * 8 + 4 * h);
+                            O[rh] = swap[b] ? V[rh][h] : U[rh][h];
                         } else {
-                            A[rh] = U[rh][h];
-                            Bv[rh] = V[rh][h];
+                            X[rh] = V[rh][h];
+                            O[rh] = U[rh][h];
                         }
                     }
-                    // rows: 0 = a0 even k, 1 = a0+1 even, 2 = a0 odd, 3 = a0+1 odd
+                    // rows: 0 = even k of the first row, 1 = of the second, 2/3 = odd k
 #pragma unroll
                     for (int s = 0; s < 4; s++) {
-                        if (4 * h + s >= ks) break;
-                        acc[b][0] = fmaf(A[2][s], Bv[2][s], fmaf(A[0][s], Bv[0][s], acc[b][0]));
-                        acc[b][1] = fmaf(A[2][s], Bv[3][s], fmaf(A[0][s], Bv[1][s], acc[b][1]));
-                        acc[b][2] = fmaf(A[3][s], Bv[2][s], fmaf(A[1][s], Bv[0][s], acc[b][2]));
-                        acc[b][3] = fmaf(A[3][s], Bv[3][s], fmaf(A[1][s], Bv[1][s], acc[b][3]));
+                        r[b][0] = fmaf(O[2][s], X[2][s], fmaf(O[0][s], X[0][s], r[b][0]));
+                        r[b][1] = fmaf(O[2][s], X[3][s], fmaf(O[0][s], X[1][s], r[b][1]));
+                        r[b][2] = fmaf(O[3][s], X[2][s], fmaf(O[1][s], X[0][s], r[b][2]));
+                        r[b][3] = fmaf(O[3][s], X[3][s], fmaf(O[1][s], X[1][s], r[b][3]));
                     }
                 }
 #pragma unroll
-                for (int k = 0; k < 4; k++) acc[b][k] = round_step<T>(acc[b][k]);
+                for (int k = 0; k < 4; k++) r[b][k] = round_step<T>(r[b][k]);
+                // one block at a time (bounds the staged rows in registers)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (cw.z > 0) {
+#pragma unroll
+                for (int b = 0; b < NB; b++) {
+                    C a[4] = {r[b][0], swap[b] ? r[b][2] : r[b][1], swap[b] ? r[b][1] : r[b][2], r[b][3]};
+                    patch_block<T>(v, sq, cw, i0, jb[b], swap[b], a);
+                    r[b][0] = a[0]; r[b][1] = swap[b] ? a[2] : a[1];
+                    r[b][2] = swap[b] ? a[1] : a[2]; r[b][3] = a[3];
+                }
             }
         }
-        if (cw.z > 0) {
+        if (pre) {
 #pragma unroll
-            for (int b = 0; b < NB; b++) patch_block<T>(v, sq, cw, i0, jb[b], swap[b], acc[b]);
+            for (int rh = 0; rh < 4; rh++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    U[rh][h] = Un[rh][h];
+                    V[rh][h] = Vn[rh][h];
+                }
         }
     }
 #pragma unroll
-    for (int b = 0; b < NB; b++) {
-        if (swap[b]) {
-            out[b][0] = from_domain<T>(acc[b][0]); out[b][1] = from_domain<T>(acc[b][2]);
-            out[b][2] = from_domain<T>(acc[b][1]); out[b][3] = from_domain<T>(acc[b][3]);
-        } else {
-            out[b][0] = from_domain<T>(acc[b][0]); out[b][1] = from_domain<T>(acc[b][1]);
-            out[b][2] = from_domain<T>(acc[b][2]); out[b][3] = from_domain<T>(acc[b][3]);
+    for (int b = 0; b < NB; b++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) out[b][k] = from_domain<T>(r[b][k]);
+}
+
+// Block (2·wa, 2·wb) of the landmark block with the pending steps applied, when both landmarks
+// are guessed columns (guess indices ta, tb): both sides' operand rows come from the staged LDS
+// image. Per element the same chain as pll_blocks.
+template <typename T>
+__device__ __forceinline__ void staged_pair_block(const PllView<T>& v, int wa, int ta, int wb, int tb,
+                                                  const float* stg, double (&out)[4])
+{
+    using C = typename Stor<T>::C;
+    const int i0 = 2 * wa, jb = 2 * wb;
+    const bool swap = (i0 >> 5) > (jb >> 5);   // stored orientation: (jb, i0)
+    const int tA = swap ? tb : ta, tB = swap ? ta : tb;
+    C acc[4];
+    load_block<T>(v, swap ? jb : i0, swap ? i0 : jb, acc);
+    for (int q = 0; q < v.npend; q++) {
+        const int4 cw = v.ctl[q];
+        if (cw.x) {
+            acc[0] = acc[1] = acc[2] = acc[3] = (C)0;
+            continue;
         }
+        {   // every k-step (see staged_blocks)
+            const float* cu = stg + (((tA * SPEC_QMAX + q) * 2 + 0) * 4) * 8;
+            const float* cv = stg + (((tB * SPEC_QMAX + q) * 2 + 1) * 4) * 8;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                f32x4v A[4], Bv[4];
+#pragma unroll
+                for (int rh = 0; rh < 4; rh++) {
+                    A[rh] = *reinterpret_cast<const f32x4v*>(cu + rh * 8 + 4 * h);
+                    Bv[rh] = *reinterpret_cast<const f32x4v*>(cv + rh * 8 + 4 * h);
+                }
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+                    acc[0] = fmaf(A[2][s], Bv[2][s], fmaf(A[0][s], Bv[0][s], acc[0]));
+                    acc[1] = fmaf(A[2][s], Bv[3][s], fmaf(A[0][s], Bv[1][s], acc[1]));
+                    acc[2] = fmaf(A[3][s], Bv[2][s], fmaf(A[1][s], Bv[0][s], acc[2]));
+                    acc[3] = fmaf(A[3][s], Bv[3][s], fmaf(A[1][s], Bv[1][s], acc[3]));
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) acc[k] = round_step<T>(acc[k]);
+        }
+        if (cw.z > 0) patch_block<T>(v, v.pend[q], cw, i0, jb, swap, acc);
+    }
+    if (swap) {
+        out[0] = from_domain<T>(acc[0]); out[1] = from_domain<T>(acc[2]);
+        out[2] = from_domain<T>(acc[1]); out[3] = from_domain<T>(acc[3]);
+    } else {
+        out[0] = from_domain<T>(acc[0]); out[1] = from_domain<T>(acc[1]);
+        out[2] = from_domain<T>(acc[2]); out[3] = from_domain<T>(acc[3]);
     }
 }
 
@@ -1268,7 +1348,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             // predicted robot-strip columns and mean, diagonal block, blocks of the earlier
             // winners' columns; and (staged replay) the guessed columns' rows of the pending
             // steps' operands ----
-            if (tid < L * (L + 1) / 2) {
+            if (!staged && tid < L * (L + 1) / 2) {
                 int u = 0, t = tid;
                 while (t > u) { t -= u + 1; u++; }
                 const int wu = sh_spec[u], wt = sh_spec[t];
@@ -1312,6 +1392,22 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             }
             if (tid == SCAN_BLOCK - 1) sh_ready = 0;
             __syncthreads();
+            if (staged) {
+                // the winners' mutual blocks from the staged rows (an LDS pass per pending step
+                // instead of two global round trips)
+                if (tid < L * (L + 1) / 2) {
+                    int u = 0, t = tid;
+                    while (t > u) { t -= u + 1; u++; }
+                    const int wu = sh_spec[u], wt = sh_spec[t];
+                    if (wu >= 0 && wt >= 0) {
+                        double bk[4];
+                        staged_pair_block<T>(pv, wu, u, wt, t, sh_stg, bk);
+                        double* r = sh_wd + u * SPEC_WD + (t == u ? 6 : 14 + 4 * t);
+                        r[0] = bk[0]; r[1] = bk[1]; r[2] = bk[2]; r[3] = bk[3];
+                    }
+                }
+                __syncthreads();
+            }
             EKF_STAMP(12);
             // ---- (f) the winners' part of the sequential chain, in the last wave (lane u carries
             // winner u's rows): per line the winner's lane evaluates it and writes the package,
@@ -1696,6 +1792,17 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         *reinterpret_cast<double2*>(Rs + n + b0) = rr1;
         *reinterpret_cast<double2*>(Rs + 2 * n + b0) = rr2;
         *reinterpret_cast<double2*>(y + b0) = yb;
+        if (sizeof(C) == 4) {
+            // f32 operands: the k columns past the matches hold −0 (U) and +0 (V), so a flush
+            // that runs every k-step unconditionally adds −0 there, which leaves every value as
+            // it is (flush_f32_wave_kernel; the other forms and the on-read replay stop at ks)
+            for (int k = 2 * m; k < d.kmax; k++)
+#pragma unroll
+                for (int pp = 0; pp < 2; pp++) {
+                    Uop[op_index_f32(2 * j + pp, k, d.kmax)] = (C)(-0.0f);
+                    Vop[op_index_f32(2 * j + pp, k, d.kmax)] = (C)0.0f;
+                }
+        }
         if (sizeof(C) == 8 && (m & 1)) {
             // f64 operands: zero the odd tail column pair of the last 4-wide k-step
 #pragma unroll
@@ -2653,26 +2760,22 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
     };
 
     if (fast) {
+        const int dbg = p.variant;   // timing probes only (EKF_FLUSH_VARIANT 81/82: results invalid)
         // raw tile words in flight (fp16 storage: converted when the wave-tile starts)
         using Raw = typename std::conditional<HALF, f16x4, f32x4>::type;
         Raw pref[WT_N][4];
         f32x4 opA[NS][WT_R][2], opB[NS][WT_C][2];
         f32x16 acc[WT_N];
-        auto load_ops = [&](int slot, const Item& t, int q) __attribute__((always_inline)) {
-            const float* U = reinterpret_cast<const float*>(p.steps[q].Uop) + t.e * opstride + lofs;
-            const float* V = reinterpret_cast<const float*>(p.steps[q].Vop) + t.e * opstride + lofs;
+        // half h (k-steps 4h..4h+3) of step q's operand rows of wave-tile t, into slot q
+        auto load_half = [&](int slot, const Item& t, int q, int h) __attribute__((always_inline)) {
+            const float* U = reinterpret_cast<const float*>(p.steps[q].Uop) + t.e * opstride + lofs + 4 * h;
+            const float* V = reinterpret_cast<const float*>(p.steps[q].Vop) + t.e * opstride + lofs + 4 * h;
 #pragma unroll
-            for (int r = 0; r < WT_R; r++) {
-                const float* src = U + (size_t)op_row(t, 0, r) * 64 * kh;
-                opA[slot][r][0] = *reinterpret_cast<const f32x4*>(src);
-                opA[slot][r][1] = *reinterpret_cast<const f32x4*>(src + 4);
-            }
+            for (int r = 0; r < WT_R; r++)
+                opA[slot][r][h] = *reinterpret_cast<const f32x4*>(U + (size_t)op_row(t, 0, r) * 64 * kh);
 #pragma unroll
-            for (int c = 0; c < WT_C; c++) {
-                const float* src = V + (size_t)op_row(t, 1, c) * 64 * kh;
-                opB[slot][c][0] = *reinterpret_cast<const f32x4*>(src);
-                opB[slot][c][1] = *reinterpret_cast<const f32x4*>(src + 4);
-            }
+            for (int c = 0; c < WT_C; c++)
+                opB[slot][c][h] = *reinterpret_cast<const f32x4*>(V + (size_t)op_row(t, 1, c) * 64 * kh);
         };
         auto load_tiles = [&](const Item& t) __attribute__((always_inline)) {
 #pragma unroll
@@ -2682,49 +2785,72 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
                 for (int qq = 0; qq < 4; qq++) pref[i][qq] = __builtin_nontemporal_load(tl + lane + qq * 64);
             }
         };
+        // k-steps 4h..4h+3 of step q. Every k-step runs: past the step's matches the scan kernel
+        // leaves (−0)·(+0) operand products, and x + (−0) == x for every x (zeros, NaN, inf too)
+        auto mfma_half = [&](int q, int h) __attribute__((always_inline)) {
+#pragma unroll
+            for (int s = 0; s < 4; s++)
+#pragma unroll
+                for (int r = 0; r < WT_R; r++)
+#pragma unroll
+                    for (int c = 0; c < WT_C; c++)
+                        acc[r * WT_C + c] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                            opA[q][r][h][s], opB[q][c][h][s], acc[r * WT_C + c], 0, 0, 0);
+        };
+        // one operand load after every group of four MFMAs (4 loads per half step)
+        auto interleave = [&]() __attribute__((always_inline)) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // VMEM read
+            }
+        };
         Item cur, nxt, nxt2;
         first_item(cur);
         next_item(cur, nxt);
         load_tiles(cur);
 #pragma unroll
-        for (int q = 0; q < NS; q++) load_ops(q, cur, q);
+        for (int q = 0; q < NS; q++) {
+            load_half(q, cur, q, 0);
+            load_half(q, cur, q, 1);
+        }
         int g = g0;
         while (true) {
             const bool more = g + K < g_end;
             next_item(nxt, nxt2);   // read now, used by the next wave-tile
+            // operand rows for the next wave-tile (the last one re-reads its own: no branch
+            // splits the MFMA stream)
+            const Item ldi = more ? nxt : cur;
 #pragma unroll
             for (int i = 0; i < WT_N; i++)
 #pragma unroll
                 for (int qq = 0; qq < 4; qq++)
 #pragma unroll
                     for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = (float)pref[i][qq][j];
-            // the next wave-tile's tiles first: they have the whole wave-tile to land
-            if (more) load_tiles(nxt);
+            // the next wave-tile's tiles first: the waits of this wave-tile only cover loads issued
+            // during the one before it, so these have the whole wave-tile to land
+            if (more && dbg != 82) load_tiles(nxt);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int q = 0; q < NS; q++) {
-                // k-steps past the step's matches are skipped (uniform branches, in-place chains)
-                const int kc = sload(p.steps[q].res + (size_t)cur.e * RES_STRIDE + RES_KSTEPS);
-#pragma unroll
-                for (int s = 0; s < SBK; s++)
-                    if (s < kc) {
-#pragma unroll
-                        for (int r = 0; r < WT_R; r++)
-#pragma unroll
-                            for (int c = 0; c < WT_C; c++)
-                                acc[r * WT_C + c] = __builtin_amdgcn_mfma_f32_32x32x2f32(
-                                    opA[q][r][s >> 2][s & 3], opB[q][c][s >> 2][s & 3], acc[r * WT_C + c], 0, 0, 0);
-                    }
-                if (kc > 0) {
-#pragma unroll
-                    for (int i = 0; i < WT_N; i++) round_acc<TS>(acc[i]);
+                // first half of step q, beside the second half of step q−1's rows for the next
+                // wave-tile (their registers were last read by step q−1)
+                mfma_half(q, 0);
+                if (q > 0) {
+                    load_half(q - 1, ldi, q - 1, 1);
+                    interleave();
                 }
-                // step q's operand registers are free: the next wave-tile's step q
-                if (more) load_ops(q, nxt, q);
-                // keep the issue order (the scheduler would hoist the loads)
+                __builtin_amdgcn_sched_barrier(0);
+                // second half, beside the first half of step q's rows for the next wave-tile
+                mfma_half(q, 1);
+#pragma unroll
+                for (int i = 0; i < WT_N; i++) round_acc<TS>(acc[i]);
+                load_half(q, ldi, q, 0);
+                interleave();
                 __builtin_amdgcn_sched_barrier(0);
             }
-            store_tiles(cur, acc);
+            load_half(NS - 1, ldi, NS - 1, 1);
+            if (dbg != 81) store_tiles(cur, acc);
             if (!more) break;
             g += K;
             cur = nxt;
@@ -3037,8 +3163,12 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
         return hipGetLastError();
     }
     const bool half = precision == EKF_PREC_F16;
-    const bool wave_ok = p.variant == 8 && p.nsteps >= 2 && p.nsteps <= 8 && p.nsteps % 2 == 0 &&
-                         p.d.kmax <= 16 && p.nwt > 0 && p.wt != nullptr;
+    // default: the wave flush for groups of 4, 6 or 8 steps; EKF_FLUSH_VARIANT 8 forces it (also
+    // for 2 steps), 9 keeps the LDS-staged forms
+    const bool wave_shape = p.nsteps >= 2 && p.nsteps <= 8 && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
+                            p.nwt > 0 && p.wt != nullptr;
+    const bool wave_ok = wave_shape && ((p.variant == 0 && p.nsteps >= 4) || p.variant == 8 ||
+                                        p.variant == 81 || p.variant == 82);
     if (wave_ok) {
         const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
 #define EKF_WAVE_CASE(NSV)                                                                              \

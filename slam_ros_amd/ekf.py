@@ -66,11 +66,13 @@ class EkfError(RuntimeError):
 _lib = None
 
 
-def load_library(path: str = LIB_PATH):
-    """Load libslam_ekf.so (never builds implicitly on a GPU box: fail loudly instead)."""
+def load_library(path: str = ""):
+    """Load libslam_ekf.so (never builds implicitly on a GPU box: fail loudly instead).
+    SLAM_EKF_LIB selects another build of the same library (A/B experiments)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("SLAM_EKF_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise EkfError(f"{path} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`"
                        " (HIP extension required; there is no CPU fallback)")

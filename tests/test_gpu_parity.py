@@ -152,6 +152,7 @@ def test_trajectory_fp64_with_reset(ekf_mod, oracle_mod):
 
 @pytest.mark.parametrize("prec", [0, 1, 2])
 @pytest.mark.parametrize("pipeline,T,drain_at", [(True, 1, ()), (False, 4, ()), (True, 3, (7,)),
+                                                 (False, 8, (5,)), (True, 8, ()), (False, 6, ()),
                                                  (False, 16, (5,)), (True, 16, ())])
 def test_deferred_flush_equals_drained(ekf_mod, oracle_mod, prec, pipeline, T, drain_at):
     """Deferred covariance downdates — the landmark block rewritten once per T scans, the
@@ -413,8 +414,8 @@ def _spec_scans(w, rng, steps, L=8):
 
 
 @pytest.mark.parametrize("prec", [0, 1])
-@pytest.mark.parametrize("N", [64, 1024, 4096])
-def test_speculative_association_identical(ekf_mod, oracle_mod, monkeypatch, prec, N):
+@pytest.mark.parametrize("N,T", [(64, 4), (1024, 4), (4096, 4), (1024, 8), (4096, 8)])
+def test_speculative_association_identical(ekf_mod, oracle_mod, monkeypatch, prec, N, T):
     """The speculative association (guessed winners, three exchanges per scan, exact local
     re-check) gives bit-identical state and results to the per-line sequential exchange, also
     when every guess is wrong (EKF_SPECULATE=2: every scan falls back); association vs the
@@ -426,7 +427,7 @@ def test_speculative_association_identical(ekf_mod, oracle_mod, monkeypatch, pre
     monkeypatch.setenv("EKF_SCAN_STAMPS", "1")
     for mode in (0, 1, 2):
         monkeypatch.setenv("EKF_SPECULATE", str(mode))
-        ens = ekf_mod.Ensemble(N, 1, prec, max_lines=8, flush_interval=4)
+        ens = ekf_mod.Ensemble(N, 1, prec, max_lines=8, flush_interval=T)
         ens.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
         if mode == 1:
             ref = oracle_mod.OracleRobot(N)
