@@ -79,7 +79,7 @@ def flush_kernel_name(prec, T):
     v = int(os.environ.get("EKF_FLUSH_VARIANT", "0"))
     if prec == ekf.PREC_F64:
         return "downdate_f64_kernel"
-    if T % 2 == 0 and 2 <= T <= 8 and ((v == 0 and T >= 4) or v in (8, 81, 82)):
+    if T % 2 == 0 and 2 <= T <= 8 and ((v == 0 and T >= 6) or v in (8, 81, 82)):
         return "flush_f32_wave_kernel"
     return "flush_f32_persist2_kernel" if T <= 4 and v != 2 else "flush_f32_sb_kernel"
 

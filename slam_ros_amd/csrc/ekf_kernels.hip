@@ -3163,11 +3163,11 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
         return hipGetLastError();
     }
     const bool half = precision == EKF_PREC_F16;
-    // default: the wave flush for groups of 4, 6 or 8 steps; EKF_FLUSH_VARIANT 8 forces it (also
-    // for 2 steps), 9 keeps the LDS-staged forms
+    // default: the wave flush for groups of 6 or 8 steps; EKF_FLUSH_VARIANT 8 forces it (also
+    // for 2 or 4 steps), 9 keeps the LDS-staged forms
     const bool wave_shape = p.nsteps >= 2 && p.nsteps <= 8 && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
                             p.nwt > 0 && p.wt != nullptr;
-    const bool wave_ok = wave_shape && ((p.variant == 0 && p.nsteps >= 4) || p.variant == 8 ||
+    const bool wave_ok = wave_shape && ((p.variant == 0 && p.nsteps >= 6) || p.variant == 8 ||
                                         p.variant == 81 || p.variant == 82);
     if (wave_ok) {
         const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
