@@ -11,11 +11,13 @@
 //        (Robot.cpp:893-904) run at the end of the same kernel; the new landmarks' rows of the
 //        landmark block go to the step's slot (patch buffers), the rank-2m operands U/V to the
 //        slot's MFMA-ordered operand buffers.
-//   2. flush (stream D): one pass over the packed landmark block applying a group of T steps in
-//        order — per step X ← X − U_t·V_tᵀ (rank 2m on MFMA, the reference's m dense n×n passes
-//        of Robot.cpp:560-572 fused), then that step's augmented rows, or the reset. Each stored
-//        tile is read and written once per group. fp32: flush_f32_sb_kernel (super-tiles, LDS
-//        operands); fp64: downdate_f64_kernel (one tile per wave).
+//   2. flush (stream S; D when pipelined): one pass over the packed landmark block applying a
+//        group of T steps in order — per step X ← X − U_t·V_tᵀ (rank 2m on MFMA, the reference's
+//        m dense n×n passes of Robot.cpp:560-572 fused), then that step's augmented rows, or the
+//        reset. Each stored tile is read and written once per group. fp32/fp16 storage:
+//        flush_f32_wave_kernel (groups of 6-8 steps: barrier-free waves, one wave-tile of
+//        prefetch), flush_f32_persist2_kernel (≤ 4 steps, LDS-staged super-tiles),
+//        flush_f32_sb_kernel (otherwise); fp64: downdate_f64_kernel (one tile per wave).
 //
 // Deferred reads: between flushes the association kernels read the landmark block with the
 // pending steps applied on read (pll_block): per element, the same k-ordered fp32/fp64 FMA chain
