@@ -977,8 +977,11 @@ template <typename T>
 __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
 {
     const Dims d = p.d;
-    const int g = blockIdx.x;
-    const int e = p.e0 + blockIdx.y;
+    // 1-D grid, instance-minor: block b is workgroup b / E of instance b % E. Workgroups are
+    // dealt round-robin over the 8 XCDs, so with 8 instances per launch each instance's
+    // workgroups share one XCD (and its L2) in every launch; correctness never depends on it
+    const int g = (int)blockIdx.x / p.E;
+    const int e = p.e0 + (int)blockIdx.x % p.E;
     const int G = p.G;
     const int tid = threadIdx.x;
     // threads < SCAN_THREADS own landmark j; the last wave (no landmark) replays the guessed
@@ -3150,11 +3153,11 @@ int scan_blocks_per_cu(int precision)
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 {
     if (precision == EKF_PREC_F64)
-        hipLaunchKernelGGL(scan_kernel<double>, dim3(p.G, p.E), dim3(SCAN_BLOCK), 0, st, p);
+        hipLaunchKernelGGL(scan_kernel<double>, dim3(p.G * p.E), dim3(SCAN_BLOCK), 0, st, p);
     else if (precision == EKF_PREC_F16)
-        hipLaunchKernelGGL(scan_kernel<_Float16>, dim3(p.G, p.E), dim3(SCAN_BLOCK), 0, st, p);
+        hipLaunchKernelGGL(scan_kernel<_Float16>, dim3(p.G * p.E), dim3(SCAN_BLOCK), 0, st, p);
     else
-        hipLaunchKernelGGL(scan_kernel<float>, dim3(p.G, p.E), dim3(SCAN_BLOCK), 0, st, p);
+        hipLaunchKernelGGL(scan_kernel<float>, dim3(p.G * p.E), dim3(SCAN_BLOCK), 0, st, p);
     return hipGetLastError();
 }
 
