@@ -2678,7 +2678,7 @@ __global__ __launch_bounds__(DD_THREADS, MINB) void flush_f32_persist2_kernel(Do
 // (partial downdates are predicated); otherwise the wave runs a plain per-wave-tile loop. Per
 // element the chain is the one every other form runs (k-ordered MFMA steps, fp16 rounding per
 // step, then the step's rows or the reset): bit-identical results.
-template <typename TS, int NS>
+template <typename TS, int NS, bool AM = (sizeof(TS) == 2)>
 __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateParams p)
 {
     static_assert(NS >= 2 && NS % 2 == 0 && NS <= PMAX, "even step count");
@@ -2836,6 +2836,80 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
             // during the one before it, so these have the whole wave-tile to land
             if (more && dbg != 82) load_tiles(nxt);
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (AM) {
+                // group-major steps (fp16 storage; fp32 opt-in, EKF_FLUSH_VARIANT=83): the
+                // per-step rounding of one group of accumulators runs on the VALU while the other
+                // group's MFMAs run, so it leaves the MFMA stream. Per element the chain is
+                // unchanged (k-ordered step q, then its rounding). Step q's operand registers are
+                // refilled for the next wave-tile during step q+1's first group; the last step's
+                // at the end. (Measured: one accumulator's 8 k-steps back to back, rounding the
+                // previous accumulator beside them, ran 0.84 ms vs 0.79 for the step-major form.)
+                // Pair-major form: group gi = accumulators (gi, 0) and (gi, 1) of the 2 × 2
+                // wave-tile, their k-steps alternating (a dependent MFMA two issues later); the
+                // previous group's 32 elements are rounded 2 per MFMA gap. The last step rounds
+                // group 0 in the first half of group 1 and stores its tiles in the second half.
+                auto mfma_grp = [&](int q, int gi, int pg, bool ld, int lq, bool last) __attribute__((always_inline)) {
+#pragma unroll
+                    for (int m = 0; m < 16; m++) {
+                        const int s = m >> 1, c = m & 1, i = gi * WT_C + c;
+                        acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(opA[q][gi][s >> 2][s & 3],
+                                                                       opB[q][c][s >> 2][s & 3], acc[i], 0, 0, 0);
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (pg >= 0 && !last) {
+                            const int a = pg * WT_C + (m >> 3), k = 2 * (m & 7);
+                            acc[a][k] = round_step<TS>(acc[a][k]);
+                            acc[a][k + 1] = round_step<TS>(acc[a][k + 1]);
+                        }
+                        if (last) {
+                            if (m < 8) {
+                                const int a = pg * WT_C + (m >> 2), k = 4 * (m & 3);
+#pragma unroll
+                                for (int u = 0; u < 4; u++) acc[a][k + u] = round_step<TS>(acc[a][k + u]);
+                            } else if (dbg != 81) {
+                                const int a = pg * WT_C + ((m - 8) >> 2), qq = (m - 8) & 3;
+                                if ((cur.w.valid >> a) & 1) tile_st(Pout + tile_ptr(cur, a), lane, qq, acc[a]);
+                            }
+                        }
+                        if (ld && (m & 1)) {
+                            // load m/2 of slot lq: half, operand row (A rows, then B rows)
+                            const int l = m >> 1, h = l >> 2, o = l & 3;
+                            const bool isA = o < WT_R;
+                            const float* base = reinterpret_cast<const float*>(isA ? p.steps[lq].Uop : p.steps[lq].Vop) +
+                                                ldi.e * opstride + lofs + 4 * h;
+                            const f32x4 v = *reinterpret_cast<const f32x4*>(
+                                base + (size_t)op_row(ldi, isA ? 0 : 1, isA ? o : o - WT_R) * 64 * kh);
+                            if (isA) opA[lq][o][h] = v;
+                            else opB[lq][o - WT_R][h] = v;
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                };
+                static_assert(WT_R == 2 && WT_C == 2, "pair-major form: two groups of two accumulators");
+#pragma unroll
+                for (int q = 0; q < NS; q++) {
+                    mfma_grp(q, 0, q > 0 ? 1 : -1, q > 0, q > 0 ? q - 1 : 0, false);
+                    mfma_grp(q, 1, 0, false, 0, q == NS - 1);
+                }
+#pragma unroll
+                for (int a = 2; a < 4; a++)
+#pragma unroll
+                    for (int k = 0; k < 16; k++) acc[a][k] = round_step<TS>(acc[a][k]);
+                load_half(NS - 1, ldi, NS - 1, 0);
+                load_half(NS - 1, ldi, NS - 1, 1);
+                if (dbg != 81)
+#pragma unroll
+                    for (int a = 2; a < 4; a++)
+                        if ((cur.w.valid >> a) & 1) {
+                            TS* tl = Pout + tile_ptr(cur, a);
+#pragma unroll
+                            for (int qq = 0; qq < 4; qq++) tile_st(tl, lane, qq, acc[a]);
+                        }
+                if (!more) break;
+                g += K;
+                cur = nxt;
+                nxt = nxt2;
+                continue;
+            }
 #pragma unroll
             for (int q = 0; q < NS; q++) {
                 // first half of step q, beside the second half of step q−1's rows for the next
@@ -3173,12 +3247,14 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     const bool wave_shape = p.nsteps >= 2 && p.nsteps <= 8 && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
                             p.nwt > 0 && p.wt != nullptr;
     const bool wave_ok = wave_shape && ((p.variant == 0 && p.nsteps >= 6) || p.variant == 8 ||
-                                        p.variant == 81 || p.variant == 82);
+                                        p.variant == 81 || p.variant == 82 || p.variant == 83);
     if (wave_ok) {
         const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
+        const bool am = p.variant == 83;   // fp32 with the accumulator-major step order
 #define EKF_WAVE_CASE(NSV)                                                                              \
     case NSV:                                                                                           \
         if (half) hipLaunchKernelGGL((flush_f32_wave_kernel<_Float16, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, p); \
+        else if (am) hipLaunchKernelGGL((flush_f32_wave_kernel<float, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, st, p); \
         else hipLaunchKernelGGL((flush_f32_wave_kernel<float, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, p);         \
         break;
         switch (p.nsteps) {

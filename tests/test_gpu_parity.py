@@ -6,6 +6,7 @@ Tolerances (BASELINE.json north_star): per scan from identical inputs,
 fp64 storage is held to 1e-10 over whole trajectories.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -463,7 +464,8 @@ def test_wave_flush_equals_drained(ekf_mod, monkeypatch, prec, N, T, lines, extr
     full groups in its pipelined loop (8 matches, or partial downdates predicated), groups with
     augmentation rows or the capacity reset in its general loop, odd tile counts (N = 80: 5 tile
     rows, a wave-tile column past the block) and several instances per XCD range."""
-    monkeypatch.setenv("EKF_FLUSH_VARIANT", "8")
+    # EKF_WAVE_TEST_VARIANT=83 checks the fp32 group-major form the same way
+    monkeypatch.setenv("EKF_FLUSH_VARIANT", os.environ.get("EKF_WAVE_TEST_VARIANT", "8"))
     E = 3
     w = G.make_world(N, active=N - 14 if extra_every else N - 10)
     st = G.initial_state(w)
