@@ -7,8 +7,10 @@ holds the pre-generated scan payloads and broadcasts each step's payload (all in
 RCCL/xGMI; every rank runs its slice of instances (no other collective on the data path).
 
 Inputs are resident in HBM before the timed region. `value` = instances × steps (all ranks)
-÷ max-over-ranks wall time of the K timed steps. The default warm-up (200 steps, ≈35 ms) lets
-the GPU reach its steady clocks first: with 8 warm-up steps the same build reads ≈12 % lower.
+÷ max-over-ranks wall time of the K timed steps. Before the W warm-up steps an untimed clock
+pre-roll (--preroll steps of the same workload, default 200 ≈ 30 ms, reported as
+`clock_preroll_steps`) lets the GPU reach the clocks it holds under this load: a step is ≈0.12 ms,
+so a few warm-up steps alone measure the clock ramp (≈12 % lower with 8 warm-up steps).
 
 Schedule (defaults): the landmark block is flushed once per T = 8 scans (flush_interval), in
 place, between association kernels (--pipeline 1 overlaps them instead); every schedule is
@@ -18,17 +20,27 @@ partial group: every step's downdate is in P. HIP events in the timed region bra
 kernel only; the association-kernel time is measured on extra steps after it.
 
 roofline: the dominant kernel is the covariance flush (rank-2m MFMA downdate of every step of the
-group, one read + write of the packed block). Per launch: algorithmic bytes = instances_per_gpu ×
-n(n+1) × 4, algorithmic flops = steps_per_launch × instances_per_gpu × 2m·n(n+1)
-(BASELINE.md §3). `bound` is whichever roof is the longer ideal time; its average duration comes
-from HIP events recorded on the stream the kernel runs on.
-cpu_baseline (rank 0, N=1 only): the CPU restatement (oracle/, fast mode, fp64, 1 thread) on a
-bounded sample of the same scans of instance 0; the same scans also give the per-scan parity
-numbers (‖P−P_ref‖_F/‖P_ref‖_F, state, association) from identical inputs.
+group, one read + write of the packed block). The timed steps may end in a partial group, whose
+flush runs another kernel form: every form used is listed in `roofline.launch_forms`, and the
+roofline itself is computed over the launches of the form with the largest total time only. Per
+launch of that form: algorithmic bytes = instances_per_gpu × n(n+1) × b,
+algorithmic flops = steps_per_launch × instances_per_gpu × 2m·n(n+1). `bound` is
+whichever roof is the longer ideal time; durations come from HIP events recorded on the stream
+the kernel runs on. `traffic` (HBM bytes per launch of that form from FETCH_SIZE/WRITE_SIZE,
+gfx950-corrected) is read from profiles/<round>/traffic.json only if it was measured on this very
+library build (sha256 of libslam_ekf.so) and configuration; otherwise null.
+cpu_baseline (rank 0, N=1 only): B1, the CPU restatement (oracle/, fast mode, fp64) built with
+OpenMP on the host cores (bit-identical to its single-thread build), timed on a bounded sample of
+the same scans of instance 0; `reference_path` carries B0 (faithful GSL-order restatement, 1 core)
+at the same N from profiles/*cpu_baselines.jsonl, measured once on the GPU box's host (≈minutes
+per update at N=4096). The same scans also give the per-scan parity numbers
+(‖P−P_ref‖_F/‖P_ref‖_F, state, association) from identical inputs.
 """
 from __future__ import annotations
 
 import argparse
+import glob
+import hashlib
 import json
 import os
 import sys
@@ -68,20 +80,49 @@ def parse():
                          "group ahead of the scans that use them")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm); gloo only to rehearse ranks on one GPU")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    ap.add_argument("--preroll", type=int, default=200,
+                    help="untimed clock pre-roll steps before the warm-up (steady GPU clocks)")
+    ap.add_argument("--traffic-json", default="",
+                    help="HBM traffic file (default: the newest profiles/*/traffic.json)")
     return ap.parse_args()
 
 
-def flush_kernel_name(prec, T):
-    """The flush form launch_downdate (slam_ros_amd/csrc/ekf_kernels.hip) picks for full groups of
-    T steps at kmax = 16 (8 lines per scan), honouring EKF_FLUSH_VARIANT."""
-    from slam_ros_amd import ekf
-    v = int(os.environ.get("EKF_FLUSH_VARIANT", "0"))
-    if prec == ekf.PREC_F64:
-        return "downdate_f64_kernel"
-    if T % 2 == 0 and 2 <= T <= 8 and ((v == 0 and T >= 6) or v in (8, 81, 82)):
-        return "flush_f32_wave_kernel"
-    return "flush_f32_persist2_kernel" if T <= 4 and v != 2 else "flush_f32_sb_kernel"
+def lib_sha(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()[:16]
+
+
+def find_traffic(explicit, sha, cfg):
+    """Counter-measured HBM bytes per launch for this build and configuration, or (None, why)."""
+    paths = [explicit] if explicit else sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json")),
+                                                key=os.path.getmtime, reverse=True)
+    for pth in paths:
+        try:
+            tj = json.load(open(pth))
+        except (OSError, ValueError):
+            continue
+        if all(tj.get(k) == v for k, v in cfg.items()):
+            if tj.get("lib_sha") != sha:
+                return None, f"{os.path.relpath(pth, ROOT)}: measured on another build ({tj.get('lib_sha')})"
+            return tj, os.path.relpath(pth, ROOT)
+    return None, "no counter file for this configuration"
+
+
+def reference_path_baseline(N):
+    """B0 (faithful GSL-order restatement, 1 core) at capacity N, measured on the GPU box host."""
+    best = None
+    for pth in sorted(glob.glob(os.path.join(ROOT, "profiles", "*cpu_baselines.jsonl"))):
+        for line in open(pth):
+            try:
+                r = json.loads(line)
+            except ValueError:
+                continue
+            if r.get("N") == N and str(r.get("baseline", "")).startswith("B0"):
+                best = dict(r, source=os.path.relpath(pth, ROOT))
+    return best
 
 
 def rel(a, b):
@@ -122,13 +163,18 @@ def main():
 
     ens = ekf.Ensemble(N, E, prec, max_lines=L_LINES, device=local, pipeline=bool(args.pipeline),
                       flush_interval=args.flush_interval)
-    stream = torch.cuda.current_stream(dev)
+    # one real stream for everything (torch's default stream has handle 0, which the C-ABI reads
+    # as "the context's own stream"): the payload copies, the RCCL waits (work.wait() orders the
+    # current stream) and the EKF kernels are then ordered on the same queue
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     ens.set_stream(stream.cuda_stream)
     for e in range(E):
         ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
 
     # ---- pre-generated scan payloads, resident in HBM (rank 0 is the sensor) ----
-    steps_total = W + K + W
+    PR = max(0, args.preroll)
+    steps_total = PR + W + K + W
     per_step = D.payload_len(E_total, L_LINES)
     payload = torch.empty((steps_total, per_step), dtype=torch.float64, device=dev)
     if rank == 0:
@@ -185,7 +231,9 @@ def main():
         lines_ptr = base + lo * 8
         ens.localize_device(enc_ptr, lines_ptr, nlines.data_ptr())
 
-    for s in range(W):
+    for s in range(PR):             # clock pre-roll (untimed)
+        step(s)
+    for s in range(PR, PR + W):     # warm-up (untimed)
         step(s)
     ens.sync()                      # flush the partial group: the timed region starts clean
     torch.cuda.synchronize(dev)
@@ -196,7 +244,7 @@ def main():
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for s in range(W, W + K):
+    for s in range(PR + W, PR + W + K):
         step(s)
     ens.sync()                      # every step's downdate is in the landmark block
     torch.cuda.synchronize(dev)
@@ -204,12 +252,13 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     prof = ens.profile_read()
+    flushes = ens.profile_flushes()
     ens.profile(0)
     # association-kernel time (informational): a few more steps with every kernel timed, outside
     # the timed region
     ens.profile(2)
     for s in range(W):
-        step(W + K + s)
+        step(PR + W + K + s)
     ens.sync()
     scan_ms = ens.profile_read()["scan_ms"]
     ens.profile(0)
@@ -227,9 +276,18 @@ def main():
         all_matched = bool(ok.item())
 
     value = E_total * K / elapsed
-    dd_ms = prof["downdate_ms"]
-    launches = max(1, prof["launches"])
-    steps_per_launch = K / launches
+    # launch forms of the timed flushes; the roofline covers the dominant one only
+    forms = {}
+    for ns, ms in flushes:
+        f = forms.setdefault(ns, {"kernel": ens.flush_kernel_name(ns), "steps_per_launch": ns,
+                                  "launches": 0, "total_ms": 0.0})
+        f["launches"] += 1
+        f["total_ms"] += ms
+    for f in forms.values():
+        f["avg_ms"] = f["total_ms"] / f["launches"]
+    dom = max(forms.values(), key=lambda f: f["total_ms"]) if forms else None
+    dd_ms = dom["avg_ms"] if dom else prof["downdate_ms"]
+    steps_per_launch = dom["steps_per_launch"] if dom else args.flush_interval
     alg_bytes = E * n * (n + 1) * bpe   # one read + write of the packed block per flush
     alg_flops = steps_per_launch * E * 2 * L_LINES * n * (n + 1)
     mfma_peak = MFMA_F64_PEAK_TFS if prec == ekf.PREC_F64 else MFMA_F32_PEAK_TFS   # f16 storage: f32 MFMA
@@ -238,18 +296,11 @@ def main():
     bound = "hbm" if t_hbm >= t_mfma else "mfma"
     gbs = alg_bytes / (dd_ms * 1e-3) / 1e9 if dd_ms > 0 else None
     tfs = alg_flops / (dd_ms * 1e-3) / 1e12 if dd_ms > 0 else None
-    traffic = None
-    traffic_src = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if (tj.get("capacity") == N and tj.get("instances") == E and tj.get("precision") == args.precision
-                    and tj.get("flush_interval") == args.flush_interval
-                    and tj.get("pipeline") == bool(args.pipeline)):
-                traffic = tj.get("hbm_bytes_per_launch")
-                traffic_src = os.path.relpath(args.traffic_json, ROOT)
-        except Exception:
-            traffic = None
+    sha = lib_sha(ekf.LIB_PATH)
+    tj, traffic_src = find_traffic(args.traffic_json, sha, {
+        "capacity": N, "instances": E, "precision": args.precision, "flush_interval": args.flush_interval,
+        "pipeline": bool(args.pipeline), "kernel": dom["kernel"] if dom else None})
+    traffic = tj.get("hbm_bytes_per_launch") if tj else None
 
     out = {
         "metric": METRIC,
@@ -271,8 +322,9 @@ def main():
             "lines_per_scan": L_LINES,
             "parallelism": (f"ensemble x{world} ({'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} "
                             f"broadcast of {B} scans per collective)") if world > 1 else "ensemble x1",
-            "pipeline": bool(args.pipeline), "flush_interval": args.flush_interval,
+                "pipeline": bool(args.pipeline), "flush_interval": args.flush_interval,
         },
+        "clock_preroll_steps": PR,
         "roofline": {
             "bound": bound,
             "achieved": gbs if bound == "hbm" else tfs,
@@ -280,7 +332,8 @@ def main():
             "unit": "GB/s" if bound == "hbm" else "TFLOP/s",
             "frac": ((gbs / HBM_PEAK_GBS) if bound == "hbm" else (tfs / mfma_peak)) if dd_ms > 0 else None,
             "traffic": traffic,
-            "kernel": flush_kernel_name(prec, args.flush_interval),
+            "kernel": dom["kernel"] if dom else None,
+            "launch_forms": sorted(forms.values(), key=lambda f: -f["total_ms"]),
             "alg_bytes_per_launch": alg_bytes,
             "alg_flops_per_launch": alg_flops,
             "steps_per_launch": steps_per_launch,
@@ -288,6 +341,7 @@ def main():
             "mfma_tflops": tfs, "mfma_frac": (tfs / mfma_peak) if tfs else None,
             "ideal_ms": max(t_hbm, t_mfma) * 1e3,
             "traffic_source": traffic_src,
+            "lib_sha": sha,
         },
         "kernel_ms": {"scan": scan_ms, "flush": dd_ms, "flush_launches": prof["launches"]},
         "all_lines_matched": all_matched,
@@ -302,7 +356,8 @@ def main():
         # identical inputs: instance 0 restarted from the state it stores (fp32-rounded P0)
         ens.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
         P0, y0, s0, pose0 = ens.download_state(0)
-        ref = O.OracleRobot(N, mode=O.FAST)
+        ref = O.OracleRobot(N, mode=O.FAST, omp=True)
+        cores = O.threads(True)
         ref.set_state(P0, y0, s0, pose0)
         del P0
         host = payload.cpu().numpy()
@@ -333,14 +388,21 @@ def main():
                 del Pg
             if t_cpu >= args.cpu_seconds or scans >= steps_total:
                 break
+        b0 = reference_path_baseline(N)
         out["cpu_baseline"] = {
-            "value": scans / t_cpu, "unit": "updates/s", "cores": 1, "kind": "port",
-            "sample": f"{scans} consecutive scans of instance 0 (N={N}, L=m={L_LINES}) through "
+            "value": scans / t_cpu, "unit": "updates/s", "cores": cores, "kind": "port",
+            "sample": f"B1: {scans} consecutive scans of instance 0 (N={N}, L=m={L_LINES}) through "
                       f"oracle/ekf_oracle.c fast mode (fp64, sparse predict/gating, dense O(n^2) "
-                      f"update per match), {t_cpu:.1f} s",
+                      f"update per match), OpenMP build on {cores} host threads, {t_cpu:.1f} s",
+            "reference_path": ({"name": "B0: faithful GSL-order restatement (n^3 predict, dense "
+                                        "H·P·Hᵀ per candidate), 1 core", "value": b0["updates_per_s"],
+                                "unit": "updates/s", "cores": 1, "host": b0.get("host_cpu"),
+                                "source": b0["source"]} if b0 else None),
         }
         out["parity"] = parity
         out["speedup_vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
+        if b0:
+            out["speedup_vs_reference_path"] = value / b0["updates_per_s"]
 
     if rank == 0:
         print(json.dumps(out))

@@ -137,9 +137,14 @@ int ekf_init_lowrank(ekf_ctx* ctx, int e, const double* diag, const double* U, i
                      const double* y, int saved, const double pose[3]);
 /* P_t0[0:3,0:3] of instance e (what getEllipse reads, Robot.cpp:75-77). */
 int ekf_get_pose_cov(ekf_ctx* ctx, int e, double P33[9]);
-/* Robot::getEllipse(axii, angle) (Robot.h:73, Robot.cpp:73-124). Returns 1 on success, 0 if
- * the 2x2 eigenproblem failed (as the reference's bool), negative on API error. */
+/* Robot::getEllipse(axii, angle) (Robot.h:73, Robot.cpp:73-124): axii sorted by |eigenvalue|,
+ * angle = atan2 of the larger eigenvalue's unit eigenvector in GSL's sign convention. Returns 1
+ * on success, 0 if the 2x2 eigenproblem failed (as the reference's bool), negative on API error. */
 int ekf_get_ellipse(ekf_ctx* ctx, int e, float axii[2], float* angle);
+/* The same computation on a given 2x2 block P22 = {P00, P01, P10, P11} (host only, no device):
+ * gsl_eigen_nonsymmv + GSL_EIGEN_SORT_ABS_ASC restated (sign convention included). Returns 1,
+ * 0 for a non-finite block or a complex eigenvalue pair, negative on API error. */
+int ekf_ellipse_of_block(const double P22[4], float axii[2], float* angle);
 
 /* Introspection for the benchmark's roofline accounting. */
 size_t ekf_landmark_block_bytes(const ekf_ctx* ctx); /* stored bytes of P_ll per instance */
@@ -152,6 +157,11 @@ int ekf_state_dim(const ekf_ctx* ctx);                /* n */
 int ekf_profile_enable(ekf_ctx* ctx, int enable);
 int ekf_profile_read(ekf_ctx* ctx, double* scan_ms, double* downdate_ms, double* augment_ms,
                      int* launches);
+/* Per-launch flush timing of the launches recorded since the last enable (level >= 1): fills
+ * nsteps[k] (steps the launch applied) and ms[k] for k < min(cap, count); returns the count
+ * (negative on error). ekf_flush_kernel_name: the kernel form a flush of nsteps steps runs. */
+int ekf_profile_flushes(ekf_ctx* ctx, int cap, int* nsteps, float* ms);
+const char* ekf_flush_kernel_name(const ekf_ctx* ctx, int nsteps);
 /* Diagnostic: association-kernel phase timers (sum over instances, 100 MHz ticks), collected
  * only when the environment had EKF_SCAN_STAMPS=1 at ekf_create. Slots: 0 predict, 1 diagonal
  * gather + barrier, 2 gating, 3 min-reduction barrier, 4 winner package, 5 broadcast barrier,

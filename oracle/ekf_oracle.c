@@ -13,6 +13,16 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* B1 "fast" baseline on all host cores: built a second time with -fopenmp (libekf_oracle_omp.so,
+ * BASELINE.md §2). Every element is still computed by one thread with the same operation order,
+ * so the threaded build returns bit-identical results; only the O(n²) loops are split by rows. */
+#ifdef _OPENMP
+#include <omp.h>
+#define ORACLE_PAR_ROWS _Pragma("omp parallel for schedule(static)")
+#else
+#define ORACLE_PAR_ROWS
+#endif
+
 #ifndef M_PI
 #define M_PI 3.14159265358979323846
 #endif
@@ -197,6 +207,20 @@ int oracle_n(const oracle_robot* o) { return o->n; }
 int oracle_capacity(const oracle_robot* o) { return o->N; }
 int oracle_saved(const oracle_robot* o) { return o->saved; }
 int oracle_status(const oracle_robot* o) { return o->status; }
+int oracle_threads(void)
+{
+#ifdef _OPENMP
+    int t = 1;
+#pragma omp parallel
+    {
+#pragma omp single
+        t = omp_get_num_threads();
+    }
+    return t;
+#else
+    return 1;
+#endif
+}
 void oracle_pose(const oracle_robot* o, double pose[3]) { memcpy(pose, o->pose, 3 * sizeof(double)); }
 double* oracle_P(oracle_robot* o) { return o->P; }
 double* oracle_y(oracle_robot* o) { return o->y; }
@@ -251,8 +275,10 @@ static void predict_fast(oracle_robot* o, const double F3[9], const double Fu3[9
     const int n = o->n;
     const double* P = o->P;
     double* Pp = o->P_pre;
-    memcpy(Pp, P, sizeof(double) * (size_t)n * n);
+    ORACLE_PAR_ROWS
+    for (int r = 0; r < n; r++) memcpy(Pp + (size_t)r * n, P + (size_t)r * n, sizeof(double) * (size_t)n);
     /* rows 0..2: (Fx·P)[a][b] = Σ_k F3[a][k] P[k][b]; cols 0..2 by the transposed product. */
+    ORACLE_PAR_ROWS
     for (int b = 3; b < n; b++) {
         for (int a = 0; a < 3; a++) {
             double s = 0.0;
@@ -426,6 +452,7 @@ int oracle_localize(oracle_robot* o, const oracle_line* lines, int L, const doub
                 /* Robot.cpp:522: P_pre·Hxᵀ (NT), 526: ·S⁻¹ */
                 oracle_dgemm(0, 1, n, 2, n, 1.0, P_pre, n, o->Hs, n, 0.0, W, 2);
             } else {
+                ORACLE_PAR_ROWS
                 for (int r = 0; r < n; r++) {
                     const double* pr = P_pre + (size_t)r * n;
                     W[2 * r + 0] = -1.0 * pr[2] + 1.0 * pr[l0] + 0.0 * pr[l1];
@@ -441,6 +468,7 @@ int oracle_localize(oracle_robot* o, const oracle_line* lines, int L, const doub
                 oracle_dgemm(0, 1, n, n, 2, 1.0, KS, 2, K, 2, 0.0, KSK, n);
                 for (size_t e = 0; e < (size_t)n * n; e++) P_pre[e] -= KSK[e];
             } else {
+                ORACLE_PAR_ROWS
                 for (int r = 0; r < n; r++) {
                     const double a0 = KS[2 * r], a1 = KS[2 * r + 1];
                     double* pr = P_pre + (size_t)r * n;
@@ -482,7 +510,8 @@ int oracle_localize(oracle_robot* o, const oracle_line* lines, int L, const doub
         o->pose[2] = oracle_normalize_radian(y[2]);
     }
     /* P_t0 ← P_pre (Robot.cpp:572 per match / :713 no match) */
-    memcpy(P, P_pre, sizeof(double) * (size_t)n * n);
+    ORACLE_PAR_ROWS
+    for (int r = 0; r < n; r++) memcpy(P + (size_t)r * n, P_pre + (size_t)r * n, sizeof(double) * (size_t)n);
 
     /* augmentation (Robot.cpp:776-866) */
     for (int e = 0; e < nextra; e++) {
@@ -522,6 +551,7 @@ int oracle_localize(oracle_robot* o, const oracle_line* lines, int L, const doub
     if (o->saved > N - 10) {
         o->saved = 0;
         for (int i = 3; i < n; ++i) y[i] = 0;
+        ORACLE_PAR_ROWS
         for (int i = 0; i < n; i++)
             for (int j = 0; j < n; j++)
                 if (i >= 3 || j >= 3) P[(size_t)i * n + j] = 0.0;

@@ -60,7 +60,9 @@ int oracle_localize(oracle_robot* o, const oracle_line* lines, int L, const doub
 int oracle_n(const oracle_robot* o);
 int oracle_capacity(const oracle_robot* o);
 int oracle_saved(const oracle_robot* o);
-int oracle_status(const oracle_robot* o);   /* OR of GSL-like error codes seen in last call */
+int oracle_status(const oracle_robot* o);
+/* threads the O(n^2) loops run on: 1 in libekf_oracle.so, the OpenMP team in libekf_oracle_omp.so */
+int oracle_threads(void);   /* OR of GSL-like error codes seen in last call */
 void oracle_pose(const oracle_robot* o, double pose[3]);
 double* oracle_P(oracle_robot* o);          /* n*n row-major P_t0 (Robot.h:62) */
 double* oracle_y(oracle_robot* o);          /* n state vector y (Robot.h:26) */

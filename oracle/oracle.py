@@ -16,7 +16,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "libekf_oracle.so")
-_lib = None
+_OMP_PATH = os.path.join(_HERE, "libekf_oracle_omp.so")   # same source, -fopenmp (B1 baseline)
+_libs = {}
 
 FAITHFUL, FAST = 0, 1
 R_INTENDED, R_AS_WRITTEN = 0, 1
@@ -32,12 +33,14 @@ def build() -> str:
     return _LIB_PATH
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(_LIB_PATH):
+def lib(omp: bool = False):
+    """The restatement (single-threaded), or its OpenMP build (bit-identical, all host cores;
+    OMP_NUM_THREADS sets the team) with omp=True."""
+    if omp not in _libs:
+        path = _OMP_PATH if omp else _LIB_PATH
+        if not os.path.exists(path):
             build()
-        L = ctypes.CDLL(_LIB_PATH)
+        L = ctypes.CDLL(path)
         vp, i, d = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
         dp = ctypes.POINTER(ctypes.c_double)
         L.oracle_create.restype = vp
@@ -59,8 +62,14 @@ def lib():
         L.oracle_lu_invert2.argtypes = [dp, dp]
         L.oracle_normalize_radian.restype = d
         L.oracle_normalize_radian.argtypes = [d]
-        _lib = L
-    return _lib
+        L.oracle_threads.restype = i
+        L.oracle_threads.argtypes = []
+        _libs[omp] = L
+    return _libs[omp]
+
+
+def threads(omp: bool = True) -> int:
+    return lib(omp).oracle_threads()
 
 
 def _dp(a: np.ndarray):
@@ -83,8 +92,8 @@ class OracleRobot:
     """CPU restatement of `Robot` (Robot.h:21-77) with runtime capacity N."""
 
     def __init__(self, capacity: int, x: float = 0.0, y: float = 0.0, theta: float = 0.0,
-                 mode: int = FAST, r_mode: int = R_INTENDED):
-        self._lib = lib()
+                 mode: int = FAST, r_mode: int = R_INTENDED, omp: bool = False):
+        self._lib = lib(omp)
         self._h = self._lib.oracle_create(int(capacity), x, y, theta, int(mode), int(r_mode))
         if not self._h:
             raise MemoryError("oracle_create failed")
@@ -172,3 +181,135 @@ def lu_invert2(S: np.ndarray):
 
 def normalize_radian(x: float) -> float:
     return lib().oracle_normalize_radian(float(x))
+
+
+# ---- Robot::getEllipse (Robot.cpp:73-124) ---------------------------------------------------
+# GSL is not vendored (system libgsl, version unpinned: slam_ros/CMakeLists.txt:43-51). This
+# restates, in Python floats (IEEE double, one operation per statement), the published GSL
+# algorithm the reference calls: gsl_eigen_nonsymmv (gsl/eigen/nonsymmv.c; default workspace
+# parameters: Schur vectors on, no balancing) on the 2x2 block, gsl_eigen_nonsymmv_sort with
+# GSL_EIGEN_SORT_ABS_ASC, then axii[i] = 2·sqrt(5.991·|Re λ_i|) and
+# angle = atan2(Re z1, Re z2) of the eigenvector of the larger |λ| (Robot.cpp:100-112).
+_DBL_EPS = 2.220446049250313e-16
+_DBL_MIN = 2.2250738585072014e-308
+
+
+def _gsl_sign(x):
+    return 1.0 if x >= 0.0 else -1.0
+
+
+def _gsl_hypot(x, y):
+    xa, ya = abs(x), abs(y)
+    mn, mx = (xa, ya) if xa < ya else (ya, xa)
+    if mn == 0.0:
+        return mx
+    u = mn / mx
+    return mx * float(np.sqrt(1.0 + u * u))
+
+
+def _dnrm2(xs):
+    # gslcblas source_nrm2_r.h: scaled sum of squares
+    scale, ssq = 0.0, 1.0
+    for x in xs:
+        if x != 0.0:
+            ax = abs(x)
+            if scale < ax:
+                ssq = 1.0 + ssq * (scale / ax) * (scale / ax)
+                scale = ax
+            else:
+                ssq += (ax / scale) * (ax / scale)
+    return scale * float(np.sqrt(ssq))
+
+
+def _francis_standardize(a, b, c, d):
+    """gsl/eigen/francis.c francis_schur_standardize (LAPACK dlanv2): Schur form of a 2x2 block
+    [a b; c d] = Z [a' b'; c' d'] Zᵀ, Z = [[cs, -sn], [sn, cs]]."""
+    sq = lambda v: float(np.sqrt(v))
+    if c == 0.0:
+        cs, sn = 1.0, 0.0
+    elif b == 0.0:
+        cs, sn = 0.0, 1.0
+        a, d = d, a
+        b, c = -c, 0.0
+    elif (a - d) == 0.0 and _gsl_sign(b) != _gsl_sign(c):
+        cs, sn = 1.0, 0.0
+    else:
+        tmp = a - d
+        p = 0.5 * tmp
+        bcmax = max(abs(b), abs(c))
+        bcmis = min(abs(b), abs(c)) * _gsl_sign(b) * _gsl_sign(c)
+        scale = max(abs(p), bcmax)
+        z = (p / scale) * p + (bcmax / scale) * bcmis
+        if z >= 4.0 * _DBL_EPS:
+            z = p + _gsl_sign(p) * abs(sq(scale) * sq(z))
+            a = d + z
+            d -= (bcmax / z) * bcmis
+            tau = _gsl_hypot(c, z)
+            cs = z / tau
+            sn = c / tau
+            b -= c
+            c = 0.0
+        else:
+            sigma = b + c
+            tau = _gsl_hypot(sigma, tmp)
+            cs = sq(0.5 * (1.0 + abs(sigma) / tau))
+            sn = -(p / (tau * cs)) * _gsl_sign(sigma)
+            aa, bb = a * cs + b * sn, -a * sn + b * cs
+            cc, dd = c * cs + d * sn, -c * sn + d * cs
+            a, b = aa * cs + cc * sn, bb * cs + dd * sn
+            c, d = -aa * sn + cc * cs, -bb * sn + dd * cs
+            tmp = 0.5 * (a + d)
+            a = d = tmp
+            if c != 0.0:
+                if b != 0.0:
+                    if _gsl_sign(b) == _gsl_sign(c):
+                        sab, sac = sq(abs(b)), sq(abs(c))
+                        p = _gsl_sign(c) * abs(sab * sac)
+                        tau = 1.0 / sq(abs(b + c))
+                        a, d = tmp + p, tmp - p
+                        b -= c
+                        c = 0.0
+                        cs1, sn1 = sab * tau, sac * tau
+                        tmp = cs * cs1 - sn * sn1
+                        sn = cs * sn1 + sn * cs1
+                        cs = tmp
+                else:
+                    b, c = -c, 0.0
+                    cs, sn = -sn, cs
+    return a, b, c, d, cs, sn
+
+
+def gsl_ellipse(P22):
+    """(ok, [axii0, axii1], angle) as float32 values, for P22 = (P00, P01, P10, P11)."""
+    P00, P01, P10, P11 = (float(v) for v in np.asarray(P22, dtype=np.float64).reshape(4))
+    if not all(np.isfinite([P00, P01, P10, P11])):
+        return False, None, None
+    a, b, c, d, cs, sn = _francis_standardize(P00, P01, P10, P11)
+    if c != 0.0:
+        return False, None, None      # complex pair (not from a symmetric covariance)
+    # right eigenvectors of [a b; 0 d]: x = (1, 0) for a; x = (-b / (a - d), 1) for d
+    # (gsl_schur_solve_equation, denominator floored at smin), v = Z x (gslcblas dgemv: y = Z[:,1]
+    # then y += Z[:,0]·x0), max-norm scaling, then unit 2-norm (nonsymmv_normalize_eigenvectors)
+    smin = max(_DBL_EPS * abs(d), _DBL_MIN * (2 / _DBL_EPS))
+    den = a - d
+    if abs(den) < smin:
+        den = smin
+    x0 = -b / den
+    vecs = [[cs, sn], [-sn + x0 * cs, cs + x0 * sn]]
+    for v in vecs:
+        emax = max(abs(v[0]), abs(v[1]))
+        if emax > 0.0:
+            r = 1.0 / emax
+            v[0] *= r
+            v[1] *= r
+        nr = _dnrm2(v)
+        if nr > 0.0:
+            s = 1.0 / nr
+            v[0] *= s
+            v[1] *= s
+    lam = [a, d]
+    order = [1, 0] if abs(lam[1]) < abs(lam[0]) else [0, 1]
+    axii = [float(np.float32(2.0) * np.float32(np.sqrt(5.991 * abs(lam[i])))) for i in order]
+    big = vecs[order[1]]
+    angle = float(np.float32(np.arctan2(big[0], big[1])))
+    return True, axii, angle

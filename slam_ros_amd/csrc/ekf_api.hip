@@ -92,6 +92,7 @@ struct ekf_ctx {
     // profiling
     int prof;
     std::vector<EvPair> ev[3];   // scan, downdate, patch
+    std::vector<int> ev_nsteps;  // steps applied by each timed flush (ev[1])
     std::vector<EvPair> pool;
 };
 
@@ -373,13 +374,27 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         if (dd_per_cu < 1) dd_per_cu = 1;
         c->dd_grid = prop.multiProcessorCount * dd_per_cu;
         c->ncu = prop.multiProcessorCount;
+        // test hook: force one of the bit-identical flush forms (tests/test_gpu_parity.py)
         c->dd_variant = getenv("EKF_FLUSH_VARIANT") ? atoi(getenv("EKF_FLUSH_VARIANT")) : 0;
-        // all G workgroups of an instance must be co-resident (they exchange per line): bound
-        // the instances per association launch by the occupancy the hardware admits, less one
-        // workgroup per CU of margin (MI355X_MICROARCH.md: the API can over-report by one)
+        if (c->dd_variant != 2 && c->dd_variant != 8) c->dd_variant = 0;
+        // all G workgroups of an instance must be co-resident (they exchange per line). A plain
+        // launch gets the same residency as a cooperative one for the same grid
+        // (cdna_hip_programming.md §1; the cooperative form only adds a launch-time check of the
+        // same occupancy query, which can over-report, for ≈17 µs per launch), so the grid is
+        // sized from a bound that cannot over-report: the LDS the kernel declares (one block per
+        // CU at 128 KB of 160 KB), capped by the occupancy query less one block of margin when
+        // the query allows more than one.
         int per_cu = ekf::scan_blocks_per_cu(cfg->precision);
         if (per_cu > 1) per_cu -= 1;
-        if (per_cu < 1) per_cu = 1;
+        const size_t lds = ekf::scan_lds_bytes(cfg->precision);
+        if (lds > 0 && prop.maxSharedMemoryPerMultiProcessor > 0) {
+            const int by_lds = (int)(prop.maxSharedMemoryPerMultiProcessor / lds);
+            if (by_lds < per_cu) per_cu = by_lds;
+        }
+        if (per_cu < 1) {
+            rc = EKF_EINVAL;
+            goto fail;
+        }
         const int resident = prop.multiProcessorCount * per_cu;
         c->scan_batch = resident / c->G;
         if (c->scan_batch < 1) {
@@ -541,10 +556,15 @@ static int enqueue_flush(ekf_ctx* c)
     dp.Pin = c->X[in];
     dp.Pout = c->X[out];
     EvPair* pr = prof_begin(c, 1, fs);
+    if (pr) c->ev_nsteps.push_back(nst);
     HIP_TRY(ekf::launch_downdate(dp, c->cfg.precision, c->dd_grid, fs));
     prof_end(c, pr, fs);
     hipEvent_t ev = c->ev_flush[c->nflush & 1];
     if (c->cfg.pipeline) HIP_TRY(hipEventRecord(ev, fs));
+    // an instance spread over several cooperating workgroups spins on its peers: serialise its
+    // association kernels after the flush in flight, so that no flush workgroup ever holds the
+    // CUs its peers wait for (single-workgroup instances overlap freely)
+    if (c->cfg.pipeline && c->G > 1) HIP_TRY(hipStreamWaitEvent(c->stream, ev, 0));
     if (c->cfg.pipeline) {
         // next scans read X[in] (= output of the previous flush) with both groups pending
         c->base = in;
@@ -794,42 +814,182 @@ extern "C" int ekf_get_pose_cov(ekf_ctx* c, int e, double P33[9])
     return EKF_OK;
 }
 
+// ---- Robot::getEllipse (Robot.cpp:73-124) on the 2×2 pose block -------------------------
+// The reference calls gsl_eigen_nonsymmv on [[P00, P01], [P10, P11]] (GSL is not vendored and its
+// version is unpinned, CMakeLists.txt:43-51), sorts with GSL_EIGEN_SORT_ABS_ASC and publishes
+// atan2(Re v0, Re v1) of the eigenvector of the larger |λ|. Restated from GSL's published
+// algorithm (gsl/eigen/nonsymmv.c with its defaults: no balancing; gsl/eigen/francis.c):
+//   * a 2×2 matrix is already Hessenberg (Z = I); the Francis QR of a 2×2 block is the
+//     standardisation francis_schur_standardize (LAPACK dlanv2): [a b; c d] = Z [a' b'; 0 d'] Zᵀ
+//     with Z = [[cs, -sn], [sn, cs]] (gsl_blas_drot applied to the columns of I);
+//   * right eigenvectors of the Schur form by back substitution, x = (1, 0) for a' and
+//     x = (-b'/(a'-d'), 1) for d' (denominator floored at smin), back-transformed v = Z·x and
+//     scaled to unit 2-norm (gslcblas dnrm2) — positive scalings only, so the sign is Z's;
+//   * eigenvalues in diagonal order (a', d'), then sorted by |λ| ascending (selection sort,
+//     ties keep their order).
+// A complex pair (c' != 0: not produced by a symmetric covariance block) returns 0.
+namespace {
+inline double gsl_sign(double x) { return x >= 0.0 ? 1.0 : -1.0; }
+
+inline double gsl_hypot_(double x, double y)
+{
+    const double xa = fabs(x), ya = fabs(y);
+    const double mn = xa < ya ? xa : ya, mx = xa < ya ? ya : xa;
+    if (mn == 0.0) return mx;
+    const double u = mn / mx;
+    return mx * sqrt(1.0 + u * u);
+}
+
+inline double cblas_dnrm2_2(double x0, double x1)
+{
+    double scale = 0.0, ssq = 1.0;
+    const double xs[2] = {x0, x1};
+    for (int i = 0; i < 2; i++) {
+        if (xs[i] != 0.0) {
+            const double ax = fabs(xs[i]);
+            if (scale < ax) {
+                ssq = 1.0 + ssq * (scale / ax) * (scale / ax);
+                scale = ax;
+            } else {
+                ssq += (ax / scale) * (ax / scale);
+            }
+        }
+    }
+    return scale * sqrt(ssq);
+}
+
+int gsl_ellipse_2x2(const double P[4], float axii[2], float* angle)
+{
+    for (int k = 0; k < 4; k++)
+        if (!isfinite(P[k])) return 0;
+    double a = P[0], b = P[1], c = P[2], d = P[3];
+    double cs, sn;
+    const double eps = 2.220446049250313e-16;   // GSL_DBL_EPSILON
+    if (c == 0.0) {
+        cs = 1.0;
+        sn = 0.0;
+    } else if (b == 0.0) {
+        cs = 0.0;
+        sn = 1.0;
+        const double t = d;
+        d = a;
+        a = t;
+        b = -c;
+        c = 0.0;
+    } else if ((a - d) == 0.0 && gsl_sign(b) != gsl_sign(c)) {
+        cs = 1.0;
+        sn = 0.0;
+    } else {
+        const double tmp = a - d;
+        double p = 0.5 * tmp;
+        const double bcmax = fmax(fabs(b), fabs(c));
+        const double bcmis = fmin(fabs(b), fabs(c)) * gsl_sign(b) * gsl_sign(c);
+        const double scale = fmax(fabs(p), bcmax);
+        double z = (p / scale) * p + (bcmax / scale) * bcmis;
+        if (z >= 4.0 * eps) {
+            z = p + gsl_sign(p) * fabs(sqrt(scale) * sqrt(z));
+            a = d + z;
+            d -= (bcmax / z) * bcmis;
+            const double tau = gsl_hypot_(c, z);
+            cs = z / tau;
+            sn = c / tau;
+            b -= c;
+            c = 0.0;
+        } else {
+            const double sigma = b + c;
+            const double tau = gsl_hypot_(sigma, tmp);
+            cs = sqrt(0.5 * (1.0 + fabs(sigma) / tau));
+            sn = -(p / (tau * cs)) * gsl_sign(sigma);
+            const double aa = a * cs + b * sn, bb = -a * sn + b * cs;
+            const double cc = c * cs + d * sn, dd = -c * sn + d * cs;
+            a = aa * cs + cc * sn;
+            b = bb * cs + dd * sn;
+            c = -aa * sn + cc * cs;
+            d = -bb * sn + dd * cs;
+            const double t2 = 0.5 * (a + d);
+            a = d = t2;
+            if (c != 0.0) {
+                if (b != 0.0) {
+                    if (gsl_sign(b) == gsl_sign(c)) {
+                        const double sab = sqrt(fabs(b)), sac = sqrt(fabs(c));
+                        p = gsl_sign(c) * fabs(sab * sac);
+                        const double tau2 = 1.0 / sqrt(fabs(b + c));
+                        a = t2 + p;
+                        d = t2 - p;
+                        b -= c;
+                        c = 0.0;
+                        const double cs1 = sab * tau2, sn1 = sac * tau2;
+                        const double t3 = cs * cs1 - sn * sn1;
+                        sn = cs * sn1 + sn * cs1;
+                        cs = t3;
+                    }
+                } else {
+                    b = -c;
+                    c = 0.0;
+                    const double t3 = cs;
+                    cs = -sn;
+                    sn = t3;
+                }
+            }
+        }
+    }
+    if (c != 0.0) return 0;   // complex pair
+    // eigenvectors: Z = [[cs, -sn], [sn, cs]]
+    double v[2][2];
+    v[0][0] = cs;
+    v[0][1] = sn;
+    {
+        const double smlnum = 2.2250738585072014e-308 * (2.0 / eps);
+        const double smin = fmax(eps * fabs(d), smlnum);
+        double den = a - d;
+        if (fabs(den) < smin) den = smin;
+        const double x0 = -b / den;
+        v[1][0] = x0 * cs + (-sn);
+        v[1][1] = x0 * sn + cs;
+    }
+    for (int k = 0; k < 2; k++) {
+        // back substitution ends with a max-norm scaling (as LAPACK dtrevc), the workspace
+        // normalises to unit 2-norm afterwards (nonsymmv_normalize_eigenvectors)
+        const double emax = fmax(fabs(v[k][0]), fabs(v[k][1]));
+        if (emax > 0.0) {
+            const double remax = 1.0 / emax;
+            v[k][0] *= remax;
+            v[k][1] *= remax;
+        }
+        const double nr = cblas_dnrm2_2(v[k][0], v[k][1]);
+        if (nr > 0.0) {
+            const double sc = 1.0 / nr;
+            v[k][0] *= sc;
+            v[k][1] *= sc;
+        }
+    }
+    double lam[2] = {a, d};
+    int ord[2] = {0, 1};
+    if (fabs(lam[1]) < fabs(lam[0])) {
+        ord[0] = 1;
+        ord[1] = 0;
+    }
+    for (int i = 0; i < 2; i++) axii[i] = 2.f * (float)sqrt(5.991 * fabs(lam[ord[i]]));
+    *angle = (float)atan2(v[ord[1]][0], v[ord[1]][1]);
+    return 1;
+}
+}  // namespace
+
+extern "C" int ekf_ellipse_of_block(const double P22[4], float axii[2], float* angle)
+{
+    if (!P22 || !axii || !angle) return -EKF_EINVAL;
+    return gsl_ellipse_2x2(P22, axii, angle);
+}
+
 extern "C" int ekf_get_ellipse(ekf_ctx* c, int e, float axii[2], float* angle)
 {
-    // Robot::getEllipse (Robot.cpp:73-124): eigen-decomposition of P_t0[0:2,0:2], eigenvalues
-    // sorted by |λ| ascending, axii[i] = 2·sqrt(5.991·|λ_i|), angle = atan2(v0, v1) of the
-    // eigenvector of the larger |λ|. GSL's nonsymmv sign convention for the eigenvector is not
-    // reproducible without GSL: here each eigenvector is unit-norm with its first non-zero
-    // component positive (angle parity is therefore modulo π).
+    // Robot::getEllipse (Robot.cpp:73-124) on P_t0[0:2, 0:2] of instance e (see above)
     if (!c || !axii || !angle) return -EKF_EINVAL;
     double P33[9];
     int rc = ekf_get_pose_cov(c, e, P33);
     if (rc) return -rc;
-    const double a = P33[0], b = P33[1], cc = P33[3], dd = P33[4];
-    if (!isfinite(a) || !isfinite(b) || !isfinite(cc) || !isfinite(dd)) return 0;
-    const double tr = 0.5 * (a + dd);
-    const double disc = 0.25 * (a - dd) * (a - dd) + b * cc;
-    if (disc < 0) return 0;   // complex pair: not produced by a covariance block
-    const double sq = sqrt(disc);
-    double lam[2] = {tr - sq, tr + sq};
-    if (fabs(lam[0]) > fabs(lam[1])) {
-        double t = lam[0];
-        lam[0] = lam[1];
-        lam[1] = t;
-    }
-    double vx = 1.0, vy = 0.0;
-    {
-        const double l = lam[1];
-        const double x1 = b, y1 = l - a, x2 = l - dd, y2 = cc;
-        const double n1 = hypot(x1, y1), n2 = hypot(x2, y2);
-        if (n1 >= n2 && n1 > 0) { vx = x1 / n1; vy = y1 / n1; }
-        else if (n2 > 0) { vx = x2 / n2; vy = y2 / n2; }
-        if (vx < 0 || (vx == 0 && vy < 0)) { vx = -vx; vy = -vy; }
-    }
-    axii[0] = 2.f * (float)sqrt(5.991 * fabs(lam[0]));
-    axii[1] = 2.f * (float)sqrt(5.991 * fabs(lam[1]));
-    *angle = (float)atan2(vx, vy);
-    return 1;
+    const double P22[4] = {P33[0], P33[1], P33[3], P33[4]};
+    return gsl_ellipse_2x2(P22, axii, angle);
 }
 
 extern "C" size_t ekf_landmark_block_bytes(const ekf_ctx* c)
@@ -848,6 +1008,7 @@ extern "C" int ekf_profile_enable(ekf_ctx* c, int enable)
         for (auto& pr : v) c->pool.push_back(pr);
         v.clear();
     }
+    c->ev_nsteps.clear();
     c->prof = enable < 0 ? 0 : (enable > 2 ? 2 : enable);
     return EKF_OK;
 }
@@ -873,6 +1034,41 @@ extern "C" int ekf_profile_read(ekf_ctx* c, double* scan_ms, double* dd_ms, doub
     if (aug_ms) *aug_ms = avg[2];
     if (launches) *launches = (int)c->ev[1].size();
     return EKF_OK;
+}
+
+extern "C" int ekf_profile_flushes(ekf_ctx* c, int cap, int* nsteps, float* ms)
+{
+    if (!c || cap < 0 || (cap > 0 && (!nsteps || !ms))) return -EKF_EINVAL;
+    if (hipStreamSynchronize(c->stream) != hipSuccess || hipStreamSynchronize(c->dstream) != hipSuccess)
+        return -EKF_EDEVICE;
+    const int n = (int)c->ev[1].size();
+    for (int k = 0; k < n && k < cap; k++) {
+        float t = 0.f;
+        if (hipEventElapsedTime(&t, c->ev[1][k].a, c->ev[1][k].b) != hipSuccess) return -EKF_EDEVICE;
+        ms[k] = t;
+        nsteps[k] = k < (int)c->ev_nsteps.size() ? c->ev_nsteps[k] : 0;
+    }
+    return n;
+}
+
+extern "C" const char* ekf_flush_kernel_name(const ekf_ctx* c, int nsteps)
+{
+    if (!c || nsteps < 1) return "";
+    if (c->cfg.precision == EKF_PREC_F64) return "downdate_f64_kernel";
+    const bool half = c->cfg.precision == EKF_PREC_F16;
+    const bool wave = nsteps >= 2 && nsteps <= 8 && nsteps % 2 == 0 && c->d.kmax <= 16 &&
+                      (nsteps >= 6 || c->dd_variant == 8);
+    if (wave) {
+        static const char* names[2][5] = {
+            {"", "flush_f32_wave_kernel<float, 2>", "flush_f32_wave_kernel<float, 4>",
+             "flush_f32_wave_kernel<float, 6>", "flush_f32_wave_kernel<float, 8>"},
+            {"", "flush_f32_wave_kernel<_Float16, 2>", "flush_f32_wave_kernel<_Float16, 4>",
+             "flush_f32_wave_kernel<_Float16, 6>", "flush_f32_wave_kernel<_Float16, 8>"}};
+        return names[half ? 1 : 0][nsteps / 2];
+    }
+    if (nsteps <= 4 && c->d.kmax <= 16 && c->dd_variant != 2)
+        return half ? "flush_f32_persist2_kernel<_Float16>" : "flush_f32_persist2_kernel<float>";
+    return half ? "flush_f32_sb_kernel<_Float16>" : "flush_f32_sb_kernel<float>";
 }
 
 extern "C" int ekf_debug_scan_stamps(ekf_ctx* c, unsigned long long out[16])

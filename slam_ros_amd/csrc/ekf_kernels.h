@@ -59,7 +59,7 @@ struct alignas(32) WtEntry {
     int rows[2];    // [0]: A row blocks (WT_R × 16 bits), [1]: B row blocks (WT_C × 16 bits)
     int rc;         // wr | wc << 16
 };
-constexpr int DD_SB = 4;   // f32 flush: tiles per super-tile side (one wave per tile row)   // pending steps (2 × flush_interval in pipeline mode)
+constexpr int DD_SB = 4;   // f32 flush: tiles per super-tile side (one wave per tile row)
 
 struct ScanParams {
     Dims d;
@@ -100,7 +100,8 @@ struct DowndateParams {
     Dims d;
     int E;
     int nsteps;
-    int variant;          // f32 flush form: 0 auto, 2 super-tile, 3 persistent 1 WG/CU
+    int variant;          // f32 flush form (tests only, EKF_FLUSH_VARIANT; all bit-identical): 0 auto,
+                          // 2 super-tile form, 8 wave form also for 2 or 4 steps
     int ncu;              // compute units (persistent grid)
     const void* Pin;
     void* Pout;
@@ -115,6 +116,7 @@ struct DowndateParams {
 
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st);
 int scan_blocks_per_cu(int precision);
+size_t scan_lds_bytes(int precision);   // static LDS of the association kernel
 hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st);
 hipError_t launch_pack(const Dims& d, int precision, const double* Pfull, void* Pll, double* Rs,
                        const int2* tile_rc, hipStream_t st);

@@ -2147,16 +2147,8 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_sb_kernel(DowndateParams
         }
 }
 
-// f32 flush, persistent software-pipelined form: one 4-wave workgroup per CU walks a range of
-// super-tiles; while it runs the MFMA chains of super-tile k, the operands and the tiles of
-// super-tile k+1 are already in flight into registers (operands first, tiles second, so that
-// the in-order vmcnt lets the operand wait pass while the tiles still stream). Operands are
-// staged to a double-buffered LDS image once per super-tile (every chunk of the group), one raw
-// barrier per super-tile. All per-super-tile control (instance, super-tile, step records) is
-// wave-uniform and read with scalar loads, so no vector-memory wait sits between issuing the
-// prefetch and the MFMA work. Used when a group has at most PST_MAXC steps and kmax <= 16 (one
-// chunk per step); otherwise flush_f32_sb_kernel runs. Per element the chain is the same as in
-// the other forms: bit-identical results.
+// Groups of at most PST_MAXC steps with kmax <= 16 (one operand chunk per step) run the
+// persistent form below; otherwise flush_f32_sb_kernel runs.
 constexpr int PST_MAXC = 4;
 
 // scalar (constant address space) load of a wave-uniform word that no kernel of this launch
@@ -2165,209 +2157,6 @@ template <typename T>
 __device__ __forceinline__ T sload(const T* ptr)
 {
     return *(const __attribute__((address_space(4))) T*)(ptr);
-}
-
-struct PstInfo {
-    int e, sbi, sbj;
-    int reset[PST_MAXC], ks[PST_MAXC], nadd[PST_MAXC], s0[PST_MAXC];
-};
-
-__device__ __forceinline__ void pst_info(const DowndateParams& p, int gg, int nst, PstInfo& t)
-{
-    t.e = __builtin_amdgcn_readfirstlane(gg / nst);
-    const int li = __builtin_amdgcn_readfirstlane(gg - t.e * nst);
-    const int* rc = reinterpret_cast<const int*>(p.stile_rc + li);
-    t.sbi = sload(rc);
-    t.sbj = sload(rc + 1);
-#pragma unroll
-    for (int q = 0; q < PST_MAXC; q++) {
-        t.reset[q] = 0;
-        t.ks[q] = 0;
-        t.nadd[q] = 0;
-        t.s0[q] = 0;
-        if (q < p.nsteps) {
-            const int* r = p.steps[q].res + (size_t)t.e * RES_STRIDE;
-            t.reset[q] = sload(r + RES_RESET);
-            t.ks[q] = t.reset[q] ? 0 : sload(r + RES_KSTEPS);
-            t.nadd[q] = sload(r + RES_NADD);
-            t.s0[q] = sload(r + RES_SAVED_IN);
-        }
-    }
-}
-
-template <typename TS>
-__global__ __launch_bounds__(DD_THREADS) void flush_f32_persist_kernel(DowndateParams p)
-{
-    const Dims d = p.d;
-    const int nsb = (d.nb + DD_SB - 1) / DD_SB;
-    const int nst = nsb * (nsb + 1) / 2;
-    const int total = p.E * nst;
-    // XCD-aware ranges: workgroup b runs on XCD b mod 8 and walks that XCD's contiguous range
-    const int per = (total + 7) / 8;
-    const int xcd = blockIdx.x & 7;
-    const int wpx = gridDim.x >> 3;
-    const int g_end = min(total, (xcd + 1) * per);
-    int g = xcd * per + (blockIdx.x >> 3);
-    if (g >= g_end) return;
-
-    const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
-    const int kh = d.kmax / 2;
-    const size_t opstride = (size_t)d.nb * 64 * kh;
-    const TS* Pin = reinterpret_cast<const TS*>(p.Pin);
-    TS* Pout = reinterpret_cast<TS*>(p.Pout);
-    // this thread's staging slot: float4 i = tid + 256 j of a chunk
-    auto tile_off = [&](const PstInfo& t, int c, bool& valid) {
-        const int bi = t.sbi * DD_SB + w, bj = t.sbj * DD_SB + c;
-        valid = bi < d.nb && bj < d.nb && bi <= bj;
-        return valid ? ((size_t)t.e * d.ntiles + tile_index(bi, bj, d.nb)) * TILE_ELEMS : (size_t)0;
-    };
-    // unconditional loads (absent steps re-read step 0's operands) keep the prefetched values
-    // in the registers the next iteration reads: no copy, so no early vmcnt(0) at the back edge
-    auto fetch = [&](const PstInfo& t, f32x4 opreg[PST_MAXC][4], f32x4 pref[DD_SB][4]) {
-#pragma unroll
-        for (int c = 0; c < PST_MAXC; c++) {
-            const int qc = t.ks[c] > 0 ? c : 0;
-            const float* U = reinterpret_cast<const float*>(p.steps[qc].Uop) + t.e * opstride;
-            const float* V = reinterpret_cast<const float*>(p.steps[qc].Vop) + t.e * opstride;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int i = threadIdx.x + 256 * j;
-                const int ln = i & 63, s4 = (i >> 6) & 1, blk = (i >> 7) & 3, ab = i >> 9;
-                const int rb = min((ab ? t.sbj : t.sbi) * DD_SB + blk, d.nb - 1);   // past the block: unused
-                opreg[c][j] = *reinterpret_cast<const f32x4*>((ab ? V : U) + ((size_t)rb * 64 + ln) * kh + 4 * s4);
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < DD_SB; c++) {
-            bool v;
-            const TS* tl = Pin + tile_off(t, c, v);
-#pragma unroll
-            for (int qq = 0; qq < 4; qq++) pref[c][qq] = tile_ld(tl, lane, qq);
-        }
-    };
-
-    __shared__ f32x4 lds[2][PST_MAXC][2][DD_SB][2][64];   // 128 KB
-
-    PstInfo cur;
-    pst_info(p, g, nst, cur);
-    f32x4 opreg[PST_MAXC][4];
-    f32x4 pref[DD_SB][4];
-    fetch(cur, opreg, pref);
-    int buf = 0;
-    f32x16 acc[DD_SB];
-
-    while (true) {
-#pragma unroll
-        for (int c = 0; c < PST_MAXC; c++) {
-            if (cur.ks[c] > 0) {
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int i = threadIdx.x + 256 * j;
-                    lds[buf][c][i >> 9][(i >> 7) & 3][(i >> 6) & 1][i & 63] = opreg[c][j];
-                }
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#pragma unroll
-        for (int c = 0; c < DD_SB; c++)
-#pragma unroll
-            for (int qq = 0; qq < 4; qq++) {
-                acc[c][4 * qq + 0] = pref[c][qq][0];
-                acc[c][4 * qq + 1] = pref[c][qq][1];
-                acc[c][4 * qq + 2] = pref[c][qq][2];
-                acc[c][4 * qq + 3] = pref[c][qq][3];
-            }
-        const int gn = g + wpx;
-        const bool more = gn < g_end;
-        PstInfo nxt;
-        pst_info(p, more ? gn : g, nst, nxt);   // the last iteration re-reads its own super-tile
-        fetch(nxt, opreg, pref);
-
-        const int e = cur.e;
-        const int bi = cur.sbi * DD_SB + w;
-        int vmask = 0;
-#pragma unroll
-        for (int c = 0; c < DD_SB; c++) {
-            bool v;
-            (void)tile_off(cur, c, v);
-            vmask |= (int)v << c;
-        }
-        auto post = [&](int q) {
-            if (cur.reset[q]) {
-#pragma unroll
-                for (int c = 0; c < DD_SB; c++)
-#pragma unroll
-                    for (int k = 0; k < 16; k++) acc[c][k] = 0.f;
-                return;
-            }
-            const int nadd = cur.nadd[q], s0 = cur.s0[q];
-            if (nadd <= 0 || (cur.sbj + 1) * DD_SB * 16 <= s0 || cur.sbj * DD_SB * 16 >= s0 + nadd) return;
-            const double* prw0 = p.steps[q].patch + (size_t)e * d.max_lines * 2 * d.M;
-            const double* pdg = p.steps[q].patch_diag + (size_t)e * d.max_lines * 4;
-#pragma nounroll
-            for (int c = 0; c < DD_SB; c++) {
-                const int bj = cur.sbj * DD_SB + c;
-                if (((vmask >> c) & 1) && bj * 16 + 15 >= s0 && bj * 16 < s0 + nadd) {
-                    const int col = bj * 32 + (lane & 31);
-#pragma unroll
-                    for (int k = 0; k < 16; k++) {
-                        const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
-                        const int hi = max(row >> 1, col >> 1);
-                        if (hi >= s0 && hi < s0 + nadd)
-                            acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s0, row, col)));
-                    }
-                }
-                const f32x16 t0 = acc[0];
-                acc[0] = acc[1];
-                acc[1] = acc[2];
-                acc[2] = acc[3];
-                acc[3] = t0;
-            }
-        };
-        // the group's steps in order: a chunk of MFMA k-steps, then the step's rows / reset
-#pragma unroll
-        for (int q = 0; q < PST_MAXC; q++) {
-            if (q >= p.nsteps) break;
-            const int kc = cur.ks[q];
-            if (kc > 0) {
-                const int c = q;
-                const f32x4 a0 = lds[buf][c][0][w][0][lane];
-                const f32x4 a1 = lds[buf][c][0][w][1][lane];
-                f32x4 b0[DD_SB], b1[DD_SB];
-#pragma unroll
-                for (int cc = 0; cc < DD_SB; cc++) {
-                    b0[cc] = lds[buf][c][1][cc][0][lane];
-                    b1[cc] = lds[buf][c][1][cc][1][lane];
-                }
-#pragma unroll
-                for (int s = 0; s < SBK; s++)
-                    if (s < kc) {
-#pragma unroll
-                        for (int cc = 0; cc < DD_SB; cc++)
-                            acc[cc] = __builtin_amdgcn_mfma_f32_32x32x2f32(s < 4 ? a0[s & 3] : a1[s & 3],
-                                                                           s < 4 ? b0[cc][s & 3] : b1[cc][s & 3],
-                                                                           acc[cc], 0, 0, 0);
-                    }
-#pragma unroll
-                for (int cc = 0; cc < DD_SB; cc++) round_acc<TS>(acc[cc]);
-            }
-            post(q);
-        }
-#pragma unroll
-        for (int c = 0; c < DD_SB; c++) {
-            bool v;
-            const size_t off = tile_off(cur, c, v);
-            if (v) {
-#pragma unroll
-                for (int qq = 0; qq < 4; qq++) tile_st(Pout + off, lane, qq, acc[c]);
-            }
-        }
-        if (!more) break;
-        g = gn;
-        cur = nxt;
-        buf ^= 1;
-    }
 }
 
 // f32/f16 flush, persistent 2-workgroups-per-CU form: super-tiles of 4 × 2 tiles (wave w: tile
@@ -2384,10 +2173,8 @@ struct P2Info {
     int flags;   // per step q, byte q: bits 0-3 ks, bit 4 reset, bit 5 augmented rows present
 };
 
-// GLDS: the operands go global → LDS by LDS-DMA (global_load_lds_dwordx4) right after the
-// super-tile's MFMA block, no register staging (48 fewer VGPRs: MINB = 3 workgroups per CU fit)
-template <typename TS, int MINB, bool GLDS>
-__global__ __launch_bounds__(DD_THREADS, MINB) void flush_f32_persist2_kernel(DowndateParams p)
+template <typename TS>
+__global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(DowndateParams p)
 {
     const Dims d = p.d;
     const int nst = p.nstiles2;
@@ -2455,50 +2242,16 @@ __global__ __launch_bounds__(DD_THREADS, MINB) void flush_f32_persist2_kernel(Do
             for (int qq = 0; qq < 4; qq++) pref[c][qq] = tile_ld(tl, lane, qq);
         }
     };
-    auto fetch_tiles = [&](const P2Info& t, f32x4 pref[P2_C][4]) {
-#pragma unroll
-        for (int c = 0; c < P2_C; c++) {
-            bool v;
-            const TS* tl = Pin + tile_off(t, c, v);
-#pragma unroll
-            for (int qq = 0; qq < 4; qq++) pref[c][qq] = tile_ld(tl, lane, qq);
-        }
-    };
-
     __shared__ f32x4 ldsA[PST_MAXC][DD_SB][2][64];   // 32 KB
     __shared__ f32x4 ldsB[PST_MAXC][P2_C][2][64];    // 16 KB
-    // LDS-DMA of a super-tile's operands: per step 3 wave-instructions (A rows rA0, rA1; B row rB)
-    // of 64 lanes × 16 B, each a contiguous 1 KB of the LDS image
-    auto stage = [&](const P2Info& t) {
-        const int rA0 = min(t.sbi * DD_SB + bl, d.nb - 1), rA1 = min(t.sbi * DD_SB + 2 + bl, d.nb - 1);
-        const int rB = min(t.sbj * P2_C + bl, d.nb - 1);
-#pragma unroll
-        for (int c = 0; c < PST_MAXC; c++) {
-            const int qc = ((t.flags >> (8 * c)) & 15) ? c : 0;
-            const float* U = reinterpret_cast<const float*>(p.steps[qc].Uop) + t.e * opstride;
-            const float* V = reinterpret_cast<const float*>(p.steps[qc].Vop) + t.e * opstride;
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(U + (size_t)rA0 * 64 * kh + in_blk),
-                                             (__attribute__((address_space(3))) void*)&ldsA[c][bl][s4][0], 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(U + (size_t)rA1 * 64 * kh + in_blk),
-                                             (__attribute__((address_space(3))) void*)&ldsA[c][2 + bl][s4][0], 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(V + (size_t)rB * 64 * kh + in_blk),
-                                             (__attribute__((address_space(3))) void*)&ldsB[c][bl][s4][0], 16, 0, 0);
-        }
-    };
-
     P2Info cur;
     cur.e = __builtin_amdgcn_readfirstlane(g / nst);
     int li = __builtin_amdgcn_readfirstlane(g - cur.e * nst);
     locate(li, cur);
     load_flags(cur);
-    f32x4 opreg[GLDS ? 1 : PST_MAXC][3];
+    f32x4 opreg[PST_MAXC][3];
     f32x4 pref[P2_C][4];
-    if constexpr (GLDS) {
-        stage(cur);
-        fetch_tiles(cur, pref);
-    } else {
-        fetch(cur, opreg, pref);
-    }
+    fetch(cur, opreg, pref);
     f32x16 acc[P2_C];
     // steady state: every step of the group a full chunk, no reset, no augmented rows
     int steady = 0;
@@ -2506,21 +2259,16 @@ __global__ __launch_bounds__(DD_THREADS, MINB) void flush_f32_persist2_kernel(Do
     for (int q = 0; q < PST_MAXC; q++) steady |= (q < nsteps ? SBK : 0) << (8 * q);
 
     while (true) {
-        if constexpr (GLDS) {
-            // this wave's DMAs (and tiles) have landed; after the barrier, every wave's
-            asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS free
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS free
 #pragma unroll
-            for (int c = 0; c < PST_MAXC; c++) {
-                if ((cur.flags >> (8 * c)) & 15) {
-                    ldsA[c][bl][s4][ln] = opreg[c][0];
-                    ldsA[c][2 + bl][s4][ln] = opreg[c][1];
-                    ldsB[c][bl][s4][ln] = opreg[c][2];
-                }
+        for (int c = 0; c < PST_MAXC; c++) {
+            if ((cur.flags >> (8 * c)) & 15) {
+                ldsA[c][bl][s4][ln] = opreg[c][0];
+                ldsA[c][2 + bl][s4][ln] = opreg[c][1];
+                ldsB[c][bl][s4][ln] = opreg[c][2];
             }
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS written
         }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS written
 #pragma unroll
         for (int c = 0; c < P2_C; c++)
 #pragma unroll
@@ -2545,8 +2293,7 @@ __global__ __launch_bounds__(DD_THREADS, MINB) void flush_f32_persist2_kernel(Do
         }
         locate(lin, nxt);
         load_flags(nxt);
-        if constexpr (GLDS) fetch_tiles(nxt, pref);
-        else fetch(nxt, opreg, pref);
+        fetch(nxt, opreg, pref);
 
         const int e = cur.e;
         const int bi = cur.sbi * DD_SB + w;
@@ -2643,11 +2390,6 @@ __global__ __launch_bounds__(DD_THREADS, MINB) void flush_f32_persist2_kernel(Do
                 post(q);
             }
         }
-        if constexpr (GLDS) {
-            // every wave is done reading the operands: the next super-tile's DMAs may land
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            if (more) stage(nxt);
-        }
 #pragma unroll
         for (int c = 0; c < P2_C; c++) {
             bool v;
@@ -2678,11 +2420,12 @@ __global__ __launch_bounds__(DD_THREADS, MINB) void flush_f32_persist2_kernel(Do
 // (partial downdates are predicated); otherwise the wave runs a plain per-wave-tile loop. Per
 // element the chain is the one every other form runs (k-ordered MFMA steps, fp16 rounding per
 // step, then the step's rows or the reset): bit-identical results.
-template <typename TS, int NS, bool AM = (sizeof(TS) == 2)>
+template <typename TS, int NS>
 __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateParams p)
 {
     static_assert(NS >= 2 && NS % 2 == 0 && NS <= PMAX, "even step count");
     constexpr bool HALF = sizeof(TS) == 2;
+    constexpr bool AM = HALF;   // fp16 storage: pair-major step order (below)
     const Dims d = p.d;
     const int nwt = p.nwt;
     const int total = p.E * nwt;
@@ -2765,7 +2508,6 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
     };
 
     if (fast) {
-        const int dbg = p.variant;   // timing probes only (EKF_FLUSH_VARIANT 81/82: results invalid)
         // raw tile words in flight (fp16 storage: converted when the wave-tile starts)
         using Raw = typename std::conditional<HALF, f16x4, f32x4>::type;
         Raw pref[WT_N][4];
@@ -2834,10 +2576,10 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
                     for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = (float)pref[i][qq][j];
             // the next wave-tile's tiles first: the waits of this wave-tile only cover loads issued
             // during the one before it, so these have the whole wave-tile to land
-            if (more && dbg != 82) load_tiles(nxt);
+            if (more) load_tiles(nxt);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (AM) {
-                // group-major steps (fp16 storage; fp32 opt-in, EKF_FLUSH_VARIANT=83): the
+                // group-major steps (fp16 storage): the
                 // per-step rounding of one group of accumulators runs on the VALU while the other
                 // group's MFMAs run, so it leaves the MFMA stream. Per element the chain is
                 // unchanged (k-ordered step q, then its rounding). Step q's operand registers are
@@ -2865,7 +2607,7 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
                                 const int a = pg * WT_C + (m >> 2), k = 4 * (m & 3);
 #pragma unroll
                                 for (int u = 0; u < 4; u++) acc[a][k + u] = round_step<TS>(acc[a][k + u]);
-                            } else if (dbg != 81) {
+                            } else {
                                 const int a = pg * WT_C + ((m - 8) >> 2), qq = (m - 8) & 3;
                                 if ((cur.w.valid >> a) & 1) tile_st(Pout + tile_ptr(cur, a), lane, qq, acc[a]);
                             }
@@ -2896,7 +2638,6 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
                     for (int k = 0; k < 16; k++) acc[a][k] = round_step<TS>(acc[a][k]);
                 load_half(NS - 1, ldi, NS - 1, 0);
                 load_half(NS - 1, ldi, NS - 1, 1);
-                if (dbg != 81)
 #pragma unroll
                     for (int a = 2; a < 4; a++)
                         if ((cur.w.valid >> a) & 1) {
@@ -2929,7 +2670,7 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
                 __builtin_amdgcn_sched_barrier(0);
             }
             load_half(NS - 1, ldi, NS - 1, 1);
-            if (dbg != 81) store_tiles(cur, acc);
+            store_tiles(cur, acc);
             if (!more) break;
             g += K;
             cur = nxt;
@@ -3224,6 +2965,16 @@ int scan_blocks_per_cu(int precision)
     return err == hipSuccess ? nb : 0;
 }
 
+size_t scan_lds_bytes(int precision)
+{
+    hipFuncAttributes a;
+    hipError_t err =
+        (precision == EKF_PREC_F64) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<double>))
+        : (precision == EKF_PREC_F16) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<_Float16>))
+        : hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<float>));
+    return err == hipSuccess ? a.sharedSizeBytes : 0;
+}
+
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 {
     if (precision == EKF_PREC_F64)
@@ -3246,15 +2997,12 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     // for 2 or 4 steps), 9 keeps the LDS-staged forms
     const bool wave_shape = p.nsteps >= 2 && p.nsteps <= 8 && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
                             p.nwt > 0 && p.wt != nullptr;
-    const bool wave_ok = wave_shape && ((p.variant == 0 && p.nsteps >= 6) || p.variant == 8 ||
-                                        p.variant == 81 || p.variant == 82 || p.variant == 83);
+    const bool wave_ok = wave_shape && (p.nsteps >= 6 || p.variant == 8);
     if (wave_ok) {
         const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
-        const bool am = p.variant == 83;   // fp32 with the accumulator-major step order
 #define EKF_WAVE_CASE(NSV)                                                                              \
     case NSV:                                                                                           \
         if (half) hipLaunchKernelGGL((flush_f32_wave_kernel<_Float16, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, p); \
-        else if (am) hipLaunchKernelGGL((flush_f32_wave_kernel<float, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, st, p); \
         else hipLaunchKernelGGL((flush_f32_wave_kernel<float, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, p);         \
         break;
         switch (p.nsteps) {
@@ -3266,43 +3014,12 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
 #undef EKF_WAVE_CASE
         return hipGetLastError();
     }
-    const bool persist_ok = p.nsteps <= PST_MAXC && p.d.kmax <= 16 && p.variant != 2;
-    if (persist_ok && p.variant == 4) {
-        const int pgrid = 24 * ((p.ncu + 7) / 8);   // three workgroups per CU, operands by LDS-DMA
-        if (half)
-            hipLaunchKernelGGL((flush_f32_persist2_kernel<_Float16, 3, true>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
-        else
-            hipLaunchKernelGGL((flush_f32_persist2_kernel<float, 3, true>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
-    } else if (persist_ok && p.variant == 5) {
-        const int pgrid = 16 * ((p.ncu + 7) / 8);   // two workgroups per CU, operands by LDS-DMA
-        if (half)
-            hipLaunchKernelGGL((flush_f32_persist2_kernel<_Float16, 2, true>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
-        else
-            hipLaunchKernelGGL((flush_f32_persist2_kernel<float, 2, true>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
-    } else if (persist_ok && p.variant == 6) {
-        const int pgrid = 8 * ((p.ncu + 7) / 8);   // one workgroup per CU, operands by LDS-DMA
-        if (half)
-            hipLaunchKernelGGL((flush_f32_persist2_kernel<_Float16, 2, true>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
-        else
-            hipLaunchKernelGGL((flush_f32_persist2_kernel<float, 2, true>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
-    } else if (persist_ok && p.variant == 7) {
-        const int pgrid = 8 * ((p.ncu + 7) / 8);   // one workgroup per CU
-        if (half)
-            hipLaunchKernelGGL((flush_f32_persist2_kernel<_Float16, 2, false>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
-        else
-            hipLaunchKernelGGL((flush_f32_persist2_kernel<float, 2, false>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
-    } else if (persist_ok && p.variant != 3) {
+    if (p.nsteps <= PST_MAXC && p.d.kmax <= 16 && p.variant != 2) {
         const int pgrid = 16 * ((p.ncu + 7) / 8);   // two workgroups per CU (48 KB LDS each)
         if (half)
-            hipLaunchKernelGGL((flush_f32_persist2_kernel<_Float16, 2, false>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+            hipLaunchKernelGGL(flush_f32_persist2_kernel<_Float16>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
         else
-            hipLaunchKernelGGL((flush_f32_persist2_kernel<float, 2, false>), dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
-    } else if (persist_ok) {
-        const int pgrid = 8 * ((p.ncu + 7) / 8);   // one workgroup per CU (128 KB LDS)
-        if (half)
-            hipLaunchKernelGGL(flush_f32_persist_kernel<_Float16>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
-        else
-            hipLaunchKernelGGL(flush_f32_persist_kernel<float>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+            hipLaunchKernelGGL(flush_f32_persist2_kernel<float>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
     } else {
         const int64_t nsb = (p.d.nb + DD_SB - 1) / DD_SB;
         const int64_t total = (int64_t)p.E * (nsb * (nsb + 1) / 2);

@@ -21,7 +21,7 @@ from . import build as _build
 EKF_MAX_LINES = 64
 PREC_F64, PREC_F32, PREC_F16 = 0, 1, 2
 R_INTENDED, R_AS_WRITTEN = 0, 1
-ST_SINGULAR_S, ST_CAPACITY, ST_NONSYM = 1, 2, 4
+ST_SINGULAR_S, ST_CAPACITY, ST_NONSYM, ST_SYNC_TIMEOUT = 1, 2, 4, 8
 
 LIB_PATH = _build.LIB_PATH
 
@@ -30,8 +30,10 @@ EXPORTED = [
     "ekf_config_init", "ekf_strerror", "ekf_abi_version", "ekf_create", "ekf_destroy",
     "ekf_set_stream", "ekf_sync", "ekf_reset_instance", "ekf_localize", "ekf_localize_device",
     "ekf_predict", "ekf_update", "ekf_read_results", "ekf_upload_state", "ekf_download_state",
-    "ekf_init_lowrank", "ekf_get_pose_cov", "ekf_get_ellipse", "ekf_landmark_block_bytes",
-    "ekf_state_dim", "ekf_profile_enable", "ekf_profile_read", "ekf_debug_scan_stamps",
+    "ekf_init_lowrank", "ekf_get_pose_cov", "ekf_get_ellipse", "ekf_ellipse_of_block",
+    "ekf_landmark_block_bytes",
+    "ekf_state_dim", "ekf_profile_enable", "ekf_profile_read", "ekf_profile_flushes",
+    "ekf_flush_kernel_name", "ekf_debug_scan_stamps",
 ]
 
 
@@ -102,10 +104,14 @@ def load_library(path: str = ""):
         "ekf_get_pose_cov": (ctypes.c_int, [vp, ctypes.c_int, dp]),
         "ekf_get_ellipse": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(ctypes.c_float)]),
+        "ekf_ellipse_of_block": (ctypes.c_int, [dp, ctypes.POINTER(ctypes.c_float),
+                                                ctypes.POINTER(ctypes.c_float)]),
         "ekf_landmark_block_bytes": (sz, [vp]),
         "ekf_state_dim": (ctypes.c_int, [vp]),
         "ekf_profile_enable": (ctypes.c_int, [vp, ctypes.c_int]),
         "ekf_profile_read": (ctypes.c_int, [vp, dp, dp, dp, ip]),
+        "ekf_profile_flushes": (ctypes.c_int, [vp, ctypes.c_int, ip, ctypes.POINTER(ctypes.c_float)]),
+        "ekf_flush_kernel_name": (ctypes.c_char_p, [vp, ctypes.c_int]),
         "ekf_debug_scan_stamps": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_ulonglong)]),
     }
     for name, (res, args) in sig.items():
@@ -135,6 +141,18 @@ def lines_array(lines, max_lines: int, instances: int = 1) -> np.ndarray:
     L = min(arr.shape[1], max_lines)
     out[: arr.shape[0], :L] = arr[:, :L, :6]
     return np.ascontiguousarray(out)
+
+
+def ellipse_of_block(P22):
+    """Robot::getEllipse arithmetic (Robot.cpp:73-124) on a given 2x2 block, host side of the
+    library (no device): (ok, [axii0, axii1], angle)."""
+    blk = np.ascontiguousarray(np.asarray(P22, dtype=np.float64).reshape(4))
+    axii = (ctypes.c_float * 2)()
+    ang = ctypes.c_float()
+    rc = load_library().ekf_ellipse_of_block(_dp(blk), axii, ctypes.byref(ang))
+    if rc < 0:
+        _check(-rc, "ekf_ellipse_of_block")
+    return rc == 1, [axii[0], axii[1]], ang.value
 
 
 class Ensemble:
@@ -266,6 +284,21 @@ class Ensemble:
         if rc < 0:
             _check(-rc, "ekf_get_ellipse")
         return rc == 1, [axii[0], axii[1]], ang.value
+
+    def profile_flushes(self) -> list[tuple[int, float]]:
+        """(steps, ms) of every flush launch timed since the last profile() call."""
+        n = self._lib.ekf_profile_flushes(self._h, 0, None, None)
+        if n < 0:
+            _check(-n, "ekf_profile_flushes")
+        ns = (ctypes.c_int32 * max(n, 1))()
+        ms = (ctypes.c_float * max(n, 1))()
+        n = self._lib.ekf_profile_flushes(self._h, n, ns, ms)
+        if n < 0:
+            _check(-n, "ekf_profile_flushes")
+        return [(ns[k], ms[k]) for k in range(n)]
+
+    def flush_kernel_name(self, nsteps: int) -> str:
+        return self._lib.ekf_flush_kernel_name(self._h, int(nsteps)).decode()
 
     def scan_stamps(self) -> list[int]:
         out = (ctypes.c_ulonglong * 16)()

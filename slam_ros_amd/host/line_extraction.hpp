@@ -4,19 +4,19 @@
 //
 //   scan_to_points  main.cpp:37-56       ranges > 0.05, alfa = θ − π, variance 0.01 (no noise:
 //                                        SIMULATIONOFF, Robot.h:18)
-//   extract_lines   lineFitting.cpp:633-702 (LineExtraction): sort by angle, split where
+//   extract_lines   lineFitting.cpp:650-702 (LineExtraction): sort by angle, split where
 //                   consecutive points are > 0.5 apart (:548-589), rotate so that the last split
 //                   starts the sequence, split again, then per segment the recursive
-//                   split-and-fit (simplifyPath.cpp:108-184), then LineConversion (:591-631)
+//                   split-and-fit (simplifyPath.cpp:108-177), then LineConversion (:608-649)
 //   to_robot_frame  main.cpp:57-61       alfa += π, folded into (−π, π]
 //   raycast_room    config 1 input: a 360-beam scan of a rectangular room with
 //                   square pillars, message layout [r0, θ0, r1, θ1, …] (main.cpp:41-56)
 //
 // The reference's constants and quirks are kept where they change numbers: π is 3.14159265 in
 // the line code (lineFitting.h:8) and M_PI in main.cpp; a fitted line passes through degrees and
-// back (lineFitting.cpp:18-24, :294); the angle part of the line covariance is 1/12·1.5 == 0
+// back (lineFitting.cpp:17-23, :280); the angle part of the line covariance is 1/12·1.5 == 0
 // (integer division, :419) and the off-diagonals are forced to 0 (:446-448); the residual sum
-// starts at 0 (its accumulator is uninitialised in the reference, :117). The pairwise sums of
+// starts at 0 (its accumulator is uninitialised in the reference, :108). The pairwise sums of
 // the fit keep the reference's O(n²) order of summation.
 #pragma once
 
@@ -59,7 +59,7 @@ inline PolarPoint to_polar(const XY& v)
     return p;
 }
 
-// line(alfa_deg, r) (lineFitting.cpp:18-24)
+// line(alfa_deg, r) (lineFitting.cpp:17-23)
 inline Line make_line_deg(double alfa_deg, double r)
 {
     Line l;
@@ -70,7 +70,7 @@ inline Line make_line_deg(double alfa_deg, double r)
     return l;
 }
 
-// Weighted total-least-squares line in polar form (lineFitting.cpp:258-296)
+// Weighted total-least-squares line in polar form (lineFitting.cpp:240-282)
 inline Line fit_line(const std::vector<PolarPoint>& P)
 {
     const size_t n = P.size();
@@ -93,7 +93,7 @@ inline Line fit_line(const std::vector<PolarPoint>& P)
 }
 
 // Sum of the points' distances to the chord of the fitted line over the points' x range
-// (lineFitting.cpp:96-126)
+// (lineFitting.cpp:96-127)
 inline double residual_error(const std::vector<PolarPoint>& P, const Line& l)
 {
     if (P.size() < 2) return 0.0;
@@ -111,7 +111,7 @@ inline double residual_error(const std::vector<PolarPoint>& P, const Line& l)
     return sum;
 }
 
-// Index of the point farthest from the chord first–last (simplifyPath.cpp:39-59)
+// Index of the point farthest from the chord first–last (simplifyPath.cpp:37-57)
 inline size_t farthest_from_chord(const std::vector<XY>& v)
 {
     const XY f = v[0], e = v.back();
@@ -130,7 +130,7 @@ inline size_t farthest_from_chord(const std::vector<XY>& v)
     return index;
 }
 
-// LineAlap / alfanorm (lineFitting.cpp:339-357)
+// LineAlap / alfanorm (lineFitting.cpp:357-378)
 inline void flip_negative(Line& l)
 {
     if (l.r < 0) {
@@ -148,7 +148,7 @@ inline double fold_once(double a)
 
 // C_AR of a fitted line: forward differences (step 1e-6) of (alfa, r) with respect to every
 // point's r and alfa, propagated through diag(1.5·variance², 1/12·1.5 == 0); off-diagonals
-// zeroed (lineFitting.cpp:380-451). The product keeps GSL dgemm's order over k.
+// zeroed (lineFitting.cpp:379-450). The product keeps GSL dgemm's order over k.
 inline void line_covariance(std::vector<PolarPoint> P, double C[4])
 {
     const size_t n = P.size();
@@ -185,7 +185,7 @@ inline void line_covariance(std::vector<PolarPoint> P, double C[4])
 }
 
 // The end points of a segment: the first / last point projected on the line through the fitted
-// line's points at the middle and at that end (simplifyPath.cpp:61-105)
+// line's points at the middle and at that end (simplifyPath.cpp:59-105)
 inline PolarPoint end_on_line(const std::vector<PolarPoint>& P, const Line& l, bool last)
 {
     const PolarPoint& at = last ? P.back() : P.front();
@@ -218,7 +218,7 @@ inline void set_end_points(Line& l)
     }
 }
 
-// Recursive split-and-fit (simplifyPath.cpp:108-184): fit a line to the points; if the points'
+// Recursive split-and-fit (simplifyPath.cpp:108-177): fit a line to the points; if the points'
 // residual exceeds the expected one by three deviations, split at the point farthest from the
 // chord and recurse, else keep the line with its covariance and end points.
 inline void split_and_fit(const std::vector<PolarPoint>& P, std::vector<Line>& out)
@@ -249,7 +249,7 @@ inline void split_and_fit(const std::vector<PolarPoint>& P, std::vector<Line>& o
     out.push_back(l);
 }
 
-// LineConversion (lineFitting.cpp:591-631): drop lines with a negative, NaN or large (> 0.01)
+// LineConversion (lineFitting.cpp:608-649): drop lines with a negative, NaN or large (> 0.01)
 // angle variance or an all-zero (alfa, r); then flip negative r
 inline void drop_and_orient(std::vector<Line>& lines)
 {
@@ -266,7 +266,7 @@ inline void drop_and_orient(std::vector<Line>& lines)
     lines.swap(kept);
 }
 
-// Split positions where consecutive points are more than 0.5 apart (lineFitting.cpp:548-589)
+// Split positions where consecutive points are more than 0.5 apart (lineFitting.cpp:561-607)
 inline std::vector<size_t> gaps(const std::vector<PolarPoint>& P)
 {
     std::vector<size_t> split;
@@ -278,7 +278,7 @@ inline std::vector<size_t> gaps(const std::vector<PolarPoint>& P)
     return split;
 }
 
-// LineExtraction (lineFitting.cpp:633-702)
+// LineExtraction (lineFitting.cpp:650-702)
 inline std::vector<Line> extract_lines(std::vector<PolarPoint> P)
 {
     std::vector<Line> lines;

@@ -6,8 +6,11 @@
 // Robot.cpp:126-904), getEllipse(axii, angle) (Robot.h:73, Robot.cpp:73-124), the public
 // xPos / yPos / thetaPos (Robot.h:54-56), lineIntervals (Robot.h:59) and P_t0 (Robot.h:62) —
 // and adds the two halves predict(encoder) / update(lines). The EKF state lives
-// on the GPU; P_t0 is a host mirror whose pose block [0:3, 0:3] is refreshed after every call
-// (what getEllipse reads) and whose full contents are fetched on demand by downloadP().
+// on the GPU; P_t0 keeps the reference's type (double[SLAMSIZE*SLAMSIZE], Robot.h:62) as a host
+// mirror. Mirror policy (setMirror): kFull (default) refreshes all of P_t0 after every call, as
+// the reference's member always holds the full P; kPoseBlock refreshes only [0:3, 0:3] (what
+// getEllipse reads, Robot.cpp:75-77) and leaves the rest as of the last downloadP() — for large
+// capacities, where the full download costs O(n²) per scan.
 //
 // The types are template parameters so that the core compiles without ROS or GSL:
 //   Line         needs .alfa, .r, .C_AR (pointer to a 2x2 matrix with .data and .tda, the
@@ -35,8 +38,10 @@ namespace slam_ekf {
 // Robot::normalizeRadian (Robot.cpp:62-71), including its non-standard fold for |rad| >= 2π
 inline void normalize_radian(double& rad)
 {
-    if (rad > M_PI) rad -= 2 * M_PI + std::floor(rad / (2 * M_PI)) * 2 * M_PI;
-    if (rad < -M_PI) rad += 2 * M_PI + std::floor(std::fabs(rad) / (2 * M_PI)) * 2 * M_PI;
+    if (rad > M_PI)
+        rad -= 2 * M_PI + std::floor(rad / (2 * M_PI)) * 2 * M_PI;
+    else if (rad < -M_PI)
+        rad += 2 * M_PI + std::floor(std::fabs(rad) / (2 * M_PI)) * 2 * M_PI;
 }
 
 template <class Line, class IntervalMsg, int N = 100>
@@ -45,13 +50,14 @@ public:
     static constexpr int kLines = N;            // LINESIZE (Robot.h:13)
     static constexpr int kState = 2 * N + 3;    // SLAMSIZE (Robot.h:14)
 
+    enum Mirror { kPoseBlock = 0, kFull = 1 };
+
     double xPos = 0, yPos = 0, thetaPos = 0;    // Robot.h:54-56
     IntervalMsg lineIntervals;                  // Robot.h:59
-    std::vector<double> P_t0;                   // Robot.h:62 (host mirror, row-major kState²)
+    double P_t0[kState * kState] = {};          // Robot.h:62 (host mirror, row-major; see Mirror)
 
     // Robot::Robot(x, y, theta), Robot.cpp:20-35
     BasicRobot(double x, double y, double theta, int precision = EKF_PREC_F64, int device = -1)
-        : P_t0((size_t)kState * kState, 0.0)
     {
         ekf_config cfg;
         ekf_config_init(&cfg);
@@ -70,7 +76,7 @@ public:
         xPos = x;
         yPos = y;
         thetaPos = theta;
-        refresh_pose_block();
+        refresh_mirror();
     }
     ~BasicRobot()
     {
@@ -90,10 +96,9 @@ public:
         }
         std::vector<ekf_line> buf;
         if (!pack(lines, buf)) return;
-        const int32_t nl = (int32_t)buf.size();
-        ekf_result res;
-        report(ekf_localize(ctx_, encoder, buf.data(), &nl, &res), "ekf_localize");
-        finish(lines, res);
+        const int32_t nl = (int32_t)lines.size();
+        ekf_result res{};
+        if (report(ekf_localize(ctx_, encoder, buf.data(), &nl, &res), "ekf_localize")) finish(lines, res);
     }
 
     // predict half: motion model and P_pre (Robot.cpp:130-286)
@@ -109,10 +114,9 @@ public:
     {
         std::vector<ekf_line> buf;
         if (!pack(lines, buf)) return;
-        const int32_t nl = (int32_t)buf.size();
-        ekf_result res;
-        report(ekf_update(ctx_, buf.data(), &nl, &res), "ekf_update");
-        finish(lines, res);
+        const int32_t nl = (int32_t)lines.size();
+        ekf_result res{};
+        if (report(ekf_update(ctx_, buf.data(), &nl, &res), "ekf_update")) finish(lines, res);
     }
 
     // Robot::getEllipse (Robot.h:73, Robot.cpp:73-124)
@@ -123,13 +127,20 @@ public:
 
     void normalizeRadian(double& rad) { normalize_radian(rad); }
 
+    void setMirror(Mirror m)
+    {
+        mirror_ = m;
+        refresh_mirror();
+    }
+    Mirror mirror() const { return mirror_; }
+
     // full covariance into P_t0 (and optionally the state vector)
     bool downloadP(std::vector<double>* y = nullptr, int* saved = nullptr)
     {
         std::vector<double> yy((size_t)kState);
         int s = 0;
         double pose[3];
-        const int rc = ekf_download_state(ctx_, 0, P_t0.data(), yy.data(), &s, pose);
+        const int rc = ekf_download_state(ctx_, 0, P_t0, yy.data(), &s, pose);
         if (rc != EKF_OK) return false;
         if (y) *y = yy;
         if (saved) *saved = s;
@@ -143,19 +154,23 @@ public:
 private:
     ekf_ctx* ctx_ = nullptr;
     ekf_result last_{};
+    Mirror mirror_ = kFull;
 
-    static void report(int rc, const char* what)
+    static bool report(int rc, const char* what)
     {
         if (rc != EKF_OK) std::fprintf(stderr, "slam_ekf: %s: %s\n", what, ekf_strerror(rc));
+        return rc == EKF_OK;
     }
 
+    // the context reads max_lines (= EKF_MAX_LINES) entries per instance: the buffer always
+    // holds that many, zero past the scan's lines
     static bool pack(const std::vector<Line>& lines, std::vector<ekf_line>& out)
     {
         if ((int)lines.size() > EKF_MAX_LINES) {
             std::fprintf(stderr, "slam_ekf: %zu lines exceed EKF_MAX_LINES\n", lines.size());
             return false;
         }
-        out.resize(lines.size());
+        out.assign((size_t)EKF_MAX_LINES, ekf_line{});
         for (size_t i = 0; i < lines.size(); i++) {
             ekf_line& o = out[i];
             o.alpha = lines[i].alfa;
@@ -189,7 +204,7 @@ private:
             push_endpoint(iv.front().alfa, iv.front().r);
             push_endpoint(iv.back().alfa, iv.back().r);
         }
-        refresh_pose_block();
+        refresh_mirror();
     }
 
     void push_endpoint(double alfa, double r)
@@ -201,8 +216,13 @@ private:
         lineIntervals.data.push_back((float)(std::sin(a) * rr));
     }
 
-    void refresh_pose_block()
+    void refresh_mirror()
     {
+        if (mirror_ == kFull) {
+            int s = 0;
+            double pose[3];
+            if (ekf_download_state(ctx_, 0, P_t0, nullptr, &s, pose) == EKF_OK) return;
+        }
         double P33[9];
         if (ekf_get_pose_cov(ctx_, 0, P33) != EKF_OK) return;
         for (int a = 0; a < 3; a++)

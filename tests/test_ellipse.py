@@ -1,0 +1,78 @@
+"""Robot::getEllipse (slam_ros/Robot.cpp:73-124) in GSL's convention, CPU only.
+
+The library's host restatement (ekf_ellipse_of_block, slam_ros_amd/csrc/ekf_api.hip) and the
+oracle's independent Python restatement (oracle/oracle.py gsl_ellipse) of gsl_eigen_nonsymmv +
+GSL_EIGEN_SORT_ABS_ASC must agree bit for bit (float32 outputs), including the eigenvector sign
+that decides the published angle (main.cpp:154-168 publishes it as robotPosition.rotation.z).
+GSL itself is absent (parity unpinned against GSL's binaries): the sanity checks below tie the
+restatement to the eigen-decomposition numpy computes, modulo the sign of the eigenvector.
+"""
+import math
+
+import numpy as np
+import pytest
+
+
+def _blocks():
+    rng = np.random.default_rng(5)
+    out = [
+        (0.05, 0.0, 0.0, 0.05),                 # Robot::Robot state (c == 0 branch, equal λ)
+        (0.05, 0.0, 0.0, 0.02),
+        (0.02, 0.0, 0.0, 0.05),
+        (0.03, 0.01, 0.0, 0.02),                 # c == 0, b != 0
+        (0.03, 0.0, 0.01, 0.02),                 # b == 0 branch (swap)
+        (0.04, 0.01, 0.01, 0.04),                # a == d
+        (0.04, -0.01, -0.01, 0.04),
+        (1e-3, 2e-4, 2e-4, 5e-3),
+        (5e-3, -2e-4, -2e-4, 1e-3),
+        (0.0, 0.0, 0.0, 0.0),
+        (1.0, 1e-17, 1e-17, 1.0),                # nearly equal eigenvalues (z < 4 eps branch)
+    ]
+    for _ in range(400):
+        A = rng.normal(size=(2, 2)) * 10 ** rng.uniform(-4, 0)
+        S = A @ A.T
+        if rng.random() < 0.3:                   # not exactly symmetric, as fp64 P blocks are
+            S[1, 0] = S[0, 1] * (1 + rng.normal() * 1e-15)
+        out.append(tuple(S.reshape(4)))
+    return out
+
+
+def test_library_equals_oracle_bitwise(ekf_mod, oracle_mod):
+    for blk in _blocks():
+        ok_l, ax_l, an_l = ekf_mod.ellipse_of_block(blk)
+        ok_o, ax_o, an_o = oracle_mod.gsl_ellipse(blk)
+        assert ok_l == ok_o, blk
+        if ok_l:
+            assert ax_l == ax_o and an_l == an_o, (blk, ax_l, ax_o, an_l, an_o)
+
+
+def test_restatement_is_an_eigendecomposition(oracle_mod):
+    for blk in _blocks():
+        ok, axii, angle = oracle_mod.gsl_ellipse(blk)
+        assert ok
+        S = np.array(blk).reshape(2, 2)
+        lam = np.linalg.eigvals(S)
+        lam = lam[np.argsort(np.abs(lam))]
+        np.testing.assert_allclose(axii, [2 * math.sqrt(5.991 * abs(v)) for v in lam.real],
+                                   rtol=2e-6, atol=1e-6)
+        if abs(abs(lam[1]) - abs(lam[0])) > 1e-9 * max(abs(lam[1]), 1e-30):
+            v = np.array([math.sin(angle), math.cos(angle)])   # angle = atan2(v0, v1)
+            r = S @ v - lam[1].real * v
+            assert np.linalg.norm(r) <= 1e-5 * max(abs(lam[1]), 1e-12) + 1e-7, (blk, angle)
+
+
+def test_sign_convention_examples(oracle_mod):
+    # diagonal block: Z = I, eigenvectors (1, 0) and (0, 1): the larger λ sits at P11 → (0, 1)
+    ok, axii, angle = oracle_mod.gsl_ellipse((0.01, 0.0, 0.0, 0.04))
+    assert ok and angle == 0.0
+    # larger λ at P00 → eigenvector (1, 0), atan2(1, 0) = π/2
+    ok, axii, angle = oracle_mod.gsl_ellipse((0.04, 0.0, 0.0, 0.01))
+    assert ok and angle == pytest.approx(math.pi / 2, abs=1e-7)
+    # b == 0 branch: the rotation swaps the diagonal, Z = [[0, -1], [1, 0]]: the eigenvector of
+    # the eigenvalue moved to the top is Z[:, 0] = (0, 1)
+    ok, axii, angle = oracle_mod.gsl_ellipse((0.01, 0.0, 0.003, 0.04))
+    assert ok and angle == 0.0
+    # generic correlated block: the standardisation rotation has cs > 0, so the eigenvector of
+    # a' (here the larger one) is (cs, sn) with a positive first component
+    ok, axii, angle = oracle_mod.gsl_ellipse((0.04, 0.01, 0.01, 0.02))
+    assert ok and 0.0 < angle < math.pi

@@ -117,7 +117,7 @@ def test_extracted_lines_match_scene(tmp_path, ekf_mod):
         assert np.all(lines[:, 3] == 0) and np.all(lines[:, 4] == 0)
         assert np.all(lines[:, 5] > 0) and np.all(lines[:, 2] >= 0) and np.all(lines[:, 2] <= 0.01)
         # every extracted line lies on a face of the scene (robot frame). The split threshold
-        # (simplifyPath.cpp:150, three deviations of a 1 cm range noise summed over the segment)
+        # (simplifyPath.cpp:149, three deviations of a 1 cm range noise summed over the segment)
         # lets a few corner points of the next face into a segment: mrad-level bias
         exact = 0
         for ln in lines:
@@ -189,13 +189,12 @@ def test_config1_end_to_end(tmp_path, ekf_mod, oracle_mod):
         assert pub["ok"] == 1
         tx, ty, tz, rx, ry, rz, rw = pub["msg"]
         assert (tx, ty, tz) == (x, y, th) and rw == 0.0
-        lam, vec = np.linalg.eigh(ref.P_t0[:2, :2])
-        ax = 2 * np.sqrt(5.991 * np.abs(lam))
-        np.testing.assert_allclose([rx, ry], [ax[1], ax[0]], rtol=1e-5)
+        ok, axii, want = oracle_mod.gsl_ellipse(ref.P_t0[:2, :2])   # GSL's convention
+        assert ok
+        np.testing.assert_allclose([rx, ry], [axii[1], axii[0]], rtol=1e-6)
+        lam = np.linalg.eigvalsh(ref.P_t0[:2, :2])
         if lam[1] - lam[0] > 1e-3 * lam[1]:    # the angle is defined (not a circle)
-            want = math.atan2(vec[0, 1], vec[1, 1])
-            dd = (rz - want) % math.pi
-            assert min(dd, math.pi - dd) < 1e-4, (k, rz, want)
+            assert abs(rz - want) < 1e-5, (k, rz, want)   # the angle itself, not modulo π
             angles += 1
         # lines (main.cpp:171-174): the end points of this cycle's new landmarks, 4 floats each
         assert len(pub["lines"]) == 4 * sum(1 for j in m if j < 0)
