@@ -165,8 +165,12 @@ const char* ekf_flush_kernel_name(const ekf_ctx* ctx, int nsteps);
 /* Diagnostic: association-kernel phase timers (sum over instances, 100 MHz ticks), collected
  * only when the environment had EKF_SCAN_STAMPS=1 at ekf_create. Slots: 0 predict, 1 diagonal
  * gather + barrier, 2 gating, 3 min-reduction barrier, 4 winner package, 5 broadcast barrier,
- * 6 gain rows, 7 commit/augmentation, 8 total, 9 launches. */
-int ekf_debug_scan_stamps(ekf_ctx* ctx, unsigned long long out[16]);
+ * 6 gain rows, 7 commit/augmentation, 8 total, 9 launches; 16-19 per-line phases of the first
+ * landmark wave (gate, wait for the package, gain rows, robot update). */
+int ekf_debug_scan_stamps(ekf_ctx* ctx, unsigned long long out[32]);
+/* Diagnostic: words 0..15 of instance e's result record as of the last ekf_read_results
+ * (word 9: association path code, 10..15: the first six guessed winners). */
+int ekf_debug_result_words(ekf_ctx* ctx, int e, int out[16]);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,35 @@
+"""Association-kernel phase timers (EKF_SCAN_STAMPS=1; thread 0 of workgroup 0 of each instance,
+s_memrealtime, 100 MHz), µs per launch averaged over instances, at the bench's shapes
+(f32, E = 8, L = m = 8). usage: python scripts/assoc_probe.py [N:T ...]"""
+import json
+import os
+import sys
+
+os.environ["EKF_SCAN_STAMPS"] = "1"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from slam_ros_amd import ekf, scan_gen as G  # noqa: E402
+
+NAMES = {0: "predict+state", 1: "diag+ctl", 5: "guess", 2: "exchange1", 10: "resolve",
+         12: "records+stage", 11: "staged_replay(w0)", 13: "replay_wave_total", 3: "rw_eval+publish",
+         4: "rw_gain+robot", 16: "lw_gate", 17: "lw_wait_pkg", 18: "lw_gain+store", 19: "lw_robot",
+         14: "landmark_total", 6: "verdict", 7: "commit", 8: "total", 15: "fallbacks"}
+E = 8
+cfgs = sys.argv[1:] or ["4096:8", "4096:1", "1024:8"]
+for c in cfgs:
+    N, T = (int(x) for x in c.split(":"))
+    w = G.make_world(N)
+    st = G.initial_state(w)
+    ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8, flush_interval=T)
+    for e in range(E):
+        ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+    base = ens.scan_stamps()
+    for s in range(1, 25):
+        enc, lines, nl = G.make_scan(w, s, instances=E)
+        r = ens.localize(enc, lines, nl)
+        assert all(x["matches"] == 8 for x in r)
+    stp = [a - b for a, b in zip(ens.scan_stamps(), base)]
+    n = stp[9] or 1
+    out = {v: round(stp[k] * 10e-3 / n, 2) for k, v in NAMES.items()}
+    out["fallbacks"] = stp[15]
+    print(json.dumps({"N": N, "T": T, "E": E, "launches_x_instances": stp[9], "us": out}), flush=True)
+    ens.close()

@@ -33,6 +33,15 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(p) > t for p in deps)
 
 
+def build_variant(out: str, defines: list[str]) -> str:
+    """An A/B build of the same sources with extra -D flags (scripts only; SLAM_EKF_LIB)."""
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-mllvm", "-amdgpu-mfma-vgpr-form", *[f"-D{d}" for d in defines],
+           "-o", out] + [os.path.join(CSRC, s) for s in SOURCES]
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
     deps.append(os.path.join(ROOT, "include", "slam_ekf.h"))

@@ -277,13 +277,14 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     ALLOC(c->d_lines, sizeof(ekf_line) * d.max_lines * E);
     ALLOC(c->d_nlines, sizeof(int) * E);
     c->G = (d.N + ekf::SCAN_THREADS - 1) / ekf::SCAN_THREADS;
-    c->mbw = ((ekf::MB_WORDS_FIXED + 4 * d.max_lines + 15) / 16) * 16;   // whole 128-B lines
+    // whole 128-B lines: the package words, then 16 words for the speculative list words
+    c->mbw = ((ekf::MB_WORDS_FIXED + 4 * d.max_lines + 15) / 16) * 16 + 16;
     c->spec = getenv("EKF_SPECULATE") ? atoi(getenv("EKF_SPECULATE")) : 1;
     ALLOC(c->mbox, sizeof(double) * 2 * c->G * c->mbw * E);
     c->sync_stride = ((ekf::SYNC_WG0 + c->G + 15) / 16) * 16;
     ALLOC(c->sync, sizeof(int) * c->sync_stride * E);
     if (getenv("EKF_SCAN_STAMPS") && atoi(getenv("EKF_SCAN_STAMPS")))
-        ALLOC(c->dbg, sizeof(unsigned long long) * 16 * E);
+        ALLOC(c->dbg, sizeof(unsigned long long) * 32 * E);
 #undef ALLOC
     if (hipHostMalloc((void**)&c->h_res, sizeof(int) * ekf::RES_STRIDE * E) != hipSuccess) goto fail;
     if (hipHostMalloc((void**)&c->h_pose, sizeof(double) * 3 * E) != hipSuccess) goto fail;
@@ -1071,17 +1072,26 @@ extern "C" const char* ekf_flush_kernel_name(const ekf_ctx* c, int nsteps)
     return half ? "flush_f32_sb_kernel<_Float16>" : "flush_f32_sb_kernel<float>";
 }
 
-extern "C" int ekf_debug_scan_stamps(ekf_ctx* c, unsigned long long out[16])
+extern "C" int ekf_debug_result_words(ekf_ctx* c, int e, int out[16])
+{
+    // Diagnostic: the first 16 words of instance e's last result record (as copied by the last
+    // ekf_read_results), including the association path code and guessed winners (RES_DBG).
+    if (!c || !out || e < 0 || e >= c->cfg.instances) return EKF_EINVAL;
+    memcpy(out, c->h_res + (size_t)e * ekf::RES_STRIDE, sizeof(int) * 16);
+    return EKF_OK;
+}
+
+extern "C" int ekf_debug_scan_stamps(ekf_ctx* c, unsigned long long out[32])
 {
     // Diagnostic: association-kernel phase times summed over instances (100 MHz ticks) since
     // context creation, when built with EKF_SCAN_STAMPS=1 in the environment; zeros otherwise.
     if (!c || !out) return EKF_EINVAL;
-    memset(out, 0, sizeof(unsigned long long) * 16);
+    memset(out, 0, sizeof(unsigned long long) * 32);
     if (!c->dbg) return EKF_OK;
     HIP_TRY(hipStreamSynchronize(c->stream));
-    std::vector<unsigned long long> h((size_t)16 * c->cfg.instances);
+    std::vector<unsigned long long> h((size_t)32 * c->cfg.instances);
     HIP_TRY(hipMemcpy(h.data(), c->dbg, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
     for (int e = 0; e < c->cfg.instances; e++)
-        for (int k = 0; k < 16; k++) out[k] += h[(size_t)e * 16 + k];
+        for (int k = 0; k < 32; k++) out[k] += h[(size_t)e * 32 + k];
     return EKF_OK;
 }

@@ -29,6 +29,7 @@ enum {
     RES_NLINES = 6,
     RES_KSTEPS = 7,   // MFMA k-steps of the downdate (0 = no downdate)
     RES_NADD = 8,     // landmarks actually added (patch rows)
+    RES_DBG = 9,      // diagnostics: association path code, then the first 6 guessed winners
     RES_MATCH = 16,                     // [EKF_MAX_LINES]
     RES_EXTRA = 16 + EKF_MAX_LINES,     // [EKF_MAX_LINES] line indices, in order
     RES_STRIDE = 16 + 2 * EKF_MAX_LINES,

@@ -32,6 +32,15 @@
 namespace ekf {
 
 #define EKF_PI 3.14159265358979323846
+#ifndef EKF_OPT_PKG_ROBOT
+#define EKF_OPT_PKG_ROBOT 1
+#endif
+#ifndef EKF_OPT_MERGED
+#define EKF_OPT_MERGED 1
+#endif
+#ifndef EKF_OPT_EARLY_DJ
+#define EKF_OPT_EARLY_DJ 1
+#endif
 
 // Storage type T of the landmark block → compute type C (MFMA / FMA chain) and tile layout L.
 // fp16 storage computes in fp32 on the f32 layout and rounds to fp16 after every step, in the
@@ -515,6 +524,7 @@ __device__ __forceinline__ bool certified_reject(const Block5& b, double ma, dou
         }                                                                       \
     } while (0)
 
+constexpr int EKF_NSTAMP = 32;   // diagnostic phase-timer slots per instance (EKF_SCAN_STAMPS=1)
 constexpr int HIST_LDS = 8;   // matches per scan whose owned U rows stay in LDS
 constexpr int HIST_V = 4;     // ... and whose V rows do (sequential path; the rest in Vst)
 
@@ -579,6 +589,37 @@ __device__ __forceinline__ int mb_poll(const double* mbox, int par, int G, int k
         v = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return (int)(v & 0xffffffu);
+}
+
+// Speculative list words carry their own tag: bits 63..40 the launch epoch (mod 2^24), bits
+// 39..0 the payload, written with one 8-byte atomic store, so a reader needs one poll of the word
+// itself (no separate tag word and second load). They live in the last 16 words of each
+// workgroup's parity-0 mailbox slot (MB_LIST_BACK), which nothing else writes, and every
+// speculative launch rewrites all SPEC_L of them.
+constexpr int LIST_TAG_SHIFT = 40;
+constexpr int MB_LIST_BACK = 16;
+
+__device__ __forceinline__ void mb_store_tagged(double* p, unsigned epoch, unsigned long long payload)
+{
+    const unsigned long long w = ((unsigned long long)(epoch & 0xffffffu) << LIST_TAG_SHIFT) | payload;
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ unsigned long long mb_wait_tagged(const double* p, unsigned epoch, int& status)
+{
+    const unsigned long long* w = reinterpret_cast<const unsigned long long*>(p);
+    const unsigned long long want = epoch & 0xffffffu;
+    unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int polls = 0;
+    while ((v >> LIST_TAG_SHIFT) != want) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++polls > (1 << 24)) {
+            status |= EKF_ST_TIMEOUT_BIT;
+            return 0;
+        }
+        v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return v & ((1ull << LIST_TAG_SHIFT) - 1);
 }
 
 // Each workgroup announces that it has read the instance's shared inputs (after its loads
@@ -789,12 +830,19 @@ __device__ __forceinline__ bool guess_pass(const Guess& gs, double za, double zr
 }
 
 constexpr int SPEC_L = HIST_LDS;                    // lines
-constexpr int SPEC_K = 6;                           // guessed candidates per line per workgroup
+#ifndef EKF_SPEC_K
+#define EKF_SPEC_K 4
+#endif
+constexpr int SPEC_K = EKF_SPEC_K;                  // guessed candidates per line per workgroup
+constexpr int LW_CNT = 8 * SPEC_K, LW_MORE = 8 * SPEC_K + 3;   // list word: count, more bits
 constexpr int SPEC_PB = 2;                          // guessed columns per pass over the pending steps
 constexpr int SPEC_QMAX = 8;                        // pending steps staged in LDS (pipelined T = 4: up to 7)
 constexpr int SPEC_GMAX = 64;                       // workgroups per instance (<= one wave)
 constexpr int SPEC_WD = 14 + 4 * (SPEC_L - 1);      // winner record: rr, Dj, y, sin/cos, column blocks
-constexpr int PKW = MB_VH;                          // package words (speculative lines; V rows in sh_wh)
+// speculative package: the words of build_package, then the robot 3×3 block and x_pre after the
+// line's update (robot_update), computed once by the replay wave for every landmark wave
+constexpr int PK_R33 = MB_VH, PK_XP = MB_VH + 9;
+constexpr int PKW = MB_VH + 12;                     // package words (speculative lines; V rows in sh_wh)
 
 // Blocks (j, cols[t]) for t < SPEC_L and (j, j) (last; only if `diag`) of the landmark block
 // with the pending steps applied, fp32 operands, every pending step with ks <= 8: the guessed
@@ -806,26 +854,40 @@ constexpr int PKW = MB_VH;                          // package words (speculativ
 // O = owned U (or owned V when transposed) and X = staged V (or staged U). Every k-step runs:
 // past a step's matches the operands hold −0 (U) and +0 (V), whose products leave a chain as it
 // is (x + (−0) == x).
+// The stored blocks of staged_blocks, in the requested orientation (issued early: their loads
+// share a memory round trip with the staging of the guessed columns' rows).
+template <typename T>
+__device__ __forceinline__ void staged_blocks_load(const PllView<T>& v, int j, const int (&cols)[8],
+                                                   typename Stor<T>::C (&r)[9][4])
+{
+    using C = typename Stor<T>::C;
+    const int i0 = 2 * j;
+#pragma unroll
+    for (int b = 0; b < 9; b++) {
+        const int jb = 2 * (b < 8 ? cols[b] : j);
+        const bool swap = (i0 >> 5) > (jb >> 5);
+        C a[4];
+        load_block<T>(v, swap ? jb : i0, swap ? i0 : jb, a);
+        r[b][0] = a[0]; r[b][1] = swap ? a[2] : a[1];
+        r[b][2] = swap ? a[1] : a[2]; r[b][3] = a[3];
+    }
+}
+
 template <typename T>
 __device__ __forceinline__ void staged_blocks(const PllView<T>& v, int j, const int (&cols)[8],
-                                              const float* stg, bool diag, double (&out)[9][4])
+                                              const float* stg, typename Stor<T>::C (&r)[9][4],
+                                              double (&out)[9][4])
 {
     using C = typename Stor<T>::C;
     constexpr int NB = 9;
     const int i0 = 2 * j;
     bool swap[NB];
     int jb[NB];
-    C r[NB][4];   // (i0, jb), (i0, jb+1), (i0+1, jb), (i0+1, jb+1)
 #pragma unroll
     for (int b = 0; b < NB; b++) {
         jb[b] = 2 * (b < 8 ? cols[b] : j);
         swap[b] = (i0 >> 5) > (jb[b] >> 5);
-        C a[4];
-        load_block<T>(v, swap[b] ? jb[b] : i0, swap[b] ? i0 : jb[b], a);
-        r[b][0] = a[0]; r[b][1] = swap[b] ? a[2] : a[1];
-        r[b][2] = swap[b] ? a[1] : a[2]; r[b][3] = a[3];
     }
-    (void)diag;
     const int kh = v.kmax / 2;
     // owned rows i0, i0+1 of U_q and V_q: [row half][2 × 4 k]
     auto load_rows = [&](int q, f32x4v (&Ux)[4][2], f32x4v (&Vx)[4][2]) {
@@ -918,15 +980,22 @@ __device__ __forceinline__ void staged_blocks(const PllView<T>& v, int j, const 
 // are guessed columns (guess indices ta, tb): both sides' operand rows come from the staged LDS
 // image. Per element the same chain as pll_blocks.
 template <typename T>
+__device__ __forceinline__ void pair_block_load(const PllView<T>& v, int wa, int wb, typename Stor<T>::C (&acc)[4])
+{
+    const int i0 = 2 * wa, jb = 2 * wb;
+    const bool swap = (i0 >> 5) > (jb >> 5);   // stored orientation: (jb, i0)
+    load_block<T>(v, swap ? jb : i0, swap ? i0 : jb, acc);
+}
+
+template <typename T>
 __device__ __forceinline__ void staged_pair_block(const PllView<T>& v, int wa, int ta, int wb, int tb,
-                                                  const float* stg, double (&out)[4])
+                                                  const float* stg, typename Stor<T>::C (&acc)[4],
+                                                  double (&out)[4])
 {
     using C = typename Stor<T>::C;
     const int i0 = 2 * wa, jb = 2 * wb;
     const bool swap = (i0 >> 5) > (jb >> 5);   // stored orientation: (jb, i0)
     const int tA = swap ? tb : ta, tB = swap ? ta : tb;
-    C acc[4];
-    load_block<T>(v, swap ? jb : i0, swap ? i0 : jb, acc);
     for (int q = 0; q < v.npend; q++) {
         const int4 cw = v.ctl[q];
         if (cw.x) {
@@ -1020,9 +1089,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     __shared__ double4 sh_wh[SPEC_L][SPEC_L][2];
     __shared__ double sh_pk[SPEC_L][PKW];
     __shared__ float sh_stg[SPEC_L * SPEC_QMAX * 2 * 4 * 8];   // staged pending-step rows
-    __shared__ unsigned long long sh_stamp[16];
-    unsigned long long* dbg = (p.dbg && lead) ? p.dbg + (size_t)e * 16 : nullptr;
-    if (p.dbg && tid < 16) sh_stamp[tid] = 0;
+    __shared__ unsigned long long sh_stamp[EKF_NSTAMP];
+    unsigned long long* dbg = (p.dbg && lead) ? p.dbg + (size_t)e * EKF_NSTAMP : nullptr;
+    if (p.dbg && tid < EKF_NSTAMP) sh_stamp[tid] = 0;
     unsigned long long t_last = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const unsigned long long t_first = t_last;
 
@@ -1089,6 +1158,15 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             xp[2] = p.xpre[3 * e + 2];
         }
     };
+    // the owned diagonal block as last flushed (the staged speculative path guesses from it),
+    // issued with the owned-state loads: the scan's inputs arrive in one memory round trip
+    typename Stor<T>::C dj0[4] = {0, 0, 0, 0};
+    if (own && (p.phase & PHASE_UPDATE)) {
+        PllView<T> v0;
+        v0.X = reinterpret_cast<const T*>(p.Pread) + (size_t)e * d.ntiles * TILE_ELEMS;
+        v0.nb = d.nb;
+        load_block<T>(v0, 2 * j, 2 * j, dj0);
+    }
     init_state();
     // the owned landmark's angle at the start of the scan and its sin/cos (sincos_near)
     double ma0 = yb.x, s0j = 0.0, c0j = 1.0;
@@ -1164,11 +1242,16 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     if (own && j < s) {
         if (staged) {
             // the guess only needs it approximately: the last flushed value (exact one below)
+#if EKF_OPT_EARLY_DJ
+#pragma unroll
+            for (int a = 0; a < 4; a++) Dj[a] = from_domain<T>(dj0[a]);
+#else
             const T* X = pv.X;
             using Lq = typename Stor<T>::L;
 #pragma unroll
             for (int a = 0; a < 4; a++)
                 Dj[a] = from_domain<T>(from_store<T>(X[ll_offset<Lq>(2 * j + (a >> 1), 2 * j + (a & 1), d.nb)]));
+#endif
         } else {
             pll_block(pv, 2 * j, 2 * j, Dj);
         }
@@ -1209,6 +1292,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
 
     bool matched = false;
     int m = 0, nextra = 0, status = 0, tstatus = 0;
+    int dpath = 0;   // diagnostic: 1 fast guess, 2 collision-resolved guess, 4 unresolved, 8 verdict failed
     int par0 = 0;   // mailbox parity of line 0 on the sequential path
     bool sequential = true;
 
@@ -1232,7 +1316,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 gp = ((gp >> 1) | (gp << (L - 1))) & ((1u << L) - 1u);
         }
         // per wave and line the guessed candidates (ballot), then the workgroup's first SPEC_K
-        // in landmark order: word = 8-bit local indices | count << 48 | more << 52
+        // in landmark order: word = 8-bit local indices | count << 32 | more << 35
         for (int t = 0; t < L; t++) {
             const unsigned long long mk = __ballot((gp >> t) & 1u);
             if ((tid & 63) == 0 && tid < SCAN_THREADS) sh_wl[t][tid >> 6] = mk;
@@ -1251,25 +1335,20 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     cnt++;
                 }
             }
-            word |= ((unsigned long long)cnt << 48) | ((unsigned long long)more << 52);
+            word |= ((unsigned long long)cnt << LW_CNT) | ((unsigned long long)more << LW_MORE);
             sh_lists[g * SPEC_L + tid] = word;
         }
         __syncthreads();
         EKF_STAMP(5);
         // ---- (b) exchange 1 (parity 0): every workgroup's lists ----
         if (G > 1) {
-            double* slot = mbox + (size_t)g * p.mbw;
-            if (tid < L) mb_store(slot + 1 + tid, __longlong_as_double((long long)sh_lists[g * SPEC_L + tid]));
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) mb_tag(slot, p.epoch, TAG_SPEC_LISTS, 0);
-            if (tid < G) (void)mb_poll(mbox, 0, G, tid, p.mbw, p.epoch, TAG_SPEC_LISTS, tstatus);
-            __syncthreads();
+            // one self-tagged word per (workgroup, line), polled directly by its readers
+            const int lb = p.mbw - MB_LIST_BACK;
+            double* slot = mbox + (size_t)g * p.mbw + lb;
+            if (tid < SPEC_L) mb_store_tagged(slot + tid, p.epoch, tid < L ? sh_lists[g * SPEC_L + tid] : 0ull);
             for (int k = tid; k < G * L; k += SCAN_BLOCK) {
                 const int gq = k / L, t = k - gq * L;
-                if (gq != g)
-                    sh_lists[gq * SPEC_L + t] =
-                        (unsigned long long)__double_as_longlong(mb_load(mbox + (size_t)gq * p.mbw + 1 + t));
+                if (gq != g) sh_lists[gq * SPEC_L + t] = mb_wait_tagged(mbox + (size_t)gq * p.mbw + lb + t, p.epoch, tstatus);
             }
             __syncthreads();
         }
@@ -1279,16 +1358,20 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         // distinct they are the winners. Otherwise, per line the first SPEC_K guessed candidates,
         // and in line order the first one not taken by an earlier line. ----
         if (tid < 64) {
+            // lane t: the first workgroup (in landmark order) with a guessed candidate for line t
+            int c = 0x7fffffff;
+            if (tid < L) {
+                for (int gq = 0; gq < G; gq++) {
+                    const unsigned long long w = sh_lists[gq * SPEC_L + tid];
+                    if ((w >> LW_CNT) & 7) {
+                        c = gq * SCAN_THREADS + (int)(w & 255);
+                        break;
+                    }
+                }
+            }
             int first[SPEC_L];
 #pragma unroll
-            for (int t = 0; t < SPEC_L; t++) {
-                int c = 0x7fffffff;
-                if (t < L && tid < G) {
-                    const unsigned long long w = sh_lists[tid * SPEC_L + t];
-                    if ((w >> 48) & 15) c = tid * SCAN_THREADS + (int)(w & 255);
-                }
-                first[t] = wave_min(c);
-            }
+            for (int t = 0; t < SPEC_L; t++) first[t] = __shfl(c, t, 64);
             if (tid == 0) {
                 bool distinct = true;
 #pragma unroll
@@ -1302,17 +1385,18 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             }
         }
         __syncthreads();
+        dpath = sh_flag == 2 ? 2 : 1;
         if (sh_flag == 2) {
             if (tid < L) {
                 int cnt = 0, more = 0;
                 for (int gq = 0; gq < G; gq++) {
                     const unsigned long long w = sh_lists[gq * SPEC_L + tid];
-                    const int c = (int)((w >> 48) & 15);
+                    const int c = (int)((w >> LW_CNT) & 7);
                     for (int k = 0; k < c; k++) {
                         if (cnt < SPEC_K) sh_glist[tid][cnt++] = gq * SCAN_THREADS + (int)((w >> (8 * k)) & 255);
                         else more = 1;
                     }
-                    if ((w >> 52) & 1) more = 1;
+                    if ((w >> LW_MORE) & 1) more = 1;
                 }
                 sh_glist[tid][SPEC_K] = cnt | (more << 8);
             }
@@ -1353,6 +1437,25 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             // predicted robot-strip columns and mean, diagonal block, blocks of the earlier
             // winners' columns; and (staged replay) the guessed columns' rows of the pending
             // steps' operands ----
+            // staged path: everything below is issued before one barrier, so that the stored
+            // blocks of the owned row (landmark waves), the winners' records and mutual blocks
+            // (replay wave) and the staged operand rows arrive in one memory round trip
+            int cols[SPEC_L];
+#pragma unroll
+            for (int t = 0; t < SPEC_L; t++) {
+                const int w = t < L ? sh_spec[t] : -1;
+                cols[t] = w >= 0 ? w : j;
+            }
+            C srow[SPEC_L + 1][4];
+            if (EKF_OPT_MERGED && staged && own) staged_blocks_load<T>(pv, j, cols, srow);
+            int pu = 0, pt = 0;   // replay-wave lane → mutual block (pu, pt), pt <= pu
+            C pacc[4] = {0, 0, 0, 0};
+            const int lane_r = tid - SCAN_THREADS;
+            if (EKF_OPT_MERGED && staged && tid >= SCAN_THREADS && lane_r < L * (L + 1) / 2) {
+                pt = lane_r;
+                while (pt > pu) { pt -= pu + 1; pu++; }
+                if (sh_spec[pu] >= 0 && sh_spec[pt] >= 0) pair_block_load<T>(pv, sh_spec[pu], sh_spec[pt], pacc);
+            }
             if (!staged && tid < L * (L + 1) / 2) {
                 int u = 0, t = tid;
                 while (t > u) { t -= u + 1; u++; }
@@ -1363,7 +1466,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     double* r = sh_wd + u * SPEC_WD + (t == u ? 6 : 14 + 4 * t);
                     r[0] = bk[0]; r[1] = bk[1]; r[2] = bk[2]; r[3] = bk[3];
                 }
-            } else if (tid >= SCAN_THREADS && tid < SCAN_THREADS + L) {
+            }
+            if (tid >= SCAN_THREADS && tid < SCAN_THREADS + L) {
                 const int u = tid - SCAN_THREADS, wu = sh_spec[u];
                 if (wu >= 0) {
                     const int bw = 3 + 2 * wu;
@@ -1397,21 +1501,36 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             }
             if (tid == SCAN_BLOCK - 1) sh_ready = 0;
             __syncthreads();
+#if !EKF_OPT_MERGED
             if (staged) {
-                // the winners' mutual blocks from the staged rows (an LDS pass per pending step
-                // instead of two global round trips)
                 if (tid < L * (L + 1) / 2) {
                     int u = 0, t = tid;
                     while (t > u) { t -= u + 1; u++; }
                     const int wu = sh_spec[u], wt = sh_spec[t];
                     if (wu >= 0 && wt >= 0) {
                         double bk[4];
-                        staged_pair_block<T>(pv, wu, u, wt, t, sh_stg, bk);
+                        C a0[4];
+                        pair_block_load<T>(pv, wu, wt, a0);
+                        staged_pair_block<T>(pv, wu, u, wt, t, sh_stg, a0, bk);
                         double* r = sh_wd + u * SPEC_WD + (t == u ? 6 : 14 + 4 * t);
                         r[0] = bk[0]; r[1] = bk[1]; r[2] = bk[2]; r[3] = bk[3];
                     }
                 }
                 __syncthreads();
+            }
+#endif
+            if (EKF_OPT_MERGED && staged && tid >= SCAN_THREADS) {
+                // the winners' mutual blocks from the staged rows, by the replay wave itself
+                // (only it reads them): the landmark waves go straight on
+                if (lane_r < L * (L + 1) / 2 && sh_spec[pu] >= 0 && sh_spec[pt] >= 0) {
+                    double bk[4];
+                    staged_pair_block<T>(pv, sh_spec[pu], pu, sh_spec[pt], pt, sh_stg, pacc, bk);
+                    double* r = sh_wd + pu * SPEC_WD + (pt == pu ? 6 : 14 + 4 * pt);
+                    r[0] = bk[0]; r[1] = bk[1]; r[2] = bk[2]; r[3] = bk[3];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             }
             EKF_STAMP(12);
             // ---- (f) the winners' part of the sequential chain, in the last wave (lane u carries
@@ -1456,6 +1575,16 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         bad |= c.pass ? 0 : 1;
                         build_package(c, R33l, w0, w1, w2, pk);   // its V rows stay in sh_wh[t]
                     }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    // the robot block after the line, once for every landmark wave
+                    robot_update(R33l, xpl, pk);
+                    if (u == 0) {
+#pragma unroll
+                        for (int a = 0; a < 9; a++) pk[PK_R33 + a] = R33l[a];
+                        pk[PK_XP + 0] = xpl[0]; pk[PK_XP + 1] = xpl[1]; pk[PK_XP + 2] = xpl[2];
+                    }
                     // the package is complete: to the other lanes of this wave, and to the
                     // landmark waves (release of all lanes' LDS writes, then the line counter)
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1472,7 +1601,6 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         sh_wh[u][ml][0] = make_double4(uu[0], uu[1], uu[2], uu[3]);
                         sh_wh[u][ml][1] = make_double4(kk[0], kk[1], kk[2], kk[3]);
                     }
-                    robot_update(R33l, xpl, pk);
                     ml++;
                     if (lst) { const unsigned long long t2 = __builtin_amdgcn_s_memrealtime(); sh_stamp[4] += t2 - tl; tl = t2; }
                 }
@@ -1486,14 +1614,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 // last wave runs (f) ----
                 if (own) {
                     if (staged) {
-                        int cols[SPEC_L];
-#pragma unroll
-                        for (int t = 0; t < SPEC_L; t++) {
-                            const int w = t < L ? sh_spec[t] : -1;
-                            cols[t] = w >= 0 ? w : j;
-                        }
                         double blk[SPEC_L + 1][4];
-                        staged_blocks<T>(pv, j, cols, sh_stg, j < s, blk);
+                        if (!EKF_OPT_MERGED) staged_blocks_load<T>(pv, j, cols, srow);
+                        staged_blocks<T>(pv, j, cols, sh_stg, srow, blk);
 #pragma unroll
                         for (int t = 0; t < SPEC_L; t++)
                             if (t < L && sh_spec[t] >= 0)
@@ -1522,6 +1645,14 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 EKF_STAMP(11);
                 // ---- (g) the landmark waves: the sequential gating and gain rows against the
                 // packages ----
+                unsigned long long tq = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+                auto sub = [&](int k) {
+                    if (dbg) {
+                        const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+                        sh_stamp[k] += t2 - tq;
+                        tq = t2;
+                    }
+                };
                 for (int i = 0; i < L && !viol; ++i) {
                     const ekf_line ln = sh_lines[i];
                     double Rm[4];
@@ -1542,6 +1673,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         // the guess must be the first passing unmatched landmark
                         if (pass ? (w < 0 || j < w) : (j == w)) viol = 1;
                     }
+                    sub(16);
                     if (w < 0) {
                         // no match: the line goes to extraLines (Robot.cpp:308-310, 492-496)
                         if (lead) {
@@ -1557,6 +1689,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         __builtin_amdgcn_s_sleep(1);
                         if (++polls > (1 << 24)) { tstatus |= EKF_ST_TIMEOUT_BIT; viol = 1; break; }
                     }
+                    sub(17);
                     const double* pk = sh_pk[i];
                     if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
                     if (own) {
@@ -1572,7 +1705,16 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                                           rr2, yb, Dj, kk, uu);
                         store_rows(m, kk, uu, false);
                     }
+                    sub(18);
+#if EKF_OPT_PKG_ROBOT
+                    // = robot_update(R33, xp, pk), computed by the replay wave
+#pragma unroll
+                    for (int a = 0; a < 9; a++) R33[a] = pk[PK_R33 + a];
+                    xp[0] = pk[PK_XP + 0]; xp[1] = pk[PK_XP + 1]; xp[2] = pk[PK_XP + 2];
+#else
                     robot_update(R33, xp, pk);
+#endif
+                    sub(19);
                     if (j == w) matched = true;
                     if (lead) res[RES_MATCH + i] = w;
                     m++;
@@ -1600,6 +1742,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             }
             EKF_STAMP(6);
             if (any) {
+                dpath |= 8;
                 if (dbg) sh_stamp[15] += 1;
                 sequential = true;
                 par0 = 1;
@@ -1612,6 +1755,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             }
         } else {
             par0 = 1;   // the lists' parity-0 words may still be read
+            // unresolved guesses: straight to the sequential path, which needs the exact owned
+            // diagonal block (the staged path only loaded the last flushed one, for the guess)
+            if (staged && own && j < s) pll_block(pv, 2 * j, 2 * j, Dj);
         }
     }
 
@@ -1852,13 +1998,15 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         res[RES_NADD] = reset ? 0 : nadd;
         res[RES_NLINES] = L;
         res[RES_KSTEPS] = (sizeof(C) == 4) ? m : (m + 1) / 2;
+        res[RES_DBG] = dpath | (sequential ? 16 : 0);
+        for (int t = 0; t < 6; t++) res[RES_DBG + 1 + t] = t < SPEC_L ? sh_spec[t] : -2;
         p.saved[e] = reset ? 0 : s + nadd;
     }
     EKF_STAMP(7);
     if (dbg) {
         // (phase times accumulate in LDS: a global read-modify-write per stamp would add a
         // memory round trip to every phase it measures)
-        for (int k = 0; k < 16; k++) dbg[k] += sh_stamp[k];
+        for (int k = 0; k < EKF_NSTAMP; k++) dbg[k] += sh_stamp[k];
         dbg[8] += t_last - t_first;
         dbg[9] += 1;
     }

@@ -33,7 +33,7 @@ EXPORTED = [
     "ekf_init_lowrank", "ekf_get_pose_cov", "ekf_get_ellipse", "ekf_ellipse_of_block",
     "ekf_landmark_block_bytes",
     "ekf_state_dim", "ekf_profile_enable", "ekf_profile_read", "ekf_profile_flushes",
-    "ekf_flush_kernel_name", "ekf_debug_scan_stamps",
+    "ekf_flush_kernel_name", "ekf_debug_scan_stamps", "ekf_debug_result_words",
 ]
 
 
@@ -113,6 +113,7 @@ def load_library(path: str = ""):
         "ekf_profile_flushes": (ctypes.c_int, [vp, ctypes.c_int, ip, ctypes.POINTER(ctypes.c_float)]),
         "ekf_flush_kernel_name": (ctypes.c_char_p, [vp, ctypes.c_int]),
         "ekf_debug_scan_stamps": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_ulonglong)]),
+        "ekf_debug_result_words": (ctypes.c_int, [vp, ctypes.c_int, ip]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -300,8 +301,13 @@ class Ensemble:
     def flush_kernel_name(self, nsteps: int) -> str:
         return self._lib.ekf_flush_kernel_name(self._h, int(nsteps)).decode()
 
+    def result_words(self, e: int = 0) -> list[int]:
+        out = (ctypes.c_int32 * 16)()
+        _check(self._lib.ekf_debug_result_words(self._h, e, out), "ekf_debug_result_words")
+        return list(out)
+
     def scan_stamps(self) -> list[int]:
-        out = (ctypes.c_ulonglong * 16)()
+        out = (ctypes.c_ulonglong * 32)()
         _check(self._lib.ekf_debug_scan_stamps(self._h, out), "ekf_debug_scan_stamps")
         return list(out)
 
