@@ -32,15 +32,7 @@
 namespace ekf {
 
 #define EKF_PI 3.14159265358979323846
-#ifndef EKF_OPT_PKG_ROBOT
-#define EKF_OPT_PKG_ROBOT 1
-#endif
-#ifndef EKF_OPT_MERGED
-#define EKF_OPT_MERGED 1
-#endif
-#ifndef EKF_OPT_EARLY_DJ
-#define EKF_OPT_EARLY_DJ 1
-#endif
+
 
 // Storage type T of the landmark block → compute type C (MFMA / FMA chain) and tile layout L.
 // fp16 storage computes in fp32 on the f32 layout and rounds to fp16 after every step, in the
@@ -514,6 +506,72 @@ __device__ __forceinline__ bool certified_reject(const Block5& b, double ma, dou
     return (q - dq) > gate * gate * (1.0 + 1e-6) * (det + ddet);
 }
 
+// Certified rejection in fp32 (the first filter of the per-line gate; certified_reject in fp64
+// and the exact evaluation run only where it cannot decide). Same bound structure as
+// certified_reject, with the fp32 roundings added to it: every input rounded to fp32 (relative
+// u = 2^-24), the short fp32 sums of S (≤ 12u of the sum of the absolute values of their terms,
+// bounded through Pm and Hs = Σ|H row 1|), and q, det (16u of their magnitudes); sin/cos of the
+// landmark angle from the fast fp32 path with EPS = 1e-4 allowed. v0 is the exact fp64 value of
+// the evaluation (innovation_angle, no trigonometry), rounded once.
+__device__ __forceinline__ bool certified_reject_f32(const Block5& b, double ma, double mr, const double xp[3],
+                                                     double za, double zr, const double Rm[4], double gate)
+{
+    if (!(fabs(ma) <= 8.0) || Rm[1] != Rm[2]) return false;
+    constexpr float U = 5.9604645e-08f, EPS = 1e-4f;
+    float sn, cs;
+    __sincosf((float)ma, &sn, &cs);
+    const float x0 = (float)xp[0], x1 = (float)xp[1];
+    const float p00 = (float)b.p00, p01 = (float)b.p01, p02 = (float)b.p02;
+    const float p10 = (float)b.p10, p11 = (float)b.p11, p12 = (float)b.p12;
+    const float p20 = (float)b.p20, p21 = (float)b.p21, p22 = (float)b.p22;
+    const float p0a = (float)b.p0a, p1a = (float)b.p1a, p2a = (float)b.p2a;
+    const float p0b = (float)b.p0b, p1b = (float)b.p1b, p2b = (float)b.p2b;
+    const float daa = (float)b.daa, dab = (float)b.dab, dba = (float)b.dba, dbb = (float)b.dbb;
+    const float R0 = (float)Rm[0], R1 = (float)Rm[1], R2 = (float)Rm[2], R3 = (float)Rm[3];
+    const float h10 = -cs, h11 = -sn, h1l = x0 * sn - x1 * cs;
+    // S = H·P5·Hᵀ + R (innovation_cov's expressions)
+    const float a0 = -p20 + p0a, a1 = -p21 + p1a, a2 = -p22 + p2a, a3 = -p2a + daa, a4 = -p2b + dab;
+    const float c0 = h10 * p00 + h11 * p10 + h1l * p0a + p0b;
+    const float c1 = h10 * p01 + h11 * p11 + h1l * p1a + p1b;
+    const float c2 = h10 * p02 + h11 * p12 + h1l * p2a + p2b;
+    const float c3 = h10 * p0a + h11 * p1a + h1l * daa + dba;
+    const float c4 = h10 * p0b + h11 * p1b + h1l * dab + dbb;
+    const float S0 = -a2 + a3 + R0;
+    const float S1 = a0 * h10 + a1 * h11 + a3 * h1l + a4 + R1;
+    const float S2 = -c2 + c3 + R2;
+    const float S3 = c0 * h10 + c1 * h11 + c3 * h1l + c4 + R3;
+    const float v0 = (float)innovation_angle(za, ma, xp[2]);
+    const float v1 = (float)zr - ((float)mr - (x0 * cs + x1 * sn));
+    const float ax = fabsf(x0) + fabsf(x1);
+    const float ex = EPS * ax;
+    float Pm = fmaxf(fmaxf(fmaxf(fabsf(p00), fabsf(p01)), fmaxf(fabsf(p02), fabsf(p10))),
+                     fmaxf(fmaxf(fabsf(p11), fabsf(p12)), fmaxf(fabsf(p20), fabsf(p21))));
+    Pm = fmaxf(Pm, fmaxf(fmaxf(fmaxf(fabsf(p22), fabsf(p0a)), fmaxf(fabsf(p1a), fabsf(p2a))),
+                         fmaxf(fmaxf(fabsf(p0b), fabsf(p1b)), fabsf(p2b))));
+    Pm = fmaxf(Pm, fmaxf(fmaxf(fabsf(daa), fabsf(dab)), fmaxf(fabsf(dba), fabsf(dbb))));
+    const float Hs = 1.f + fabsf(h10) + fabsf(h11) + fabsf(h1l);
+    const float dh = (2.f * EPS + ex) * Pm;
+    const float dS00 = 12.f * U * (4.f * Pm + fabsf(R0));
+    const float dS01 = EPS * (fabsf(a0) + fabsf(a1)) + ex * fabsf(a3) + 12.f * U * (2.f * Hs * Pm + fabsf(R1));
+    const float dS10 = 2.f * dh + 12.f * U * (2.f * Hs * Pm + fabsf(R2));
+    const float dS11 = dh * (3.f + fabsf(h1l) + ex) + EPS * (fabsf(c0) + fabsf(c1)) + ex * fabsf(c3) +
+                       12.f * U * (Hs * Hs * Pm + fabsf(R3));
+    const float dv1 = ex + 8.f * U * ((float)fabs(zr) + (float)fabs(mr) + ax);
+    const float q = v0 * v0 * S3 - v0 * v1 * (S1 + S2) + v1 * v1 * S0;
+    const float det = S0 * S3 - S1 * S2;
+    const float mag_det = fabsf(S0 * S3) + fabsf(S1 * S2);
+    const float mag_q = v0 * v0 * fabsf(S3) + fabsf(v0 * v1) * (fabsf(S1) + fabsf(S2)) + v1 * v1 * fabsf(S0);
+    const float av1 = fabsf(v1) + dv1;
+    const float dq = v0 * v0 * dS11 + fabsf(v0) * av1 * (dS01 + dS10) + fabsf(v0) * dv1 * fabsf(S1 + S2) +
+                     (2.f * fabsf(v1) * dv1 + dv1 * dv1) * fabsf(S0) + av1 * av1 * dS00 + 16.f * U * mag_q + 1e-30f;
+    const float ddet = fabsf(S0) * dS11 + fabsf(S3) * dS00 + fabsf(S1) * dS10 + fabsf(S2) * dS01 + dS01 * dS10 +
+                       dS00 * dS11 + 16.f * U * mag_det + 1e-30f;
+    const float det_lo = det - ddet;
+    if (!(det_lo > 1e-4f * mag_det)) return false;              // also false for NaN / Inf
+    const float g2 = (float)(gate * gate) * (1.f + 1e-4f);
+    return (q - dq) > g2 * (det + ddet);
+}
+
 // Diagnostic phase timers (thread 0 of each workgroup; only when p.dbg is set).
 #define EKF_STAMP(k)                                                            \
     do {                                                                        \
@@ -799,34 +857,49 @@ __device__ __forceinline__ void robot_update(double R33[9], double xp[3], const 
 // speculative association; every decision it feeds is re-checked exactly. The landmark's part
 // (predicted measurement, H·P·Hᵀ) does not depend on the line and is computed once.
 struct Guess {
-    double h0, h1, S[4];
+    float h0, h1, S[4];
 };
 
 __device__ __forceinline__ void guess_prep(const Block5& b, double ma, double mr, const double xp[3],
                                            Guess& gs)
 {
     float sf, cf;
-    sincosf((float)ma, &sf, &cf);
-    const double sn = sf, cs = cf;
-    const double h10 = -cs, h11 = -sn, h1l = xp[0] * sn - xp[1] * cs;
-    const double R0[4] = {0.0, 0.0, 0.0, 0.0};
-    double hp0[5], hp1[5];
-    innovation_cov(b, h10, h11, h1l, R0, gs.S, hp0, hp1);
-    gs.h0 = normalize_radian(ma - xp[2]);
-    gs.h1 = mr - (xp[0] * cs + xp[1] * sn);
+    __sincosf((float)ma, &sf, &cf);
+    const float x0 = (float)xp[0], x1 = (float)xp[1];
+    const float h10 = -cf, h11 = -sf, h1l = x0 * sf - x1 * cf;
+    const float p00 = (float)b.p00, p01 = (float)b.p01, p02 = (float)b.p02;
+    const float p10 = (float)b.p10, p11 = (float)b.p11, p12 = (float)b.p12;
+    const float p20 = (float)b.p20, p21 = (float)b.p21, p22 = (float)b.p22;
+    const float p0a = (float)b.p0a, p1a = (float)b.p1a, p2a = (float)b.p2a;
+    const float p0b = (float)b.p0b, p1b = (float)b.p1b, p2b = (float)b.p2b;
+    const float daa = (float)b.daa, dab = (float)b.dab, dba = (float)b.dba, dbb = (float)b.dbb;
+    const float a0 = -p20 + p0a, a1 = -p21 + p1a, a2 = -p22 + p2a, a3 = -p2a + daa, a4 = -p2b + dab;
+    const float c0 = h10 * p00 + h11 * p10 + h1l * p0a + p0b;
+    const float c1 = h10 * p01 + h11 * p11 + h1l * p1a + p1b;
+    const float c2 = h10 * p02 + h11 * p12 + h1l * p2a + p2b;
+    const float c3 = h10 * p0a + h11 * p1a + h1l * daa + dba;
+    const float c4 = h10 * p0b + h11 * p1b + h1l * dab + dbb;
+    gs.S[0] = -a2 + a3;
+    gs.S[1] = a0 * h10 + a1 * h11 + a3 * h1l + a4;
+    gs.S[2] = -c2 + c3;
+    gs.S[3] = c0 * h10 + c1 * h11 + c3 * h1l + c4;
+    gs.h0 = (float)normalize_radian(ma - xp[2]);
+    gs.h1 = (float)mr - (x0 * cf + x1 * sf);
 }
 
 __device__ __forceinline__ bool guess_pass(const Guess& gs, double za, double zr, const double Rm[4],
                                            double gate)
 {
-    double v0 = za - gs.h0;
-    if (fabs(v0 - 2.0 * EKF_PI) < fabs(v0)) v0 -= 2.0 * EKF_PI;
-    else if (fabs(v0 + 2.0 * EKF_PI) < fabs(v0)) v0 += 2.0 * EKF_PI;
-    const double v1 = zr - gs.h1;
-    const double S0 = gs.S[0] + Rm[0], S1 = gs.S[1] + Rm[1], S2 = gs.S[2] + Rm[2], S3 = gs.S[3] + Rm[3];
-    const double q = v0 * v0 * S3 - v0 * v1 * (S1 + S2) + v1 * v1 * S0;
-    const double det = S0 * S3 - S1 * S2;
-    return !(det > 0.0) || q <= gate * gate * det;
+    constexpr float TWO_PI = 6.283185307179586f;
+    float v0 = (float)za - gs.h0;
+    if (fabsf(v0 - TWO_PI) < fabsf(v0)) v0 -= TWO_PI;
+    else if (fabsf(v0 + TWO_PI) < fabsf(v0)) v0 += TWO_PI;
+    const float v1 = (float)zr - gs.h1;
+    const float S0 = gs.S[0] + (float)Rm[0], S1 = gs.S[1] + (float)Rm[1];
+    const float S2 = gs.S[2] + (float)Rm[2], S3 = gs.S[3] + (float)Rm[3];
+    const float q = v0 * v0 * S3 - v0 * v1 * (S1 + S2) + v1 * v1 * S0;
+    const float det = S0 * S3 - S1 * S2;
+    return !(det > 0.f) || q <= (float)(gate * gate) * det;
 }
 
 constexpr int SPEC_L = HIST_LDS;                    // lines
@@ -1242,16 +1315,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     if (own && j < s) {
         if (staged) {
             // the guess only needs it approximately: the last flushed value (exact one below)
-#if EKF_OPT_EARLY_DJ
 #pragma unroll
             for (int a = 0; a < 4; a++) Dj[a] = from_domain<T>(dj0[a]);
-#else
-            const T* X = pv.X;
-            using Lq = typename Stor<T>::L;
-#pragma unroll
-            for (int a = 0; a < 4; a++)
-                Dj[a] = from_domain<T>(from_store<T>(X[ll_offset<Lq>(2 * j + (a >> 1), 2 * j + (a & 1), d.nb)]));
-#endif
         } else {
             pll_block(pv, 2 * j, 2 * j, Dj);
         }
@@ -1447,11 +1512,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 cols[t] = w >= 0 ? w : j;
             }
             C srow[SPEC_L + 1][4];
-            if (EKF_OPT_MERGED && staged && own) staged_blocks_load<T>(pv, j, cols, srow);
+            if (staged && own) staged_blocks_load<T>(pv, j, cols, srow);
             int pu = 0, pt = 0;   // replay-wave lane → mutual block (pu, pt), pt <= pu
             C pacc[4] = {0, 0, 0, 0};
             const int lane_r = tid - SCAN_THREADS;
-            if (EKF_OPT_MERGED && staged && tid >= SCAN_THREADS && lane_r < L * (L + 1) / 2) {
+            if (staged && tid >= SCAN_THREADS && lane_r < L * (L + 1) / 2) {
                 pt = lane_r;
                 while (pt > pu) { pt -= pu + 1; pu++; }
                 if (sh_spec[pu] >= 0 && sh_spec[pt] >= 0) pair_block_load<T>(pv, sh_spec[pu], sh_spec[pt], pacc);
@@ -1501,25 +1566,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             }
             if (tid == SCAN_BLOCK - 1) sh_ready = 0;
             __syncthreads();
-#if !EKF_OPT_MERGED
-            if (staged) {
-                if (tid < L * (L + 1) / 2) {
-                    int u = 0, t = tid;
-                    while (t > u) { t -= u + 1; u++; }
-                    const int wu = sh_spec[u], wt = sh_spec[t];
-                    if (wu >= 0 && wt >= 0) {
-                        double bk[4];
-                        C a0[4];
-                        pair_block_load<T>(pv, wu, wt, a0);
-                        staged_pair_block<T>(pv, wu, u, wt, t, sh_stg, a0, bk);
-                        double* r = sh_wd + u * SPEC_WD + (t == u ? 6 : 14 + 4 * t);
-                        r[0] = bk[0]; r[1] = bk[1]; r[2] = bk[2]; r[3] = bk[3];
-                    }
-                }
-                __syncthreads();
-            }
-#endif
-            if (EKF_OPT_MERGED && staged && tid >= SCAN_THREADS) {
+            if (staged && tid >= SCAN_THREADS) {
                 // the winners' mutual blocks from the staged rows, by the replay wave itself
                 // (only it reads them): the landmark waves go straight on
                 if (lane_r < L * (L + 1) / 2 && sh_spec[pu] >= 0 && sh_spec[pt] >= 0) {
@@ -1615,7 +1662,6 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 if (own) {
                     if (staged) {
                         double blk[SPEC_L + 1][4];
-                        if (!EKF_OPT_MERGED) staged_blocks_load<T>(pv, j, cols, srow);
                         staged_blocks<T>(pv, j, cols, sh_stg, srow, blk);
 #pragma unroll
                         for (int t = 0; t < SPEC_L; t++)
@@ -1662,9 +1708,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         Block5 b5;
                         fill_block5(b5, R33, rr0, rr1, rr2, Dj);
                         bool pass = false;
-                        double sn, cs;
-                        sincos_near(yb.x, ma0, s0j, c0j, sn, cs);
-                        if (!certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate)) {
+                        double sn = 0.0, cs = 1.0;
+                        if (!certified_reject_f32(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate) &&
+                            (sincos_near(yb.x, ma0, s0j, c0j, sn, cs),
+                             !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate))) {
                             Cand c;
                             eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, c);
                             status |= c.singular ? EKF_ST_SINGULAR : 0;
@@ -1706,14 +1753,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         store_rows(m, kk, uu, false);
                     }
                     sub(18);
-#if EKF_OPT_PKG_ROBOT
                     // = robot_update(R33, xp, pk), computed by the replay wave
 #pragma unroll
                     for (int a = 0; a < 9; a++) R33[a] = pk[PK_R33 + a];
                     xp[0] = pk[PK_XP + 0]; xp[1] = pk[PK_XP + 1]; xp[2] = pk[PK_XP + 2];
-#else
-                    robot_update(R33, xp, pk);
-#endif
                     sub(19);
                     if (j == w) matched = true;
                     if (lead) res[RES_MATCH + i] = w;
