@@ -1,0 +1,67 @@
+"""Summarise a scripts/pmc_profile.sh run into profiles/<tag>/: kernel stats, per-kernel counter
+averages, and traffic.json for the bench's dominant flush form (HBM bytes per launch =
+2 × FETCH_SIZE + WRITE_SIZE, in KB × 1024: MI355X_MICROARCH.md HBM section, gfx950 FETCH_SIZE
+reports half of a 16-B/lane streaming read), stamped with the sha256 of libslam_ekf.so so that
+bench.py uses it only for this very build. usage: python scripts/pmc_summary.py <tag>"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def counters(path):
+    acc = defaultdict(lambda: defaultdict(list))
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
+
+
+def main(tag):
+    import bench
+    from slam_ros_amd import ekf
+    src = os.path.join(ROOT, "gpurun_out", tag)
+    out = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(out, exist_ok=True)
+    shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(out, "kernel_stats.csv"))
+    shutil.copy(os.path.join(src, "bench.json"), os.path.join(out, "bench.json"))
+    ctr = {}
+    for sub in ("fetch", "write", "sq"):
+        for k, v in counters(os.path.join(src, sub, "run_counter_collection.csv")).items():
+            ctr.setdefault(k, {}).update(v)
+    json.dump(ctr, open(os.path.join(out, "counters_avg_per_dispatch.json"), "w"), indent=1)
+    b = json.load(open(os.path.join(out, "bench.json")))
+    kern = b["roofline"]["kernel"]
+    match = [k for k in ctr if kern.split("<")[0] in k and
+             (("<" not in kern) or kern[kern.index("<"):].replace(" ", "") in k.replace(" ", ""))]
+    if not match:
+        print("no counters for", kern, list(ctr)[:5])
+        return
+    c = ctr[match[0]]
+    hbm = 2 * c.get("FETCH_SIZE", 0) * 1024 + c.get("WRITE_SIZE", 0) * 1024
+    cfg = b["config"]
+    tj = {"capacity": cfg["capacity"], "instances": cfg["instances_per_gpu"], "precision": b["dtype"],
+          "flush_interval": cfg["flush_interval"], "pipeline": cfg["pipeline"], "kernel": kern,
+          "hbm_bytes_per_launch": hbm, "fetch_bytes_corrected": 2 * c.get("FETCH_SIZE", 0) * 1024,
+          "write_bytes": c.get("WRITE_SIZE", 0) * 1024,
+          "alg_bytes_per_launch": b["roofline"]["alg_bytes_per_launch"],
+          "traffic_over_alg": hbm / b["roofline"]["alg_bytes_per_launch"],
+          "sq": {k: v for k, v in c.items() if k.startswith("SQ_") or k.startswith("GRBM")},
+          "lib_sha": bench.lib_sha(ekf.LIB_PATH), "source": f"profiles/{tag}/counters_avg_per_dispatch.json"}
+    json.dump(tj, open(os.path.join(out, "traffic.json"), "w"), indent=1)
+    print(json.dumps({k: tj[k] for k in ("kernel", "hbm_bytes_per_launch", "traffic_over_alg")}))
+    sq = tj["sq"]
+    if sq.get("SQ_WAVE_CYCLES"):
+        print("SQ_WAIT_ANY/WAVE", sq.get("SQ_WAIT_ANY", 0) / sq["SQ_WAVE_CYCLES"],
+              "MFMA_BUSY/BUSY", sq.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / max(sq.get("SQ_BUSY_CYCLES", 1), 1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

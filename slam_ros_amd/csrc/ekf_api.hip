@@ -61,6 +61,8 @@ struct ekf_ctx {
     int nstiles2;
     ekf::WtEntry* wt;
     int nwt;
+    ekf::WtEntry* wt64;
+    int nwt64;
     double* d_enc;
     ekf_line* d_lines;
     int* d_nlines;
@@ -141,7 +143,7 @@ int ekf_abi_version(void) { return SLAM_EKF_ABI_VERSION; }
 static void free_all(ekf_ctx* c)
 {
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->pose, c->xpre, c->saved, c->D,
-                               c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->mbox,
+                               c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->mbox,
                                c->sync, c->Ust, c->Vst};
     for (auto& sl : c->ring) {
         ptrs.push_back(sl.Uop);
@@ -366,6 +368,32 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         if (hipMemcpy(c->wt, wt.data(), sizeof(ekf::WtEntry) * wt.size(), hipMemcpyHostToDevice) !=
             hipSuccess)
             goto fail;
+        // the f64 wave flush: wave-tiles of 1 × WT64_C tiles, same panel walk
+        std::vector<ekf::WtEntry> w64;
+        const int nwc64 = (d.nb + ekf::WT64_C - 1) / ekf::WT64_C;
+        for (int pc = 0; pc < nwc64; pc += 16)
+            for (int wr = 0; wr < d.nb; wr++)
+                for (int wc = pc; wc < pc + 16 && wc < nwc64; wc++) {
+                    if (wc * ekf::WT64_C + ekf::WT64_C - 1 < wr) continue;
+                    ekf::WtEntry v;
+                    memset(&v, 0, sizeof(v));
+                    const int fbj = std::min(wc * ekf::WT64_C + ekf::WT64_C - 1, d.nb - 1);   // stored
+                    for (int cc = 0; cc < ekf::WT64_C; cc++) {
+                        const int bj = wc * ekf::WT64_C + cc;
+                        const bool ok = bj < d.nb && wr <= bj;
+                        v.tile[cc] = (int)(ok ? ekf::tile_index(wr, bj, d.nb) : ekf::tile_index(wr, fbj, d.nb));
+                        v.valid |= (ok ? 1 : 0) << cc;
+                        v.rows[1] |= std::min(bj, d.nb - 1) << (16 * cc);
+                    }
+                    v.rows[0] = wr;
+                    v.rc = wr | (wc << 16);
+                    w64.push_back(v);
+                }
+        c->nwt64 = (int)w64.size();
+        if (hipMalloc((void**)&c->wt64, sizeof(ekf::WtEntry) * w64.size()) != hipSuccess) goto fail;
+        if (hipMemcpy(c->wt64, w64.data(), sizeof(ekf::WtEntry) * w64.size(), hipMemcpyHostToDevice) !=
+            hipSuccess)
+            goto fail;
     }
     {
         hipDeviceProp_t prop;
@@ -551,6 +579,8 @@ static int enqueue_flush(ekf_ctx* c)
     dp.nstiles2 = c->nstiles2;
     dp.wt = c->wt;
     dp.nwt = c->nwt;
+    dp.wt64 = c->wt64;
+    dp.nwt64 = c->nwt64;
     for (int q = 0; q < nst; q++) dp.steps[q] = slot_of(c, c->unflushed0 + q);
     const int in = c->last_out;
     const int out = c->cfg.pipeline ? 1 - in : in;
@@ -1055,7 +1085,12 @@ extern "C" int ekf_profile_flushes(ekf_ctx* c, int cap, int* nsteps, float* ms)
 extern "C" const char* ekf_flush_kernel_name(const ekf_ctx* c, int nsteps)
 {
     if (!c || nsteps < 1) return "";
-    if (c->cfg.precision == EKF_PREC_F64) return "downdate_f64_kernel";
+    if (c->cfg.precision == EKF_PREC_F64) {
+        static const char* f64w[5] = {"", "flush_f64_wave_kernel<1>", "flush_f64_wave_kernel<2>",
+                                      "flush_f64_wave_kernel<3>", "flush_f64_wave_kernel<4>"};
+        if (nsteps <= 4 && c->d.kmax == 16 && c->dd_variant != 2) return f64w[nsteps];
+        return "downdate_f64_kernel";
+    }
     const bool half = c->cfg.precision == EKF_PREC_F16;
     const bool wave = nsteps >= 2 && nsteps <= 8 && nsteps % 2 == 0 && c->d.kmax <= 16 &&
                       (nsteps >= 6 || c->dd_variant == 8);

@@ -49,6 +49,8 @@ struct Slot {
 
 constexpr int PMAX = 32;
 constexpr int WT_R = 2, WT_C = 2, WT_N = WT_R * WT_C;   // f32 wave flush: tiles per wave-tile
+constexpr int WT64_C = 2;                                 // f64 wave flush: 1 × 2 tiles per wave-tile
+constexpr int F64_WAVE_MAXS = 4;                          // f64 wave flush: steps per launch
 
 // one wave-tile of the wave flush (host-built table, read with scalar loads): the linear indices
 // of its WT_N tiles (positions below the diagonal or past the block point at a stored tile of
@@ -112,6 +114,8 @@ struct DowndateParams {
     int nstiles2;
     const WtEntry* wt;    // [nwt] wave-tiles of WT_R × WT_C tiles holding a stored tile, panel order
     int nwt;
+    const WtEntry* wt64;  // [nwt64] f64 wave-tiles of 1 × WT64_C tiles (tile[0..1], rows[0] = A row block)
+    int nwt64;
     Slot steps[PMAX];
 };
 

@@ -1997,15 +1997,16 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     Vop[op_index_f32(2 * j + pp, k, d.kmax)] = (C)0.0f;
                 }
         }
-        if (sizeof(C) == 8 && (m & 1)) {
-            // f64 operands: zero the odd tail column pair of the last 4-wide k-step
+        if (sizeof(C) == 8) {
+            // f64 operands: the same −0 (U) / +0 (V) padding past the matches, so that the f64
+            // wave flush may run every k-step (flush_f64_wave_kernel) while downdate_f64_kernel
+            // and the on-read replay stop at the last 4-wide k-step holding a match
+            for (int k = 2 * m; k < d.kmax; k++)
 #pragma unroll
-            for (int pp = 0; pp < 2; pp++) {
-                Uop[op_index_f64(2 * j + pp, 2 * m, d.kmax)] = (C)0;
-                Uop[op_index_f64(2 * j + pp, 2 * m + 1, d.kmax)] = (C)0;
-                Vop[op_index_f64(2 * j + pp, 2 * m, d.kmax)] = (C)0;
-                Vop[op_index_f64(2 * j + pp, 2 * m + 1, d.kmax)] = (C)0;
-            }
+                for (int pp = 0; pp < 2; pp++) {
+                    Uop[op_index_f64(2 * j + pp, k, d.kmax)] = (C)(-0.0);
+                    Vop[op_index_f64(2 * j + pp, k, d.kmax)] = (C)0.0;
+                }
         }
     }
     // status bits seen by this workgroup's threads → its status word (read by ekf_read_results)
@@ -2960,6 +2961,242 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
     }
 }
 
+// f64 flush, barrier-free per-wave form for groups of NS <= F64_WAVE_MAXS steps (kmax <= 16):
+// the f32 wave kernel's scheme at fp64. One wave per SIMD walks wave-tiles of 1 × 2 tiles (eight
+// 16×16 v_mfma_f64_16x16x4_f64 accumulators, 64 registers); while wave-tile k runs its NS × 32
+// MFMAs, the tiles of wave-tile k+1 (issued first) and, step by step, its operand rows stream
+// into registers. fp64 is HBM-bound at T = 4 (8 B per element: 0.54 ms of traffic vs 0.44 ms of
+// MFMA per launch at E = 8, N = 4096), so the wave keeps a whole wave-tile of loads in flight.
+// Every k-step runs (the scan pads the operands past the matches with −0·(+0)); per element the
+// chain is that of downdate_f64_kernel and of the on-read replay: bit-identical results. Groups
+// with a reset or augmented rows for the wave's instances take a plain per-wave-tile loop.
+template <int NS>
+__global__ __launch_bounds__(DD_THREADS, 1) void flush_f64_wave_kernel(DowndateParams p)
+{
+    static_assert(NS >= 1 && NS <= F64_WAVE_MAXS, "steps per launch");
+    const Dims d = p.d;
+    const int nwt = p.nwt64;
+    const int total = p.E * nwt;
+    const int per = (total + 7) / 8;
+    const int xcd = blockIdx.x & 7;
+    const int K = (int)(gridDim.x >> 3) * (DD_THREADS / 64);     // waves per XCD
+    const int g_end = min(total, (xcd + 1) * per);
+    const int g0 = __builtin_amdgcn_readfirstlane(
+        xcd * per + (int)(blockIdx.x >> 3) * (DD_THREADS / 64) + (int)(threadIdx.x >> 6));
+    if (g0 >= g_end) return;
+    const int lane = threadIdx.x & 63;
+    const int kh = d.kmax / 2;   // doubles per lane per row block (2 halves × kmax/4)
+    const int kq = d.kmax / 4;
+    const size_t opstride = (size_t)d.nb * 64 * kh;
+    const size_t inst_elems = (size_t)d.ntiles * TILE_ELEMS;
+    const double* Pin = reinterpret_cast<const double*>(p.Pin);
+    double* Pout = reinterpret_cast<double*>(p.Pout);
+
+    bool fast = d.kmax == 16;
+    {
+        const int e_lo = g0 / nwt, e_hi = (g_end - 1) / nwt;
+        for (int e = e_lo; e <= e_hi; e++)
+#pragma unroll
+            for (int q = 0; q < NS; q++) {
+                const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
+                fast = fast && !sload(r + RES_RESET) && sload(r + RES_NADD) == 0;
+            }
+    }
+    struct Item {
+        int e, li;
+        int tile[WT64_C];
+        int valid, rowA, rowsB;
+    };
+    typedef int i32x8 __attribute__((ext_vector_type(8)));
+    auto load_entry = [&](int li, Item& t) __attribute__((always_inline)) {
+        const i32x8 v = sload(reinterpret_cast<const i32x8*>(p.wt64 + li));
+        t.tile[0] = v[0];
+        t.tile[1] = v[1];
+        t.valid = v[WT_N];
+        t.rowA = v[WT_N + 1];
+        t.rowsB = v[WT_N + 2];
+    };
+    auto first_item = [&](Item& t) __attribute__((always_inline)) {
+        t.e = g0 / nwt;
+        t.li = g0 - t.e * nwt;
+        load_entry(t.li, t);
+    };
+    auto next_item = [&](const Item& c, Item& t) __attribute__((always_inline)) {
+        int li = c.li + K, e = c.e;
+        while (li >= nwt) {
+            li -= nwt;
+            e++;
+        }
+        t.e = e;
+        t.li = li;
+        load_entry(e < p.E ? li : 0, t);
+    };
+    auto tile_base = [&](const Item& t, int i) __attribute__((always_inline)) {
+        return (size_t)t.e * inst_elems + (size_t)t.tile[i] * TILE_ELEMS;
+    };
+    // lane's registers 0-1 of 16×16 block b of a tile at f64x2 b·128 + lane, 2-3 at b·128 + 64 + lane
+    auto load_tiles = [&](const Item& t, f64x2 (&pref)[WT64_C][8]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < WT64_C; i++) {
+            const f64x2* src = reinterpret_cast<const f64x2*>(Pin + tile_base(t, i)) + lane;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                pref[i][2 * b] = __builtin_nontemporal_load(src + b * 128);
+                pref[i][2 * b + 1] = __builtin_nontemporal_load(src + b * 128 + 64);
+            }
+        }
+    };
+    auto store_tiles = [&](const Item& t, const f64x4 (&acc)[WT64_C][4]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < WT64_C; i++)
+            if ((t.valid >> i) & 1) {
+                f64x2* dst = reinterpret_cast<f64x2*>(Pout + tile_base(t, i)) + lane;
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const f64x2 v0 = {acc[i][b][0], acc[i][b][1]};
+                    const f64x2 v1 = {acc[i][b][2], acc[i][b][3]};
+                    __builtin_nontemporal_store(v0, dst + b * 128);
+                    __builtin_nontemporal_store(v1, dst + b * 128 + 64);
+                }
+            }
+    };
+    // operand rows of step q for wave-tile t: A (its row block), B (its two column blocks), each
+    // 8 doubles per lane ([half h][k-step s] at h·kq + s)
+    auto load_ops = [&](const Item& t, int q, f64x2 (&a)[4], f64x2 (&b)[WT64_C][4]) __attribute__((always_inline)) {
+        const double* U = reinterpret_cast<const double*>(p.steps[q].Uop) + t.e * opstride + lane * kh;
+        const double* V = reinterpret_cast<const double*>(p.steps[q].Vop) + t.e * opstride + lane * kh;
+        const f64x2* ua = reinterpret_cast<const f64x2*>(U + (size_t)t.rowA * 64 * kh);
+#pragma unroll
+        for (int k = 0; k < 4; k++) a[k] = ua[k];
+#pragma unroll
+        for (int c = 0; c < WT64_C; c++) {
+            const int rb = (t.rowsB >> (16 * c)) & 0xffff;
+            const f64x2* vb = reinterpret_cast<const f64x2*>(V + (size_t)rb * 64 * kh);
+#pragma unroll
+            for (int k = 0; k < 4; k++) b[c][k] = vb[k];
+        }
+    };
+    // the 4 k-steps of one step: acc[c][h·2 + hc] += A[h] · B[c][hc]
+    auto mfma_step = [&](const f64x2 (&a)[4], const f64x2 (&b)[WT64_C][4], f64x4 (&acc)[WT64_C][4]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++) {
+            const double a0 = a[s4 >> 1][s4 & 1], a1 = a[2 + (s4 >> 1)][s4 & 1];
+#pragma unroll
+            for (int c = 0; c < WT64_C; c++) {
+                const double b0 = b[c][s4 >> 1][s4 & 1], b1 = b[c][2 + (s4 >> 1)][s4 & 1];
+                acc[c][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[c][0], 0, 0, 0);
+                acc[c][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[c][1], 0, 0, 0);
+                acc[c][2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[c][2], 0, 0, 0);
+                acc[c][3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[c][3], 0, 0, 0);
+            }
+        }
+    };
+    auto to_acc = [&](const f64x2 (&pref)[WT64_C][8], f64x4 (&acc)[WT64_C][4]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < WT64_C; i++)
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                acc[i][b] = f64x4{pref[i][2 * b][0], pref[i][2 * b][1], pref[i][2 * b + 1][0], pref[i][2 * b + 1][1]};
+    };
+
+    if (fast) {
+        f64x2 pref[WT64_C][8];
+        f64x2 opa[NS][4], opb[NS][WT64_C][4];
+        f64x4 acc[WT64_C][4];
+        Item cur, nxt, nxt2;
+        first_item(cur);
+        next_item(cur, nxt);
+        load_tiles(cur, pref);
+#pragma unroll
+        for (int q = 0; q < NS; q++) load_ops(cur, q, opa[q], opb[q]);
+        int g = g0;
+        while (true) {
+            const bool more = g + K < g_end;
+            next_item(nxt, nxt2);
+            const Item ldi = more ? nxt : cur;   // the last wave-tile re-reads its own (no branch)
+            to_acc(pref, acc);
+            if (more) load_tiles(nxt, pref);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < NS; q++) {
+                mfma_step(opa[q], opb[q], acc);
+                __builtin_amdgcn_sched_barrier(0);
+                load_ops(ldi, q, opa[q], opb[q]);   // step q's rows of the next wave-tile
+            }
+            store_tiles(cur, acc);
+            if (!more) break;
+            g += K;
+            cur = nxt;
+            nxt = nxt2;
+        }
+        return;
+    }
+
+    // general loop: per wave-tile, every step in order (reset, or the k-steps of its matches, then
+    // its augmented rows), operands loaded in place
+    Item t;
+    first_item(t);
+    for (int g = g0; g < g_end; g += K) {
+        if (g != g0) {
+            Item n;
+            next_item(t, n);
+            t = n;
+        }
+        f64x2 pref[WT64_C][8];
+        f64x4 acc[WT64_C][4];
+        load_tiles(t, pref);
+        to_acc(pref, acc);
+        const int wc0 = (t.rowsB & 0xffff);
+        for (int q = 0; q < NS; q++) {
+            const int* r = p.steps[q].res + (size_t)t.e * RES_STRIDE;
+            if (sload(r + RES_RESET)) {
+#pragma unroll
+                for (int i = 0; i < WT64_C; i++)
+#pragma unroll
+                    for (int b = 0; b < 4; b++) acc[i][b] = f64x4{0.0, 0.0, 0.0, 0.0};
+                continue;
+            }
+            const int ks = sload(r + RES_KSTEPS);
+            if (ks > 0) {
+                const double* U = reinterpret_cast<const double*>(p.steps[q].Uop) + t.e * opstride + lane * kh;
+                const double* V = reinterpret_cast<const double*>(p.steps[q].Vop) + t.e * opstride + lane * kh;
+                const double* A = U + (size_t)t.rowA * 64 * kh;
+                for (int s4 = 0; s4 < ks; s4++) {
+                    const double a0 = A[s4], a1 = A[kq + s4];
+#pragma unroll
+                    for (int c = 0; c < WT64_C; c++) {
+                        const double* B = V + (size_t)((t.rowsB >> (16 * c)) & 0xffff) * 64 * kh;
+                        const double b0 = B[s4], b1 = B[kq + s4];
+                        acc[c][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[c][0], 0, 0, 0);
+                        acc[c][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[c][1], 0, 0, 0);
+                        acc[c][2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[c][2], 0, 0, 0);
+                        acc[c][3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[c][3], 0, 0, 0);
+                    }
+                }
+            }
+            const int nadd = sload(r + RES_NADD), s0 = sload(r + RES_SAVED_IN);
+            if (nadd <= 0 || (wc0 + WT64_C) * 16 <= s0 || wc0 * 16 >= s0 + nadd) continue;
+            const double* prw0 = p.steps[q].patch + (size_t)t.e * d.max_lines * 2 * d.M;
+            const double* pdg = p.steps[q].patch_diag + (size_t)t.e * d.max_lines * 4;
+#pragma unroll
+            for (int c = 0; c < WT64_C; c++) {
+                const int bj = wc0 + c;
+                if (!((t.valid >> c) & 1) || bj * 16 + 15 < s0 || bj * 16 >= s0 + nadd) continue;
+#pragma unroll
+                for (int blk = 0; blk < 4; blk++)
+#pragma unroll
+                    for (int reg = 0; reg < 4; reg++) {
+                        const int row = t.rowA * 32 + (lane >> 4) + 4 * reg + 16 * (blk >> 1);
+                        const int col = bj * 32 + (lane & 15) + 16 * (blk & 1);
+                        const int hi = max(row >> 1, col >> 1);
+                        if (hi >= s0 && hi < s0 + nadd) acc[c][blk][reg] = patched_value(prw0, pdg, d.M, s0, row, col);
+                    }
+            }
+        }
+        store_tiles(t, acc);
+    }
+}
+
 __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams p)
 {
     const Dims d = p.d;
@@ -2974,8 +3211,9 @@ __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams
         const int e = (int)(g / d.ntiles);
         const int64_t t = g - (int64_t)e * d.ntiles;
         const size_t toff = ((size_t)e * d.ntiles + t) * TILE_ELEMS;
-        const f64x2* src = reinterpret_cast<const f64x2*>(reinterpret_cast<const double*>(p.Pin) + toff) + 2 * lane;
-        f64x2* dst = reinterpret_cast<f64x2*>(reinterpret_cast<double*>(p.Pout) + toff) + 2 * lane;
+        // lane's registers 0-1 of block qq at qq·128 + lane, registers 2-3 at qq·128 + 64 + lane
+        const f64x2* src = reinterpret_cast<const f64x2*>(reinterpret_cast<const double*>(p.Pin) + toff) + lane;
+        f64x2* dst = reinterpret_cast<f64x2*>(reinterpret_cast<double*>(p.Pout) + toff) + lane;
         const int2 rc = p.tile_rc[t];
         bool work = false;
         for (int q = 0; q < p.nsteps; q++) {
@@ -2989,7 +3227,7 @@ __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams
 #pragma unroll
                 for (int qq = 0; qq < 4; qq++) {
                     __builtin_nontemporal_store(__builtin_nontemporal_load(src + qq * 128), dst + qq * 128);
-                    __builtin_nontemporal_store(__builtin_nontemporal_load(src + qq * 128 + 1), dst + qq * 128 + 1);
+                    __builtin_nontemporal_store(__builtin_nontemporal_load(src + qq * 128 + 64), dst + qq * 128 + 64);
                 }
             }
             continue;
@@ -2998,7 +3236,7 @@ __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams
 #pragma unroll
         for (int qq = 0; qq < 4; qq++) {
             const f64x2 v0 = __builtin_nontemporal_load(src + qq * 128);
-            const f64x2 v1 = __builtin_nontemporal_load(src + qq * 128 + 1);
+            const f64x2 v1 = __builtin_nontemporal_load(src + qq * 128 + 64);
             acc[qq][0] = v0[0];
             acc[qq][1] = v0[1];
             acc[qq][2] = v1[0];
@@ -3048,7 +3286,7 @@ __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams
             const f64x2 v0 = {acc[qq][0], acc[qq][1]};
             const f64x2 v1 = {acc[qq][2], acc[qq][3]};
             __builtin_nontemporal_store(v0, dst + qq * 128);
-            __builtin_nontemporal_store(v1, dst + qq * 128 + 1);
+            __builtin_nontemporal_store(v1, dst + qq * 128 + 64);
         }
     }
 }
@@ -3064,7 +3302,7 @@ __device__ __forceinline__ void tile_rc_of(int rem, int& r, int& c)
         c = lane & 31;
         r = q + 4 * (lane >> 5) + 8 * grp;
     } else {
-        const int reg = rem & 3, lane = (rem >> 2) & 63, blk = rem >> 8;
+        const int reg = (rem & 1) + 2 * ((rem >> 7) & 1), lane = (rem >> 1) & 63, blk = rem >> 8;
         c = (lane & 15) + 16 * (blk & 1);
         r = (lane >> 4) + 4 * reg + 16 * (blk >> 1);
     }
@@ -3180,12 +3418,22 @@ hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st)
 {
     if (precision == EKF_PREC_F64) {
+        if (p.nsteps <= F64_WAVE_MAXS && p.d.kmax == 16 && p.nwt64 > 0 && p.wt64 != nullptr && p.variant != 2) {
+            const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
+            switch (p.nsteps) {
+            case 1: hipLaunchKernelGGL((flush_f64_wave_kernel<1>), dim3(wgrid), dim3(DD_THREADS), 0, st, p); break;
+            case 2: hipLaunchKernelGGL((flush_f64_wave_kernel<2>), dim3(wgrid), dim3(DD_THREADS), 0, st, p); break;
+            case 3: hipLaunchKernelGGL((flush_f64_wave_kernel<3>), dim3(wgrid), dim3(DD_THREADS), 0, st, p); break;
+            default: hipLaunchKernelGGL((flush_f64_wave_kernel<4>), dim3(wgrid), dim3(DD_THREADS), 0, st, p); break;
+            }
+            return hipGetLastError();
+        }
         hipLaunchKernelGGL(downdate_f64_kernel, dim3(grid), dim3(DD_THREADS), 0, st, p);
         return hipGetLastError();
     }
     const bool half = precision == EKF_PREC_F16;
     // default: the wave flush for groups of 6 or 8 steps; EKF_FLUSH_VARIANT 8 forces it (also
-    // for 2 or 4 steps), 9 keeps the LDS-staged forms
+    // for 2 or 4 steps)
     const bool wave_shape = p.nsteps >= 2 && p.nsteps <= 8 && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
                             p.nwt > 0 && p.wt != nullptr;
     const bool wave_ok = wave_shape && (p.nsteps >= 6 || p.variant == 8);

@@ -15,7 +15,8 @@
 //   stored at ((reg>>2)*64 + lane)*4 + (reg&3)   → one dwordx4 per lane per register quad.
 // f64 tile (four 16×16 v_mfma_f64_16x16x4_f64 blocks; C/D map col = lane&15,
 //   row = (lane>>4) + 4*reg): block (r>>4, c>>4), lane = (c&15) + 16*(r&3), reg = (r&15)>>2;
-//   stored at ((blk*64) + lane)*4 + reg           → two dwordx4 per lane.
+//   stored at ((blk*2 + (reg>>1))*64 + lane)*2 + (reg&1) → per block two dwordx4 per lane, each
+//   instruction's 64 lanes one contiguous 1 KB (registers 0-1 of every lane, then 2-3).
 #pragma once
 
 #include <stddef.h>
@@ -78,7 +79,8 @@ EKF_HD int tile_off_f64(int r, int c)
     const int blk = (r >> 4) * 2 + (c >> 4);
     const int rr = r & 15, cc = c & 15;
     const int lane = cc + 16 * (rr & 3);
-    return (blk * 64 + lane) * 4 + (rr >> 2);
+    const int reg = rr >> 2;
+    return ((blk * 2 + (reg >> 1)) * 64 + lane) * 2 + (reg & 1);
 }
 
 // element offset of P_ll(i, j) (0 <= i, j < M) in the packed tile array; symmetric lookup

@@ -50,7 +50,7 @@ def record(key, value):
 
 
 def run_config(ekf_mod, oracle_mod, prec, T, scans, pipeline=False):
-    import torch
+    from tests.hipmem import DeviceArray
     world = G.make_world(N)
     st = G.initial_state(world)
     ens = ekf_mod.Ensemble(N, E, prec, max_lines=L, flush_interval=T, pipeline=pipeline)
@@ -63,14 +63,13 @@ def run_config(ekf_mod, oracle_mod, prec, T, scans, pipeline=False):
         refs[e].set_state(P0, y0, s0, pose0)
         del P0
     host = np.stack([D.pack(*G.make_scan(world, s + 1, instances=E, lines=L)[:2]) for s in range(scans)])
-    dev = torch.device("cuda", torch.cuda.current_device())
-    payload = torch.from_numpy(host).to(dev)
-    nlines = torch.full((E,), L, dtype=torch.int32, device=dev)
+    payload = DeviceArray(host)
+    nlines = DeviceArray(np.full(E, L, dtype=np.int32))
     eo, lo = D.offsets(E, L, 0)
     out = {"P": [], "y": [], "pose": []}
     for s in range(scans):
-        base = payload[s].data_ptr()
-        ens.localize_device(base + eo * 8, base + lo * 8, nlines.data_ptr())
+        base = payload.address + s * host.shape[1] * 8
+        ens.localize_device(base + eo * 8, base + lo * 8, nlines.address)
         res = ens.read_results()                        # stream sync only: no flush added
         for e in CHECK:
             m = refs[e].localize(host[s, lo + e * L * 6: lo + (e + 1) * L * 6].reshape(L, 6),
@@ -93,6 +92,8 @@ def run_config(ekf_mod, oracle_mod, prec, T, scans, pipeline=False):
                 assert ry <= 1e-8, (prec, k, e, ry)
                 assert dp <= (1e-12 if prec == 0 else 1e-8 * np.linalg.norm(refs[e].y)), (prec, k, e, dp)
     ens.close()
+    payload.close()
+    nlines.close()
     return out
 
 

@@ -38,8 +38,8 @@ def build_driver(tmp_path, ekf_mod, robot_h=False, extra=()):
 
 @pytest.mark.parametrize("robot_h", [False, True])
 def test_dropin_compiles_and_fails_loudly_without_gpu(tmp_path, ekf_mod, robot_h):
-    import torch
-    if torch.cuda.is_available():
+    from tests.hipmem import gpu_present
+    if gpu_present():
         pytest.skip("GPU present: covered by the gpu test")
     exe = build_driver(tmp_path, ekf_mod, robot_h)
     scen = tmp_path / "s.txt"

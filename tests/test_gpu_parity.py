@@ -494,3 +494,42 @@ def test_wave_flush_equals_drained(ekf_mod, monkeypatch, prec, N, T, lines, extr
         assert bad.size == 0, (e, bad[:12].tolist(), rel(Pa, Pb))
         np.testing.assert_array_equal(ya, yb)
         assert sa == sb
+
+
+@pytest.mark.parametrize("N,T,lines,extra_every", [(80, 4, 8, 0), (80, 4, 6, 3), (64, 3, 6, 2), (100, 2, 8, 0),
+                                                   (96, 1, 5, 0)])
+def test_f64_wave_flush_equals_tile_kernel(ekf_mod, monkeypatch, N, T, lines, extra_every):
+    """fp64 storage: the wave flush (1 × 2-tile wave-tiles, every k-step run over the −0·(+0)
+    operand padding; default for groups of ≤ 4 steps) gives bit-identical state to the per-tile
+    downdate_f64_kernel (EKF_FLUSH_VARIANT=2) flushed after every scan — fast loop, predicated
+    partial downdates, and the general loop for groups with augmentation rows or the reset."""
+    E = 3
+    w = G.make_world(N, active=N - 14 if extra_every else N - 10)
+    st = G.initial_state(w)
+    a = ekf_mod.Ensemble(N, E, 0, max_lines=8, flush_interval=T)
+    monkeypatch.setenv("EKF_FLUSH_VARIANT", "2")
+    b = ekf_mod.Ensemble(N, E, 0, max_lines=8)
+    monkeypatch.delenv("EKF_FLUSH_VARIANT")
+    for ens in (a, b):
+        for e in range(E):
+            ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+    rng = np.random.default_rng(9)
+    for step in range(1, 3 * T + 2):
+        enc, ln, nl = G.make_scan(w, step, instances=E, lines=lines)
+        if extra_every and step % extra_every == 0:
+            ex = G.random_lines(rng, 2)[None].repeat(E, axis=0)
+            ln = np.concatenate([ln, ex], axis=1)
+            nl = np.full(E, ln.shape[1], dtype=np.int32)
+        ra = a.localize(enc, ln, nl)
+        rb = b.localize(enc, ln, nl)
+        b.download_state(0, with_P=False)
+        for e in range(E):
+            assert ra[e]["match"] == rb[e]["match"], (step, e)
+            assert ra[e]["status"] == 0
+    for e in range(E):
+        Pa, ya, sa, pa = a.download_state(e)
+        Pb, yb, sb, pb = b.download_state(e)
+        bad = np.argwhere(Pa != Pb)
+        assert bad.size == 0, (e, bad[:12].tolist(), rel(Pa, Pb))
+        np.testing.assert_array_equal(ya, yb)
+        assert sa == sb

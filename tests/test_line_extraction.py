@@ -152,8 +152,8 @@ def test_extraction_segments_and_sort_edge_cases(tmp_path, ekf_mod):
 
 
 def test_config1_driver_fails_loudly_without_gpu(tmp_path, ekf_mod):
-    import torch
-    if torch.cuda.is_available():
+    from tests.hipmem import gpu_present
+    if gpu_present():
         pytest.skip("GPU present: covered by the gpu test")
     exe = build(tmp_path, ekf_mod)
     out = run(exe, "slam", scenario(tmp_path, trajectory(2)))
