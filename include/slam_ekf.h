@@ -45,6 +45,10 @@ enum {
                               symmetric storage keeps the upper triangle. */
     EKF_ST_SYNC_TIMEOUT = 8, /* the instance's cooperating workgroups did not all arrive at an
                                 exchange within the spin bound (results of that call invalid) */
+    EKF_ST_RANGE = 16,     /* EKF_PREC_F16 only: a landmark this call added has a variance above a
+                              quarter of the fp16 range at the instance's storage exponent
+                              (2^exp·P stored; values are still finite). ekf_rescale re-chooses
+                              the exponent; ignoring it lets later landmarks saturate to ±inf. */
 };
 
 /* storage precision of the landmark-landmark covariance block (robot rows, mean: always fp64).
@@ -135,6 +139,15 @@ int ekf_download_state(ekf_ctx* ctx, int e, double* P_full, double* y, int* save
 /* Device-side initialisation P = diag(d) + U·Uᵀ (U: n×rank row-major, host pointers). */
 int ekf_init_lowrank(ekf_ctx* ctx, int e, const double* diag, const double* U, int rank,
                      const double* y, int saved, const double pose[3]);
+/* EKF_PREC_F16 storage exponent: the landmark block is stored as fp16(2^exp·P). Upload and
+ * init_lowrank choose it from the largest landmark variance v (exp = min(10, ⌊log2(4096/v)⌋),
+ * at least -24; 10 for an empty map); ekf_rescale(ctx, e, EKF_EXP_AUTO) re-chooses it from the
+ * current P (EKF_ST_RANGE), or sets the given exponent. Power-of-two rescaling is exact except
+ * for values that leave fp16's normal range. For f32 / f64 storage the exponent is 0 and
+ * rescale is a no-op. */
+#define EKF_EXP_AUTO (-1000)
+int ekf_storage_exponent(const ekf_ctx* ctx, int e);
+int ekf_rescale(ekf_ctx* ctx, int e, int exp);
 /* P_t0[0:3,0:3] of instance e (what getEllipse reads, Robot.cpp:75-77). */
 int ekf_get_pose_cov(ekf_ctx* ctx, int e, double P33[9]);
 /* Robot::getEllipse(axii, angle) (Robot.h:73, Robot.cpp:73-124): axii sorted by |eigenvalue|,

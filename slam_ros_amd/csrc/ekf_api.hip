@@ -80,6 +80,8 @@ struct ekf_ctx {
     int* sync;
     int sync_stride;
     unsigned long long* dbg;  // association-kernel phase timers (EKF_SCAN_STAMPS=1)
+    int* pexp;                // [E] fp16 storage exponents (device), host copy below
+    std::vector<int> pexp_h;
     // flush scheduling (see the top of this file)
     int T;                    // flush interval
     long long nsteps;         // update steps enqueued
@@ -143,7 +145,7 @@ int ekf_abi_version(void) { return SLAM_EKF_ABI_VERSION; }
 static void free_all(ekf_ctx* c)
 {
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->pose, c->xpre, c->saved, c->D,
-                               c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->mbox,
+                               c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->pexp, c->mbox,
                                c->sync, c->Ust, c->Vst};
     for (auto& sl : c->ring) {
         ptrs.push_back(sl.Uop);
@@ -186,6 +188,23 @@ static int drain(ekf_ctx* c)
 
 static inline int cur_buf(const ekf_ctx* c) { return c->last_out; }
 
+static int set_exponent(ekf_ctx* c, int e, int ex)
+{
+    c->pexp_h[e] = ex;
+    HIP_TRY(hipMemcpy(c->pexp + e, &ex, sizeof(int), hipMemcpyHostToDevice));
+    return EKF_OK;
+}
+
+// fp16 storage exponent for a landmark block whose largest variance is vmax: the largest
+// 2^x <= 2^10 with 2^x·vmax <= 2^12 (16× below the fp16 range, 4× below the EKF_ST_RANGE warning)
+static int choose_exponent(const ekf_ctx* c, double vmax)
+{
+    if (c->cfg.precision != EKF_PREC_F16) return 0;
+    if (!(vmax > 0.0) || !std::isfinite(vmax)) return ekf::F16_EXP_DEFAULT;
+    const int x = (int)std::floor(std::log2(4096.0 / vmax));
+    return std::max(-24, std::min(ekf::F16_EXP_DEFAULT, x));
+}
+
 static int set_robot_ctor(ekf_ctx* c, int e, double x, double y, double th)
 {
     // Robot::Robot (Robot.cpp:20-35): P_t0[0][0] = P_t0[1][1] = 0.05, P_t0[2][2] = 0, the rest
@@ -206,7 +225,7 @@ static int set_robot_ctor(ekf_ctx* c, int e, double x, double y, double th)
     const int zero = 0;
     HIP_TRY(hipMemcpyAsync(c->saved + e, &zero, sizeof(int), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    return EKF_OK;
+    return set_exponent(c, e, c->cfg.precision == EKF_PREC_F16 ? ekf::F16_EXP_DEFAULT : 0);
 }
 
 extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
@@ -278,6 +297,8 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     ALLOC(c->d_enc, sizeof(double) * 3 * E);
     ALLOC(c->d_lines, sizeof(ekf_line) * d.max_lines * E);
     ALLOC(c->d_nlines, sizeof(int) * E);
+    ALLOC(c->pexp, sizeof(int) * E);
+    c->pexp_h.assign(E, 0);
     c->G = (d.N + ekf::SCAN_THREADS - 1) / ekf::SCAN_THREADS;
     // whole 128-B lines: the package words, then 16 words for the speculative list words
     c->mbw = ((ekf::MB_WORDS_FIXED + 4 * d.max_lines + 15) / 16) * 16 + 16;
@@ -528,6 +549,7 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.lines = lines;
     p.nlines = nlines;
     p.dbg = c->dbg;
+    p.pexp = c->pexp;
     p.G = c->G;
     p.mbw = c->mbw;
     p.spec = c->spec;
@@ -581,6 +603,7 @@ static int enqueue_flush(ekf_ctx* c)
     dp.nwt = c->nwt;
     dp.wt64 = c->wt64;
     dp.nwt64 = c->nwt64;
+    dp.pexp = c->pexp;
     for (int q = 0; q < nst; q++) dp.steps[q] = slot_of(c, c->unflushed0 + q);
     const int in = c->last_out;
     const int out = c->cfg.pipeline ? 1 - in : in;
@@ -748,6 +771,11 @@ extern "C" int ekf_upload_state(ekf_ctx* c, int e, const double* P, const double
     if (rc) return rc;
     const Dims& d = c->d;
     if (P) {
+        double vmax = 0.0;
+        if (c->cfg.precision == EKF_PREC_F16)
+            for (int i = 3; i < d.n; i++) vmax = std::max(vmax, std::fabs(P[(size_t)i * d.n + i]));
+        rc = set_exponent(c, e, choose_exponent(c, vmax));
+        if (rc) return rc;
         double* tmp = nullptr;
         HIP_TRY(hipMalloc((void**)&tmp, sizeof(double) * d.n * d.n));
         hipError_t err = hipMemcpyAsync(tmp, P, sizeof(double) * d.n * d.n, hipMemcpyHostToDevice,
@@ -755,7 +783,7 @@ extern "C" int ekf_upload_state(ekf_ctx* c, int e, const double* P, const double
         if (err == hipSuccess)
             err = ekf::launch_pack(d, c->cfg.precision, tmp,
                                    (char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem,
-                                   c->Rs + (size_t)e * 3 * d.n, c->tile_rc, c->stream);
+                                   c->Rs + (size_t)e * 3 * d.n, c->tile_rc, c->pexp_h[e], c->stream);
         if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
         (void)hipFree(tmp);
         HIP_TRY(err);
@@ -787,7 +815,7 @@ extern "C" int ekf_download_state(ekf_ctx* c, int e, double* P, double* y, int* 
         HIP_TRY(hipMalloc((void**)&tmp, sizeof(double) * d.n * d.n));
         hipError_t err = ekf::launch_unpack(d, c->cfg.precision, tmp,
                                             (const char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem,
-                                            c->Rs + (size_t)e * 3 * d.n, c->stream);
+                                            c->Rs + (size_t)e * 3 * d.n, c->pexp_h[e], c->stream);
         if (err == hipSuccess)
             err = hipMemcpyAsync(P, tmp, sizeof(double) * d.n * d.n, hipMemcpyDeviceToHost,
                                  c->stream);
@@ -815,6 +843,15 @@ extern "C" int ekf_init_lowrank(ekf_ctx* c, int e, const double* diag, const dou
     int rc = drain(c);
     if (rc) return rc;
     const Dims& d = c->d;
+    double vmax = 0.0;
+    if (c->cfg.precision == EKF_PREC_F16)
+        for (int i = 3; i < d.n; i++) {
+            double v = diag[i];
+            for (int k = 0; k < rank; k++) v += U[(size_t)i * rank + k] * U[(size_t)i * rank + k];
+            vmax = std::max(vmax, std::fabs(v));
+        }
+    rc = set_exponent(c, e, choose_exponent(c, vmax));
+    if (rc) return rc;
     double *dd = nullptr, *du = nullptr;
     HIP_TRY(hipMalloc((void**)&dd, sizeof(double) * d.n));
     hipError_t err = hipMalloc((void**)&du, sizeof(double) * d.n * (rank > 0 ? rank : 1));
@@ -825,12 +862,52 @@ extern "C" int ekf_init_lowrank(ekf_ctx* c, int e, const double* diag, const dou
     if (err == hipSuccess)
         err = ekf::launch_lowrank(d, c->cfg.precision, dd, du, rank,
                                   (char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem,
-                                  c->Rs + (size_t)e * 3 * d.n, c->tile_rc, c->stream);
+                                  c->Rs + (size_t)e * 3 * d.n, c->tile_rc, c->pexp_h[e], c->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
     (void)hipFree(dd);
     if (du) (void)hipFree(du);
     HIP_TRY(err);
     return ekf_upload_state(c, e, nullptr, y, saved, pose);
+}
+
+extern "C" int ekf_storage_exponent(const ekf_ctx* c, int e)
+{
+    if (!c) return 0;
+    if (e < 0 || e >= c->cfg.instances) return 0;
+    return c->pexp_h[e];
+}
+
+extern "C" int ekf_rescale(ekf_ctx* c, int e, int ex)
+{
+    if (!c) return EKF_EINVAL;
+    if (e < 0 || e >= c->cfg.instances) return EKF_ERANGE;
+    if (c->cfg.precision != EKF_PREC_F16) return EKF_OK;
+    if (ex != EKF_EXP_AUTO && (ex < -24 || ex > 24)) return EKF_ERANGE;
+    int rc = drain(c);
+    if (rc) return rc;
+    const Dims& d = c->d;
+    void* X = (char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem;
+    double* Rs = c->Rs + (size_t)e * 3 * d.n;
+    double* tmp = nullptr;
+    HIP_TRY(hipMalloc((void**)&tmp, sizeof(double) * d.n * d.n));
+    std::vector<double> dg(d.n);
+    hipError_t err = ekf::launch_unpack(d, c->cfg.precision, tmp, X, Rs, c->pexp_h[e], c->stream);
+    if (err == hipSuccess)   // the diagonal of the dense copy (stride n + 1)
+        err = hipMemcpy2DAsync(dg.data(), sizeof(double), tmp, sizeof(double) * (d.n + 1), sizeof(double),
+                               d.n, hipMemcpyDeviceToHost, c->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
+    if (err == hipSuccess) {
+        double vmax = 0.0;
+        for (int i = 3; i < d.n; i++) vmax = std::max(vmax, std::fabs(dg[i]));
+        rc = set_exponent(c, e, ex == EKF_EXP_AUTO ? choose_exponent(c, vmax) : ex);
+        if (rc == EKF_OK) {
+            err = ekf::launch_pack(d, c->cfg.precision, tmp, X, Rs, c->tile_rc, c->pexp_h[e], c->stream);
+            if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
+        }
+    }
+    (void)hipFree(tmp);
+    HIP_TRY(err);
+    return rc;
 }
 
 extern "C" int ekf_get_pose_cov(ekf_ctx* c, int e, double P33[9])

@@ -10,7 +10,10 @@ namespace ekf {
 
 enum { PHASE_PREDICT = 1, PHASE_UPDATE = 2, PHASE_BOTH = 3 };
 enum { EKF_ST_SINGULAR = EKF_ST_SINGULAR_S, EKF_ST_CAP = EKF_ST_CAPACITY, EKF_ST_NSYM = EKF_ST_NONSYM,
-       EKF_ST_TIMEOUT_BIT = EKF_ST_SYNC_TIMEOUT };
+       EKF_ST_TIMEOUT_BIT = EKF_ST_SYNC_TIMEOUT, EKF_ST_RANGE_BIT = EKF_ST_RANGE };
+// fp16 storage: a stored variance above 2^14 (a quarter of the fp16 range) raises EKF_ST_RANGE
+constexpr double F16_RANGE_WARN = 16384.0;
+constexpr int F16_EXP_DEFAULT = 10;
 
 // per-instance synchronisation words of the association kernel (never reset): a monotonic
 // start counter, then one status word per workgroup, rewritten by every launch
@@ -94,6 +97,7 @@ struct ScanParams {
     const double* enc;    // [E][3]
     const ekf_line* lines;// [E][max_lines]
     const int* nlines;    // [E]
+    const int* pexp;      // [E] fp16 storage exponent (P stored as 2^pexp·P)
     unsigned long long* dbg;  // optional [E][16] phase timers (s_memrealtime ticks, 100 MHz)
 };
 
@@ -116,6 +120,7 @@ struct DowndateParams {
     int nwt;
     const WtEntry* wt64;  // [nwt64] f64 wave-tiles of 1 × WT64_C tiles (tile[0..1], rows[0] = A row block)
     int nwt64;
+    const int* pexp;      // [E] fp16 storage exponent
     Slot steps[PMAX];
 };
 
@@ -123,11 +128,12 @@ hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st);
 int scan_blocks_per_cu(int precision);
 size_t scan_lds_bytes(int precision);   // static LDS of the association kernel
 hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st);
+// ex: fp16 storage exponent of the instance (ignored for f32 / f64)
 hipError_t launch_pack(const Dims& d, int precision, const double* Pfull, void* Pll, double* Rs,
-                       const int2* tile_rc, hipStream_t st);
+                       const int2* tile_rc, int ex, hipStream_t st);
 hipError_t launch_unpack(const Dims& d, int precision, double* Pfull, const void* Pll,
-                         const double* Rs, hipStream_t st);
+                         const double* Rs, int ex, hipStream_t st);
 hipError_t launch_lowrank(const Dims& d, int precision, const double* diag, const double* U,
-                          int rank, void* Pll, double* Rs, const int2* tile_rc, hipStream_t st);
+                          int rank, void* Pll, double* Rs, const int2* tile_rc, int ex, hipStream_t st);
 
 }  // namespace ekf

@@ -37,22 +37,21 @@ namespace ekf {
 // Storage type T of the landmark block → compute type C (MFMA / FMA chain) and tile layout L.
 // fp16 storage computes in fp32 on the f32 layout and rounds to fp16 after every step, in the
 // flush and in the on-read replay alike, so the stored value never depends on when it is flushed.
-// It holds 2^10·P (|P| < 64 representable, normal down to 6e-8, no subnormal loss for
-// landmark covariances). The fp16 path computes in that scaled domain throughout: the scan
-// writes the U operand scaled by 2^10 (exact), so flush and on-read replay both run
-// acc = 2^10·X − (2^10·U)·Vᵀ, bit-for-bit 2^10 × the unscaled chain, and round with two
+// It holds 2^x·P with a per-instance exponent x (ScanParams/DowndateParams::pexp, default 10:
+// |P| < 64 representable, normal down to 6e-8; chosen at upload from the largest landmark
+// variance, ekf_api.hip choose_exponent). The fp16 path computes in that scaled domain
+// throughout: the scan writes the U operand scaled by 2^x (exact), so flush and on-read replay
+// both run acc = 2^x·X − (2^x·U)·Vᵀ, bit-for-bit 2^x × the unscaled chain, and round with two
 // conversions per element; values leave the scaled domain only where they are read as P.
 template <typename T> struct Stor {
     using C = T;
     using L = T;
     static constexpr bool half = false;
-    static constexpr float scale = 1.f;
 };
 template <> struct Stor<_Float16> {
     using C = float;
     using L = float;
     static constexpr bool half = true;
-    static constexpr float scale = 1024.f;
 };
 
 template <typename T>
@@ -82,18 +81,29 @@ __device__ __forceinline__ typename Stor<T>::C round_step(typename Stor<T>::C x)
     }
 }
 
-// P value (fp64) → scaled compute domain, and back
+// P value (fp64) → scaled compute domain (exponent ex, fp16 storage only), and back: power-of-two
+// scalings, exact in fp32 / fp64
 template <typename T>
-__device__ __forceinline__ typename Stor<T>::C to_domain(double v)
+__device__ __forceinline__ typename Stor<T>::C to_domain(double v, int ex)
 {
     using C = typename Stor<T>::C;
-    return (C)v * (C)Stor<T>::scale;
+    if constexpr (Stor<T>::half) return ldexpf((C)v, ex);
+    else return (C)v;
 }
 
 template <typename T>
-__device__ __forceinline__ double from_domain(typename Stor<T>::C x)
+__device__ __forceinline__ double from_domain(typename Stor<T>::C x, int ex)
 {
-    return (double)x * (1.0 / (double)Stor<T>::scale);
+    if constexpr (Stor<T>::half) return ldexp((double)x, -ex);
+    else return (double)x;
+}
+
+// the storage exponent of instance e (0 unless fp16)
+template <typename T>
+__device__ __forceinline__ int storage_exp(const int* pexp, int e)
+{
+    if constexpr (Stor<T>::half) return pexp[e];
+    else return 0;
 }
 
 __device__ __forceinline__ double normalize_radian(double rad)
@@ -138,14 +148,6 @@ __device__ __forceinline__ bool lu_invert2(const double S[4], double Si[4])
     return true;
 }
 
-template <typename T>
-__device__ __forceinline__ void ll_store_sym(T* P, int i, int j, int nb, double v)
-{
-    using L = typename Stor<T>::L;
-    P[ll_offset<L>(i, j, nb)] = to_store<T>(to_domain<T>(v));
-    if ((i >> 5) == (j >> 5) && i != j) P[ll_offset<L>(j, i, nb)] = to_store<T>(to_domain<T>(v));
-}
-
 // ---------------------------------------------------------------------------------------
 // Landmark block as seen by a step: X plus the pending (not yet flushed) steps, in order.
 // ---------------------------------------------------------------------------------------
@@ -154,6 +156,7 @@ struct PllView {
     const T* X;
     int nb, kmax, M, max_lines;
     int e;            // instance
+    int ex;           // storage exponent of instance e (fp16)
     size_t opstride;  // operand elements per instance
     int npend;        // pending steps (oldest first)
     const Slot* pend;
@@ -216,11 +219,11 @@ __device__ __forceinline__ void patch_block(const PllView<T>& v, const Slot& sq,
             raw[2] = prw[i0 + 1]; raw[3] = prw[v.M + i0 + 1];
         }
         if (swap) {
-            acc[0] = round_step<T>(to_domain<T>(raw[0])); acc[1] = round_step<T>(to_domain<T>(raw[2]));
-            acc[2] = round_step<T>(to_domain<T>(raw[1])); acc[3] = round_step<T>(to_domain<T>(raw[3]));
+            acc[0] = round_step<T>(to_domain<T>(raw[0], v.ex)); acc[1] = round_step<T>(to_domain<T>(raw[2], v.ex));
+            acc[2] = round_step<T>(to_domain<T>(raw[1], v.ex)); acc[3] = round_step<T>(to_domain<T>(raw[3], v.ex));
         } else {
-            acc[0] = round_step<T>(to_domain<T>(raw[0])); acc[1] = round_step<T>(to_domain<T>(raw[1]));
-            acc[2] = round_step<T>(to_domain<T>(raw[2])); acc[3] = round_step<T>(to_domain<T>(raw[3]));
+            acc[0] = round_step<T>(to_domain<T>(raw[0], v.ex)); acc[1] = round_step<T>(to_domain<T>(raw[1], v.ex));
+            acc[2] = round_step<T>(to_domain<T>(raw[2], v.ex)); acc[3] = round_step<T>(to_domain<T>(raw[3], v.ex));
         }
     }
 }
@@ -330,11 +333,11 @@ __device__ __forceinline__ void pll_blocks(const PllView<T>& v, int i0, const in
 #pragma unroll
     for (int b = 0; b < B; b++) {
         if (swap[b]) {
-            out[b][0] = from_domain<T>(acc[b][0]); out[b][1] = from_domain<T>(acc[b][2]);
-            out[b][2] = from_domain<T>(acc[b][1]); out[b][3] = from_domain<T>(acc[b][3]);
+            out[b][0] = from_domain<T>(acc[b][0], v.ex); out[b][1] = from_domain<T>(acc[b][2], v.ex);
+            out[b][2] = from_domain<T>(acc[b][1], v.ex); out[b][3] = from_domain<T>(acc[b][3], v.ex);
         } else {
-            out[b][0] = from_domain<T>(acc[b][0]); out[b][1] = from_domain<T>(acc[b][1]);
-            out[b][2] = from_domain<T>(acc[b][2]); out[b][3] = from_domain<T>(acc[b][3]);
+            out[b][0] = from_domain<T>(acc[b][0], v.ex); out[b][1] = from_domain<T>(acc[b][1], v.ex);
+            out[b][2] = from_domain<T>(acc[b][2], v.ex); out[b][3] = from_domain<T>(acc[b][3], v.ex);
         }
     }
 }
@@ -1046,7 +1049,7 @@ __device__ __forceinline__ void staged_blocks(const PllView<T>& v, int j, const 
 #pragma unroll
     for (int b = 0; b < NB; b++)
 #pragma unroll
-        for (int k = 0; k < 4; k++) out[b][k] = from_domain<T>(r[b][k]);
+        for (int k = 0; k < 4; k++) out[b][k] = from_domain<T>(r[b][k], v.ex);
 }
 
 // Block (2·wa, 2·wb) of the landmark block with the pending steps applied, when both landmarks
@@ -1100,11 +1103,11 @@ __device__ __forceinline__ void staged_pair_block(const PllView<T>& v, int wa, i
         if (cw.z > 0) patch_block<T>(v, v.pend[q], cw, i0, jb, swap, acc);
     }
     if (swap) {
-        out[0] = from_domain<T>(acc[0]); out[1] = from_domain<T>(acc[2]);
-        out[2] = from_domain<T>(acc[1]); out[3] = from_domain<T>(acc[3]);
+        out[0] = from_domain<T>(acc[0], v.ex); out[1] = from_domain<T>(acc[2], v.ex);
+        out[2] = from_domain<T>(acc[1], v.ex); out[3] = from_domain<T>(acc[3], v.ex);
     } else {
-        out[0] = from_domain<T>(acc[0]); out[1] = from_domain<T>(acc[1]);
-        out[2] = from_domain<T>(acc[2]); out[3] = from_domain<T>(acc[3]);
+        out[0] = from_domain<T>(acc[0], v.ex); out[1] = from_domain<T>(acc[1], v.ex);
+        out[2] = from_domain<T>(acc[2], v.ex); out[3] = from_domain<T>(acc[3], v.ex);
     }
 }
 
@@ -1284,6 +1287,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     pv.M = M;
     pv.max_lines = d.max_lines;
     pv.e = e;
+    pv.ex = storage_exp<T>(p.pexp, e);
     pv.opstride = opstride;
     pv.npend = p.npend;
     pv.pend = p.pend;
@@ -1316,7 +1320,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         if (staged) {
             // the guess only needs it approximately: the last flushed value (exact one below)
 #pragma unroll
-            for (int a = 0; a < 4; a++) Dj[a] = from_domain<T>(dj0[a]);
+            for (int a = 0; a < 4; a++) Dj[a] = from_domain<T>(dj0[a], pv.ex);
         } else {
             pll_block(pv, 2 * j, 2 * j, Dj);
         }
@@ -1339,8 +1343,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         for (int pp = 0; pp < 2; pp++) {
             const int lr = 2 * j + pp;
             if constexpr (sizeof(C) == 4) {
-                Uop[op_index_f32(lr, 2 * t, d.kmax)] = to_domain<T>(-uu[2 * pp]);
-                Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = to_domain<T>(-uu[2 * pp + 1]);
+                Uop[op_index_f32(lr, 2 * t, d.kmax)] = to_domain<T>(-uu[2 * pp], pv.ex);
+                Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = to_domain<T>(-uu[2 * pp + 1], pv.ex);
                 Vop[op_index_f32(lr, 2 * t, d.kmax)] = (C)kk[2 * pp];
                 Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (C)kk[2 * pp + 1];
             } else {
@@ -1973,6 +1977,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         for (int k = 0; k < 3; k++) gsum += GP[a * 3 + k] * Gx[b * 3 + k];
                         const double h = GlR[a * 2 + 0] * Gl[b * 2 + 0] + GlR[a * 2 + 1] * Gl[b * 2 + 1];
                         pdiag[q * 4 + a * 2 + b] = gsum + h;
+                        // fp16 storage: the new landmark's variances bound its whole row and
+                        // column (|P_ij| <= sqrt(P_ii P_jj)), and downdates only shrink them
+                        if (Stor<T>::half && fabs(ldexp(gsum + h, pv.ex)) > F16_RANGE_WARN)
+                            status |= EKF_ST_RANGE_BIT;
                     }
             }
         }
@@ -2270,7 +2278,7 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_sb_kernel(DowndateParams
                     const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
                     const int hi = max(row >> 1, col >> 1);
                     if (hi >= s.s0 && hi < s.s0 + s.nadd)
-                        acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s.s0, row, col)));
+                        acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s.s0, row, col), storage_exp<TS>(p.pexp, e)));
                 }
             }
             const f32x16 t0 = acc[0];
@@ -2536,6 +2544,7 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
                 if ((cur.sbj + 1) * P2_C * 16 <= s0 || cur.sbj * P2_C * 16 >= s0 + nadd) return;
                 const double* prw0 = p.steps[q].patch + (size_t)e * d.max_lines * 2 * d.M;
                 const double* pdg = p.steps[q].patch_diag + (size_t)e * d.max_lines * 4;
+                const int ex = storage_exp<TS>(p.pexp, e);
 #pragma nounroll
                 for (int c = 0; c < P2_C; c++) {
                     const int bj = cur.sbj * P2_C + c;
@@ -2546,7 +2555,7 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
                             const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
                             const int hi = max(row >> 1, col >> 1);
                             if (hi >= s0 && hi < s0 + nadd)
-                                acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s0, row, col)));
+                                acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s0, row, col), ex));
                         }
                     }
                     const f32x16 t0 = acc[0];
@@ -2938,6 +2947,7 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
             if (nadd <= 0 || (wc + 1) * WT_C * 16 <= s0 || wc * WT_C * 16 >= s0 + nadd) continue;
             const double* prw0 = p.steps[q].patch + (size_t)t.e * d.max_lines * 2 * d.M;
             const double* pdg = p.steps[q].patch_diag + (size_t)t.e * d.max_lines * 4;
+            const int ex = storage_exp<TS>(p.pexp, t.e);
 #pragma nounroll
             for (int i = 0; i < WT_N; i++) {
                 const int bi = wr * WT_R + i / WT_C, bj = wc * WT_C + i % WT_C;
@@ -2948,7 +2958,7 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
                         const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
                         const int hi = max(row >> 1, col >> 1);
                         if (hi >= s0 && hi < s0 + nadd)
-                            acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s0, row, col)));
+                            acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s0, row, col), ex));
                     }
                 }
                 const f32x16 t0 = acc[0];
@@ -3310,7 +3320,7 @@ __device__ __forceinline__ void tile_rc_of(int rem, int& r, int& c)
 
 template <typename T>
 __global__ void pack_kernel(Dims d, const double* __restrict__ Pfull, T* __restrict__ Pll,
-                            double* __restrict__ Rs, const int2* __restrict__ tile_rc)
+                            double* __restrict__ Rs, const int2* __restrict__ tile_rc, int ex)
 {
     const int64_t total = d.ntiles * TILE_ELEMS;
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
@@ -3322,7 +3332,7 @@ __global__ void pack_kernel(Dims d, const double* __restrict__ Pfull, T* __restr
         const int i = rc.x * TILE + r, j = rc.y * TILE + c;
         double v = 0.0;
         if (i < d.M && j < d.M) v = Pfull[(size_t)(3 + i) * d.n + (3 + j)];
-        Pll[g] = to_store<T>(to_domain<T>(v));
+        Pll[g] = to_store<T>(to_domain<T>(v, ex));
     }
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < 3 * (int64_t)d.n;
          g += (int64_t)gridDim.x * blockDim.x) {
@@ -3333,7 +3343,7 @@ __global__ void pack_kernel(Dims d, const double* __restrict__ Pfull, T* __restr
 
 template <typename T>
 __global__ void unpack_kernel(Dims d, double* __restrict__ Pfull, const T* __restrict__ Pll,
-                              const double* __restrict__ Rs)
+                              const double* __restrict__ Rs, int ex)
 {
     const int64_t total = (int64_t)d.n * d.n;
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
@@ -3342,7 +3352,7 @@ __global__ void unpack_kernel(Dims d, double* __restrict__ Pfull, const T* __res
         double v;
         if (a < 3) v = Rs[(size_t)a * d.n + b];
         else if (b < 3) v = Rs[(size_t)b * d.n + a];
-        else v = from_domain<T>(from_store<T>(Pll[ll_offset<typename Stor<T>::L>(a - 3, b - 3, d.nb)]));
+        else v = from_domain<T>(from_store<T>(Pll[ll_offset<typename Stor<T>::L>(a - 3, b - 3, d.nb)]), ex);
         Pfull[g] = v;
     }
 }
@@ -3350,7 +3360,7 @@ __global__ void unpack_kernel(Dims d, double* __restrict__ Pfull, const T* __res
 template <typename T>
 __global__ void lowrank_kernel(Dims d, const double* __restrict__ diag,
                                const double* __restrict__ U, int rank, T* __restrict__ Pll,
-                               double* __restrict__ Rs, const int2* __restrict__ tile_rc)
+                               double* __restrict__ Rs, const int2* __restrict__ tile_rc, int ex)
 {
     const int64_t total = d.ntiles * TILE_ELEMS;
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
@@ -3367,7 +3377,7 @@ __global__ void lowrank_kernel(Dims d, const double* __restrict__ diag,
             for (int k = 0; k < rank; k++) v += ui[k] * uj[k];
             if (i == j) v += diag[3 + i];
         }
-        Pll[g] = to_store<T>(to_domain<T>(v));
+        Pll[g] = to_store<T>(to_domain<T>(v, ex));
     }
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < 3 * (int64_t)d.n;
          g += (int64_t)gridDim.x * blockDim.x) {
@@ -3480,50 +3490,50 @@ static int grid_for(int64_t work, int block)
 }
 
 hipError_t launch_pack(const Dims& d, int precision, const double* Pfull, void* Pll, double* Rs,
-                       const int2* tile_rc, hipStream_t st)
+                       const int2* tile_rc, int ex, hipStream_t st)
 {
     const int grid = grid_for(d.ntiles * TILE_ELEMS, 256);
     if (precision == EKF_PREC_F64)
         hipLaunchKernelGGL(pack_kernel<double>, dim3(grid), dim3(256), 0, st, d, Pfull,
-                           (double*)Pll, Rs, tile_rc);
+                           (double*)Pll, Rs, tile_rc, ex);
     else if (precision == EKF_PREC_F16)
         hipLaunchKernelGGL(pack_kernel<_Float16>, dim3(grid), dim3(256), 0, st, d, Pfull,
-                           (_Float16*)Pll, Rs, tile_rc);
+                           (_Float16*)Pll, Rs, tile_rc, ex);
     else
         hipLaunchKernelGGL(pack_kernel<float>, dim3(grid), dim3(256), 0, st, d, Pfull,
-                           (float*)Pll, Rs, tile_rc);
+                           (float*)Pll, Rs, tile_rc, ex);
     return hipGetLastError();
 }
 
 hipError_t launch_unpack(const Dims& d, int precision, double* Pfull, const void* Pll,
-                         const double* Rs, hipStream_t st)
+                         const double* Rs, int ex, hipStream_t st)
 {
     const int grid = grid_for((int64_t)d.n * d.n, 256);
     if (precision == EKF_PREC_F64)
         hipLaunchKernelGGL(unpack_kernel<double>, dim3(grid), dim3(256), 0, st, d, Pfull,
-                           (const double*)Pll, Rs);
+                           (const double*)Pll, Rs, ex);
     else if (precision == EKF_PREC_F16)
         hipLaunchKernelGGL(unpack_kernel<_Float16>, dim3(grid), dim3(256), 0, st, d, Pfull,
-                           (const _Float16*)Pll, Rs);
+                           (const _Float16*)Pll, Rs, ex);
     else
         hipLaunchKernelGGL(unpack_kernel<float>, dim3(grid), dim3(256), 0, st, d, Pfull,
-                           (const float*)Pll, Rs);
+                           (const float*)Pll, Rs, ex);
     return hipGetLastError();
 }
 
 hipError_t launch_lowrank(const Dims& d, int precision, const double* diag, const double* U,
-                          int rank, void* Pll, double* Rs, const int2* tile_rc, hipStream_t st)
+                          int rank, void* Pll, double* Rs, const int2* tile_rc, int ex, hipStream_t st)
 {
     const int grid = grid_for(d.ntiles * TILE_ELEMS, 256);
     if (precision == EKF_PREC_F64)
         hipLaunchKernelGGL(lowrank_kernel<double>, dim3(grid), dim3(256), 0, st, d, diag, U,
-                           rank, (double*)Pll, Rs, tile_rc);
+                           rank, (double*)Pll, Rs, tile_rc, ex);
     else if (precision == EKF_PREC_F16)
         hipLaunchKernelGGL(lowrank_kernel<_Float16>, dim3(grid), dim3(256), 0, st, d, diag, U,
-                           rank, (_Float16*)Pll, Rs, tile_rc);
+                           rank, (_Float16*)Pll, Rs, tile_rc, ex);
     else
         hipLaunchKernelGGL(lowrank_kernel<float>, dim3(grid), dim3(256), 0, st, d, diag, U,
-                           rank, (float*)Pll, Rs, tile_rc);
+                           rank, (float*)Pll, Rs, tile_rc, ex);
     return hipGetLastError();
 }
 

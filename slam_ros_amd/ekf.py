@@ -21,7 +21,8 @@ from . import build as _build
 EKF_MAX_LINES = 64
 PREC_F64, PREC_F32, PREC_F16 = 0, 1, 2
 R_INTENDED, R_AS_WRITTEN = 0, 1
-ST_SINGULAR_S, ST_CAPACITY, ST_NONSYM, ST_SYNC_TIMEOUT = 1, 2, 4, 8
+ST_SINGULAR_S, ST_CAPACITY, ST_NONSYM, ST_SYNC_TIMEOUT, ST_RANGE = 1, 2, 4, 8, 16
+EXP_AUTO = -1000
 
 LIB_PATH = _build.LIB_PATH
 
@@ -30,7 +31,7 @@ EXPORTED = [
     "ekf_config_init", "ekf_strerror", "ekf_abi_version", "ekf_create", "ekf_destroy",
     "ekf_set_stream", "ekf_sync", "ekf_reset_instance", "ekf_localize", "ekf_localize_device",
     "ekf_predict", "ekf_update", "ekf_read_results", "ekf_upload_state", "ekf_download_state",
-    "ekf_init_lowrank", "ekf_get_pose_cov", "ekf_get_ellipse", "ekf_ellipse_of_block",
+    "ekf_init_lowrank", "ekf_storage_exponent", "ekf_rescale", "ekf_get_pose_cov", "ekf_get_ellipse", "ekf_ellipse_of_block",
     "ekf_landmark_block_bytes",
     "ekf_state_dim", "ekf_profile_enable", "ekf_profile_read", "ekf_profile_flushes",
     "ekf_flush_kernel_name", "ekf_debug_scan_stamps", "ekf_debug_result_words",
@@ -101,6 +102,8 @@ def load_library(path: str = ""):
         "ekf_download_state": (ctypes.c_int, [vp, ctypes.c_int, dp, dp, ip, dp]),
         "ekf_init_lowrank": (ctypes.c_int, [vp, ctypes.c_int, dp, dp, ctypes.c_int, dp,
                                             ctypes.c_int, dp]),
+        "ekf_storage_exponent": (ctypes.c_int, [vp, ctypes.c_int]),
+        "ekf_rescale": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int]),
         "ekf_get_pose_cov": (ctypes.c_int, [vp, ctypes.c_int, dp]),
         "ekf_get_ellipse": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(ctypes.c_float)]),
@@ -272,6 +275,14 @@ class Ensemble:
         _check(self._lib.ekf_download_state(self._h, e, _dp(P), _dp(y), ctypes.byref(saved), _dp(pose)),
                "ekf_download_state")
         return P, y, saved.value, pose
+
+    def storage_exponent(self, e: int = 0) -> int:
+        """fp16 storage: the landmark block holds fp16(2^exp·P); 0 for f32 / f64."""
+        return int(self._lib.ekf_storage_exponent(self._h, e))
+
+    def rescale(self, e: int = 0, exp: int = EXP_AUTO):
+        """Re-choose (or set) instance e's fp16 storage exponent (after ST_RANGE)."""
+        _check(self._lib.ekf_rescale(self._h, e, int(exp)), "ekf_rescale")
 
     def pose_cov(self, e: int = 0) -> np.ndarray:
         out = np.zeros(9)

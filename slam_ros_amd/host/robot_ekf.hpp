@@ -191,6 +191,8 @@ private:
             std::fprintf(stderr, "slam_ekf: landmark capacity exceeded\n");
         if (res.status & EKF_ST_SYNC_TIMEOUT)
             std::fprintf(stderr, "slam_ekf: association exchange timed out\n");
+        if (res.status & EKF_ST_RANGE)   // fp16 storage near its range: re-choose the exponent
+            report(ekf_rescale(ctx_, 0, EKF_EXP_AUTO), "ekf_rescale");
         xPos = res.pose[0];
         yPos = res.pose[1];
         thetaPos = res.pose[2];

@@ -1,0 +1,140 @@
+"""fp16 storage range (EKF_PREC_F16, BASELINE config 5): the landmark block is stored as
+fp16(2^x·P) with a per-instance exponent x, chosen at upload from the largest landmark variance
+(x = min(10, ⌊log2(4096/v)⌋)), raised EKF_ST_RANGE when a scan adds a landmark whose variance
+passes 2^14 at that exponent, and re-chosen by ekf_rescale.
+
+Parity: per scan from the identical stored state against the CPU restatement (oracle/), P within
+the fp16 bound of tests/test_gpu_parity.py (1e-3 relative Frobenius), association identical.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from slam_ros_amd import scan_gen as G
+
+pytestmark = pytest.mark.gpu
+
+P_TOL16 = 1e-3
+
+
+def rel(a, b):
+    nb = np.linalg.norm(b)
+    return np.linalg.norm(a - b) / (nb if nb > 0 else 1.0)
+
+
+def f16_round(P, x):
+    return np.ldexp(np.ldexp(P.astype(np.float32), x).astype(np.float16).astype(np.float64), -x)
+
+
+@pytest.mark.parametrize("vmax", [0.5, 100.0, 3000.0, 2.0e6])
+def test_upload_chooses_exponent(ekf_mod, vmax):
+    """|P| well above 64 (the fixed 2^10 scale's limit) round-trips at the chosen exponent."""
+    N = 40
+    n = 3 + 2 * N
+    rng = np.random.default_rng(7)
+    A = rng.normal(size=(n, n))
+    P = A @ A.T
+    P = (P + P.T) / 2
+    P *= vmax / np.max(np.diag(P)[3:])
+    ens = ekf_mod.Ensemble(N, 2, ekf_mod.PREC_F16)
+    assert ens.storage_exponent(0) == 10 and ens.storage_exponent(1) == 10
+    ens.upload_state(1, P, np.zeros(n), N // 2, [0.0, 0.0, 0.0])
+    x = ens.storage_exponent(1)
+    assert x == min(10, math.floor(math.log2(4096.0 / vmax)))
+    assert ens.storage_exponent(0) == 10
+    Pg = ens.download_state(1)[0]
+    assert np.all(np.isfinite(Pg))
+    np.testing.assert_array_equal(Pg[:3], P[:3])
+    np.testing.assert_array_equal(Pg[3:, 3:], f16_round(P[3:, 3:], x))
+    assert rel(Pg, P) <= P_TOL16
+    # explicit exponent, then back to the automatic choice: power-of-two rescaling is exact here
+    ens.rescale(1, x - 3)
+    assert ens.storage_exponent(1) == x - 3
+    np.testing.assert_array_equal(ens.download_state(1)[0], Pg)
+    ens.rescale(1)
+    assert ens.storage_exponent(1) == x
+    np.testing.assert_array_equal(ens.download_state(1)[0], Pg)
+    # f32 / f64 storage: exponent 0, rescale a no-op
+    e32 = ekf_mod.Ensemble(N, 1, ekf_mod.PREC_F32)
+    e32.upload_state(0, P, np.zeros(n), N // 2, [0.0, 0.0, 0.0])
+    assert e32.storage_exponent(0) == 0
+    e32.rescale(0, 5)
+    assert e32.storage_exponent(0) == 0
+
+
+def test_large_covariance_updates(ekf_mod, oracle_mod):
+    """Scans on a map whose landmark covariances are in the hundreds (2^x with x < 10)."""
+    N = 48
+    w = G.make_world(N, active=N - 12)
+    st = G.initial_state(w)
+    P0 = st.dense_P()
+    P0 *= 300.0 / np.max(np.diag(P0)[3:])      # landmark variances up to 300
+    ens = ekf_mod.Ensemble(N, 1, ekf_mod.PREC_F16, max_lines=8)
+    ens.upload_state(0, P0, st.y, st.saved, st.pose)
+    assert ens.storage_exponent(0) < 10
+    ref = oracle_mod.OracleRobot(N)
+    ref.set_state(*ens.download_state(0))
+    matched = 0
+    for step in range(1, 13):
+        enc, lines, _ = G.make_scan(w, step, lines=6)
+        res = ens.localize(enc, lines, [lines.shape[1]])[0]
+        m = ref.localize(lines[0], enc[0])
+        assert res["match"] == m, (step, res["match"], m)
+        assert res["status"] & ~ekf_mod.ST_RANGE == 0, res["status"]
+        P, y, s, pose = ens.download_state(0)
+        assert np.all(np.isfinite(P))
+        assert rel(P, ref.P_t0) <= P_TOL16, (step, rel(P, ref.P_t0))
+        np.testing.assert_allclose(y, ref.y, rtol=0, atol=1e-8 * np.linalg.norm(ref.y))
+        matched += sum(1 for j in m if j >= 0)
+        ref.set_state(P, y, s, pose)
+    assert matched >= 12
+
+
+def _match_free_run(ekf_mod, oracle_mod, rescale, nscans):
+    """A long trajectory of new lines only, with large encoder motions: the pose covariance and
+    with it every new landmark's variance grow past the fp16 range at 2^10 (to ≈500)."""
+    N = 24
+    ens = ekf_mod.Ensemble(N, 1, ekf_mod.PREC_F16, max_lines=8)
+    ref = oracle_mod.OracleRobot(N)
+    rng = np.random.default_rng(5)
+    log = []
+    for k in range(nscans):
+        enc = [ref.xPos + 1.0, ref.yPos + 0.6, ref.thetaPos + 0.05]
+        ln = G.random_lines(rng, 3)
+        res = ens.localize(enc, ln[None], [3])[0]
+        m = ref.localize(ln, enc)
+        P, y, s, pose = ens.download_state(0)
+        log.append(dict(k=k, status=res["status"], finite=bool(np.all(np.isfinite(P))),
+                        exp=ens.storage_exponent(0), match=res["match"], m=m,
+                        rel=rel(P, ref.P_t0) if np.all(np.isfinite(P)) else np.inf,
+                        vmax=float(np.max(np.diag(ref.P_t0)[3:])) if ref.savedLineCount else 0.0))
+        if rescale and res["status"] & ekf_mod.ST_RANGE:
+            ens.rescale(0)
+            P, y, s, pose = ens.download_state(0)
+        if not log[-1]["finite"]:
+            break
+        ref.set_state(P, y, s, pose)
+    return log
+
+
+def test_match_free_trajectory_rescales(ekf_mod, oracle_mod):
+    log = _match_free_run(ekf_mod, oracle_mod, True, 200)
+    assert len(log) == 200 and all(r["finite"] for r in log)
+    assert max(r["vmax"] for r in log) > 256          # far past the 2^10 scale's |P| < 64
+    assert any(r["status"] & ekf_mod.ST_RANGE for r in log)
+    assert min(r["exp"] for r in log) <= 4          # 10 → 8 → 6 → 4 as the variances pass 16, 64, 256
+    for r in log:
+        assert r["match"] == r["m"], r["k"]
+        assert r["status"] & ~ekf_mod.ST_RANGE == 0, (r["k"], r["status"])
+        assert r["rel"] <= P_TOL16, (r["k"], r["rel"])
+
+
+def test_match_free_trajectory_warns_before_saturating(ekf_mod, oracle_mod):
+    """Without rescaling the block eventually saturates to inf; EKF_ST_RANGE came first."""
+    log = _match_free_run(ekf_mod, oracle_mod, False, 200)
+    first_bad = next((r["k"] for r in log if not r["finite"]), None)
+    first_warn = next((r["k"] for r in log if r["status"] & ekf_mod.ST_RANGE), None)
+    assert first_warn is not None
+    assert first_bad is None or first_warn < first_bad, (first_warn, first_bad)
+    assert all(r["rel"] <= P_TOL16 for r in log if r["k"] < first_warn)
