@@ -185,47 +185,16 @@ def main():
         payload.copy_(torch.from_numpy(host))
     nlines = torch.full((E,), L_LINES, dtype=torch.int32, device=dev)
     # N > 1: rank 0 broadcasts B scans (all instances) per collective, one group ahead of the
-    # scans that use them; double-buffered receive groups
+    # scans that use them (slam_ros_amd/dist.py GroupedBroadcast)
     B = max(1, args.bcast_every or args.flush_interval)
-    recv = torch.empty((2, B, per_step), dtype=torch.float64, device=dev) if world > 1 else None
-    inflight = {}
-
     host_coll = world > 1 and args.dist_backend != "nccl"   # rehearsal: collectives on host tensors
-
-    class _Done:
-        def wait(self):
-            pass
-
-    def issue(gi):
-        if world == 1 or gi * B >= steps_total:
-            return
-        buf = recv[gi & 1]
-        cnt = min(B, steps_total - gi * B)
-        if host_coll:
-            torch.cuda.synchronize(dev)   # the group's previous user of this buffer is done
-            hb = (payload[gi * B: gi * B + cnt].cpu() if rank == 0
-                  else torch.empty((cnt, per_step), dtype=torch.float64))
-            D.broadcast_step(hb, dist, src=0)
-            buf[:cnt].copy_(hb[:cnt].to(dev))
-            inflight[gi] = _Done()
-            return
-        if rank == 0:
-            buf[:cnt].copy_(payload[gi * B: gi * B + cnt], non_blocking=True)
-        inflight[gi] = D.broadcast_async(buf, dist, src=0)
-
-    issue(0)
+    bc = D.GroupedBroadcast(payload, B, dist, rank, world, src=0, host_coll=host_coll,
+                            sync=lambda: torch.cuda.synchronize(dev))
+    bc.start()
     torch.cuda.synchronize(dev)
 
     def step(s):
-        if world == 1:
-            buf = payload[s]
-        else:
-            gi, k = divmod(s, B)
-            if k == 0:
-                inflight.pop(gi).wait()   # the current stream waits for this group's scans
-                issue(gi + 1)             # the next group's broadcast overlaps these steps
-            buf = recv[gi & 1][k]
-        base = buf.data_ptr()
+        base = bc.step_buffer(s).data_ptr()
         eo, lo = D.offsets(E_total, L_LINES, first)
         enc_ptr = base + eo * 8
         lines_ptr = base + lo * 8

@@ -62,3 +62,66 @@ def broadcast_async(buf, dist, src: int = 0):
     """Same for a group of steps, asynchronously; `.wait()` on the returned work orders the
     caller's current stream after it (NCCL/RCCL) or blocks until it is done (gloo)."""
     return dist.broadcast(buf, src=src, async_op=True)
+
+
+class GroupedBroadcast:
+    """The scan stream of bench.py's multi-rank run: rank `src` holds every step's payload
+    (`payload`, shape (steps_total, per_step)); groups of B consecutive steps go out in one
+    collective, issued one group ahead of the steps that consume them, into a double-buffered
+    receive area. Step s reads row s % B of group s // B:
+
+        gi, k = divmod(s, B)
+        k == 0: wait for group gi (NCCL/RCCL: the current stream waits; gloo: blocks), then issue
+                group gi + 1 into the other buffer (it overlaps group gi's steps)
+
+    Buffer reuse is ordered by construction: group gi + 1 overwrites the buffer group gi − 1's
+    steps read, and those were issued before it (stream order on the GPU; synchronous on CPU).
+    `host_coll`: the collective runs on host copies (gloo rehearsal of GPU ranks)."""
+
+    def __init__(self, payload, B: int, dist, rank: int, world: int, src: int = 0,
+                 host_coll: bool = False, sync=None):
+        self.payload, self.B, self.dist = payload, max(1, int(B)), dist
+        self.rank, self.world, self.src = rank, world, src
+        self.steps_total = payload.shape[0]
+        self.host_coll, self.sync = host_coll, sync
+        self.recv = payload.new_empty((2, self.B, payload.shape[1])) if world > 1 else None
+        self.inflight = {}
+        self.issued = []        # group indices in issue order (tests)
+
+    class _Done:
+        def wait(self):
+            pass
+
+    def issue(self, gi: int) -> None:
+        if self.world == 1 or gi * self.B >= self.steps_total:
+            return
+        import torch
+        B = self.B
+        buf = self.recv[gi & 1]
+        cnt = min(B, self.steps_total - gi * B)
+        self.issued.append(gi)
+        if self.host_coll:
+            if self.sync:
+                self.sync()     # the previous user of this buffer is done
+            hb = (self.payload[gi * B: gi * B + cnt].cpu() if self.rank == self.src
+                  else torch.empty((cnt, self.payload.shape[1]), dtype=self.payload.dtype))
+            broadcast_step(hb, self.dist, src=self.src)
+            buf[:cnt].copy_(hb[:cnt].to(buf.device))
+            self.inflight[gi] = self._Done()
+            return
+        if self.rank == self.src:
+            buf[:cnt].copy_(self.payload[gi * B: gi * B + cnt], non_blocking=True)
+        self.inflight[gi] = broadcast_async(buf, self.dist, src=self.src)
+
+    def start(self) -> None:
+        self.issue(0)
+
+    def step_buffer(self, s: int):
+        """The payload row step s consumes (a view into the receive area for world > 1)."""
+        if self.world == 1:
+            return self.payload[s]
+        gi, k = divmod(s, self.B)
+        if k == 0:
+            self.inflight.pop(gi).wait()
+            self.issue(gi + 1)
+        return self.recv[gi & 1][k]

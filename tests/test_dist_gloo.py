@@ -102,3 +102,56 @@ def test_two_rank_broadcast_sharding_matches_single_process(oracle_mod):
     single = run_instances(oracle_mod, payload_stream(), 0, E_TOTAL)
     np.testing.assert_array_equal(sharded, single)
     assert single[:, -1].min() > 0     # the instances did associate lines
+
+
+SCHED_STEPS, SCHED_PLEN = 11, 7
+
+
+def schedule_worker(rank, world, port, B, q):
+    """bench.py's scan stream (slam_ros_amd/dist.py GroupedBroadcast, the class bench.py runs) on
+    CPU tensors: every rank records the row each step consumes."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    payload = torch.empty((SCHED_STEPS, SCHED_PLEN), dtype=torch.float64)
+    if rank == 0:   # the sensor rank: step s's payload holds s·1000 + column
+        payload.copy_(torch.arange(SCHED_STEPS, dtype=torch.float64)[:, None] * 1000
+                      + torch.arange(SCHED_PLEN, dtype=torch.float64)[None])
+    else:
+        payload.fill_(-1.0)     # never read on the other ranks
+    bc = D.GroupedBroadcast(payload, B, dist, rank, world, src=0)
+    bc.start()
+    issued_before = []
+    seen = []
+    for s in range(SCHED_STEPS):
+        issued_before.append(list(bc.issued))
+        seen.append(bc.step_buffer(s).clone().numpy())
+    q.put((rank, np.array(seen), issued_before, list(bc.issued)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("B", [1, 3, 4])
+def test_grouped_broadcast_schedule(B):
+    """Step k consumes group ⌊k/B⌋'s payload (row k mod B), on every rank; group g + 1 is issued
+    when step g·B starts (one group ahead), never earlier; partial last group (11 steps)."""
+    port = free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=schedule_worker, args=(r, 2, port, B, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = (np.arange(SCHED_STEPS)[:, None] * 1000.0 + np.arange(SCHED_PLEN)[None])
+    ngroups = -(-SCHED_STEPS // B)
+    for rank, seen, issued_before, issued in got:
+        np.testing.assert_array_equal(seen, want)
+        assert issued == list(range(ngroups))
+        for s in range(SCHED_STEPS):
+            g, k = divmod(s, B)
+            # entering step s: groups 0..g issued at a group start (g + 1 goes out now, after
+            # group g's wait), 0..g + 1 inside a group
+            assert issued_before[s] == list(range(min(g + (1 if k == 0 else 2), ngroups))), \
+                (rank, s, issued_before[s])
