@@ -26,7 +26,8 @@ for c in cfgs:
     for s in range(1, 25):
         enc, lines, nl = G.make_scan(w, s, instances=E)
         r = ens.localize(enc, lines, nl)
-        assert all(x["matches"] == 8 for x in r)
+        if not os.environ.get("PROBE_NOASSERT"):
+            assert all(x["matches"] == 8 for x in r)
     stp = [a - b for a, b in zip(ens.scan_stamps(), base)]
     n = stp[9] or 1
     out = {v: round(stp[k] * 10e-3 / n, 2) for k, v in NAMES.items()}

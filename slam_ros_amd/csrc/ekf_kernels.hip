@@ -164,6 +164,13 @@ struct PllView {
 };
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+// Staged rows of a guessed column (LDS, per column and pending step: [U | V][row half][8]):
+// the U side as in the operand layout, row half rh = (k parity) · 2 + (row of the pair), 8 k each;
+// the V side interleaved by row pair, (rh, k) at (rh >> 1) · 16 + 2k + (rh & 1), so that one
+// float2 holds both rows of a k (a packed-FMA operand).
+__device__ __forceinline__ int stage_v_index(int rh, int k) { return (rh >> 1) * 16 + 2 * k + (rh & 1); }
 
 // Stored 2×2 block at rows a0, a0+1 and columns b0, b0+1 (a0, b0 even, a0's tile <= b0's):
 // acc = {(a0,b0), (a0,b0+1), (a0+1,b0), (a0+1,b0+1)}. In the f32 tile layout the two rows of a
@@ -744,6 +751,31 @@ __device__ __forceinline__ void fill_block5(Block5& b5, const double R33[9], dou
     b5.daa = Dj[0]; b5.dab = Dj[1]; b5.dba = Dj[2]; b5.dbb = Dj[3];
 }
 
+// Symmetric downdate operands (fp32 operand storage, every mode but the reference's asymmetric
+// R): the landmark block's share of P −= K·S·Kᵀ (Robot.cpp:560-568) is stored as U·Vᵀ with
+// V = K·F and U = −2^x·V (x the fp16 storage exponent, else 0), F·Fᵀ = S: the lower Cholesky
+// factor of the symmetrised S, in fp32 like the operands themselves (a non-positive pivot
+// contributes 0, which happens only where S is singular and K = 0). Every stored element then
+// gets the same products whichever orientation is stored (staged_blocks). The scan's own fp64
+// chain (gain_rows: W, K, y, the eager robot-strip and diagonal-block downdates, the corrections
+// of later lines) keeps K·S·Kᵀ; only the stored operands take this form.
+__device__ __forceinline__ void sym_factor(const double* pk, float F[3])
+{
+    const float a = (float)pk[MB_S], b = 0.5f * ((float)pk[MB_S + 1] + (float)pk[MB_S + 2]);
+    const float c = (float)pk[MB_S + 3];
+    // v_rsq_f32 (1 ulp): F need not be correctly rounded, only the same on every thread
+    F[0] = F[1] = F[2] = 0.f;
+    if (a > 0.f) {
+        const float ra = __builtin_amdgcn_rsqf(a);
+        F[0] = a * ra;
+        F[1] = b * ra;
+        const float dd = c - F[1] * F[1];
+        F[2] = dd > 0.f ? dd * __builtin_amdgcn_rsqf(dd) : 0.f;
+    } else {
+        F[2] = c > 0.f ? c * __builtin_amdgcn_rsqf(c) : 0.f;
+    }
+}
+
 // The uniform gain package of a match from the matching landmark's state: S, S⁻¹, v, H row 1
 // and the robot rows of K = W·S⁻¹ and U = K·S (Robot.cpp:522-602 for rows 0..2).
 __device__ __forceinline__ void build_package(const Cand& c, const double R33[9], double2 rr0,
@@ -912,13 +944,16 @@ constexpr int SPEC_L = HIST_LDS;                    // lines
 constexpr int SPEC_K = EKF_SPEC_K;                  // guessed candidates per line per workgroup
 constexpr int LW_CNT = 8 * SPEC_K, LW_MORE = 8 * SPEC_K + 3;   // list word: count, more bits
 constexpr int SPEC_PB = 2;                          // guessed columns per pass over the pending steps
+#ifndef EKF_STAGED_DEPTH
+#define EKF_STAGED_DEPTH 1
+#endif
 constexpr int SPEC_QMAX = 8;                        // pending steps staged in LDS (pipelined T = 4: up to 7)
 constexpr int SPEC_GMAX = 64;                       // workgroups per instance (<= one wave)
 constexpr int SPEC_WD = 14 + 4 * (SPEC_L - 1);      // winner record: rr, Dj, y, sin/cos, column blocks
 // speculative package: the words of build_package, then the robot 3×3 block and x_pre after the
 // line's update (robot_update), computed once by the replay wave for every landmark wave
-constexpr int PK_R33 = MB_VH, PK_XP = MB_VH + 9;
-constexpr int PKW = MB_VH + 12;                     // package words (speculative lines; V rows in sh_wh)
+constexpr int PK_R33 = MB_VH, PK_XP = MB_VH + 9, PK_F = MB_VH + 12;   // + the symmetric factor (sym_factor)
+constexpr int PKW = MB_VH + 15;                     // package words (speculative lines; V rows in sh_wh)
 
 // Blocks (j, cols[t]) for t < SPEC_L and (j, j) (last; only if `diag`) of the landmark block
 // with the pending steps applied, fp32 operands, every pending step with ks <= 8: the guessed
@@ -965,64 +1000,66 @@ __device__ __forceinline__ void staged_blocks(const PllView<T>& v, int j, const 
         swap[b] = (i0 >> 5) > (jb[b] >> 5);
     }
     const int kh = v.kmax / 2;
-    // owned rows i0, i0+1 of U_q and V_q: [row half][2 × 4 k]
-    auto load_rows = [&](int q, f32x4v (&Ux)[4][2], f32x4v (&Vx)[4][2]) {
+    // owned rows i0, i0+1 of U_q: [row half][2 × 4 k]. Symmetric operands (U = −2^x·V, x the
+    // fp16 storage exponent, 0 otherwise: gain_rows) make every block's chain one pattern on the
+    // owned U rows and the column's V rows, whatever the stored orientation: a block stored
+    // transposed evolves as fma(V_own, U_col) terms, and V_own·U_col == U_own·V_col exactly
+    // (power-of-two scaling; fma(a, b, c) == fma(b, a, c)).
+    auto load_rows = [&](int q, f32x4v (&Ux)[4][2]) {
         const Slot& sq = v.pend[q];
         const float* ou = reinterpret_cast<const float*>(sq.Uop) + v.e * v.opstride +
-                          ((size_t)(i0 >> 5) * 64 + (i0 & 31)) * kh;
-        const float* ov = reinterpret_cast<const float*>(sq.Vop) + v.e * v.opstride +
                           ((size_t)(i0 >> 5) * 64 + (i0 & 31)) * kh;
 #pragma unroll
         for (int rh = 0; rh < 4; rh++) {
             const int roff = (rh & 1) * kh + (rh >> 1) * 32 * kh;
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                Ux[rh][h] = *reinterpret_cast<const f32x4v*>(ou + roff + 4 * h);
-                Vx[rh][h] = *reinterpret_cast<const f32x4v*>(ov + roff + 4 * h);
-            }
+            for (int h = 0; h < 2; h++) Ux[rh][h] = *reinterpret_cast<const f32x4v*>(ou + roff + 4 * h);
         }
     };
-    f32x4v U[4][2], V[4][2];
-    if (v.npend > 0) load_rows(0, U, V);
-    for (int q = 0; q < v.npend; q++) {
-        f32x4v Un[4][2], Vn[4][2];
-        const bool pre = q + 1 < v.npend;
-        if (pre) load_rows(q + 1, Un, Vn);
+    const float vscale = -ldexpf(1.0f, -v.ex);   // V_own = U_own · (−2^−x), exact
+    // one pending step on the nine blocks, with that step's owned rows
+    auto apply_step = [&](int q, const f32x4v (&U)[4][2]) __attribute__((always_inline)) {
         const Slot& sq = v.pend[q];
         const int4 cw = v.ctl[q];
         if (cw.x) {
 #pragma unroll
             for (int b = 0; b < NB; b++) r[b][0] = r[b][1] = r[b][2] = r[b][3] = (C)0;
         } else {
+            // staged V rows of column b, interleaved by row pair (stage_v_index; block b + 1's
+            // read from LDS while block b computes); the diagonal block's are the owned V rows
+            auto read_x = [&](int b, f32x4v (&X)[2][4]) __attribute__((always_inline)) {
+                const float* xs = stg + (((b * SPEC_QMAX + q) * 2 + 1) * 4) * 8;
+#pragma unroll
+                for (int pr = 0; pr < 2; pr++)
+#pragma unroll
+                    for (int kc = 0; kc < 4; kc++) X[pr][kc] = *reinterpret_cast<const f32x4v*>(xs + pr * 16 + 4 * kc);
+            };
+            f32x4v Xa[2][4], Xb[2][4];
+            read_x(0, Xa);
 #pragma unroll
             for (int b = 0; b < NB; b++) {
-                // staged rows of the column: its V rows, or its U rows when the block is stored
-                // transposed
-                const float* xs = stg + (((b * SPEC_QMAX + q) * 2 + (swap[b] ? 0 : 1)) * 4) * 8;
+                f32x4v (&Xc)[2][4] = (b & 1) ? Xb : Xa;
+                f32x4v (&Xn)[2][4] = (b & 1) ? Xa : Xb;
+                if (b + 1 < 8) read_x(b + 1, Xn);
+                f32x2v r01 = {(float)r[b][0], (float)r[b][1]}, r23 = {(float)r[b][2], (float)r[b][3]};   // fp32 operands only
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    f32x4v O[4], X[4];
-#pragma unroll
-                    for (int rh = 0; rh < 4; rh++) {
-                        if (b < 8) {
-                            X[rh] = *reinterpret_cast<const f32x4v*>(xs + rh * 8 + 4 * h);
-                            O[rh] = swap[b] ? V[rh][h] : U[rh][h];
-                        } else {
-                            X[rh] = V[rh][h];
-                            O[rh] = U[rh][h];
-                        }
+                for (int kp = 0; kp < 8; kp++) {
+                    const int h = kp >> 2, s4 = kp & 3;
+                    f32x2v x01, x23;   // (column row 0, row 1) at k-pair kp, even and odd k
+                    if (b < 8) {
+                        x01 = f32x2v{Xc[0][kp >> 1][2 * (kp & 1)], Xc[0][kp >> 1][2 * (kp & 1) + 1]};
+                        x23 = f32x2v{Xc[1][kp >> 1][2 * (kp & 1)], Xc[1][kp >> 1][2 * (kp & 1) + 1]};
+                    } else {
+                        x01 = f32x2v{U[0][h][s4], U[1][h][s4]} * vscale;
+                        x23 = f32x2v{U[2][h][s4], U[3][h][s4]} * vscale;
                     }
-                    // rows: 0 = even k of the first row, 1 = of the second, 2/3 = odd k
-#pragma unroll
-                    for (int s = 0; s < 4; s++) {
-                        r[b][0] = fmaf(O[2][s], X[2][s], fmaf(O[0][s], X[0][s], r[b][0]));
-                        r[b][1] = fmaf(O[2][s], X[3][s], fmaf(O[0][s], X[1][s], r[b][1]));
-                        r[b][2] = fmaf(O[3][s], X[2][s], fmaf(O[1][s], X[0][s], r[b][2]));
-                        r[b][3] = fmaf(O[3][s], X[3][s], fmaf(O[1][s], X[1][s], r[b][3]));
-                    }
+                    r01 = __builtin_elementwise_fma(f32x2v{U[0][h][s4], U[0][h][s4]}, x01, r01);
+                    r01 = __builtin_elementwise_fma(f32x2v{U[2][h][s4], U[2][h][s4]}, x23, r01);
+                    r23 = __builtin_elementwise_fma(f32x2v{U[1][h][s4], U[1][h][s4]}, x01, r23);
+                    r23 = __builtin_elementwise_fma(f32x2v{U[3][h][s4], U[3][h][s4]}, x23, r23);
                 }
-#pragma unroll
-                for (int k = 0; k < 4; k++) r[b][k] = round_step<T>(r[b][k]);
+                r[b][0] = round_step<T>(r01[0]); r[b][1] = round_step<T>(r01[1]);
+                r[b][2] = round_step<T>(r23[0]); r[b][3] = round_step<T>(r23[1]);
                 // one block at a time (bounds the staged rows in registers)
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -1036,16 +1073,43 @@ __device__ __forceinline__ void staged_blocks(const PllView<T>& v, int j, const 
                 }
             }
         }
-        if (pre) {
-#pragma unroll
-            for (int rh = 0; rh < 4; rh++)
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    U[rh][h] = Un[rh][h];
-                    V[rh][h] = Vn[rh][h];
-                }
+    };
+    // The next step's rows are loaded while this one runs. The loads are issued on every
+    // iteration (the last one re-reads its own step): a conditional prefetch makes the compiler's
+    // wait-count merge at the loop join wait for ALL outstanding loads (vmcnt(0)) before the
+    // body, which serialised every step behind its successor's loads.
+    const int np = v.npend;
+#if EKF_STAGED_DEPTH >= 2
+    // two steps ahead: three register sets, the loop unrolled by three (static names)
+    f32x4v UA[4][2], UB[4][2], UC[4][2];
+    if (np > 0) {
+        load_rows(0, UA);
+        load_rows(min(1, np - 1), UB);
+        for (int q = 0; q < np; q += 3) {
+            load_rows(min(q + 2, np - 1), UC);
+            apply_step(q, UA);
+            if (q + 1 >= np) break;
+            load_rows(min(q + 3, np - 1), UA);
+            apply_step(q + 1, UB);
+            if (q + 2 >= np) break;
+            load_rows(min(q + 4, np - 1), UB);
+            apply_step(q + 2, UC);
         }
     }
+#else
+    // one step ahead: two register sets, the loop unrolled by two (static names, no copies)
+    f32x4v UA[4][2], UB[4][2];
+    if (np > 0) {
+        load_rows(0, UA);
+        for (int q = 0; q < np; q += 2) {
+            load_rows(min(q + 1, np - 1), UB);
+            apply_step(q, UA);
+            if (q + 1 >= np) break;
+            load_rows(min(q + 2, np - 1), UA);
+            apply_step(q + 1, UB);
+        }
+    }
+#endif
 #pragma unroll
     for (int b = 0; b < NB; b++)
 #pragma unroll
@@ -1083,18 +1147,18 @@ __device__ __forceinline__ void staged_pair_block(const PllView<T>& v, int wa, i
             const float* cv = stg + (((tB * SPEC_QMAX + q) * 2 + 1) * 4) * 8;
 #pragma unroll
             for (int h = 0; h < 2; h++) {
-                f32x4v A[4], Bv[4];
+                f32x4v A[4];
 #pragma unroll
-                for (int rh = 0; rh < 4; rh++) {
-                    A[rh] = *reinterpret_cast<const f32x4v*>(cu + rh * 8 + 4 * h);
-                    Bv[rh] = *reinterpret_cast<const f32x4v*>(cv + rh * 8 + 4 * h);
-                }
+                for (int rh = 0; rh < 4; rh++) A[rh] = *reinterpret_cast<const f32x4v*>(cu + rh * 8 + 4 * h);
 #pragma unroll
                 for (int s = 0; s < 4; s++) {
-                    acc[0] = fmaf(A[2][s], Bv[2][s], fmaf(A[0][s], Bv[0][s], acc[0]));
-                    acc[1] = fmaf(A[2][s], Bv[3][s], fmaf(A[0][s], Bv[1][s], acc[1]));
-                    acc[2] = fmaf(A[3][s], Bv[2][s], fmaf(A[1][s], Bv[0][s], acc[2]));
-                    acc[3] = fmaf(A[3][s], Bv[3][s], fmaf(A[1][s], Bv[1][s], acc[3]));
+                    // the V side is interleaved (stage_v_index): rows 0 and 1 of k = 4h + s
+                    const f32x2v b01 = *reinterpret_cast<const f32x2v*>(cv + stage_v_index(0, 4 * h + s));
+                    const f32x2v b23 = *reinterpret_cast<const f32x2v*>(cv + stage_v_index(2, 4 * h + s));
+                    acc[0] = fmaf(A[2][s], b23[0], fmaf(A[0][s], b01[0], acc[0]));
+                    acc[1] = fmaf(A[2][s], b23[1], fmaf(A[0][s], b01[1], acc[1]));
+                    acc[2] = fmaf(A[3][s], b23[0], fmaf(A[1][s], b01[0], acc[2]));
+                    acc[3] = fmaf(A[3][s], b23[1], fmaf(A[1][s], b01[1], acc[3]));
                 }
             }
 #pragma unroll
@@ -1307,10 +1371,13 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     signal_started(sync, tid);
 
     const bool spec_ok = p.spec && L > 0 && L <= SPEC_L && s > 0 && G <= SPEC_GMAX;
+    // symmetric downdate operands (sym_factor): fp32 operand storage, every mode but the
+    // reference's asymmetric R
+    const bool sym = p.r_mode != 1 && sizeof(typename Stor<T>::C) == 4;
     // speculative path with fp32 operands and few pending steps: the pending steps' rows of the
     // guessed columns are staged in LDS and one pass per step updates all owned blocks
     bool staged = false;
-    if (spec_ok && sizeof(typename Stor<T>::C) == 4 && p.npend <= SPEC_QMAX && d.kmax / 2 >= 8) {
+    if (spec_ok && sym && sizeof(typename Stor<T>::C) == 4 && p.npend <= SPEC_QMAX && d.kmax / 2 >= 8) {
         __syncthreads();   // sh_ctl
         staged = true;
         for (int q = 0; q < p.npend; q++) staged &= sh_ctl[q].y <= 8;
@@ -1328,7 +1395,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     EKF_STAMP(1);
 
     // writes a match's owned rows: U/V history and the MFMA downdate operands
-    auto store_rows = [&](int t, const double kk[4], const double uu[4], bool vhist) {
+    // F: the line's symmetric operand factor (sym_factor; unused otherwise)
+    auto store_rows = [&](int t, const double kk[4], const double uu[4], bool vhist, const float F[3]) {
         if (t < HIST_LDS)
             sh_uhist[t][tid] = make_double4(uu[0], uu[1], uu[2], uu[3]);
         else
@@ -1343,10 +1411,17 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         for (int pp = 0; pp < 2; pp++) {
             const int lr = 2 * j + pp;
             if constexpr (sizeof(C) == 4) {
-                Uop[op_index_f32(lr, 2 * t, d.kmax)] = to_domain<T>(-uu[2 * pp], pv.ex);
-                Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = to_domain<T>(-uu[2 * pp + 1], pv.ex);
-                Vop[op_index_f32(lr, 2 * t, d.kmax)] = (C)kk[2 * pp];
-                Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (C)kk[2 * pp + 1];
+                double o0 = uu[2 * pp], o1 = uu[2 * pp + 1], v0 = kk[2 * pp], v1 = kk[2 * pp + 1];
+                if (sym) {   // V = K·F, U = −2^x·V (sym_factor)
+                    v0 = kk[2 * pp] * (double)F[0] + kk[2 * pp + 1] * (double)F[1];
+                    v1 = kk[2 * pp + 1] * (double)F[2];
+                    o0 = (double)(float)v0;
+                    o1 = (double)(float)v1;
+                }
+                Uop[op_index_f32(lr, 2 * t, d.kmax)] = to_domain<T>(-o0, pv.ex);
+                Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = to_domain<T>(-o1, pv.ex);
+                Vop[op_index_f32(lr, 2 * t, d.kmax)] = (C)v0;
+                Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (C)v1;
             } else {
                 Uop[op_index_f64(lr, 2 * t, d.kmax)] = (C)(-uu[2 * pp]);
                 Uop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (C)(-uu[2 * pp + 1]);
@@ -1552,20 +1627,29 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 }
             }
             if (staged) {
-                // rows 2w, 2w+1 of U_q and V_q of every guessed column w, pending step q
-                // (4 row halves × 8 k each)
+                // rows 2w, 2w+1 of U_q and V_q of every guessed column w, pending step q (4 row
+                // halves × 8 k each; the V side interleaved, stage_v_index): 16 pieces of 4 floats
                 const int kh = d.kmax / 2;
-                const int nld = L * p.npend * 2 * 4 * 2;
+                const int nld = L * p.npend * 16;
                 for (int k = tid; k < nld; k += SCAN_BLOCK) {
-                    const int half = k & 1, rh = (k >> 1) & 3, side = (k >> 3) & 1;
-                    const int tq = k >> 4, q = tq % p.npend, t = tq / p.npend;
+                    const int piece = k & 15, tq = k >> 4, q = tq % p.npend, t = tq / p.npend;
                     const int w = sh_spec[t];
                     if (w < 0) continue;
-                    const float* base = reinterpret_cast<const float*>(side ? p.pend[q].Vop : p.pend[q].Uop) +
-                                        e * opstride + ((size_t)((2 * w) >> 5) * 64 + ((2 * w) & 31)) * kh;
-                    const int roff = (rh & 1) * kh + (rh >> 1) * 32 * kh;
-                    *reinterpret_cast<f32x4v*>(sh_stg + ((((t * SPEC_QMAX + q) * 2 + side) * 4 + rh) * 8) + half * 4) =
-                        *reinterpret_cast<const f32x4v*>(base + roff + half * 4);
+                    const size_t rowb = ((size_t)((2 * w) >> 5) * 64 + ((2 * w) & 31)) * kh;
+                    float* dst = sh_stg + ((t * SPEC_QMAX + q) * 2) * 32;
+                    if (piece < 8) {   // U: row half rh, 4 k
+                        const int half = piece & 1, rh = piece >> 1;
+                        const float* base = reinterpret_cast<const float*>(p.pend[q].Uop) + e * opstride + rowb;
+                        const int roff = (rh & 1) * kh + (rh >> 1) * 32 * kh;
+                        *reinterpret_cast<f32x4v*>(dst + rh * 8 + half * 4) =
+                            *reinterpret_cast<const f32x4v*>(base + roff + half * 4);
+                    } else {           // V: rows of pair pr, k-pairs 2kc, 2kc + 1, interleaved
+                        const int pr = (piece - 8) >> 2, kc = (piece - 8) & 3;
+                        const float* base = reinterpret_cast<const float*>(p.pend[q].Vop) + e * opstride + rowb;
+                        const f32x2v a = *reinterpret_cast<const f32x2v*>(base + (2 * pr) / 2 * 32 * kh + 2 * kc);
+                        const f32x2v c = *reinterpret_cast<const f32x2v*>(base + kh + pr * 32 * kh + 2 * kc);
+                        *reinterpret_cast<f32x4v*>(dst + 32 + pr * 16 + 4 * kc) = f32x4v{a[0], c[0], a[1], c[1]};
+                    }
                 }
             }
             if (tid == SCAN_BLOCK - 1) sh_ready = 0;
@@ -1625,6 +1709,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         eval_candidate(b5, wy.x, wy.y, sn, cs, xpl, ln.alpha, ln.r, Rm, p.gate, c);
                         bad |= c.pass ? 0 : 1;
                         build_package(c, R33l, w0, w1, w2, pk);   // its V rows stay in sh_wh[t]
+                        if (sym) {   // once per line for every landmark's operand stores
+                            float F[3];
+                            sym_factor(pk, F);
+                            pk[PK_F + 0] = F[0]; pk[PK_F + 1] = F[1]; pk[PK_F + 2] = F[2];
+                        }
                     }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                     __builtin_amdgcn_wave_barrier();
@@ -1754,7 +1843,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         double kk[4], uu[4];
                         gain_rows<SPEC_L>(pk, m, uq_owned, [&](int q) { return sh_wh[i][q][1]; }, blk, rr0, rr1,
                                           rr2, yb, Dj, kk, uu);
-                        store_rows(m, kk, uu, false);
+                        const float F[3] = {(float)pk[PK_F], (float)pk[PK_F + 1], (float)pk[PK_F + 2]};
+                        store_rows(m, kk, uu, false, F);
                     }
                     sub(18);
                     // = robot_update(R33, xp, pk), computed by the replay wave
@@ -1912,7 +2002,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                              return make_double4(vh[0], vh[1], vh[2], vh[3]);
                          },
                          blk, rr0, rr1, rr2, yb, Dj, kk, uu);
-            store_rows(m, kk, uu, true);
+            float F[3] = {0.f, 0.f, 0.f};
+            if (sym) sym_factor(sh_pkg, F);
+            store_rows(m, kk, uu, true, F);
         }
         robot_update(R33, xp, sh_pkg);
         if (j == jstar) matched = true;

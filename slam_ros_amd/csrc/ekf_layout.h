@@ -32,7 +32,10 @@ namespace ekf {
 
 constexpr int TILE = 32;            // tile edge (both precisions)
 constexpr int TILE_ELEMS = TILE * TILE;
-constexpr int SCAN_THREADS = 192;   // association kernel: threads (= owned landmarks) per workgroup
+#ifndef EKF_SCAN_THREADS
+#define EKF_SCAN_THREADS 192
+#endif
+constexpr int SCAN_THREADS = EKF_SCAN_THREADS;   // association kernel: threads (= owned landmarks) per workgroup
 constexpr int SCAN_BLOCK = SCAN_THREADS + 64;   // + one wave that replays the guessed winners' chain
 constexpr int MAX_CAPACITY = 32768;             // landmarks per instance
 constexpr int DD_THREADS = 256;     // downdate kernel: 4 waves, one tile per wave
