@@ -1807,7 +1807,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                              !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate))) {
                             Cand c;
                             eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, c);
-                            status |= c.singular ? EKF_ST_SINGULAR : 0;
+                            // GSL_EDOM counts only for candidates the reference evaluates: the
+                            // unmatched ones up to the winner (Robot.cpp:313-498 stops there)
+                            if (c.singular && (w < 0 || j <= w)) status |= EKF_ST_SINGULAR;
                             pass = c.pass;
                         }
                         // the guess must be the first passing unmatched landmark
@@ -1904,6 +1906,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         line_R(ln, i, p.r_mode, Rm);
         // gating of the owned candidate (Robot.cpp:313-498); the first passing unmatched j wins
         int best = 0x7fffffff;
+        bool sing = false;
         Cand c;
         if (own && j < s && !matched) {
             Block5 b5;
@@ -1912,7 +1915,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             sincos_near(yb.x, ma0, s0j, c0j, sn, cs);
             if (!certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate)) {
                 eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, c);
-                status |= c.singular ? EKF_ST_SINGULAR : 0;
+                sing = c.singular;
                 if (c.pass) best = j;
             }
         }
@@ -1965,6 +1968,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             EKF_STAMP(3);   // one workgroup: the package never leaves LDS
         }
         EKF_STAMP(4);
+        // GSL_EDOM counts only for the candidates the reference evaluates (up to the winner)
+        if (sing && j <= jstar) status |= EKF_ST_SINGULAR;
         if (jstar == 0x7fffffff) {
             // no match (or s == 0): the line goes to extraLines (Robot.cpp:308-310, 492-496)
             if (lead) {

@@ -533,3 +533,33 @@ def test_f64_wave_flush_equals_tile_kernel(ekf_mod, monkeypatch, N, T, lines, ex
         assert bad.size == 0, (e, bad[:12].tolist(), rel(Pa, Pb))
         np.testing.assert_array_equal(ya, yb)
         assert sa == sb
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("spec", ["1", "0"])
+def test_singular_status_counts_only_evaluated_candidates(ekf_mod, oracle_mod, monkeypatch, prec, spec):
+    """GSL_EDOM (EKF_ST_SINGULAR_S) is raised only for candidates the reference evaluates: the
+    unmatched landmarks up to the line's winner (Robot.cpp:313-498 stops at the first passing
+    one). Landmark 1 has a zero covariance and the lines an exact R = 0, so its S is singular;
+    observing landmark 0 never evaluates it, observing landmark 1 does (after landmark 0 fails).
+    Speculative and sequential association paths."""
+    monkeypatch.setenv("EKF_SPECULATE", spec)
+    N = 16
+    n = 3 + 2 * N
+    P = np.zeros((n, n))
+    P[3:5, 3:5] = [[0.01, 0.0], [0.0, 0.02]]
+    y = np.zeros(n)
+    y[3:5] = (0.5, 2.0)
+    y[5:7] = (1.2, 3.0)
+    for target, want in ((0, 0), (1, 1)):
+        ens = ekf_mod.Ensemble(N, 1, prec, max_lines=8)
+        ens.upload_state(0, P, y, 2, [0.0, 0.0, 0.0])
+        ref = oracle_mod.OracleRobot(N)
+        ref.set_state(*ens.download_state(0))
+        line = np.array([[y[3 + 2 * target], y[4 + 2 * target], 0.0, 0.0, 0.0, 0.0]])
+        res = ens.localize([0.0, 0.0, 0.0], line[None], [1])[0]
+        m = ref.localize(line, [0.0, 0.0, 0.0])
+        assert res["match"] == m == [target], (res["match"], m)
+        assert ref.status & 1 == want
+        assert res["status"] & ekf_mod.ST_SINGULAR_S == want, (target, res["status"])
+        ens.close()
