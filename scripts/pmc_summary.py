@@ -14,13 +14,27 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def demangle(name):
+    """rocprofv3 leaves some names mangled (the _Float16 instantiations)."""
+    if not name.startswith("_Z"):
+        return name
+    try:
+        import subprocess
+        tool = "/opt/rocm/lib/llvm/bin/llvm-cxxfilt"
+        tool = tool if os.path.exists(tool) else "c++filt"
+        out = subprocess.run([tool, name], capture_output=True, text=True).stdout.strip()
+        return out or name
+    except OSError:
+        return name
+
+
 def counters(path):
     acc = defaultdict(lambda: defaultdict(list))
     if not os.path.exists(path):
         return {}
     with open(path) as f:
         for r in csv.DictReader(f):
-            acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            acc[demangle(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
 
 
@@ -39,8 +53,20 @@ def main(tag):
     json.dump(ctr, open(os.path.join(out, "counters_avg_per_dispatch.json"), "w"), indent=1)
     b = json.load(open(os.path.join(out, "bench.json")))
     kern = b["roofline"]["kernel"]
-    match = [k for k in ctr if kern.split("<")[0] in k and
-             (("<" not in kern) or kern[kern.index("<"):].replace(" ", "") in k.replace(" ", ""))]
+    def same(k):
+        if kern.split("<")[0] not in k:
+            return False
+        if "<" not in kern:
+            return True
+        if kern[kern.index("<"):].replace(" ", "") in k.replace(" ", ""):
+            return True
+        if k.startswith("_Z"):   # still mangled: Itanium template arguments
+            args = [a.strip() for a in kern[kern.index("<") + 1:-1].split(",")]
+            code = {"float": "f", "double": "d", "_Float16": "DF16_"}
+            want = "I" + "".join(code.get(a, "Li%sE" % a) for a in args) + "E"
+            return want in k
+        return False
+    match = [k for k in ctr if same(k)]
     if not match:
         print("no counters for", kern, list(ctr)[:5])
         return
