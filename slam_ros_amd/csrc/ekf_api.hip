@@ -81,6 +81,10 @@ struct ekf_ctx {
     int sync_stride;
     unsigned long long* dbg;  // association-kernel phase timers (EKF_SCAN_STAMPS=1)
     int* pexp;                // [E] fp16 storage exponents (device), host copy below
+    void* sink;               // scratch tile for the wave flushes (DowndateParams::sink)
+    void* ops_u;              // operand rows of every ring slot (U), slot_bytes apart
+    void* ops_v;              // ... (V)
+    long long slot_bytes;
     std::vector<int> pexp_h;
     // flush scheduling (see the top of this file)
     int T;                    // flush interval
@@ -145,11 +149,11 @@ int ekf_abi_version(void) { return SLAM_EKF_ABI_VERSION; }
 static void free_all(ekf_ctx* c)
 {
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->pose, c->xpre, c->saved, c->D,
-                               c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->pexp, c->mbox,
+                               c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->pexp, c->sink, c->mbox,
                                c->sync, c->Ust, c->Vst};
+    ptrs.push_back(c->ops_u);
+    ptrs.push_back(c->ops_v);
     for (auto& sl : c->ring) {
-        ptrs.push_back(sl.Uop);
-        ptrs.push_back(sl.Vop);
         ptrs.push_back(sl.patch);
         ptrs.push_back(sl.patch_diag);
         ptrs.push_back(sl.res);
@@ -281,9 +285,15 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     ALLOC(c->Vst, sizeof(double) * d.max_lines * d.n * 2 * E);
     c->T = cfg->flush_interval > 0 ? cfg->flush_interval : 1;
     c->ring.assign((size_t)c->T * (cfg->pipeline ? 2 : 1), ekf::Slot{});
-    for (auto& sl : c->ring) {
-        ALLOC(sl.Uop, c->op_inst * c->op_elem * E);
-        ALLOC(sl.Vop, c->op_inst * c->op_elem * E);
+    // the operand rows of all slots in two contiguous buffers (fixed slot stride): the wave
+    // flush addresses step q's rows from one base and its ring index (DowndateParams::ubase)
+    c->slot_bytes = (long long)(((c->op_inst * c->op_elem * E) + 255) / 256 * 256);
+    ALLOC(c->ops_u, (size_t)c->slot_bytes * c->ring.size());
+    ALLOC(c->ops_v, (size_t)c->slot_bytes * c->ring.size());
+    for (size_t i = 0; i < c->ring.size(); i++) {
+        ekf::Slot& sl = c->ring[i];
+        sl.Uop = (char*)c->ops_u + (size_t)c->slot_bytes * i;
+        sl.Vop = (char*)c->ops_v + (size_t)c->slot_bytes * i;
         ALLOC(sl.patch, sizeof(double) * d.max_lines * 2 * d.M * E);
         ALLOC(sl.patch_diag, sizeof(double) * d.max_lines * 4 * E);
         ALLOC(sl.res, sizeof(int) * ekf::RES_STRIDE * E);
@@ -298,6 +308,7 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     ALLOC(c->d_lines, sizeof(ekf_line) * d.max_lines * E);
     ALLOC(c->d_nlines, sizeof(int) * E);
     ALLOC(c->pexp, sizeof(int) * E);
+    ALLOC(c->sink, 8 * ekf::TILE_ELEMS);
     c->pexp_h.assign(E, 0);
     c->G = (d.N + ekf::SCAN_THREADS - 1) / ekf::SCAN_THREADS;
     // whole 128-B lines: the package words, then 16 words for the speculative list words
@@ -604,6 +615,12 @@ static int enqueue_flush(ekf_ctx* c)
     dp.wt64 = c->wt64;
     dp.nwt64 = c->nwt64;
     dp.pexp = c->pexp;
+    dp.sink = c->sink;
+    dp.ubase = c->ops_u;
+    dp.vbase = c->ops_v;
+    dp.slot_bytes = c->slot_bytes;
+    dp.nslots = (int)c->ring.size();
+    dp.slot0 = (int)(c->unflushed0 % (long long)c->ring.size());
     for (int q = 0; q < nst; q++) dp.steps[q] = slot_of(c, c->unflushed0 + q);
     const int in = c->last_out;
     const int out = c->cfg.pipeline ? 1 - in : in;

@@ -121,6 +121,11 @@ struct DowndateParams {
     const WtEntry* wt64;  // [nwt64] f64 wave-tiles of 1 × WT64_C tiles (tile[0..1], rows[0] = A row block)
     int nwt64;
     const int* pexp;      // [E] fp16 storage exponent
+    void* sink;           // one scratch tile (8 KB): the wave flushes' stores of slots outside the triangle
+    const void* ubase;    // operand rows of ring slot i at ubase / vbase + i·slot_bytes; the
+    const void* vbase;    // group's step q is slot (slot0 + q) mod nslots (= steps[q].Uop / .Vop)
+    long long slot_bytes;
+    int slot0, nslots;
     Slot steps[PMAX];
 };
 

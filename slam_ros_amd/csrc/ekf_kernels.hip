@@ -1797,14 +1797,16 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     double Rm[4];
                     line_R(ln, i, p.r_mode, Rm);
                     const int w = sh_spec[i];
+                    int deep = 0;   // diagnostics: 1 past the fp32 filter, 2 past the fp64 one
                     if (own && j < s && !matched) {
                         Block5 b5;
                         fill_block5(b5, R33, rr0, rr1, rr2, Dj);
                         bool pass = false;
                         double sn = 0.0, cs = 1.0;
                         if (!certified_reject_f32(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate) &&
-                            (sincos_near(yb.x, ma0, s0j, c0j, sn, cs),
+                            (deep = 1, sincos_near(yb.x, ma0, s0j, c0j, sn, cs),
                              !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate))) {
+                            deep = 2;
                             Cand c;
                             eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, c);
                             // GSL_EDOM counts only for candidates the reference evaluates: the
@@ -1814,6 +1816,14 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         }
                         // the guess must be the first passing unmatched landmark
                         if (pass ? (w < 0 || j < w) : (j == w)) viol = 1;
+                    }
+                    if (p.dbg && g == 0) {   // waves of workgroup 0 whose lanes went deeper
+                        const bool d1 = __any(deep >= 1), d2 = __any(deep >= 2);
+                        if ((tid & 63) == 0) {
+                            if (d1) atomicAdd(&sh_stamp[20], 1ull);
+                            if (d2) atomicAdd(&sh_stamp[21], 1ull);
+                            atomicAdd(&sh_stamp[22], 1ull);
+                        }
                     }
                     sub(16);
                     if (w < 0) {
@@ -2741,6 +2751,7 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
     const size_t inst_elems = (size_t)d.ntiles * TILE_ELEMS;
     const TS* Pin = reinterpret_cast<const TS*>(p.Pin);
     TS* Pout = reinterpret_cast<TS*>(p.Pout);
+    TS* sink = reinterpret_cast<TS*>(p.sink);
     const int lofs = lane * kh;
 
     // the pipelined loop needs every step of every instance this wave visits to be a plain
@@ -2792,17 +2803,28 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
     auto tile_ptr = [&](const Item& t, int i) __attribute__((always_inline)) {
         return (size_t)t.e * inst_elems + (size_t)t.w.tile[i] * TILE_ELEMS;
     };
+    // every slot is stored, the invalid ones (outside the packed triangle) to the sink tile: no
+    // branch around a store (a conditional store splits the wait-count tracking, and the join
+    // then waits for every outstanding load, the next wave-tile's prefetch included)
     auto store_tiles = [&](const Item& t, const f32x16 (&acc)[WT_N]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < WT_N; i++)
-            if ((t.w.valid >> i) & 1) {
-                TS* tl = Pout + tile_ptr(t, i);
+        for (int i = 0; i < WT_N; i++) {
+            TS* tl = ((t.w.valid >> i) & 1) ? Pout + tile_ptr(t, i) : sink;
 #pragma unroll
-                for (int qq = 0; qq < 4; qq++) tile_st(tl, lane, qq, acc[i]);
-            }
+            for (int qq = 0; qq < 4; qq++) tile_st(tl, lane, qq, acc[i]);
+        }
     };
     auto op_row = [&](const Item& t, int side, int k) __attribute__((always_inline)) {
         return (t.w.rows[side] >> (16 * k)) & 0xffff;
+    };
+    // step q's operand rows (side 0: U, 1: V) from the contiguous slot buffers: scalar arithmetic
+    // on a few kernel arguments, not 2·NS pointers (which the compiler reloaded from the kernel
+    // arguments inside the loop, each load waited on before the next MFMA could issue)
+    auto op_base = [&](int q, int side) __attribute__((always_inline)) {
+        int sl = p.slot0 + q;
+        if (sl >= p.nslots) sl -= p.nslots;
+        return reinterpret_cast<const float*>(reinterpret_cast<const char*>(side ? p.vbase : p.ubase) +
+                                              (size_t)sl * (size_t)p.slot_bytes);
     };
 
     if (fast) {
@@ -2813,8 +2835,8 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
         f32x16 acc[WT_N];
         // half h (k-steps 4h..4h+3) of step q's operand rows of wave-tile t, into slot q
         auto load_half = [&](int slot, const Item& t, int q, int h) __attribute__((always_inline)) {
-            const float* U = reinterpret_cast<const float*>(p.steps[q].Uop) + t.e * opstride + lofs + 4 * h;
-            const float* V = reinterpret_cast<const float*>(p.steps[q].Vop) + t.e * opstride + lofs + 4 * h;
+            const float* U = op_base(q, 0) + t.e * opstride + lofs + 4 * h;
+            const float* V = op_base(q, 1) + t.e * opstride + lofs + 4 * h;
 #pragma unroll
             for (int r = 0; r < WT_R; r++)
                 opA[slot][r][h] = *reinterpret_cast<const f32x4*>(U + (size_t)op_row(t, 0, r) * 64 * kh);
@@ -2907,15 +2929,14 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
                                 for (int u = 0; u < 4; u++) acc[a][k + u] = round_step<TS>(acc[a][k + u]);
                             } else {
                                 const int a = pg * WT_C + ((m - 8) >> 2), qq = (m - 8) & 3;
-                                if ((cur.w.valid >> a) & 1) tile_st(Pout + tile_ptr(cur, a), lane, qq, acc[a]);
+                                tile_st(((cur.w.valid >> a) & 1) ? Pout + tile_ptr(cur, a) : sink, lane, qq, acc[a]);
                             }
                         }
                         if (ld && (m & 1)) {
                             // load m/2 of slot lq: half, operand row (A rows, then B rows)
                             const int l = m >> 1, h = l >> 2, o = l & 3;
                             const bool isA = o < WT_R;
-                            const float* base = reinterpret_cast<const float*>(isA ? p.steps[lq].Uop : p.steps[lq].Vop) +
-                                                ldi.e * opstride + lofs + 4 * h;
+                            const float* base = op_base(lq, isA ? 0 : 1) + ldi.e * opstride + lofs + 4 * h;
                             const f32x4 v = *reinterpret_cast<const f32x4*>(
                                 base + (size_t)op_row(ldi, isA ? 0 : 1, isA ? o : o - WT_R) * 64 * kh);
                             if (isA) opA[lq][o][h] = v;
@@ -2937,12 +2958,11 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
                 load_half(NS - 1, ldi, NS - 1, 0);
                 load_half(NS - 1, ldi, NS - 1, 1);
 #pragma unroll
-                    for (int a = 2; a < 4; a++)
-                        if ((cur.w.valid >> a) & 1) {
-                            TS* tl = Pout + tile_ptr(cur, a);
+                for (int a = 2; a < 4; a++) {
+                    TS* tl = ((cur.w.valid >> a) & 1) ? Pout + tile_ptr(cur, a) : sink;
 #pragma unroll
-                            for (int qq = 0; qq < 4; qq++) tile_st(tl, lane, qq, acc[a]);
-                        }
+                    for (int qq = 0; qq < 4; qq++) tile_st(tl, lane, qq, acc[a]);
+                }
                 if (!more) break;
                 g += K;
                 cur = nxt;
@@ -3153,19 +3173,20 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f64_wave_kernel(DowndateP
             }
         }
     };
+    // invalid slots to the sink tile (no branch around a store: see flush_f32_wave_kernel)
     auto store_tiles = [&](const Item& t, const f64x4 (&acc)[WT64_C][4]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < WT64_C; i++)
-            if ((t.valid >> i) & 1) {
-                f64x2* dst = reinterpret_cast<f64x2*>(Pout + tile_base(t, i)) + lane;
+        for (int i = 0; i < WT64_C; i++) {
+            f64x2* dst = reinterpret_cast<f64x2*>(((t.valid >> i) & 1) ? Pout + tile_base(t, i)
+                                                                      : reinterpret_cast<double*>(p.sink)) + lane;
 #pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    const f64x2 v0 = {acc[i][b][0], acc[i][b][1]};
-                    const f64x2 v1 = {acc[i][b][2], acc[i][b][3]};
-                    __builtin_nontemporal_store(v0, dst + b * 128);
-                    __builtin_nontemporal_store(v1, dst + b * 128 + 64);
-                }
+            for (int b = 0; b < 4; b++) {
+                const f64x2 v0 = {acc[i][b][0], acc[i][b][1]};
+                const f64x2 v1 = {acc[i][b][2], acc[i][b][3]};
+                __builtin_nontemporal_store(v0, dst + b * 128);
+                __builtin_nontemporal_store(v1, dst + b * 128 + 64);
             }
+        }
     };
     // operand rows of step q for wave-tile t: A (its row block), B (its two column blocks), each
     // 8 doubles per lane ([half h][k-step s] at h·kq + s)
