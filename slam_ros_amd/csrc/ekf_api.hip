@@ -621,6 +621,7 @@ static int enqueue_flush(ekf_ctx* c)
     dp.slot_bytes = c->slot_bytes;
     dp.nslots = (int)c->ring.size();
     dp.slot0 = (int)(c->unflushed0 % (long long)c->ring.size());
+    dp.dbg = c->dbg;
     for (int q = 0; q < nst; q++) dp.steps[q] = slot_of(c, c->unflushed0 + q);
     const int in = c->last_out;
     const int out = c->cfg.pipeline ? 1 - in : in;

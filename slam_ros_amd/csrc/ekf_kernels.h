@@ -126,6 +126,7 @@ struct DowndateParams {
     const void* vbase;    // group's step q is slot (slot0 + q) mod nslots (= steps[q].Uop / .Vop)
     long long slot_bytes;
     int slot0, nslots;
+    unsigned long long* dbg;  // EKF_SCAN_STAMPS buffer (timing experiments of the flush only)
     Slot steps[PMAX];
 };
 

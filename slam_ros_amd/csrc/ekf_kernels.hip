@@ -2882,7 +2882,13 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
             load_half(q, cur, q, 1);
         }
         int g = g0;
+#ifdef EKF_XP_FLUSH_STAMPS   // timing experiment: shader cycles per wave-tile section
+        unsigned long long xs_b = 0, xs_m = 0, xs_s = 0, xs_n = 0;
+#endif
         while (true) {
+#ifdef EKF_XP_FLUSH_STAMPS
+            const unsigned long long xt0 = __builtin_amdgcn_s_memtime();
+#endif
             const bool more = g + K < g_end;
             next_item(nxt, nxt2);   // read now, used by the next wave-tile
             // operand rows for the next wave-tile (the last one re-reads its own: no branch
@@ -2898,6 +2904,9 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
             // during the one before it, so these have the whole wave-tile to land
             if (more) load_tiles(nxt);
             __builtin_amdgcn_sched_barrier(0);
+#ifdef EKF_XP_FLUSH_STAMPS
+            const unsigned long long xt1 = __builtin_amdgcn_s_memtime();
+#endif
             if constexpr (AM) {
                 // group-major steps (fp16 storage): the
                 // per-step rounding of one group of accumulators runs on the VALU while the other
@@ -2988,12 +2997,26 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
                 __builtin_amdgcn_sched_barrier(0);
             }
             load_half(NS - 1, ldi, NS - 1, 1);
+#ifdef EKF_XP_FLUSH_STAMPS
+            const unsigned long long xt2 = __builtin_amdgcn_s_memtime();
+#endif
             store_tiles(cur, acc);
+#ifdef EKF_XP_FLUSH_STAMPS
+            __builtin_amdgcn_sched_barrier(0);
+            const unsigned long long xt3 = __builtin_amdgcn_s_memtime();
+            xs_b += xt1 - xt0; xs_m += xt2 - xt1; xs_s += xt3 - xt2; xs_n += 1;
+#endif
             if (!more) break;
             g += K;
             cur = nxt;
             nxt = nxt2;
         }
+#ifdef EKF_XP_FLUSH_STAMPS
+        if (p.dbg && lane == 0) {
+            atomicAdd(p.dbg + 24, xs_b); atomicAdd(p.dbg + 25, xs_m);
+            atomicAdd(p.dbg + 26, xs_s); atomicAdd(p.dbg + 27, xs_n);
+        }
+#endif
         return;
     }
 
