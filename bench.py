@@ -55,6 +55,7 @@ METRIC = "EKF updates/s at N=4096 landmarks, 1→8 MI355X; ‖P−P_ref‖_F rel
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: dense fp32 MFMA (v_mfma_f32_32x32x2_f32)
 MFMA_F64_PEAK_TFS = 78.6    # MI355X_MICROARCH.md: dense fp64 MFMA
+MFMA_BF16_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (v_mfma_f32_32x32x16_bf16)
 L_LINES = 8
 
 
@@ -82,6 +83,10 @@ def parse():
                     help="nccl (= RCCL on ROCm); gloo only to rehearse ranks on one GPU")
     ap.add_argument("--preroll", type=int, default=200,
                     help="untimed clock pre-roll steps before the warm-up (steady GPU clocks)")
+    ap.add_argument("--arith", choices=["exact", "bf16x6"], default="exact",
+                    help="fp32 flush arithmetic (slam_ekf.h EKF_ARITH_*): exact = fp32 MFMA, the state "
+                         "bit-identical for every T; bf16x6 = fp32 operands split exactly into three "
+                         "bf16 parts, six bf16 MFMAs per product (f32 storage only)")
     ap.add_argument("--traffic-json", default="",
                     help="HBM traffic file (default: the newest profiles/*/traffic.json)")
     return ap.parse_args()
@@ -161,8 +166,11 @@ def main():
     world_map = G.make_world(N)
     st = G.initial_state(world_map)
 
+    arith = {"exact": ekf.ARITH_EXACT, "bf16x6": ekf.ARITH_BF16X6}[args.arith]
+    if prec != ekf.PREC_F32:
+        arith = ekf.ARITH_EXACT   # the split-bf16 flush serves fp32 storage only
     ens = ekf.Ensemble(N, E, prec, max_lines=L_LINES, device=local, pipeline=bool(args.pipeline),
-                      flush_interval=args.flush_interval)
+                      flush_interval=args.flush_interval, arith=arith)
     # one real stream for everything (torch's default stream has handle 0, which the C-ABI reads
     # as "the context's own stream"): the payload copies, the RCCL waits (work.wait() orders the
     # current stream) and the EKF kernels are then ordered on the same queue
@@ -260,8 +268,10 @@ def main():
     alg_bytes = E * n * (n + 1) * bpe   # one read + write of the packed block per flush
     alg_flops = steps_per_launch * E * 2 * L_LINES * n * (n + 1)
     mfma_peak = MFMA_F64_PEAK_TFS if prec == ekf.PREC_F64 else MFMA_F32_PEAK_TFS   # f16 storage: f32 MFMA
+    bf_form = bool(dom and dom["kernel"].endswith(", true>"))
     t_hbm = alg_bytes / (HBM_PEAK_GBS * 1e9)
-    t_mfma = alg_flops / (mfma_peak * 1e12)
+    # split-bf16 flush: six bf16 MFMA products per fp32 product, at the dense bf16 rate
+    t_mfma = (6 * alg_flops / (MFMA_BF16_PEAK_TFS * 1e12)) if bf_form else alg_flops / (mfma_peak * 1e12)
     bound = "hbm" if t_hbm >= t_mfma else "mfma"
     gbs = alg_bytes / (dd_ms * 1e-3) / 1e9 if dd_ms > 0 else None
     tfs = alg_flops / (dd_ms * 1e-3) / 1e12 if dd_ms > 0 else None
@@ -292,6 +302,7 @@ def main():
             "parallelism": (f"ensemble x{world} ({'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} "
                             f"broadcast of {B} scans per collective)") if world > 1 else "ensemble x1",
                 "pipeline": bool(args.pipeline), "flush_interval": args.flush_interval,
+            "arith": "bf16x6" if arith == ekf.ARITH_BF16X6 else "exact",
         },
         "clock_preroll_steps": PR,
         "roofline": {
@@ -308,6 +319,9 @@ def main():
             "steps_per_launch": steps_per_launch,
             "hbm_gbs": gbs, "hbm_frac": (gbs / HBM_PEAK_GBS) if gbs else None,
             "mfma_tflops": tfs, "mfma_frac": (tfs / mfma_peak) if tfs else None,
+            "mfma_frac_basis": ("fp32-equivalent flops vs the dense fp32 MFMA peak; executed as six "
+                                "bf16 MFMA products each (bf16 roof: 6x the flops at "
+                                f"{MFMA_BF16_PEAK_TFS:.0f} TF/s)") if bf_form else "dense MFMA peak of the dtype",
             "ideal_ms": max(t_hbm, t_mfma) * 1e3,
             "traffic_source": traffic_src,
             "lib_sha": sha,

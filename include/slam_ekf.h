@@ -57,6 +57,16 @@ enum {
 enum { EKF_PREC_F64 = 0, EKF_PREC_F32 = 1, EKF_PREC_F16 = 2 };
 /* R source inside the association loop (SURVEY.md §8a parity-mode flags) */
 enum { EKF_R_INTENDED = 0, EKF_R_AS_WRITTEN = 1 };
+/* arithmetic of the fp32 covariance flush (ekf_config.arith).
+ * EXACT: v_mfma_f32_32x32x2_f32; the flush's per-element chain is the ordered fp32 FMA chain the
+ *   association kernel replays on read, so the state is bit-identical for every flush interval
+ *   and schedule (default; the C++ drop-in uses it).
+ * BF16X6: EKF_PREC_F32 with EKF_R_INTENDED and max_lines <= 8 (else EXACT is used): every fp32
+ *   operand split exactly into three bf16 parts (hi + mid + lo), six v_mfma_f32_32x32x16_bf16 per
+ *   product (all part products down to 2^-16 relative; the dropped ones are below 2^-24),
+ *   accumulated in fp32. Within fp32 rounding of EXACT (the 1e-6 bound of BASELINE holds) but no
+ *   longer bit-identical across flush intervals: the on-read replay stays the fp32 chain. */
+enum { EKF_ARITH_EXACT = 0, EKF_ARITH_BF16X6 = 1 };
 
 typedef struct ekf_config {
     int32_t capacity;      /* N = LINESIZE (Robot.h:13); landmarks per instance */
@@ -73,7 +83,7 @@ typedef struct ekf_config {
                               rank-2·Σm MFMA pass; scans in between read it with the pending
                               downdates applied on read. Bit-identical state for every T (the
                               MFMA chain is an ordered FMA chain); T = 1: once per scan. <= 16 */
-    int32_t reserved;
+    int32_t arith;         /* EKF_ARITH_* (fp32 flush arithmetic); formerly reserved, 0 = EXACT */
     double mahalanobis;    /* MAHALANOBIS gate, Robot.h:15 (0.4) */
     double encoder_noise;  /* ENCODERNOISE, Robot.h:17 (0.024) */
 } ekf_config;

@@ -85,6 +85,9 @@ struct ekf_ctx {
     void* ops_u;              // operand rows of every ring slot (U), slot_bytes apart
     void* ops_v;              // ... (V)
     long long slot_bytes;
+    void* ops_b;              // EKF_ARITH_BF16X6: bf16 planes of V of every ring slot (else null)
+    long long bslot_bytes;
+    bool bf;                  // the split-bf16 flush applies (arith, fp32, symmetric R, kmax 16)
     std::vector<int> pexp_h;
     // flush scheduling (see the top of this file)
     int T;                    // flush interval
@@ -153,6 +156,7 @@ static void free_all(ekf_ctx* c)
                                c->sync, c->Ust, c->Vst};
     ptrs.push_back(c->ops_u);
     ptrs.push_back(c->ops_v);
+    ptrs.push_back(c->ops_b);
     for (auto& sl : c->ring) {
         ptrs.push_back(sl.patch);
         ptrs.push_back(sl.patch_diag);
@@ -245,7 +249,8 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         (cfg->precision != EKF_PREC_F64 && cfg->precision != EKF_PREC_F32 &&
          cfg->precision != EKF_PREC_F16) ||
         (cfg->r_mode != EKF_R_INTENDED && cfg->r_mode != EKF_R_AS_WRITTEN) ||
-        cfg->flush_interval < 0 || cfg->flush_interval > 16)
+        cfg->flush_interval < 0 || cfg->flush_interval > 16 ||
+        (cfg->arith != EKF_ARITH_EXACT && cfg->arith != EKF_ARITH_BF16X6))
         return EKF_EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return EKF_EDEVICE;
@@ -290,10 +295,20 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     c->slot_bytes = (long long)(((c->op_inst * c->op_elem * E) + 255) / 256 * 256);
     ALLOC(c->ops_u, (size_t)c->slot_bytes * c->ring.size());
     ALLOC(c->ops_v, (size_t)c->slot_bytes * c->ring.size());
+    // split-bf16 flush: V's three bf16 planes per slot (written by the association kernel)
+    c->bf = cfg->arith == EKF_ARITH_BF16X6 && cfg->precision == EKF_PREC_F32 &&
+            cfg->r_mode == EKF_R_INTENDED && d.kmax == 16;
+    c->ops_b = nullptr;
+    c->bslot_bytes = 0;
+    if (c->bf) {
+        c->bslot_bytes = (long long)((c->op_inst * 3 * 2 * E + 255) / 256 * 256);
+        ALLOC(c->ops_b, (size_t)c->bslot_bytes * c->ring.size());
+    }
     for (size_t i = 0; i < c->ring.size(); i++) {
         ekf::Slot& sl = c->ring[i];
         sl.Uop = (char*)c->ops_u + (size_t)c->slot_bytes * i;
         sl.Vop = (char*)c->ops_v + (size_t)c->slot_bytes * i;
+        sl.Bop = c->bf ? (char*)c->ops_b + (size_t)c->bslot_bytes * i : nullptr;
         ALLOC(sl.patch, sizeof(double) * d.max_lines * 2 * d.M * E);
         ALLOC(sl.patch_diag, sizeof(double) * d.max_lines * 4 * E);
         ALLOC(sl.res, sizeof(int) * ekf::RES_STRIDE * E);
@@ -517,8 +532,9 @@ extern "C" int ekf_reset_instance(ekf_ctx* c, int e, double x, double y, double 
 }
 
 // profiling level 1 times the flush only (what the roofline needs, 2 events per group);
-// level 2 also every association kernel
-static EvPair* prof_begin(ekf_ctx* c, int kind, hipStream_t st)
+// level 2 also every association kernel. record = false: the caller hands the pair to the launch
+// (hipExtLaunchKernelGGL timestamps the dispatch itself; no marker packets around the flush)
+static EvPair* prof_begin(ekf_ctx* c, int kind, hipStream_t st, bool record = true)
 {
     if (!c->prof || (kind == 0 && c->prof < 2)) return nullptr;
     EvPair pr;
@@ -530,7 +546,7 @@ static EvPair* prof_begin(ekf_ctx* c, int kind, hipStream_t st)
         if (hipEventCreate(&pr.b) != hipSuccess) return nullptr;
     }
     c->ev[kind].push_back(pr);
-    (void)hipEventRecord(pr.a, st);
+    if (record) (void)hipEventRecord(pr.a, st);
     return &c->ev[kind].back();
 }
 
@@ -622,15 +638,18 @@ static int enqueue_flush(ekf_ctx* c)
     dp.nslots = (int)c->ring.size();
     dp.slot0 = (int)(c->unflushed0 % (long long)c->ring.size());
     dp.dbg = c->dbg;
+    dp.bf = c->bf ? 1 : 0;
+    dp.bbase = c->ops_b;
+    dp.bslot_bytes = c->bslot_bytes;
     for (int q = 0; q < nst; q++) dp.steps[q] = slot_of(c, c->unflushed0 + q);
     const int in = c->last_out;
     const int out = c->cfg.pipeline ? 1 - in : in;
     dp.Pin = c->X[in];
     dp.Pout = c->X[out];
-    EvPair* pr = prof_begin(c, 1, fs);
+    EvPair* pr = prof_begin(c, 1, fs, false);
     if (pr) c->ev_nsteps.push_back(nst);
-    HIP_TRY(ekf::launch_downdate(dp, c->cfg.precision, c->dd_grid, fs));
-    prof_end(c, pr, fs);
+    HIP_TRY(ekf::launch_downdate(dp, c->cfg.precision, c->dd_grid, fs, pr ? pr->a : nullptr,
+                                 pr ? pr->b : nullptr));
     hipEvent_t ev = c->ev_flush[c->nflush & 1];
     if (c->cfg.pipeline) HIP_TRY(hipEventRecord(ev, fs));
     // an instance spread over several cooperating workgroups spins on its peers: serialise its
@@ -1187,6 +1206,11 @@ extern "C" const char* ekf_flush_kernel_name(const ekf_ctx* c, int nsteps)
         return "downdate_f64_kernel";
     }
     const bool half = c->cfg.precision == EKF_PREC_F16;
+    if (c->bf && nsteps >= 2 && nsteps <= 8 && nsteps % 2 == 0) {
+        static const char* bfn[5] = {"", "flush_f32_wave_kernel<float, 2, true>", "flush_f32_wave_kernel<float, 4, true>",
+                                     "flush_f32_wave_kernel<float, 6, true>", "flush_f32_wave_kernel<float, 8, true>"};
+        return bfn[nsteps / 2];
+    }
     const bool wave = nsteps >= 2 && nsteps <= 8 && nsteps % 2 == 0 && c->d.kmax <= 16 &&
                       (nsteps >= 6 || c->dd_variant == 8);
     if (wave) {

@@ -48,6 +48,8 @@ struct Slot {
     double* patch;      // [E][max_lines][2][M]   rows of landmarks added by this step
     double* patch_diag; // [E][max_lines][4]      their 2x2 diagonal blocks
     int* res;           // [E][RES_STRIDE]
+    void* Bop;          // [E][nb][3][64][8] bf16: V split into hi + mid + lo planes, in the operand
+                        // order of v_mfma_f32_32x32x16_bf16 (EKF_ARITH_BF16X6 only, else nullptr)
 };
 
 constexpr int PMAX = 32;
@@ -127,13 +129,19 @@ struct DowndateParams {
     long long slot_bytes;
     int slot0, nslots;
     unsigned long long* dbg;  // EKF_SCAN_STAMPS buffer (timing experiments of the flush only)
+    const void* bbase;    // EKF_ARITH_BF16X6: bf16 operand planes of ring slot i at bbase + i·bslot_bytes
+    long long bslot_bytes;
+    int bf;               // 1: plain groups of 2, 4, 6 or 8 steps run the split-bf16 wave flush
     Slot steps[PMAX];
 };
 
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st);
 int scan_blocks_per_cu(int precision);
 size_t scan_lds_bytes(int precision);   // static LDS of the association kernel
-hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st);
+// ev_a / ev_b (optional): events timestamped by the dispatch packet itself (hipExtLaunchKernelGGL),
+// so timing a flush inserts no marker packets on the stream
+hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st,
+                           hipEvent_t ev_a = nullptr, hipEvent_t ev_b = nullptr);
 // ex: fp16 storage exponent of the instance (ignored for f32 / f64)
 hipError_t launch_pack(const Dims& d, int precision, const double* Pfull, void* Pll, double* Rs,
                        const int2* tile_rc, int ex, hipStream_t st);

@@ -24,6 +24,7 @@
 // the MFMA executes, then the patch rounded to storage, so every read sees bit-for-bit the value
 // the flush will store (tests/test_gpu_parity.py::test_deferred_flush_equals_drained).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <type_traits>
 
@@ -171,6 +172,21 @@ typedef float f32x2v __attribute__((ext_vector_type(2)));
 // the V side interleaved by row pair, (rh, k) at (rh >> 1) · 16 + 2k + (rh & 1), so that one
 // float2 holds both rows of a k (a packed-FMA operand).
 __device__ __forceinline__ int stage_v_index(int rh, int k) { return (rh >> 1) * 16 + 2 * k + (rh & 1); }
+
+// EKF_ARITH_BF16X6: v = hi + mid + lo, each a bf16 (the upper half of an fp32): truncation leaves
+// an exact fp32 remainder of at most 16, then 8 significant bits, so the three parts are exact.
+// Packs (a, b) into one dword per part, a in the low half (operand element order)
+__device__ __forceinline__ void split_pack(float a, float b, unsigned (&o)[3])
+{
+#pragma unroll
+    for (int pl = 0; pl < 3; pl++) {
+        const unsigned ua = __builtin_bit_cast(unsigned, a) & 0xffff0000u;
+        const unsigned ub = __builtin_bit_cast(unsigned, b) & 0xffff0000u;
+        o[pl] = (ua >> 16) | ub;
+        a -= __builtin_bit_cast(float, ua);
+        b -= __builtin_bit_cast(float, ub);
+    }
+}
 
 // Stored 2×2 block at rows a0, a0+1 and columns b0, b0+1 (a0, b0 even, a0's tile <= b0's):
 // acc = {(a0,b0), (a0,b0+1), (a0+1,b0), (a0+1,b0+1)}. In the f32 tile layout the two rows of a
@@ -1230,6 +1246,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     __shared__ double sh_pk[SPEC_L][PKW];
     __shared__ float sh_stg[SPEC_L * SPEC_QMAX * 2 * 4 * 8];   // staged pending-step rows
     __shared__ unsigned long long sh_stamp[EKF_NSTAMP];
+    // EKF_ARITH_BF16X6 (fp32 storage): the bf16 planes of the workgroup's rows, in the global
+    // plane layout of its 2·SCAN_THREADS / 32 row blocks, copied out at the end with 16-byte stores
+    static_assert(SCAN_THREADS % 16 == 0, "whole 32-row blocks per workgroup");
+    constexpr int BPL_RB = 2 * SCAN_THREADS / 32;
+    __shared__ __attribute__((aligned(16))) unsigned short sh_bpl[std::is_same<T, float>::value ? BPL_RB * 3 * 512 : 8];
     unsigned long long* dbg = (p.dbg && lead) ? p.dbg + (size_t)e * EKF_NSTAMP : nullptr;
     if (p.dbg && tid < EKF_NSTAMP) sh_stamp[tid] = 0;
     unsigned long long t_last = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -1340,6 +1361,12 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     using C = typename Stor<T>::C;   // operand (compute) type
     C* Uop = reinterpret_cast<C*>(p.cur.Uop) + (size_t)e * opstride;
     C* Vop = reinterpret_cast<C*>(p.cur.Vop) + (size_t)e * opstride;
+    // EKF_ARITH_BF16X6: V's bf16 planes for the split-bf16 flush (null otherwise)
+    unsigned short* Bop = p.cur.Bop ? reinterpret_cast<unsigned short*>(p.cur.Bop) + (size_t)e * opstride * 3
+                                    : nullptr;
+    // (staged in LDS, sh_bpl, and written once at the end: per-match 2-byte global stores cost
+    // ≈4 µs of the chain, since on CDNA every store counts in vmcnt and each later load wait
+    // then also waited for them)
     double* patch = p.cur.patch + (size_t)e * d.max_lines * 2 * M;
     double* pdiag = p.cur.patch_diag + (size_t)e * d.max_lines * 4;
     int* res = p.cur.res + (size_t)e * RES_STRIDE;
@@ -1422,6 +1449,16 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = to_domain<T>(-o1, pv.ex);
                 Vop[op_index_f32(lr, 2 * t, d.kmax)] = (C)v0;
                 Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (C)v1;
+                if constexpr (std::is_same<T, float>::value)
+                    if (Bop) {
+                        unsigned o[3];
+                        split_pack((float)v0, (float)v1, o);
+#pragma unroll
+                        for (int pl = 0; pl < 3; pl++) {
+                            sh_bpl[op_index_bf(2 * tid + pp, 2 * t, pl)] = (unsigned short)(o[pl] & 0xffffu);
+                            sh_bpl[op_index_bf(2 * tid + pp, 2 * t + 1, pl)] = (unsigned short)(o[pl] >> 16);
+                        }
+                    }
             } else {
                 Uop[op_index_f64(lr, 2 * t, d.kmax)] = (C)(-uu[2 * pp]);
                 Uop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (C)(-uu[2 * pp + 1]);
@@ -2130,7 +2167,30 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         int st = status;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) st |= __shfl_xor(st, off, 64);
+        __shared__ int sh_m;
+        if (tid == 0) sh_m = m;   // the matches, as a landmark wave counted them
         __syncthreads();
+        if constexpr (std::is_same<T, float>::value)
+            if (Bop) {
+                const int m = sh_m;
+                // the planes of the workgroup's row blocks: one 16-byte lane row (k = 2s + h,
+                // s = 0..7) per chunk; k past the matches and rows past the capacity are +0
+                typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+                const int rb0 = g * BPL_RB;
+                for (int c = tid; c < BPL_RB * 3 * 64; c += SCAN_BLOCK) {
+                    const int rbl = c / 192, ln = c & 63;
+                    if (rb0 + rbl >= d.nb) break;
+                    const bool live = (rb0 + rbl) * 32 + (ln & 31) < 2 * N;
+                    u32x4v w = *reinterpret_cast<const u32x4v*>(sh_bpl + (size_t)c * 8);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const unsigned lo = (live && 2 * q < m) ? 0xffffu : 0u;
+                        const unsigned hi = (live && 2 * q + 1 < m) ? 0xffff0000u : 0u;
+                        w[q] &= lo | hi;
+                    }
+                    *reinterpret_cast<u32x4v*>(Bop + (size_t)rb0 * 3 * 512 + (size_t)c * 8) = w;
+                }
+            }
         if ((tid & 63) == 0 && tid < SCAN_THREADS) sh_red[tid >> 6] = st;
         __syncthreads();
 #pragma unroll
@@ -2224,6 +2284,7 @@ __device__ __forceinline__ void tile_st(TS* tile, int lane, int qq, const f32x16
         __builtin_nontemporal_store(v, reinterpret_cast<f16x4*>(tile) + lane + qq * 64);
     }
 }
+
 
 // fp16 storage: the value a step leaves in the block is its fp16 rounding (see Stor)
 template <typename TS>
@@ -2728,10 +2789,17 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
 // (partial downdates are predicated); otherwise the wave runs a plain per-wave-tile loop. Per
 // element the chain is the one every other form runs (k-ordered MFMA steps, fp16 rounding per
 // step, then the step's rows or the reset): bit-identical results.
-template <typename TS, int NS>
+//
+// BF (EKF_ARITH_BF16X6, fp32 storage, symmetric operands): the plain groups run each step as six
+// v_mfma_f32_32x32x16_bf16 per accumulator on V's exact three-part bf16 split (the scan's
+// planes, Slot::Bop). With U = −V the accumulators hold −X (negated on load and store, exact), so
+// both operands are V planes: of the wave-tile's row blocks (A) and column blocks (B). Operands
+// stream through a ring of RD step-sets, RD − 1 steps ahead, across wave-tile boundaries.
+template <typename TS, int NS, bool BF = false>
 __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateParams p)
 {
     static_assert(NS >= 2 && NS % 2 == 0 && NS <= PMAX, "even step count");
+    static_assert(!BF || sizeof(TS) == 4, "split-bf16 flush: fp32 storage");
     constexpr bool HALF = sizeof(TS) == 2;
     constexpr bool AM = HALF;   // fp16 storage: pair-major step order (below)
     const Dims d = p.d;
@@ -2827,7 +2895,98 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
                                               (size_t)sl * (size_t)p.slot_bytes);
     };
 
-    if (fast) {
+    if constexpr (BF) {
+        if (fast) {
+            typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+            constexpr int RD = NS % 4 == 0 ? 4 : (NS % 3 == 0 ? 3 : 2);   // operand ring depth
+            const size_t pstride = (size_t)d.nb * 3 * 64;   // bf16x8 per instance
+            // step q's planes: slot (slot0 + q) mod nslots
+            auto pl_base = [&](int q) __attribute__((always_inline)) {
+                int sl = p.slot0 + q;
+                if (sl >= p.nslots) sl -= p.nslots;
+                return reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(p.bbase) +
+                                                       (size_t)sl * (size_t)p.bslot_bytes);
+            };
+            f32x4 pref[WT_N][4];
+            f32x16 acc[WT_N];
+            bf16x8 R[RD][WT_R + WT_C][3];
+            // step q of wave-tile t into ring set r: A row blocks, then B row blocks, three planes
+            auto load_ops = [&](int r, const Item& t, int q) __attribute__((always_inline)) {
+                const bf16x8* b = pl_base(q) + t.e * pstride + lane;
+#pragma unroll
+                for (int i = 0; i < WT_R + WT_C; i++) {
+                    const bf16x8* rb = b + (size_t)(i < WT_R ? op_row(t, 0, i) : op_row(t, 1, i - WT_R)) * 3 * 64;
+#pragma unroll
+                    for (int pl = 0; pl < 3; pl++) R[r][i][pl] = rb[pl * 64];
+                }
+            };
+            auto load_tiles = [&](const Item& t) __attribute__((always_inline)) {
+#pragma unroll
+                for (int i = 0; i < WT_N; i++) {
+                    const f32x4* tl = reinterpret_cast<const f32x4*>(Pin + tile_ptr(t, i));
+#pragma unroll
+                    for (int qq = 0; qq < 4; qq++) pref[i][qq] = __builtin_nontemporal_load(tl + lane + qq * 64);
+                }
+            };
+            Item cur, nxt, nxt2;
+            first_item(cur);
+            next_item(cur, nxt);
+            load_tiles(cur);
+#pragma unroll
+            for (int q = 0; q < RD - 1; q++) load_ops(q, cur, q);
+            int g = g0;
+            while (true) {
+                const bool more = g + K < g_end;
+                next_item(nxt, nxt2);
+                const Item ldi = more ? nxt : cur;   // the last wave-tile re-reads its own rows
+#pragma unroll
+                for (int i = 0; i < WT_N; i++)
+#pragma unroll
+                    for (int qq = 0; qq < 4; qq++)
+#pragma unroll
+                        for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = -pref[i][qq][j];
+                if (more) load_tiles(nxt);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 0; q < NS; q++) {
+                    // ring set of step q + RD − 1 (this wave-tile's, else the next one's)
+                    const int ql = q + RD - 1;
+                    if (ql < NS) load_ops(ql % RD, cur, ql);
+                    else load_ops(ql % RD, ldi, ql - NS);
+                    const int r = q % RD;
+                    // part products smallest first: (mid, mid), (hi, lo), (lo, hi), (hi, mid),
+                    // (mid, hi), (hi, hi)
+#pragma unroll
+                    for (int pp = 0; pp < 6; pp++) {
+                        const int pa = (0x102010 >> (4 * (5 - pp))) & 0xf;
+                        const int pb = (0x120100 >> (4 * (5 - pp))) & 0xf;
+#pragma unroll
+                        for (int rr = 0; rr < WT_R; rr++)
+#pragma unroll
+                            for (int c = 0; c < WT_C; c++)
+                                acc[rr * WT_C + c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                    R[r][rr][pa], R[r][WT_R + c][pb], acc[rr * WT_C + c], 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 12; i++) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
+                        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // VMEM read
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int i = 0; i < WT_N; i++)
+#pragma unroll
+                    for (int k = 0; k < 16; k++) acc[i][k] = -acc[i][k];
+                store_tiles(cur, acc);
+                if (!more) break;
+                g += K;
+                cur = nxt;
+                nxt = nxt2;
+            }
+            return;
+        }
+    } else if (fast) {
         // raw tile words in flight (fp16 storage: converted when the wave-tile starts)
         using Raw = typename std::conditional<HALF, f16x4, f32x4>::type;
         Raw pref[WT_N][4];
@@ -3566,20 +3725,21 @@ hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
     return hipGetLastError();
 }
 
-hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st)
+hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st, hipEvent_t ev_a,
+                           hipEvent_t ev_b)
 {
     if (precision == EKF_PREC_F64) {
         if (p.nsteps <= F64_WAVE_MAXS && p.d.kmax == 16 && p.nwt64 > 0 && p.wt64 != nullptr && p.variant != 2) {
             const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
             switch (p.nsteps) {
-            case 1: hipLaunchKernelGGL((flush_f64_wave_kernel<1>), dim3(wgrid), dim3(DD_THREADS), 0, st, p); break;
-            case 2: hipLaunchKernelGGL((flush_f64_wave_kernel<2>), dim3(wgrid), dim3(DD_THREADS), 0, st, p); break;
-            case 3: hipLaunchKernelGGL((flush_f64_wave_kernel<3>), dim3(wgrid), dim3(DD_THREADS), 0, st, p); break;
-            default: hipLaunchKernelGGL((flush_f64_wave_kernel<4>), dim3(wgrid), dim3(DD_THREADS), 0, st, p); break;
+            case 1: hipExtLaunchKernelGGL((flush_f64_wave_kernel<1>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p); break;
+            case 2: hipExtLaunchKernelGGL((flush_f64_wave_kernel<2>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p); break;
+            case 3: hipExtLaunchKernelGGL((flush_f64_wave_kernel<3>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p); break;
+            default: hipExtLaunchKernelGGL((flush_f64_wave_kernel<4>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p); break;
             }
             return hipGetLastError();
         }
-        hipLaunchKernelGGL(downdate_f64_kernel, dim3(grid), dim3(DD_THREADS), 0, st, p);
+        hipExtLaunchKernelGGL(downdate_f64_kernel, dim3(grid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p);
         return hipGetLastError();
     }
     const bool half = precision == EKF_PREC_F16;
@@ -3588,12 +3748,28 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     const bool wave_shape = p.nsteps >= 2 && p.nsteps <= 8 && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
                             p.nwt > 0 && p.wt != nullptr;
     const bool wave_ok = wave_shape && (p.nsteps >= 6 || p.variant == 8);
+    if (p.bf && !half && wave_shape) {   // EKF_ARITH_BF16X6: split-bf16 wave flush, 2..8 steps
+        const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));
+#define EKF_BF_CASE(NSV)                                                                                \
+    case NSV:                                                                                           \
+        hipExtLaunchKernelGGL((flush_f32_wave_kernel<float, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, st, \
+                              ev_a, ev_b, 0, p);                                                        \
+        break;
+        switch (p.nsteps) {
+            EKF_BF_CASE(2)
+            EKF_BF_CASE(4)
+            EKF_BF_CASE(6)
+            EKF_BF_CASE(8)
+        }
+#undef EKF_BF_CASE
+        return hipGetLastError();
+    }
     if (wave_ok) {
         const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
 #define EKF_WAVE_CASE(NSV)                                                                              \
     case NSV:                                                                                           \
-        if (half) hipLaunchKernelGGL((flush_f32_wave_kernel<_Float16, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, p); \
-        else hipLaunchKernelGGL((flush_f32_wave_kernel<float, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, p);         \
+        if (half) hipExtLaunchKernelGGL((flush_f32_wave_kernel<_Float16, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p); \
+        else hipExtLaunchKernelGGL((flush_f32_wave_kernel<float, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p);         \
         break;
         switch (p.nsteps) {
             EKF_WAVE_CASE(2)
@@ -3607,17 +3783,17 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     if (p.nsteps <= PST_MAXC && p.d.kmax <= 16 && p.variant != 2) {
         const int pgrid = 16 * ((p.ncu + 7) / 8);   // two workgroups per CU (48 KB LDS each)
         if (half)
-            hipLaunchKernelGGL(flush_f32_persist2_kernel<_Float16>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+            hipExtLaunchKernelGGL(flush_f32_persist2_kernel<_Float16>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p);
         else
-            hipLaunchKernelGGL(flush_f32_persist2_kernel<float>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, p);
+            hipExtLaunchKernelGGL(flush_f32_persist2_kernel<float>, dim3((unsigned)pgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p);
     } else {
         const int64_t nsb = (p.d.nb + DD_SB - 1) / DD_SB;
         const int64_t total = (int64_t)p.E * (nsb * (nsb + 1) / 2);
         const unsigned sgrid = (unsigned)(8 * ((total + 7) / 8));
         if (half)
-            hipLaunchKernelGGL(flush_f32_sb_kernel<_Float16>, dim3(sgrid), dim3(DD_THREADS), 0, st, p);
+            hipExtLaunchKernelGGL(flush_f32_sb_kernel<_Float16>, dim3(sgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p);
         else
-            hipLaunchKernelGGL(flush_f32_sb_kernel<float>, dim3(sgrid), dim3(DD_THREADS), 0, st, p);
+            hipExtLaunchKernelGGL(flush_f32_sb_kernel<float>, dim3(sgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p);
     }
     return hipGetLastError();
 }

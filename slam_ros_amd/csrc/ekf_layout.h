@@ -125,6 +125,18 @@ EKF_HD int64_t op_index_f32(int row, int k, int kmax)
     return ((int64_t)rb * 64 + lane) * (kmax / 2) + s;
 }
 
+// bf16 operand planes (EKF_ARITH_BF16X6, kmax = 16): element (row, k) of plane pl (0 hi, 1 mid,
+// 2 lo) in bf16 units; lane and slot as op_index_f32, so a lane's 8 values of one plane are one
+// 16-byte v_mfma_f32_32x32x16_bf16 operand (its k-slot 8h + s carries k = 2s + h: the same
+// permutation on both operands leaves every dot product's terms unchanged)
+EKF_HD int64_t op_index_bf(int row, int k, int pl)
+{
+    const int rb = row >> 5;
+    const int lane = (row & 31) + 32 * (k & 1);
+    const int s = k >> 1;
+    return (((int64_t)rb * 3 + pl) * 64 + lane) * 8 + s;
+}
+
 EKF_HD int64_t op_index_f64(int row, int k, int kmax)
 {
     const int rb = row >> 5;

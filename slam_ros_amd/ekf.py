@@ -21,6 +21,7 @@ from . import build as _build
 EKF_MAX_LINES = 64
 PREC_F64, PREC_F32, PREC_F16 = 0, 1, 2
 R_INTENDED, R_AS_WRITTEN = 0, 1
+ARITH_EXACT, ARITH_BF16X6 = 0, 1   # fp32 flush arithmetic (slam_ekf.h EKF_ARITH_*)
 ST_SINGULAR_S, ST_CAPACITY, ST_NONSYM, ST_SYNC_TIMEOUT, ST_RANGE = 1, 2, 4, 8, 16
 EXP_AUTO = -1000
 
@@ -44,7 +45,7 @@ class EkfConfig(ctypes.Structure):
         ("precision", ctypes.c_int32), ("device", ctypes.c_int32),
         ("max_lines", ctypes.c_int32), ("r_mode", ctypes.c_int32),
         ("reset_margin", ctypes.c_int32), ("pipeline", ctypes.c_int32),
-        ("flush_interval", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("flush_interval", ctypes.c_int32), ("arith", ctypes.c_int32),
         ("mahalanobis", ctypes.c_double), ("encoder_noise", ctypes.c_double),
     ]
 
@@ -165,7 +166,7 @@ class Ensemble:
     def __init__(self, capacity: int, instances: int = 1, precision: int = PREC_F64,
                  max_lines: int = 20, device: int = -1, r_mode: int = R_INTENDED,
                  reset_margin: int = 10, mahalanobis: float = 0.4, encoder_noise: float = 0.024,
-                 pipeline: bool = False, flush_interval: int = 1):
+                 pipeline: bool = False, flush_interval: int = 1, arith: int = ARITH_EXACT):
         self._lib = load_library()
         cfg = EkfConfig()
         self._lib.ekf_config_init(ctypes.byref(cfg))
@@ -174,11 +175,13 @@ class Ensemble:
         cfg.reset_margin, cfg.mahalanobis, cfg.encoder_noise = reset_margin, mahalanobis, encoder_noise
         cfg.pipeline = 1 if pipeline else 0
         cfg.flush_interval = int(flush_interval)
+        cfg.arith = int(arith)
         h = ctypes.c_void_p()
         _check(self._lib.ekf_create(ctypes.byref(cfg), ctypes.byref(h)), "ekf_create")
         self._h = h
         self.capacity, self.instances, self.precision = capacity, instances, precision
         self.max_lines = max_lines
+        self.arith = int(arith)
         self.n = self._lib.ekf_state_dim(h)
         self._res = (EkfResult * instances)()
 

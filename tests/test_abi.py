@@ -54,6 +54,11 @@ def test_cpu_only_calls(ekf_mod):
     lib.ekf_config_init(ctypes.byref(bad))
     bad.max_lines = 1000
     assert lib.ekf_create(ctypes.byref(bad), ctypes.byref(h)) == 1   # EKF_EINVAL before any HIP call
+    # ekf_config.arith (the former reserved word): EXACT by default, unknown values rejected
+    assert cfg.arith == ekf_mod.ARITH_EXACT == 0
+    lib.ekf_config_init(ctypes.byref(bad))
+    bad.arith = 7
+    assert lib.ekf_create(ctypes.byref(bad), ctypes.byref(h)) == 1
 
 
 def test_struct_layouts_match_header():
@@ -61,6 +66,7 @@ def test_struct_layouts_match_header():
     from slam_ros_amd import ekf
     assert ctypes.sizeof(ekf.EkfLine) == 48
     assert ctypes.sizeof(ekf.EkfConfig) == 56
+    assert ekf.EkfConfig.arith.offset == 36   # after the nine int32 fields, as in slam_ekf.h
     assert ctypes.sizeof(ekf.EkfResult) == 24 + 6 * 4 + 4 * ekf.EKF_MAX_LINES
 
 

@@ -49,11 +49,11 @@ def record(key, value):
     json.dump(data, open(path, "w"), indent=1)
 
 
-def run_config(ekf_mod, oracle_mod, prec, T, scans, pipeline=False):
+def run_config(ekf_mod, oracle_mod, prec, T, scans, pipeline=False, arith=0):
     from tests.hipmem import DeviceArray
     world = G.make_world(N)
     st = G.initial_state(world)
-    ens = ekf_mod.Ensemble(N, E, prec, max_lines=L, flush_interval=T, pipeline=pipeline)
+    ens = ekf_mod.Ensemble(N, E, prec, max_lines=L, flush_interval=T, pipeline=pipeline, arith=arith)
     for e in range(E):
         ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
     refs = {}
@@ -77,8 +77,10 @@ def run_config(ekf_mod, oracle_mod, prec, T, scans, pipeline=False):
             assert res[e]["match"] == m, (prec, s, e, res[e]["match"], m)
             assert res[e]["matches"] == L
         assert all(r["status"] == 0 for r in res), [r["status"] for r in res]
-        if (s + 1) % T == 0:                           # a group end: the flush has run
+        if (s + 1) % T == 0 or s + 1 == scans:         # a group end: the flush has run
             k = s + 1
+            if k % T:
+                ens.sync()                              # the partial last group (bench's ekf_sync)
             for e in CHECK:
                 P, y, saved, pose = ens.download_state(e)
                 rp, ry = rel(P, refs[e].P_t0), rel(y, refs[e].y)
@@ -117,3 +119,16 @@ def test_bench_config_fp16_t8(ekf_mod, oracle_mod):
 def test_bench_config_fp64_t4(ekf_mod, oracle_mod):
     out = run_config(ekf_mod, oracle_mod, 0, 4, 8)
     record("f64_T4_N4096_E8", out)
+
+
+def test_bench_config_fp32_t8_bf16x6(ekf_mod, oracle_mod):
+    """EKF_ARITH_BF16X6 (the split-bf16 flush, flush_f32_wave_kernel<float, NS, true>) over the
+    bench's exact step count: 20 scans = two groups of 8 and a partial group of 4 flushed by
+    ekf_sync. The same per-scan bar (1e-6 on P, 1e-8 on y) against the fp64 restatement."""
+    out = run_config(ekf_mod, oracle_mod, 1, 8, 20, arith=ekf_mod.ARITH_BF16X6)
+    record("f32_T8_N4096_E8_bf16x6", out)
+
+
+def test_bench_config_fp32_t8_bf16x6_pipelined(ekf_mod, oracle_mod):
+    out = run_config(ekf_mod, oracle_mod, 1, 8, 16, pipeline=True, arith=ekf_mod.ARITH_BF16X6)
+    record("f32_T8_N4096_E8_bf16x6_pipelined", out)

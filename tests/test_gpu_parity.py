@@ -496,6 +496,63 @@ def test_wave_flush_equals_drained(ekf_mod, monkeypatch, prec, N, T, lines, extr
         assert sa == sb
 
 
+@pytest.mark.parametrize("N,T,lines,extra_every", [(80, 8, 6, 3), (80, 2, 8, 0), (64, 6, 6, 4),
+                                                  (1024, 8, 8, 0), (1024, 4, 6, 5), (96, 3, 8, 0)])
+def test_bf16x6_flush_close_to_exact(ekf_mod, oracle_mod, N, T, lines, extra_every):
+    """EKF_ARITH_BF16X6 (split-bf16 wave flush for plain groups of 2, 4, 6 or 8 steps; groups
+    with augmentation rows or the reset, odd group sizes and the partial last group fall back to
+    the fp32 forms): same associations as the exact arithmetic drained after every scan, and the
+    state within the fp32 bar — P ≤ 1e-6 relative (BASELINE's bound), y ≤ 1e-8 — also against
+    the fp64 restatement for instance 0."""
+    E = 3
+    w = G.make_world(N, active=N - 14 if extra_every else N - 10)
+    st = G.initial_state(w)
+    a = ekf_mod.Ensemble(N, E, 1, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
+    b = ekf_mod.Ensemble(N, E, 1, max_lines=8)
+    if T % 2 == 0:
+        assert a.flush_kernel_name(T).endswith(", true>"), a.flush_kernel_name(T)
+    assert not b.flush_kernel_name(8).endswith(", true>")
+    for ens in (a, b):
+        for e in range(E):
+            ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+    ref = oracle_mod.OracleRobot(N)
+    ref.set_state(*b.download_state(0))
+    rng = np.random.default_rng(5)
+    for step in range(1, 3 * T + 2):
+        enc, ln, nl = G.make_scan(w, step, instances=E, lines=lines)
+        if extra_every and step % extra_every == 0:
+            ex = G.random_lines(rng, 2)[None].repeat(E, axis=0)
+            ln = np.concatenate([ln, ex], axis=1)
+            nl = np.full(E, ln.shape[1], dtype=np.int32)
+        ra = a.localize(enc, ln, nl)
+        rb = b.localize(enc, ln, nl)
+        b.download_state(0, with_P=False)
+        m = ref.localize(ln[0], enc[0])
+        assert ra[0]["match"] == m, (step, ra[0]["match"], m)
+        for e in range(E):
+            assert ra[e]["match"] == rb[e]["match"], (step, e)
+            assert ra[e]["status"] == 0, (step, e, ra[e]["status"])
+    k = 3 * T + 1
+    meas = {}
+    for e in range(E):
+        Pa, ya, sa, pa = a.download_state(e)
+        Pb, yb, sb, pb = b.download_state(e)
+        meas[e] = {"P_bf_vs_exact": rel(Pa, Pb), "y_bf_vs_exact": rel(ya, yb)}
+        if e == 0:
+            meas[e].update(P_bf_vs_fp64=rel(Pa, ref.P_t0), P_exact_vs_fp64=rel(Pb, ref.P_t0),
+                           y_bf_vs_fp64=rel(ya, ref.y), y_exact_vs_fp64=rel(yb, ref.y))
+        # k scans, never re-synchronised: the per-scan bars (1e-6 on P, 1e-8 on y) times k
+        assert rel(Pa, Pb) <= k * 1e-6 and rel(ya, yb) <= k * 1e-8, (e, meas[e])
+        assert sa == sb
+        if e == 0:
+            assert meas[0]["P_bf_vs_fp64"] <= k * 1e-6 and meas[0]["y_bf_vs_fp64"] <= k * 1e-8, meas[0]
+    from tests.test_bench_config import record
+    record(f"bf16x6_vs_exact_N{N}_T{T}_L{lines}_x{extra_every}", meas)
+    # kmax > 16 (max_lines 16): the exact forms serve every group
+    c = ekf_mod.Ensemble(N, 1, 1, max_lines=16, flush_interval=8, arith=ekf_mod.ARITH_BF16X6)
+    assert not c.flush_kernel_name(8).endswith(", true>")
+
+
 @pytest.mark.parametrize("N,T,lines,extra_every", [(80, 4, 8, 0), (80, 4, 6, 3), (64, 3, 6, 2), (100, 2, 8, 0),
                                                    (96, 1, 5, 0)])
 def test_f64_wave_flush_equals_tile_kernel(ekf_mod, monkeypatch, N, T, lines, extra_every):
