@@ -74,8 +74,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="1: overlap the association kernels with the previous group's flush")
-    ap.add_argument("--flush-interval", type=int, default=8,
-                    help="T: rewrite the landmark block once per T scans (bit-identical state)")
+    ap.add_argument("--flush-interval", type=int, default=0,
+                    help="T: rewrite the landmark block once per T scans (0: 12 for f32 with the "
+                         "split-bf16 flush, 8 for f32 exact and f16, 4 for f64)")
     ap.add_argument("--bcast-every", type=int, default=0,
                     help="scans per broadcast (default: the flush interval); broadcasts run one "
                          "group ahead of the scans that use them")
@@ -83,7 +84,7 @@ def parse():
                     help="nccl (= RCCL on ROCm); gloo only to rehearse ranks on one GPU")
     ap.add_argument("--preroll", type=int, default=200,
                     help="untimed clock pre-roll steps before the warm-up (steady GPU clocks)")
-    ap.add_argument("--arith", choices=["exact", "bf16x6"], default="exact",
+    ap.add_argument("--arith", choices=["exact", "bf16x6"], default="bf16x6",
                     help="fp32 flush arithmetic (slam_ekf.h EKF_ARITH_*): exact = fp32 MFMA, the state "
                          "bit-identical for every T; bf16x6 = fp32 operands split exactly into three "
                          "bf16 parts, six bf16 MFMAs per product (f32 storage only)")
@@ -169,6 +170,9 @@ def main():
     arith = {"exact": ekf.ARITH_EXACT, "bf16x6": ekf.ARITH_BF16X6}[args.arith]
     if prec != ekf.PREC_F32:
         arith = ekf.ARITH_EXACT   # the split-bf16 flush serves fp32 storage only
+    if args.flush_interval <= 0:
+        args.flush_interval = {ekf.PREC_F64: 4, ekf.PREC_F16: 8}.get(
+            prec, 12 if arith == ekf.ARITH_BF16X6 else 8)
     ens = ekf.Ensemble(N, E, prec, max_lines=L_LINES, device=local, pipeline=bool(args.pipeline),
                       flush_interval=args.flush_interval, arith=arith)
     # one real stream for everything (torch's default stream has handle 0, which the C-ABI reads

@@ -47,7 +47,7 @@ def main(tag):
     shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(out, "kernel_stats.csv"))
     shutil.copy(os.path.join(src, "bench.json"), os.path.join(out, "bench.json"))
     ctr = {}
-    for sub in ("fetch", "write", "sq"):
+    for sub in ("fetch", "write", "sq", "l2"):
         for k, v in counters(os.path.join(src, sub, "run_counter_collection.csv")).items():
             ctr.setdefault(k, {}).update(v)
     json.dump(ctr, open(os.path.join(out, "counters_avg_per_dispatch.json"), "w"), indent=1)
@@ -80,6 +80,7 @@ def main(tag):
           "alg_bytes_per_launch": b["roofline"]["alg_bytes_per_launch"],
           "traffic_over_alg": hbm / b["roofline"]["alg_bytes_per_launch"],
           "sq": {k: v for k, v in c.items() if k.startswith("SQ_") or k.startswith("GRBM")},
+          "l2": {k: v for k, v in c.items() if k.startswith("TCC_HIT") or k.startswith("TCC_MISS")},
           "lib_sha": bench.lib_sha(ekf.LIB_PATH), "source": f"profiles/{tag}/counters_avg_per_dispatch.json"}
     json.dump(tj, open(os.path.join(out, "traffic.json"), "w"), indent=1)
     print(json.dumps({k: tj[k] for k in ("kernel", "hbm_bytes_per_launch", "traffic_over_alg")}))

@@ -1206,9 +1206,11 @@ extern "C" const char* ekf_flush_kernel_name(const ekf_ctx* c, int nsteps)
         return "downdate_f64_kernel";
     }
     const bool half = c->cfg.precision == EKF_PREC_F16;
-    if (c->bf && nsteps >= 2 && nsteps <= 8 && nsteps % 2 == 0) {
-        static const char* bfn[5] = {"", "flush_f32_wave_kernel<float, 2, true>", "flush_f32_wave_kernel<float, 4, true>",
-                                     "flush_f32_wave_kernel<float, 6, true>", "flush_f32_wave_kernel<float, 8, true>"};
+    if (c->bf && nsteps >= 2 && nsteps <= 16 && nsteps % 2 == 0 && nsteps != 10 && nsteps != 14) {
+        static const char* bfn[9] = {"", "flush_f32_wave_kernel<float, 2, true>", "flush_f32_wave_kernel<float, 4, true>",
+                                     "flush_f32_wave_kernel<float, 6, true>", "flush_f32_wave_kernel<float, 8, true>",
+                                     "flush_f32_wave_kernel<float, 10, true>", "flush_f32_wave_kernel<float, 12, true>",
+                                     "flush_f32_wave_kernel<float, 14, true>", "flush_f32_wave_kernel<float, 16, true>"};
         return bfn[nsteps / 2];
     }
     const bool wave = nsteps >= 2 && nsteps <= 8 && nsteps % 2 == 0 && c->d.kmax <= 16 &&

@@ -963,7 +963,7 @@ constexpr int SPEC_PB = 2;                          // guessed columns per pass 
 #ifndef EKF_STAGED_DEPTH
 #define EKF_STAGED_DEPTH 1
 #endif
-constexpr int SPEC_QMAX = 8;                        // pending steps staged in LDS (pipelined T = 4: up to 7)
+constexpr int SPEC_QMAX = 16;                       // pending steps staged in LDS (T = 16: up to 15)
 constexpr int SPEC_GMAX = 64;                       // workgroups per instance (<= one wave)
 constexpr int SPEC_WD = 14 + 4 * (SPEC_L - 1);      // winner record: rr, Dj, y, sin/cos, column blocks
 // speculative package: the words of build_package, then the robot 3×3 block and x_pre after the
@@ -1246,11 +1246,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     __shared__ double sh_pk[SPEC_L][PKW];
     __shared__ float sh_stg[SPEC_L * SPEC_QMAX * 2 * 4 * 8];   // staged pending-step rows
     __shared__ unsigned long long sh_stamp[EKF_NSTAMP];
-    // EKF_ARITH_BF16X6 (fp32 storage): the bf16 planes of the workgroup's rows, in the global
-    // plane layout of its 2·SCAN_THREADS / 32 row blocks, copied out at the end with 16-byte stores
-    static_assert(SCAN_THREADS % 16 == 0, "whole 32-row blocks per workgroup");
-    constexpr int BPL_RB = 2 * SCAN_THREADS / 32;
-    __shared__ __attribute__((aligned(16))) unsigned short sh_bpl[std::is_same<T, float>::value ? BPL_RB * 3 * 512 : 8];
+    // EKF_ARITH_BF16X6 (fp32 storage): the owned rows' V values of this scan's matches (k-major
+    // per row), split into bf16 planes and stored once at the end
+    __shared__ __attribute__((aligned(16))) float sh_vpl[std::is_same<T, float>::value ? SCAN_THREADS * 32 : 4];
     unsigned long long* dbg = (p.dbg && lead) ? p.dbg + (size_t)e * EKF_NSTAMP : nullptr;
     if (p.dbg && tid < EKF_NSTAMP) sh_stamp[tid] = 0;
     unsigned long long t_last = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -1364,7 +1362,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // EKF_ARITH_BF16X6: V's bf16 planes for the split-bf16 flush (null otherwise)
     unsigned short* Bop = p.cur.Bop ? reinterpret_cast<unsigned short*>(p.cur.Bop) + (size_t)e * opstride * 3
                                     : nullptr;
-    // (staged in LDS, sh_bpl, and written once at the end: per-match 2-byte global stores cost
+    // (staged in LDS, sh_vpl, and written once at the end: per-match 2-byte global stores cost
     // ≈4 µs of the chain, since on CDNA every store counts in vmcnt and each later load wait
     // then also waited for them)
     double* patch = p.cur.patch + (size_t)e * d.max_lines * 2 * M;
@@ -1450,15 +1448,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 Vop[op_index_f32(lr, 2 * t, d.kmax)] = (C)v0;
                 Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (C)v1;
                 if constexpr (std::is_same<T, float>::value)
-                    if (Bop) {
-                        unsigned o[3];
-                        split_pack((float)v0, (float)v1, o);
-#pragma unroll
-                        for (int pl = 0; pl < 3; pl++) {
-                            sh_bpl[op_index_bf(2 * tid + pp, 2 * t, pl)] = (unsigned short)(o[pl] & 0xffffu);
-                            sh_bpl[op_index_bf(2 * tid + pp, 2 * t + 1, pl)] = (unsigned short)(o[pl] >> 16);
-                        }
-                    }
+                    if (Bop)
+                        *reinterpret_cast<f32x2v*>(sh_vpl + tid * 32 + pp * 16 + 2 * t) = f32x2v{(float)v0, (float)v1};
             } else {
                 Uop[op_index_f64(lr, 2 * t, d.kmax)] = (C)(-uu[2 * pp]);
                 Uop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (C)(-uu[2 * pp + 1]);
@@ -2171,24 +2162,36 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         if (tid == 0) sh_m = m;   // the matches, as a landmark wave counted them
         __syncthreads();
         if constexpr (std::is_same<T, float>::value)
-            if (Bop) {
+            if (Bop && own) {
+                // the owned rows' planes: per row and k parity h (k = 2s + h, s = 0..7) one
+                // 16-byte lane row per part; k past the matches +0
                 const int m = sh_m;
-                // the planes of the workgroup's row blocks: one 16-byte lane row (k = 2s + h,
-                // s = 0..7) per chunk; k past the matches and rows past the capacity are +0
                 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-                const int rb0 = g * BPL_RB;
-                for (int c = tid; c < BPL_RB * 3 * 64; c += SCAN_BLOCK) {
-                    const int rbl = c / 192, ln = c & 63;
-                    if (rb0 + rbl >= d.nb) break;
-                    const bool live = (rb0 + rbl) * 32 + (ln & 31) < 2 * N;
-                    u32x4v w = *reinterpret_cast<const u32x4v*>(sh_bpl + (size_t)c * 8);
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const unsigned lo = (live && 2 * q < m) ? 0xffffu : 0u;
-                        const unsigned hi = (live && 2 * q + 1 < m) ? 0xffff0000u : 0u;
-                        w[q] &= lo | hi;
+                for (int pp = 0; pp < 2; pp++) {
+                    const f32x4v* src = reinterpret_cast<const f32x4v*>(sh_vpl + tid * 32 + pp * 16);
+                    float v[16];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const f32x4v x = src[i];
+#pragma unroll
+                        for (int u = 0; u < 4; u++) v[4 * i + u] = (4 * i + u) < 2 * m ? x[u] : 0.f;
                     }
-                    *reinterpret_cast<u32x4v*>(Bop + (size_t)rb0 * 3 * 512 + (size_t)c * 8) = w;
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        unsigned w[3][4];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            unsigned o[3];
+                            split_pack(v[4 * q + h], v[4 * q + 2 + h], o);
+#pragma unroll
+                            for (int pl = 0; pl < 3; pl++) w[pl][q] = o[pl];
+                        }
+#pragma unroll
+                        for (int pl = 0; pl < 3; pl++)
+                            *reinterpret_cast<u32x4v*>(Bop + op_index_bf(2 * j + pp, h, pl)) =
+                                u32x4v{w[pl][0], w[pl][1], w[pl][2], w[pl][3]};
+                    }
                 }
             }
         if ((tid & 63) == 0 && tid < SCAN_THREADS) sh_red[tid >> 6] = st;
@@ -2795,11 +2798,15 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
 // planes, Slot::Bop). With U = −V the accumulators hold −X (negated on load and store, exact), so
 // both operands are V planes: of the wave-tile's row blocks (A) and column blocks (B). Operands
 // stream through a ring of RD step-sets, RD − 1 steps ahead, across wave-tile boundaries.
+#ifndef EKF_BF_WAVES
+#define EKF_BF_WAVES 1   // split-bf16 flush: waves per SIMD (2: ≤ 256 registers, ring depth 2; measured equal)
+#endif
 template <typename TS, int NS, bool BF = false>
-__global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateParams p)
+__global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_wave_kernel(DowndateParams p)
 {
     static_assert(NS >= 2 && NS % 2 == 0 && NS <= PMAX, "even step count");
     static_assert(!BF || sizeof(TS) == 4, "split-bf16 flush: fp32 storage");
+    static_assert(BF || NS <= 8, "fp32 wave flush: at most 8 steps (operands of every step in registers)");
     constexpr bool HALF = sizeof(TS) == 2;
     constexpr bool AM = HALF;   // fp16 storage: pair-major step order (below)
     const Dims d = p.d;
@@ -2898,7 +2905,7 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateP
     if constexpr (BF) {
         if (fast) {
             typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-            constexpr int RD = NS % 4 == 0 ? 4 : (NS % 3 == 0 ? 3 : 2);   // operand ring depth
+            constexpr int RD = EKF_BF_WAVES > 1 ? 2 : (NS % 4 == 0 ? 4 : (NS % 3 == 0 ? 3 : 2));   // operand ring depth
             const size_t pstride = (size_t)d.nb * 3 * 64;   // bf16x8 per instance
             // step q's planes: slot (slot0 + q) mod nslots
             auto pl_base = [&](int q) __attribute__((always_inline)) {
@@ -3748,8 +3755,11 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     const bool wave_shape = p.nsteps >= 2 && p.nsteps <= 8 && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
                             p.nwt > 0 && p.wt != nullptr;
     const bool wave_ok = wave_shape && (p.nsteps >= 6 || p.variant == 8);
-    if (p.bf && !half && wave_shape) {   // EKF_ARITH_BF16X6: split-bf16 wave flush, 2..8 steps
-        const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));
+    const bool bf_shape = p.nsteps >= 2 && p.nsteps <= 16 && p.nsteps % 2 == 0 && p.nsteps != 10 && p.nsteps != 14 &&
+                          p.d.kmax <= 16 &&
+                          p.nwt > 0 && p.wt != nullptr;
+    if (p.bf && !half && bf_shape) {   // EKF_ARITH_BF16X6: split-bf16 wave flush, 2-8, 12 or 16 steps
+        const unsigned wgrid = (unsigned)(8 * EKF_BF_WAVES * ((p.ncu + 7) / 8));   // EKF_BF_WAVES workgroups per CU
 #define EKF_BF_CASE(NSV)                                                                                \
     case NSV:                                                                                           \
         hipExtLaunchKernelGGL((flush_f32_wave_kernel<float, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, st, \
@@ -3760,6 +3770,8 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
             EKF_BF_CASE(4)
             EKF_BF_CASE(6)
             EKF_BF_CASE(8)
+            EKF_BF_CASE(12)
+            EKF_BF_CASE(16)
         }
 #undef EKF_BF_CASE
         return hipGetLastError();

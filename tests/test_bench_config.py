@@ -132,3 +132,15 @@ def test_bench_config_fp32_t8_bf16x6(ekf_mod, oracle_mod):
 def test_bench_config_fp32_t8_bf16x6_pipelined(ekf_mod, oracle_mod):
     out = run_config(ekf_mod, oracle_mod, 1, 8, 16, pipeline=True, arith=ekf_mod.ARITH_BF16X6)
     record("f32_T8_N4096_E8_bf16x6_pipelined", out)
+
+
+def test_bench_config_fp32_t12_bf16x6(ekf_mod, oracle_mod):
+    """bench.py's default line: EKF_ARITH_BF16X6 at T = 12 over its 20 timed steps (a group of 12,
+    then 8 flushed by ekf_sync); up to 11 pending steps replayed on read (staged in LDS)."""
+    out = run_config(ekf_mod, oracle_mod, 1, 12, 20, arith=ekf_mod.ARITH_BF16X6)
+    record("f32_T12_N4096_E8_bf16x6", out)
+
+
+def test_bench_config_fp32_t16_bf16x6(ekf_mod, oracle_mod):
+    out = run_config(ekf_mod, oracle_mod, 1, 16, 20, arith=ekf_mod.ARITH_BF16X6)
+    record("f32_T16_N4096_E8_bf16x6", out)
