@@ -12,8 +12,11 @@ pre-roll (--preroll steps of the same workload, default 200 ≈ 30 ms, reported 
 `clock_preroll_steps`) lets the GPU reach the clocks it holds under this load: a step is ≈0.12 ms,
 so a few warm-up steps alone measure the clock ramp (≈12 % lower with 8 warm-up steps).
 
-Schedule (defaults): the landmark block is flushed once per T = 8 scans (flush_interval), in
-place, between association kernels (--pipeline 1 overlaps them instead); every schedule is
+Schedule (defaults): the landmark block is flushed once per T = 12 scans (flush_interval), in
+place, between association kernels (--pipeline 1 overlaps them instead), by the split-bf16 flush
+(--arith bf16x6, slam_ekf.h EKF_ARITH_BF16X6: fp32 operands split exactly into three bf16
+parts, six bf16 MFMAs per product, fp32 accumulation; held to the fp32 parity bar,
+tests/test_bench_config.py). With --arith exact (fp32 MFMA, T = 8) every schedule is
 bit-identical to a per-scan in-place update (tests/test_gpu_parity.py::
 test_deferred_flush_equals_drained). The timed region ends with ekf_sync, which flushes the
 partial group: every step's downdate is in P. HIP events in the timed region bracket the flush
