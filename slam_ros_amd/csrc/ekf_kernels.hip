@@ -2942,7 +2942,14 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
 #pragma unroll
             for (int q = 0; q < RD - 1; q++) load_ops(q, cur, q);
             int g = g0;
+#ifdef EKF_XP_FLUSH_STAMPS   // timing experiment: shader cycles per wave-tile section, in-kernel clock
+            unsigned long long xs_b = 0, xs_m = 0, xs_s = 0, xs_n = 0;
+            const unsigned long long xc0 = __builtin_amdgcn_s_memtime(), xr0 = __builtin_amdgcn_s_memrealtime();
+#endif
             while (true) {
+#ifdef EKF_XP_FLUSH_STAMPS
+                const unsigned long long xt0 = __builtin_amdgcn_s_memtime();
+#endif
                 const bool more = g + K < g_end;
                 next_item(nxt, nxt2);
                 const Item ldi = more ? nxt : cur;   // the last wave-tile re-reads its own rows
@@ -2954,6 +2961,9 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
                         for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = -pref[i][qq][j];
                 if (more) load_tiles(nxt);
                 __builtin_amdgcn_sched_barrier(0);
+#ifdef EKF_XP_FLUSH_STAMPS
+                const unsigned long long xt1 = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll
                 for (int q = 0; q < NS; q++) {
                     // ring set of step q + RD − 1 (this wave-tile's, else the next one's)
@@ -2981,16 +2991,32 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
+#ifdef EKF_XP_FLUSH_STAMPS
+                const unsigned long long xt2 = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll
                 for (int i = 0; i < WT_N; i++)
 #pragma unroll
                     for (int k = 0; k < 16; k++) acc[i][k] = -acc[i][k];
                 store_tiles(cur, acc);
+#ifdef EKF_XP_FLUSH_STAMPS
+                __builtin_amdgcn_sched_barrier(0);
+                const unsigned long long xt3 = __builtin_amdgcn_s_memtime();
+                xs_b += xt1 - xt0; xs_m += xt2 - xt1; xs_s += xt3 - xt2; xs_n += 1;
+#endif
                 if (!more) break;
                 g += K;
                 cur = nxt;
                 nxt = nxt2;
             }
+#ifdef EKF_XP_FLUSH_STAMPS
+            if (p.dbg && lane == 0) {
+                atomicAdd(p.dbg + 24, xs_b); atomicAdd(p.dbg + 25, xs_m);
+                atomicAdd(p.dbg + 26, xs_s); atomicAdd(p.dbg + 27, xs_n);
+                atomicAdd(p.dbg + 28, __builtin_amdgcn_s_memtime() - xc0);
+                atomicAdd(p.dbg + 29, __builtin_amdgcn_s_memrealtime() - xr0);
+            }
+#endif
             return;
         }
     } else if (fast) {
