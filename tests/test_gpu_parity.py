@@ -333,6 +333,35 @@ def test_edge_cases(ekf_mod, oracle_mod, prec):
     assert res["saved"] == N and res["status"] & ekf_mod.ST_CAPACITY
 
 
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("theta", [7.0, -7.0, 13.0, 3.2, -3.5, 2 * np.pi])
+def test_normalize_radian_quirk_on_gpu(ekf_mod, oracle_mod, prec, theta):
+    """Robot.cpp:62-71's fold for |rad| >= 2π (if / else-if, no loop: 7 → −5.566, not 0.717) on the
+    device: a pose heading past ±π (and past ±2π) goes through the no-match commit
+    (Robot.cpp:702-716: pose = normalizeRadian(x_pre)), the innovation angles of the gate
+    (Robot.cpp:347-349) and the post-update heading (Robot.cpp:596), against the restatement."""
+    N = 30
+    w = G.make_world(N, active=12)
+    st = G.initial_state(w)
+    y0 = st.y.copy()
+    y0[2] = theta
+    pose0 = np.array([st.pose[0], st.pose[1], theta])
+    state = (st.dense_P(), y0, st.saved, pose0)
+    # no lines: the prediction is committed through normalizeRadian
+    ens, ref = make_pair(ekf_mod, oracle_mod, N, prec, state)
+    res = ens.localize([0.05, -0.02, 0.3], np.zeros((1, 0, 6)), [0])[0]
+    ref.localize(np.zeros((0, 6)), [0.05, -0.02, 0.3])
+    assert res["matches"] == 0
+    check_same(ens, ref, prec, where=f"no lines, theta {theta}")
+    # lines: gating angles and the updated heading, two scans in a row
+    ens, ref = make_pair(ekf_mod, oracle_mod, N, prec, state)
+    for step in (1, 2):
+        enc, lines, nl = G.make_scan(w, step)
+        res = ens.localize(enc, lines, nl)[0]
+        m = ref.localize(lines[0][:nl[0]], enc[0])
+        check_same(ens, ref, prec, res, m, f"lines, theta {theta}, scan {step}")
+
+
 def test_ellipse_matches_eigen(ekf_mod):
     N = 8
     ens = ekf_mod.Ensemble(N, 1, 0)
