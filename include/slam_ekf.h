@@ -24,7 +24,10 @@
 extern "C" {
 #endif
 
-#define SLAM_EKF_ABI_VERSION 1
+/* 2: ekf_debug_scan_stamps fills 32 slots (was 16); ekf_config.arith (formerly reserved) selects
+ *    the fp32 flush arithmetic and EKF_ARITH_BF16X6 is rejected (EKF_EINVAL) for configurations
+ *    that can never use it; EKF_ST_SYNC_TIMEOUT rolls the call back instead of committing it. */
+#define SLAM_EKF_ABI_VERSION 2
 #define EKF_MAX_LINES 64 /* lines per scan per instance; main.cpp:99 reserves 20 */
 
 /* status codes */
@@ -44,7 +47,9 @@ enum {
                               K·S·Kᵀ — and from then on its P — is not symmetric; the packed
                               symmetric storage keeps the upper triangle. */
     EKF_ST_SYNC_TIMEOUT = 8, /* the instance's cooperating workgroups did not all arrive at an
-                                exchange within the spin bound (results of that call invalid) */
+                                exchange within the spin bound: the call is rolled back (the
+                                instance keeps its state from before the call, as if the scan had
+                                not been received; the result record reports no matches) */
     EKF_ST_RANGE = 16,     /* EKF_PREC_F16 only: a landmark this call added has a variance above a
                               quarter of the fp16 range at the instance's storage exponent
                               (2^exp·P stored; values are still finite). ekf_rescale re-chooses
@@ -61,11 +66,15 @@ enum { EKF_R_INTENDED = 0, EKF_R_AS_WRITTEN = 1 };
  * EXACT: v_mfma_f32_32x32x2_f32; the flush's per-element chain is the ordered fp32 FMA chain the
  *   association kernel replays on read, so the state is bit-identical for every flush interval
  *   and schedule (default; the C++ drop-in uses it).
- * BF16X6: EKF_PREC_F32 with EKF_R_INTENDED and max_lines <= 8 (else EXACT is used): every fp32
- *   operand split exactly into three bf16 parts (hi + mid + lo), six v_mfma_f32_32x32x16_bf16 per
- *   product (all part products down to 2^-16 relative; the dropped ones are below 2^-24),
- *   accumulated in fp32. Within fp32 rounding of EXACT (the 1e-6 bound of BASELINE holds) but no
- *   longer bit-identical across flush intervals: the on-read replay stays the fp32 chain. */
+ * BF16X6: requires EKF_PREC_F32, EKF_R_INTENDED and max_lines <= 8; any other configuration is
+ *   rejected by ekf_create with EKF_EINVAL. Every fp32 operand is split exactly into three bf16
+ *   parts (hi + mid + lo), six v_mfma_f32_32x32x16_bf16 per product (all part products down to
+ *   2^-16 relative; the dropped ones are below 2^-24), accumulated in fp32. Within fp32 rounding of
+ *   EXACT (the 1e-6 bound of BASELINE holds) but no longer bit-identical across flush intervals:
+ *   the on-read replay stays the fp32 chain. Groups of an even number of steps (2..16) without
+ *   augmented rows or a reset take the split-bf16 flush; a group with augmentation or the reset,
+ *   and an odd-sized group (a partial group flushed by a drain), take the EXACT forms
+ *   (ekf_flush_kernel_name reports the form a group size runs). */
 enum { EKF_ARITH_EXACT = 0, EKF_ARITH_BF16X6 = 1 };
 
 typedef struct ekf_config {
@@ -77,8 +86,12 @@ typedef struct ekf_config {
     int32_t r_mode;        /* EKF_R_* */
     int32_t reset_margin;  /* map wiped when savedLineCount > N - margin (Robot.cpp:893: 10) */
     int32_t pipeline;      /* 1: double-buffer the landmark block so that association kernels
-                              overlap the covariance downdate of earlier scans (applying it on
-                              read, bit-identically); 0: in-place, strictly sequential */
+                              may overlap the covariance downdate of earlier scans (applying it on
+                              read, bit-identically); 0: in-place, strictly sequential. Overlap
+                              happens only when an instance fits one association workgroup
+                              (N <= 192): otherwise its cooperating workgroups must not wait on
+                              CUs a flush holds, so its association kernels are ordered after the
+                              flush in flight, and the second buffer is not allocated */
     int32_t flush_interval;/* T >= 1: the landmark block is rewritten once per T scans by one
                               rank-2·Σm MFMA pass; scans in between read it with the pending
                               downdates applied on read. Bit-identical state for every T (the
@@ -186,13 +199,15 @@ int ekf_profile_read(ekf_ctx* ctx, double* scan_ms, double* downdate_ms, double*
 int ekf_profile_flushes(ekf_ctx* ctx, int cap, int* nsteps, float* ms);
 const char* ekf_flush_kernel_name(const ekf_ctx* ctx, int nsteps);
 /* Diagnostic: association-kernel phase timers (sum over instances, 100 MHz ticks), collected
- * only when the environment had EKF_SCAN_STAMPS=1 at ekf_create. Slots: 0 predict, 1 diagonal
- * gather + barrier, 2 gating, 3 min-reduction barrier, 4 winner package, 5 broadcast barrier,
- * 6 gain rows, 7 commit/augmentation, 8 total, 9 launches; 16-19 per-line phases of the first
- * landmark wave (gate, wait for the package, gain rows, robot update). */
+ * only when the environment had EKF_SCAN_STAMPS=1 at ekf_create. 32 slots (ABI 2; ABI 1 had 16):
+ * 0 predict, 1 diagonal gather + barrier, 2 gating, 3 min-reduction barrier, 4 winner package,
+ * 5 broadcast barrier, 6 gain rows, 7 commit/augmentation, 8 total, 9 launches; 16-19 per-line
+ * phases of the first landmark wave (gate, wait for the package, gain rows, robot update);
+ * 20-22 gate-filter counts; the rest scripts/assoc_probe.py names. */
 int ekf_debug_scan_stamps(ekf_ctx* ctx, unsigned long long out[32]);
 /* Diagnostic: words 0..15 of instance e's result record as of the last ekf_read_results
- * (word 9: association path code, 10..15: the first six guessed winners). */
+ * (word 9: association path code, 10..14: the first five guessed winners, 15: 1 if the call was
+ * rolled back after EKF_ST_SYNC_TIMEOUT). */
 int ekf_debug_result_words(ekf_ctx* ctx, int e, int out[16]);
 
 #ifdef __cplusplus

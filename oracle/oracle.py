@@ -72,6 +72,34 @@ def threads(omp: bool = True) -> int:
     return lib(omp).oracle_threads()
 
 
+def host_cpus() -> dict:
+    """What the CPU baseline may use on this host: logical CPUs, the affinity mask, the cgroup CPU
+    quota and OMP_NUM_THREADS (the OpenMP build uses the latter; on the GPU pool it is set to the
+    process's share of the host, which the pool also enforces)."""
+    import os
+    out = {"logical_cpus": os.cpu_count(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        out["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        out["affinity_cpus"] = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                out["cgroup_cpu_max"] = f.read().strip()
+            break
+        except OSError:
+            continue
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    out["model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return out
+
+
 def _dp(a: np.ndarray):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
 

@@ -15,7 +15,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libslam_ekf.so")
 SOURCES = ["ekf_kernels.hip", "ekf_api.hip"]
-HEADERS = ["ekf_kernels.h", "ekf_layout.h"]
+HEADERS = ["ekf_kernels.h", "ekf_layout.h", "ekf_commit.h"]
 ARCH = "gfx950"
 
 

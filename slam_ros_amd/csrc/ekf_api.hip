@@ -46,8 +46,9 @@ struct ekf_ctx {
     size_t pll_inst;          // elements per instance
     size_t op_inst;           // operand elements per instance
     void* X[2];
-    double* Rs;
-    double* y;
+    double* Rs;               // [2][E][3][n] robot strip, two copies (the association kernel reads
+    double* y;                // [2][E][n]    copy cur[e] and writes the other; the lead commits it)
+    int* cur;                 // [E] committed copy per instance (device; read back when needed)
     double* pose;
     double* xpre;
     int* saved;
@@ -74,6 +75,8 @@ struct ekf_ctx {
     int G;                    // association workgroups per instance
     int mbw;                  // mailbox words per workgroup slot
     int spec;                 // speculative association (EKF_SPECULATE)
+    int spin_log2;            // spin bound of the association kernel's waits (EKF_SPIN_LOG2, tests)
+    int test_drop;            // test hook (EKF_TEST_DROP_WG = e): instance e's last workgroup never runs
     int scan_batch;           // instances per association launch (co-residency bound)
     unsigned scan_epoch;      // association launches so far (mailbox tags)
     double* mbox;
@@ -151,7 +154,7 @@ int ekf_abi_version(void) { return SLAM_EKF_ABI_VERSION; }
 
 static void free_all(ekf_ctx* c)
 {
-    std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->pose, c->xpre, c->saved, c->D,
+    std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->cur, c->pose, c->xpre, c->saved, c->D,
                                c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->pexp, c->sink, c->mbox,
                                c->sync, c->Ust, c->Vst};
     ptrs.push_back(c->ops_u);
@@ -196,6 +199,26 @@ static int drain(ekf_ctx* c)
 
 static inline int cur_buf(const ekf_ctx* c) { return c->last_out; }
 
+// Committed copy of instance e's robot strip and mean (the association kernel flips it when it
+// commits a launch): read back after the stream has drained up to here.
+static int strip_copy(ekf_ctx* c, int e, int* cb)
+{
+    HIP_TRY(hipMemcpyAsync(cb, c->cur + e, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (*cb != 0 && *cb != 1) return EKF_EDEVICE;
+    return EKF_OK;
+}
+
+static inline double* strip_of(const ekf_ctx* c, int cb, int e)
+{
+    return c->Rs + ((size_t)cb * c->cfg.instances + e) * 3 * c->d.n;
+}
+
+static inline double* mean_of(const ekf_ctx* c, int cb, int e)
+{
+    return c->y + ((size_t)cb * c->cfg.instances + e) * c->d.n;
+}
+
 static int set_exponent(ekf_ctx* c, int e, int ex)
 {
     c->pexp_h[e] = ex;
@@ -220,17 +243,19 @@ static int set_robot_ctor(ekf_ctx* c, int e, double x, double y, double th)
     const Dims& d = c->d;
     HIP_TRY(hipMemsetAsync((char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem, 0,
                            c->pll_inst * c->elem, c->stream));
-    HIP_TRY(hipMemsetAsync(c->Rs + (size_t)e * 3 * d.n, 0, sizeof(double) * 3 * d.n, c->stream));
-    HIP_TRY(hipMemsetAsync(c->y + (size_t)e * d.n, 0, sizeof(double) * d.n, c->stream));
+    const int zero = 0;
     const double v = 0.05;
-    HIP_TRY(hipMemcpyAsync(c->Rs + (size_t)e * 3 * d.n + 0, &v, sizeof(double),
-                           hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->Rs + (size_t)e * 3 * d.n + d.n + 1, &v, sizeof(double),
-                           hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->cur + e, &zero, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    for (int cb = 0; cb < 2; cb++) {
+        HIP_TRY(hipMemsetAsync(strip_of(c, cb, e), 0, sizeof(double) * 3 * d.n, c->stream));
+        HIP_TRY(hipMemsetAsync(mean_of(c, cb, e), 0, sizeof(double) * d.n, c->stream));
+        HIP_TRY(hipMemcpyAsync(strip_of(c, cb, e) + 0, &v, sizeof(double), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(strip_of(c, cb, e) + d.n + 1, &v, sizeof(double), hipMemcpyHostToDevice,
+                               c->stream));
+    }
     const double pose[3] = {x, y, th};
     HIP_TRY(hipMemcpyAsync(c->pose + 3 * e, pose, sizeof(pose), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->xpre + 3 * e, pose, sizeof(pose), hipMemcpyHostToDevice, c->stream));
-    const int zero = 0;
     HIP_TRY(hipMemcpyAsync(c->saved + e, &zero, sizeof(int), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return set_exponent(c, e, c->cfg.precision == EKF_PREC_F16 ? ekf::F16_EXP_DEFAULT : 0);
@@ -250,7 +275,10 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
          cfg->precision != EKF_PREC_F16) ||
         (cfg->r_mode != EKF_R_INTENDED && cfg->r_mode != EKF_R_AS_WRITTEN) ||
         cfg->flush_interval < 0 || cfg->flush_interval > 16 ||
-        (cfg->arith != EKF_ARITH_EXACT && cfg->arith != EKF_ARITH_BF16X6))
+        (cfg->arith != EKF_ARITH_EXACT && cfg->arith != EKF_ARITH_BF16X6) ||
+        // the split-bf16 flush needs symmetric fp32 operands with kmax = 16 (slam_ekf.h)
+        (cfg->arith == EKF_ARITH_BF16X6 &&
+         (cfg->precision != EKF_PREC_F32 || cfg->r_mode != EKF_R_INTENDED || cfg->max_lines > 8)))
         return EKF_EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return EKF_EDEVICE;
@@ -271,6 +299,11 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     c->op_elem = (cfg->precision == EKF_PREC_F64) ? 8 : 4;   // operands in the compute type
     c->pll_inst = (size_t)d.ntiles * ekf::TILE_ELEMS;
     c->op_inst = (size_t)d.nb * 64 * (d.kmax / 2);
+    c->G = (d.N + ekf::SCAN_THREADS - 1) / ekf::SCAN_THREADS;
+    // pipeline: the association kernels of an instance spread over G > 1 cooperating workgroups
+    // must never wait on CUs a flush holds, so they are ordered after the flush in flight, and
+    // nothing would overlap: such contexts run the sequential schedule (slam_ekf.h)
+    if (c->G > 1) c->cfg.pipeline = 0;
     int rc = EKF_ENOMEM;
 #define ALLOC(ptr, bytes)                                                       \
     do {                                                                        \
@@ -278,10 +311,11 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         if (hipMemset((void*)(ptr), 0, (bytes)) != hipSuccess) goto fail;       \
     } while (0)
     ALLOC(c->X[0], c->pll_inst * c->elem * E);
-    if (cfg->pipeline) ALLOC(c->X[1], c->pll_inst * c->elem * E);
+    if (c->cfg.pipeline) ALLOC(c->X[1], c->pll_inst * c->elem * E);
     else c->X[1] = nullptr;
-    ALLOC(c->Rs, sizeof(double) * 3 * d.n * E);
-    ALLOC(c->y, sizeof(double) * d.n * E);
+    ALLOC(c->Rs, sizeof(double) * 3 * d.n * E * 2);
+    ALLOC(c->y, sizeof(double) * d.n * E * 2);
+    ALLOC(c->cur, sizeof(int) * E);
     ALLOC(c->pose, sizeof(double) * 3 * E);
     ALLOC(c->xpre, sizeof(double) * 3 * E);
     ALLOC(c->saved, sizeof(int) * E);
@@ -289,15 +323,14 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     ALLOC(c->Ust, sizeof(double) * d.max_lines * d.n * 2 * E);
     ALLOC(c->Vst, sizeof(double) * d.max_lines * d.n * 2 * E);
     c->T = cfg->flush_interval > 0 ? cfg->flush_interval : 1;
-    c->ring.assign((size_t)c->T * (cfg->pipeline ? 2 : 1), ekf::Slot{});
+    c->ring.assign((size_t)c->T * (c->cfg.pipeline ? 2 : 1), ekf::Slot{});
     // the operand rows of all slots in two contiguous buffers (fixed slot stride): the wave
     // flush addresses step q's rows from one base and its ring index (DowndateParams::ubase)
     c->slot_bytes = (long long)(((c->op_inst * c->op_elem * E) + 255) / 256 * 256);
     ALLOC(c->ops_u, (size_t)c->slot_bytes * c->ring.size());
     ALLOC(c->ops_v, (size_t)c->slot_bytes * c->ring.size());
     // split-bf16 flush: V's three bf16 planes per slot (written by the association kernel)
-    c->bf = cfg->arith == EKF_ARITH_BF16X6 && cfg->precision == EKF_PREC_F32 &&
-            cfg->r_mode == EKF_R_INTENDED && d.kmax == 16;
+    c->bf = cfg->arith == EKF_ARITH_BF16X6;   // (validated above: fp32, symmetric R, kmax 16)
     c->ops_b = nullptr;
     c->bslot_bytes = 0;
     if (c->bf) {
@@ -325,10 +358,11 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     ALLOC(c->pexp, sizeof(int) * E);
     ALLOC(c->sink, 8 * ekf::TILE_ELEMS);
     c->pexp_h.assign(E, 0);
-    c->G = (d.N + ekf::SCAN_THREADS - 1) / ekf::SCAN_THREADS;
     // whole 128-B lines: the package words, then 16 words for the speculative list words
     c->mbw = ((ekf::MB_WORDS_FIXED + 4 * d.max_lines + 15) / 16) * 16 + 16;
     c->spec = getenv("EKF_SPECULATE") ? atoi(getenv("EKF_SPECULATE")) : 1;
+    c->spin_log2 = getenv("EKF_SPIN_LOG2") ? std::max(8, std::min(24, atoi(getenv("EKF_SPIN_LOG2")))) : 24;
+    c->test_drop = getenv("EKF_TEST_DROP_WG") ? atoi(getenv("EKF_TEST_DROP_WG")) + 1 : 0;
     ALLOC(c->mbox, sizeof(double) * 2 * c->G * c->mbw * E);
     c->sync_stride = ((ekf::SYNC_WG0 + c->G + 15) / 16) * 16;
     ALLOC(c->sync, sizeof(int) * c->sync_stride * E);
@@ -569,6 +603,10 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.enc_noise = c->cfg.encoder_noise;
     p.Rs = c->Rs;
     p.y = c->y;
+    p.live = c->cur;
+    p.Etot = c->cfg.instances;
+    p.spin_log2 = c->spin_log2;
+    p.test_drop = c->test_drop;
     p.pose = c->pose;
     p.xpre = c->xpre;
     p.saved = c->saved;
@@ -652,10 +690,6 @@ static int enqueue_flush(ekf_ctx* c)
                                  pr ? pr->b : nullptr));
     hipEvent_t ev = c->ev_flush[c->nflush & 1];
     if (c->cfg.pipeline) HIP_TRY(hipEventRecord(ev, fs));
-    // an instance spread over several cooperating workgroups spins on its peers: serialise its
-    // association kernels after the flush in flight, so that no flush workgroup ever holds the
-    // CUs its peers wait for (single-workgroup instances overlap freely)
-    if (c->cfg.pipeline && c->G > 1) HIP_TRY(hipStreamWaitEvent(c->stream, ev, 0));
     if (c->cfg.pipeline) {
         // next scans read X[in] (= output of the previous flush) with both groups pending
         c->base = in;
@@ -740,7 +774,8 @@ extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (int e = 0; e < E; e++)
         for (int gq = 0; gq < c->G; gq++)
-            c->h_res[(size_t)e * ekf::RES_STRIDE + ekf::RES_STATUS] |= hs[(size_t)e * c->sync_stride + ekf::SYNC_WG0 + gq];
+            c->h_res[(size_t)e * ekf::RES_STRIDE + ekf::RES_STATUS] |=
+                hs[(size_t)e * c->sync_stride + ekf::SYNC_WG0 + gq] & 0xff;   // done_word: status bits
     if (!out) return EKF_OK;
     for (int e = 0; e < E; e++) {
         const int* r = c->h_res + (size_t)e * ekf::RES_STRIDE;
@@ -807,6 +842,9 @@ extern "C" int ekf_upload_state(ekf_ctx* c, int e, const double* P, const double
     int rc = drain(c);
     if (rc) return rc;
     const Dims& d = c->d;
+    int cb = 0;
+    rc = strip_copy(c, e, &cb);
+    if (rc) return rc;
     if (P) {
         double vmax = 0.0;
         if (c->cfg.precision == EKF_PREC_F16)
@@ -820,13 +858,13 @@ extern "C" int ekf_upload_state(ekf_ctx* c, int e, const double* P, const double
         if (err == hipSuccess)
             err = ekf::launch_pack(d, c->cfg.precision, tmp,
                                    (char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem,
-                                   c->Rs + (size_t)e * 3 * d.n, c->tile_rc, c->pexp_h[e], c->stream);
+                                   strip_of(c, cb, e), c->tile_rc, c->pexp_h[e], c->stream);
         if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
         (void)hipFree(tmp);
         HIP_TRY(err);
     }
     if (y)
-        HIP_TRY(hipMemcpyAsync(c->y + (size_t)e * d.n, y, sizeof(double) * d.n,
+        HIP_TRY(hipMemcpyAsync(mean_of(c, cb, e), y, sizeof(double) * d.n,
                                hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->saved + e, &saved, sizeof(int), hipMemcpyHostToDevice, c->stream));
     if (pose) {
@@ -847,12 +885,15 @@ extern "C" int ekf_download_state(ekf_ctx* c, int e, double* P, double* y, int* 
     int rc = drain(c);
     if (rc) return rc;
     const Dims& d = c->d;
+    int cb = 0;
+    rc = strip_copy(c, e, &cb);
+    if (rc) return rc;
     if (P) {
         double* tmp = nullptr;
         HIP_TRY(hipMalloc((void**)&tmp, sizeof(double) * d.n * d.n));
         hipError_t err = ekf::launch_unpack(d, c->cfg.precision, tmp,
                                             (const char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem,
-                                            c->Rs + (size_t)e * 3 * d.n, c->pexp_h[e], c->stream);
+                                            strip_of(c, cb, e), c->pexp_h[e], c->stream);
         if (err == hipSuccess)
             err = hipMemcpyAsync(P, tmp, sizeof(double) * d.n * d.n, hipMemcpyDeviceToHost,
                                  c->stream);
@@ -861,7 +902,7 @@ extern "C" int ekf_download_state(ekf_ctx* c, int e, double* P, double* y, int* 
         HIP_TRY(err);
     }
     if (y)
-        HIP_TRY(hipMemcpyAsync(y, c->y + (size_t)e * d.n, sizeof(double) * d.n,
+        HIP_TRY(hipMemcpyAsync(y, mean_of(c, cb, e), sizeof(double) * d.n,
                                hipMemcpyDeviceToHost, c->stream));
     if (saved)
         HIP_TRY(hipMemcpyAsync(saved, c->saved + e, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -880,6 +921,9 @@ extern "C" int ekf_init_lowrank(ekf_ctx* c, int e, const double* diag, const dou
     int rc = drain(c);
     if (rc) return rc;
     const Dims& d = c->d;
+    int cb = 0;
+    rc = strip_copy(c, e, &cb);
+    if (rc) return rc;
     double vmax = 0.0;
     if (c->cfg.precision == EKF_PREC_F16)
         for (int i = 3; i < d.n; i++) {
@@ -899,7 +943,7 @@ extern "C" int ekf_init_lowrank(ekf_ctx* c, int e, const double* diag, const dou
     if (err == hipSuccess)
         err = ekf::launch_lowrank(d, c->cfg.precision, dd, du, rank,
                                   (char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem,
-                                  c->Rs + (size_t)e * 3 * d.n, c->tile_rc, c->pexp_h[e], c->stream);
+                                  strip_of(c, cb, e), c->tile_rc, c->pexp_h[e], c->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
     (void)hipFree(dd);
     if (du) (void)hipFree(du);
@@ -923,8 +967,11 @@ extern "C" int ekf_rescale(ekf_ctx* c, int e, int ex)
     int rc = drain(c);
     if (rc) return rc;
     const Dims& d = c->d;
+    int cb = 0;
+    rc = strip_copy(c, e, &cb);
+    if (rc) return rc;
     void* X = (char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem;
-    double* Rs = c->Rs + (size_t)e * 3 * d.n;
+    double* Rs = strip_of(c, cb, e);
     double* tmp = nullptr;
     HIP_TRY(hipMalloc((void**)&tmp, sizeof(double) * d.n * d.n));
     std::vector<double> dg(d.n);
@@ -952,8 +999,11 @@ extern "C" int ekf_get_pose_cov(ekf_ctx* c, int e, double P33[9])
     if (!c || !P33) return EKF_EINVAL;
     if (e < 0 || e >= c->cfg.instances) return EKF_ERANGE;
     const Dims& d = c->d;
+    int cb = 0;
+    const int rc = strip_copy(c, e, &cb);
+    if (rc) return rc;
     for (int a = 0; a < 3; a++)
-        HIP_TRY(hipMemcpyAsync(P33 + 3 * a, c->Rs + (size_t)e * 3 * d.n + (size_t)a * d.n,
+        HIP_TRY(hipMemcpyAsync(P33 + 3 * a, strip_of(c, cb, e) + (size_t)a * d.n,
                                sizeof(double) * 3, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return EKF_OK;
@@ -1206,7 +1256,7 @@ extern "C" const char* ekf_flush_kernel_name(const ekf_ctx* c, int nsteps)
         return "downdate_f64_kernel";
     }
     const bool half = c->cfg.precision == EKF_PREC_F16;
-    if (c->bf && nsteps >= 2 && nsteps <= 16 && nsteps % 2 == 0 && nsteps != 10 && nsteps != 14) {
+    if (c->bf && nsteps >= 2 && nsteps <= 16 && nsteps % 2 == 0) {
         static const char* bfn[9] = {"", "flush_f32_wave_kernel<float, 2, true>", "flush_f32_wave_kernel<float, 4, true>",
                                      "flush_f32_wave_kernel<float, 6, true>", "flush_f32_wave_kernel<float, 8, true>",
                                      "flush_f32_wave_kernel<float, 10, true>", "flush_f32_wave_kernel<float, 12, true>",

@@ -1,0 +1,31 @@
+// ekf_commit.h — the association kernel's commit decision (host + device, no HIP dependency, so
+// that tests/test_abi.py compiles it on the host).
+#pragma once
+
+#include "../../include/slam_ekf.h"
+#include "ekf_layout.h"
+
+namespace ekf {
+
+// Completion word of an association workgroup (sync[SYNC_WG0 + g]): bits 31..8 the launch epoch
+// (mod 2^24), 7..0 the status bits it saw. The lead commits the launch only if every workgroup's
+// word carries this epoch and no timeout (commit_status); otherwise the instance keeps the state
+// from before the call (the launch wrote only the inactive copy of the robot strip and mean).
+EKF_HD unsigned done_word(unsigned epoch, int status) { return ((epoch & 0xffffffu) << 8) | ((unsigned)status & 0xffu); }
+
+// The lead's decision from the G completion words as last seen (words[0] is its own): the OR of
+// the status bits, with EKF_ST_SYNC_TIMEOUT added for every word not (yet) of this epoch. The
+// launch commits iff the result has no timeout bit.
+EKF_HD int commit_fold(int st, unsigned word, unsigned epoch)
+{
+    return st | (((word >> 8) != (epoch & 0xffffffu)) ? (int)EKF_ST_SYNC_TIMEOUT : (int)(word & 0xffu));
+}
+
+EKF_HD int commit_status(const unsigned* words, int G, unsigned epoch)
+{
+    int st = 0;
+    for (int g = 0; g < G; g++) st = commit_fold(st, words[g], epoch);
+    return st;
+}
+
+}  // namespace ekf

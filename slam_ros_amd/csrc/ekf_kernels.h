@@ -5,6 +5,7 @@
 
 #include "../../include/slam_ekf.h"
 #include "ekf_layout.h"
+#include "ekf_commit.h"
 
 namespace ekf {
 
@@ -32,7 +33,8 @@ enum {
     RES_NLINES = 6,
     RES_KSTEPS = 7,   // MFMA k-steps of the downdate (0 = no downdate)
     RES_NADD = 8,     // landmarks actually added (patch rows)
-    RES_DBG = 9,      // diagnostics: association path code, then the first 6 guessed winners
+    RES_DBG = 9,      // diagnostics: association path code, then the first 5 guessed winners
+    RES_ROLLBACK = 15,// 1: the call timed out and was rolled back (no downdate, rows or reset)
     RES_MATCH = 16,                     // [EKF_MAX_LINES]
     RES_EXTRA = 16 + EKF_MAX_LINES,     // [EKF_MAX_LINES] line indices, in order
     RES_STRIDE = 16 + 2 * EKF_MAX_LINES,
@@ -87,8 +89,12 @@ struct ScanParams {
     double gate;
     double enc_noise;
     const void* Pread;    // [E][ntiles][1024] landmark block to read
-    double* Rs;           // [E][3][n]  robot strip (rows 0..2 of P)
-    double* y;            // [E][n]
+    double* Rs;           // [2][Etot][3][n]  robot strip (rows 0..2 of P), two copies: a launch reads
+    double* y;            // [2][Etot][n]     copy live[e] and writes the other, which the lead commits
+    int* live;            // [Etot] committed copy of Rs / y per instance (flipped by the lead)
+    int Etot;             // instances of the context
+    int spin_log2;        // spin bound of every wait: 2^spin_log2 polls (24; tests lower it)
+    int test_drop;        // test hook: e + 1 = the last workgroup of instance e never runs (0: off)
     double* pose;         // [E][3]
     double* xpre;         // [E][3]
     int* saved;           // [E]

@@ -656,8 +656,10 @@ __device__ __forceinline__ void mb_tag(double* slot, unsigned epoch, unsigned co
 
 // Thread k < G polls workgroup k's tag of the given parity until it carries (epoch, code);
 // returns its payload (-1 on timeout, with the status bit set).
+// Every wait gives up after 2^spin polls (≈0.5 s at 24) and sets the timeout bit; a thread whose
+// status already holds it does not wait again (the launch is rolled back anyway).
 __device__ __forceinline__ int mb_poll(const double* mbox, int par, int G, int k, int mbw,
-                                       unsigned epoch, unsigned code, int& status)
+                                       unsigned epoch, unsigned code, int& status, int spin)
 {
     const unsigned long long want = ((unsigned long long)epoch << 8) | code;
     const unsigned long long* tw =
@@ -666,7 +668,7 @@ __device__ __forceinline__ int mb_poll(const double* mbox, int par, int G, int k
     int polls = 0;
     while ((v >> 24) != want) {
         __builtin_amdgcn_s_sleep(1);
-        if (++polls > (1 << 24)) {   // ~seconds: a workgroup never arrived
+        if ((status & EKF_ST_TIMEOUT_BIT) || ++polls > (1 << spin)) {   // a workgroup never arrived
             status |= EKF_ST_TIMEOUT_BIT;
             return -1;
         }
@@ -689,7 +691,7 @@ __device__ __forceinline__ void mb_store_tagged(double* p, unsigned epoch, unsig
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ unsigned long long mb_wait_tagged(const double* p, unsigned epoch, int& status)
+__device__ __forceinline__ unsigned long long mb_wait_tagged(const double* p, unsigned epoch, int& status, int spin)
 {
     const unsigned long long* w = reinterpret_cast<const unsigned long long*>(p);
     const unsigned long long want = epoch & 0xffffffu;
@@ -697,7 +699,7 @@ __device__ __forceinline__ unsigned long long mb_wait_tagged(const double* p, un
     int polls = 0;
     while ((v >> LIST_TAG_SHIFT) != want) {
         __builtin_amdgcn_s_sleep(1);
-        if (++polls > (1 << 24)) {
+        if ((status & EKF_ST_TIMEOUT_BIT) || ++polls > (1 << spin)) {
             status |= EKF_ST_TIMEOUT_BIT;
             return 0;
         }
@@ -706,27 +708,35 @@ __device__ __forceinline__ unsigned long long mb_wait_tagged(const double* p, un
     return v & ((1ull << LIST_TAG_SHIFT) - 1);
 }
 
-// Each workgroup announces that it has read the instance's shared inputs (after its loads
-// returned); the lead waits for all G before overwriting them. Bounded spin.
-__device__ __forceinline__ void signal_started(int* sync, int tid)
+// End of a launch (rollback protocol). Every workgroup has written its owned columns of the
+// robot strip and mean into the inactive copy; it publishes its completion word (done_word) after
+// its loads and stores have returned. The lead (workgroup 0, thread 0) waits for the other G − 1
+// words of this epoch, bounded, and returns commit_status over all G: the launch commits (the lead
+// flips cur[e] and writes the shared state) only if no timeout is in it. The shared inputs every
+// workgroup read at its start (pose, saved, x_pre) are rewritten only after every word arrived,
+// i.e. after every workgroup has finished reading them.
+__device__ __forceinline__ void publish_done(int* sync, int g, unsigned epoch, int st)
 {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0)
-        __hip_atomic_fetch_add(&sync[SYNC_START], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<unsigned*>(&sync[SYNC_WG0 + g]), done_word(epoch, st),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The start counter is never reset: launch `epoch` is complete once it reaches epoch·G.
-__device__ __forceinline__ int wait_all_started(int* sync, int G, unsigned epoch)
+__device__ __forceinline__ int lead_collect(int* sync, int G, unsigned epoch, int own_status, int spin)
 {
-    const unsigned target = epoch * (unsigned)G;
+    int st = commit_fold(0, done_word(epoch, own_status), epoch);
     int polls = 0;
-    while ((int)((unsigned)__hip_atomic_load(&sync[SYNC_START], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
-                 target) < 0) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++polls > (1 << 24)) return EKF_ST_TIMEOUT_BIT;
+    bool late = (own_status & EKF_ST_TIMEOUT_BIT) != 0;
+    for (int k = 1; k < G; k++) {
+        const unsigned* w = reinterpret_cast<const unsigned*>(&sync[SYNC_WG0 + k]);
+        unsigned v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while ((v >> 8) != (epoch & 0xffffffu) && !late) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++polls > (1 << spin)) late = true;
+            v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        st = commit_fold(st, v, epoch);   // (= commit_status over the G words)
     }
-    return 0;
+    return st;
 }
 
 // rows 0..2 of Fx·P for one landmark's robot-strip columns (Robot.cpp:242)
@@ -1040,7 +1050,7 @@ __device__ __forceinline__ void staged_blocks(const PllView<T>& v, int j, const 
         if (cw.x) {
 #pragma unroll
             for (int b = 0; b < NB; b++) r[b][0] = r[b][1] = r[b][2] = r[b][3] = (C)0;
-        } else {
+        } else if (cw.y > 0 || cw.z > 0) {   // (ks = 0: no match, or a rolled-back step: nothing to apply)
             // staged V rows of column b, interleaved by row pair (stage_v_index; block b + 1's
             // read from LDS while block b computes); the diagonal block's are the owned V rows
             auto read_x = [&](int b, f32x4v (&X)[2][4]) __attribute__((always_inline)) {
@@ -1158,7 +1168,7 @@ __device__ __forceinline__ void staged_pair_block(const PllView<T>& v, int wa, i
             acc[0] = acc[1] = acc[2] = acc[3] = (C)0;
             continue;
         }
-        {   // every k-step (see staged_blocks)
+        if (cw.y > 0) {   // every k-step (see staged_blocks); ks = 0: nothing (rolled back or no match)
             const float* cu = stg + (((tA * SPEC_QMAX + q) * 2 + 0) * 4) * 8;
             const float* cv = stg + (((tB * SPEC_QMAX + q) * 2 + 1) * 4) * 8;
 #pragma unroll
@@ -1215,11 +1225,17 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     const bool own = tid < SCAN_THREADS && j < d.N;
     const int n = d.n, N = d.N, M = d.M;
     const int b0 = 3 + 2 * j;                   // its first row of P
-    double* Rs = p.Rs + (size_t)e * 3 * n;
-    double* y = p.y + (size_t)e * n;
+    // robot strip and mean: read the committed copy, write the other (committed by the lead at
+    // the end only if every workgroup completed: a timed-out launch leaves the state untouched)
+    const int cb = p.live[e];
+    const double* Rs = p.Rs + ((size_t)cb * p.Etot + e) * 3 * n;
+    const double* y = p.y + ((size_t)cb * p.Etot + e) * n;
+    double* Rsw = p.Rs + ((size_t)(1 - cb) * p.Etot + e) * 3 * n;
+    double* yw = p.y + ((size_t)(1 - cb) * p.Etot + e) * n;
     int* sync = p.sync + (size_t)e * p.sync_stride;
     double* mbox = p.mbox + (size_t)e * 2 * G * p.mbw;
     const bool lead = (g == 0 && tid == 0);
+    if (p.test_drop == e + 1 && G > 1 && g == G - 1) return;   // test hook: a workgroup that never runs
 
     __shared__ double sh_pkg[MB_VH + 4 * EKF_MAX_LINES];
     __shared__ int sh_red[SCAN_THREADS / 64];
@@ -1332,21 +1348,28 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     if (own && (p.phase & PHASE_UPDATE)) sincos(ma0, &s0j, &c0j);
 
     if (!(p.phase & PHASE_UPDATE)) {
-        // predict only: write the predicted robot strip, 3×3 block and x_pre
+        // predict only: the predicted robot strip (and the mean, unchanged) into the other copy,
+        // the 3×3 block and x_pre by the lead once every workgroup completed
         if (own) {
-            *reinterpret_cast<double2*>(Rs + b0) = rr0;
-            *reinterpret_cast<double2*>(Rs + n + b0) = rr1;
-            *reinterpret_cast<double2*>(Rs + 2 * n + b0) = rr2;
+            *reinterpret_cast<double2*>(Rsw + b0) = rr0;
+            *reinterpret_cast<double2*>(Rsw + n + b0) = rr1;
+            *reinterpret_cast<double2*>(Rsw + 2 * n + b0) = rr2;
+            *reinterpret_cast<double2*>(yw + b0) = yb;
         }
-        signal_started(sync, tid);
-        if (tid == 0 && !lead) sync[SYNC_WG0 + g] = 0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0 && !lead) publish_done(sync, g, p.epoch, 0);
         if (lead) {
-            const int to = wait_all_started(sync, G, p.epoch);
-            sync[SYNC_WG0 + g] = to;
-            for (int a = 0; a < 9; a++) Rs[(a / 3) * n + (a % 3)] = R33[a];
-            p.xpre[3 * e + 0] = xp[0];
-            p.xpre[3 * e + 1] = xp[1];
-            p.xpre[3 * e + 2] = xp[2];
+            const int st = lead_collect(sync, G, p.epoch, 0, p.spin_log2);
+            sync[SYNC_WG0] = (int)done_word(p.epoch, st);
+            if (!(st & EKF_ST_TIMEOUT_BIT)) {
+                for (int a = 0; a < 9; a++) Rsw[(a / 3) * n + (a % 3)] = R33[a];
+                yw[0] = y[0]; yw[1] = y[1]; yw[2] = y[2];
+                p.xpre[3 * e + 0] = xp[0];
+                p.xpre[3 * e + 1] = xp[1];
+                p.xpre[3 * e + 2] = xp[2];
+                p.live[e] = 1 - cb;
+            }
         }
         return;
     }
@@ -1392,8 +1415,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     const ekf_line* lines = p.lines + (size_t)e * d.max_lines;
     for (int k = tid; k < L * 6; k += SCAN_BLOCK)
         reinterpret_cast<double*>(sh_lines)[k] = reinterpret_cast<const double*>(lines)[k];
-    // all per-instance inputs that the lead rewrites at the end (robot 3×3, pose, saved) are read
-    signal_started(sync, tid);
+    __syncthreads();   // sh_lines, sh_ctl
 
     const bool spec_ok = p.spec && L > 0 && L <= SPEC_L && s > 0 && G <= SPEC_GMAX;
     // symmetric downdate operands (sym_factor): fp32 operand storage, every mode but the
@@ -1520,7 +1542,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             if (tid < SPEC_L) mb_store_tagged(slot + tid, p.epoch, tid < L ? sh_lists[g * SPEC_L + tid] : 0ull);
             for (int k = tid; k < G * L; k += SCAN_BLOCK) {
                 const int gq = k / L, t = k - gq * L;
-                if (gq != g) sh_lists[gq * SPEC_L + t] = mb_wait_tagged(mbox + (size_t)gq * p.mbw + lb + t, p.epoch, tstatus);
+                if (gq != g) sh_lists[gq * SPEC_L + t] = mb_wait_tagged(mbox + (size_t)gq * p.mbw + lb + t, p.epoch, tstatus, p.spin_log2);
             }
             __syncthreads();
         }
@@ -1867,7 +1889,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     int polls = 0;
                     while (__hip_atomic_load(&sh_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= i) {
                         __builtin_amdgcn_s_sleep(1);
-                        if (++polls > (1 << 24)) { tstatus |= EKF_ST_TIMEOUT_BIT; viol = 1; break; }
+                        if ((tstatus & EKF_ST_TIMEOUT_BIT) || ++polls > (1 << p.spin_log2)) { tstatus |= EKF_ST_TIMEOUT_BIT; viol = 1; break; }
                     }
                     sub(17);
                     const double* pk = sh_pk[i];
@@ -1911,7 +1933,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             if (G > 1) {
                 if (tid == 0) mb_tag(mbox + (size_t)g * p.mbw, p.epoch, TAG_SPEC_VERDICT, (unsigned)any);
                 if (tid < G) {
-                    const int v = mb_poll(mbox, 0, G, tid, p.mbw, p.epoch, TAG_SPEC_VERDICT, tstatus);
+                    const int v = mb_poll(mbox, 0, G, tid, p.mbw, p.epoch, TAG_SPEC_VERDICT, tstatus, p.spin_log2);
                     sh_best[tid] = v != 0;
                 }
                 __syncthreads();
@@ -1993,7 +2015,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             if (tid == 0) mb_tag(slot, p.epoch, (unsigned)(i + 1), (unsigned)(gbest == 0x7fffffff ? 0 : gbest + 1));
             EKF_STAMP(3);
             for (int k = tid; k < G; k += SCAN_BLOCK) {
-                const int bq = mb_poll(mbox, par, G, k, p.mbw, p.epoch, (unsigned)(i + 1), tstatus);
+                const int bq = mb_poll(mbox, par, G, k, p.mbw, p.epoch, (unsigned)(i + 1), tstatus, p.spin_log2);
                 sh_best[k] = bq <= 0 ? 0x7fffffff : bq - 1;
             }
             __syncthreads();
@@ -2125,10 +2147,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         if (reset) {
             rr0 = rr1 = rr2 = yb = make_double2(0.0, 0.0);
         }
-        *reinterpret_cast<double2*>(Rs + b0) = rr0;
-        *reinterpret_cast<double2*>(Rs + n + b0) = rr1;
-        *reinterpret_cast<double2*>(Rs + 2 * n + b0) = rr2;
-        *reinterpret_cast<double2*>(y + b0) = yb;
+        *reinterpret_cast<double2*>(Rsw + b0) = rr0;
+        *reinterpret_cast<double2*>(Rsw + n + b0) = rr1;
+        *reinterpret_cast<double2*>(Rsw + 2 * n + b0) = rr2;
+        *reinterpret_cast<double2*>(yw + b0) = yb;
         if (sizeof(C) == 4) {
             // f32 operands: the k columns past the matches hold −0 (U) and +0 (V), so a flush
             // that runs every k-step unconditionally adds −0 there, which leaves every value as
@@ -2199,30 +2221,49 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
 #pragma unroll
         for (int w = 0; w < SCAN_THREADS / 64; w++) wgst |= sh_red[w];
     }
-    if (tid == 0 && !lead) sync[SYNC_WG0 + g] = wgst;
+    // completion (rollback protocol, publish_done / lead_collect): the lead commits the launch —
+    // flips the instance to the copy of the robot strip and mean written above, writes the shared
+    // state and the step's result record — only if every workgroup completed without a timeout.
+    // Otherwise the instance keeps its state from before the call, and the step's record applies
+    // nothing (no downdate, rows or reset: the flush and later on-read replays skip it).
+    if (tid == 0 && !lead) publish_done(sync, g, p.epoch, wgst);
     if (lead) {
-        // every workgroup read the robot 3×3 block, pose and savedLineCount at its start
-        wgst |= wait_all_started(sync, G, p.epoch);
-        sync[SYNC_WG0 + g] = wgst;
-        y[0] = xp[0];
-        y[1] = xp[1];
-        y[2] = xp[2];
-        p.pose[3 * e + 0] = pose[0];
-        p.pose[3 * e + 1] = pose[1];
-        p.pose[3 * e + 2] = pose[2];
-        for (int a = 0; a < 9; a++) Rs[(a / 3) * n + (a % 3)] = R33[a];
-        res[RES_STATUS] = ((nextra > nadd) ? EKF_ST_CAP : 0);
-        res[RES_M] = m;
-        res[RES_NEXTRA] = nextra;
-        res[RES_SAVED_IN] = s;
-        res[RES_SAVED] = reset ? 0 : s + nadd;
-        res[RES_RESET] = reset;
-        res[RES_NADD] = reset ? 0 : nadd;
+        wgst = lead_collect(sync, G, p.epoch, wgst, p.spin_log2);
+        sync[SYNC_WG0] = (int)done_word(p.epoch, wgst);
+        const bool commit = !(wgst & EKF_ST_TIMEOUT_BIT);
         res[RES_NLINES] = L;
-        res[RES_KSTEPS] = (sizeof(C) == 4) ? m : (m + 1) / 2;
+        res[RES_SAVED_IN] = s;
         res[RES_DBG] = dpath | (sequential ? 16 : 0);
-        for (int t = 0; t < 6; t++) res[RES_DBG + 1 + t] = t < SPEC_L ? sh_spec[t] : -2;
-        p.saved[e] = reset ? 0 : s + nadd;
+        for (int t = 0; t < 5; t++) res[RES_DBG + 1 + t] = t < SPEC_L ? sh_spec[t] : -2;
+        if (commit) {
+            yw[0] = xp[0];
+            yw[1] = xp[1];
+            yw[2] = xp[2];
+            for (int a = 0; a < 9; a++) Rsw[(a / 3) * n + (a % 3)] = R33[a];
+            p.pose[3 * e + 0] = pose[0];
+            p.pose[3 * e + 1] = pose[1];
+            p.pose[3 * e + 2] = pose[2];
+            res[RES_STATUS] = ((nextra > nadd) ? EKF_ST_CAP : 0);
+            res[RES_M] = m;
+            res[RES_NEXTRA] = nextra;
+            res[RES_SAVED] = reset ? 0 : s + nadd;
+            res[RES_RESET] = reset;
+            res[RES_NADD] = reset ? 0 : nadd;
+            res[RES_KSTEPS] = (sizeof(C) == 4) ? m : (m + 1) / 2;
+            res[RES_ROLLBACK] = 0;
+            p.saved[e] = reset ? 0 : s + nadd;
+            p.live[e] = 1 - cb;
+        } else {
+            res[RES_STATUS] = 0;
+            res[RES_M] = 0;
+            res[RES_NEXTRA] = 0;
+            res[RES_SAVED] = s;
+            res[RES_RESET] = 0;
+            res[RES_NADD] = 0;
+            res[RES_KSTEPS] = 0;
+            res[RES_ROLLBACK] = 1;
+            for (int i = 0; i < L; i++) res[RES_MATCH + i] = -1;
+        }
     }
     EKF_STAMP(7);
     if (dbg) {
@@ -2838,7 +2879,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
 #pragma unroll
             for (int q = 0; q < NS; q++) {
                 const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
-                fast = fast && !sload(r + RES_RESET) && sload(r + RES_NADD) == 0;
+                fast = fast && !sload(r + RES_RESET) && sload(r + RES_NADD) == 0 && !sload(r + RES_ROLLBACK);
             }
     }
 
@@ -2939,8 +2980,13 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
             first_item(cur);
             next_item(cur, nxt);
             load_tiles(cur);
+#ifdef EKF_XP_BF_NO_OPS   // timing experiment (results invalid): operands loaded once, never in the loop
+#pragma unroll
+            for (int q = 0; q < RD; q++) load_ops(q, cur, q);
+#else
 #pragma unroll
             for (int q = 0; q < RD - 1; q++) load_ops(q, cur, q);
+#endif
             int g = g0;
 #ifdef EKF_XP_FLUSH_STAMPS   // timing experiment: shader cycles per wave-tile section, in-kernel clock
             unsigned long long xs_b = 0, xs_m = 0, xs_s = 0, xs_n = 0;
@@ -2959,7 +3005,9 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
                     for (int qq = 0; qq < 4; qq++)
 #pragma unroll
                         for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = -pref[i][qq][j];
+#ifndef EKF_XP_BF_NO_TILES   // timing experiment (results invalid): no tile stream after the first
                 if (more) load_tiles(nxt);
+#endif
                 __builtin_amdgcn_sched_barrier(0);
 #ifdef EKF_XP_FLUSH_STAMPS
                 const unsigned long long xt1 = __builtin_amdgcn_s_memtime();
@@ -2968,8 +3016,10 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
                 for (int q = 0; q < NS; q++) {
                     // ring set of step q + RD − 1 (this wave-tile's, else the next one's)
                     const int ql = q + RD - 1;
+#ifndef EKF_XP_BF_NO_OPS
                     if (ql < NS) load_ops(ql % RD, cur, ql);
                     else load_ops(ql % RD, ldi, ql - NS);
+#endif
                     const int r = q % RD;
                     // part products smallest first: (mid, mid), (hi, lo), (lo, hi), (hi, mid),
                     // (mid, hi), (hi, hi)
@@ -2998,6 +3048,9 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
                 for (int i = 0; i < WT_N; i++)
 #pragma unroll
                     for (int k = 0; k < 16; k++) acc[i][k] = -acc[i][k];
+#ifdef EKF_XP_BF_NO_TILES
+                if (acc[0][0] == 1234.5f && acc[3][15] == -1234.5f)   // (never true: keeps the MFMAs live)
+#endif
                 store_tiles(cur, acc);
 #ifdef EKF_XP_FLUSH_STAMPS
                 __builtin_amdgcn_sched_barrier(0);
@@ -3341,7 +3394,7 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f64_wave_kernel(DowndateP
 #pragma unroll
             for (int q = 0; q < NS; q++) {
                 const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
-                fast = fast && !sload(r + RES_RESET) && sload(r + RES_NADD) == 0;
+                fast = fast && !sload(r + RES_RESET) && sload(r + RES_NADD) == 0 && !sload(r + RES_ROLLBACK);
             }
     }
     struct Item {
@@ -3781,10 +3834,9 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     const bool wave_shape = p.nsteps >= 2 && p.nsteps <= 8 && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
                             p.nwt > 0 && p.wt != nullptr;
     const bool wave_ok = wave_shape && (p.nsteps >= 6 || p.variant == 8);
-    const bool bf_shape = p.nsteps >= 2 && p.nsteps <= 16 && p.nsteps % 2 == 0 && p.nsteps != 10 && p.nsteps != 14 &&
-                          p.d.kmax <= 16 &&
+    const bool bf_shape = p.nsteps >= 2 && p.nsteps <= 16 && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
                           p.nwt > 0 && p.wt != nullptr;
-    if (p.bf && !half && bf_shape) {   // EKF_ARITH_BF16X6: split-bf16 wave flush, 2-8, 12 or 16 steps
+    if (p.bf && !half && bf_shape) {   // EKF_ARITH_BF16X6: split-bf16 wave flush, groups of 2-16 steps (even)
         const unsigned wgrid = (unsigned)(8 * EKF_BF_WAVES * ((p.ncu + 7) / 8));   // EKF_BF_WAVES workgroups per CU
 #define EKF_BF_CASE(NSV)                                                                                \
     case NSV:                                                                                           \
@@ -3796,7 +3848,9 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
             EKF_BF_CASE(4)
             EKF_BF_CASE(6)
             EKF_BF_CASE(8)
+            EKF_BF_CASE(10)
             EKF_BF_CASE(12)
+            EKF_BF_CASE(14)
             EKF_BF_CASE(16)
         }
 #undef EKF_BF_CASE

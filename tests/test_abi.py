@@ -42,7 +42,7 @@ def test_library_is_gfx950_code_object(ekf_mod):
 
 def test_cpu_only_calls(ekf_mod):
     lib = ekf_mod.load_library()
-    assert lib.ekf_abi_version() == 1
+    assert lib.ekf_abi_version() == 2   # ABI 2: 32 stamp slots, arith validated, rollback
     assert lib.ekf_strerror(0) == b"ok"
     cfg = ekf_mod.EkfConfig()
     lib.ekf_config_init(ctypes.byref(cfg))
@@ -59,6 +59,13 @@ def test_cpu_only_calls(ekf_mod):
     lib.ekf_config_init(ctypes.byref(bad))
     bad.arith = 7
     assert lib.ekf_create(ctypes.byref(bad), ctypes.byref(h)) == 1
+    # EKF_ARITH_BF16X6 only where it can run (fp32, intended R, max_lines <= 8): EKF_EINVAL
+    # otherwise, before any HIP call (no silent fallback to the exact arithmetic)
+    for field, val in (("precision", ekf_mod.PREC_F64), ("r_mode", ekf_mod.R_AS_WRITTEN), ("max_lines", 9)):
+        lib.ekf_config_init(ctypes.byref(bad))
+        bad.precision, bad.max_lines, bad.arith = ekf_mod.PREC_F32, 8, ekf_mod.ARITH_BF16X6
+        setattr(bad, field, val)
+        assert lib.ekf_create(ctypes.byref(bad), ctypes.byref(h)) == 1, field
 
 
 def test_struct_layouts_match_header():
@@ -111,6 +118,43 @@ int main() {
 }
 ''')
     exe = tmp_path / "t"
+    inc = os.path.join(ROOT, "slam_ros_amd", "csrc")
+    subprocess.run(["g++", "-std=c++17", "-O1", f"-I{inc}", str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.returncode
+
+
+def test_commit_decision(tmp_path):
+    """The association kernel's rollback bookkeeping (ekf_commit.h, host-compiled): a launch
+    commits only if every workgroup's completion word carries this launch's epoch and no timeout
+    bit; a stale word (a workgroup that never completed) or a timeout anywhere rolls it back; the
+    other status bits are OR-ed; epochs wrap modulo 2^24."""
+    src = tmp_path / "c.cpp"
+    src.write_text(r"""
+#include "ekf_commit.h"
+#include <cstdio>
+using namespace ekf;
+int main() {
+  const unsigned ep = 77;
+  unsigned w[4] = {done_word(ep, 0), done_word(ep, EKF_ST_SINGULAR_S), done_word(ep, 0), done_word(ep, EKF_ST_RANGE)};
+  int st = commit_status(w, 4, ep);
+  if (st != (EKF_ST_SINGULAR_S | EKF_ST_RANGE)) return 1;                // commits, bits OR-ed
+  w[2] = done_word(ep - 1, 0);                                          // stale: never completed
+  st = commit_status(w, 4, ep);
+  if (!(st & EKF_ST_SYNC_TIMEOUT) || !(st & EKF_ST_SINGULAR_S)) return 2;
+  w[2] = done_word(ep, EKF_ST_SYNC_TIMEOUT);                            // timed out itself
+  if (!(commit_status(w, 4, ep) & EKF_ST_SYNC_TIMEOUT)) return 3;
+  if (commit_status(w, 1, ep) & EKF_ST_SYNC_TIMEOUT) return 4;          // G = 1: its own word only
+  const unsigned big = (1u << 24) + 5;                                  // epoch tags wrap mod 2^24
+  unsigned v[2] = {done_word(big, 0), done_word(5, 0)};
+  if (commit_status(v, 2, big) != 0) return 5;
+  if (done_word(ep, 0x1ff) & ~0xffffff00u & 0x100u) return 6;           // status confined to 8 bits
+  if (commit_fold(0, 0u, 0u) != 0) return 7;                            // epoch 0 = a zeroed word: "arrived"
+  puts("ok");
+  return 0;
+}
+""")
+    exe = tmp_path / "c"
     inc = os.path.join(ROOT, "slam_ros_amd", "csrc")
     subprocess.run(["g++", "-std=c++17", "-O1", f"-I{inc}", str(src), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True)

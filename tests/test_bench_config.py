@@ -14,9 +14,10 @@ after each group end the full P, y and pose of both instances.
 
 Bound on P over k scans: the per-scan bar is 1e-6 (BASELINE.json north_star); rounding to the
 storage precision enters once per scan and (I − K·H) does not amplify earlier errors, so after k
-scans ‖ΔP‖_F/‖P‖_F ≤ k · (per-scan bar). fp32 is held to the per-scan bar itself over the whole
-trajectory (measured 3.1e-7 after 8 scans, 4.6e-7 after 16); fp16 storage (config 5) to
-k · 1e-3; fp64 storage to 1e-10. State vector: ‖Δy‖/‖y‖ ≤ 1e-8, and the pose
+scans ‖ΔP‖_F/‖P‖_F ≤ k · (per-scan bar). Every precision is held to its per-scan bar itself over
+the whole trajectory, at every group end: fp32 1e-6 (measured 3.1e-7 after 8 scans, 4.6e-7 after
+16), fp16 storage (config 5) 1e-3 flat (measured 9.4e-4 after 16: the bound re-stated in DESIGN
+§4.5, so a regression of the fp16 rounding shows), fp64 storage 1e-10. State vector: ‖Δy‖/‖y‖ ≤ 1e-8, and the pose
 (y[0:3]) within the same absolute amount, 1e-8·‖y‖ (fp64: 1e-12). The measured values are
 written to gpurun_out/bench_config_parity.json.
 """
@@ -89,7 +90,7 @@ def run_config(ekf_mod, oracle_mod, prec, T, scans, pipeline=False, arith=0):
                 out["P"].append(rp)
                 out["y"].append(ry)
                 out["pose"].append(dp)
-                bound = {0: 1e-10, 1: 1e-6, 2: k * PER_SCAN[2]}[prec]
+                bound = PER_SCAN[prec]
                 assert rp <= bound, (prec, k, e, rp, bound)
                 assert ry <= 1e-8, (prec, k, e, ry)
                 assert dp <= (1e-12 if prec == 0 else 1e-8 * np.linalg.norm(refs[e].y)), (prec, k, e, dp)
@@ -105,8 +106,8 @@ def test_bench_config_fp32_t8(ekf_mod, oracle_mod):
 
 
 def test_bench_config_fp32_t8_pipelined(ekf_mod, oracle_mod):
-    """pipeline = 1 at G = 22 cooperating workgroups per instance (its association kernels are
-    serialised after the flush in flight, ekf_api.hip enqueue_flush)."""
+    """pipeline = 1 at G = 22 cooperating workgroups per instance: such a context runs the
+    sequential schedule (slam_ekf.h ekf_config.pipeline), so the results are those of T = 8."""
     out = run_config(ekf_mod, oracle_mod, 1, 8, 16, pipeline=True)
     record("f32_T8_N4096_E8_pipelined", out)
 

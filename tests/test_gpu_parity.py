@@ -579,9 +579,9 @@ def test_bf16x6_flush_close_to_exact(ekf_mod, oracle_mod, N, T, lines, extra_eve
             assert meas[0]["y_bf_vs_fp64"] <= meas[0]["y_exact_vs_fp64"] + k * 1e-8, meas[0]
     from tests.test_bench_config import record
     record(f"bf16x6_vs_exact_N{N}_T{T}_L{lines}_x{extra_every}", meas)
-    # kmax > 16 (max_lines 16): the exact forms serve every group
-    c = ekf_mod.Ensemble(N, 1, 1, max_lines=16, flush_interval=8, arith=ekf_mod.ARITH_BF16X6)
-    assert not c.flush_kernel_name(8).endswith(", true>")
+    # kmax > 16 (max_lines 16) can never take the split-bf16 flush: rejected, no silent fallback
+    with pytest.raises(ekf_mod.EkfError):
+        ekf_mod.Ensemble(N, 1, 1, max_lines=16, flush_interval=8, arith=ekf_mod.ARITH_BF16X6)
 
 
 @pytest.mark.parametrize("N,T,lines,extra_every", [(80, 4, 8, 0), (80, 4, 6, 3), (64, 3, 6, 2), (100, 2, 8, 0),
