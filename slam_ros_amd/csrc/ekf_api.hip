@@ -52,7 +52,8 @@ struct ekf_ctx {
     double* pose;
     double* xpre;
     int* saved;
-    double* D;
+    double* D;                // [2][E][N][4] diagonal landmark blocks after the last committed step
+                              // (split-bf16 contexts: the association kernel's MFMA replay)
     std::vector<ekf::Slot> ring;   // R per-step slots
     double* Ust;              // fp64 gain scratch of the running scan
     double* Vst;
@@ -319,7 +320,7 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     ALLOC(c->pose, sizeof(double) * 3 * E);
     ALLOC(c->xpre, sizeof(double) * 3 * E);
     ALLOC(c->saved, sizeof(int) * E);
-    ALLOC(c->D, sizeof(double) * 4 * d.N * E);
+    ALLOC(c->D, sizeof(double) * 4 * d.N * E * 2);
     ALLOC(c->Ust, sizeof(double) * d.max_lines * d.n * 2 * E);
     ALLOC(c->Vst, sizeof(double) * d.max_lines * d.n * 2 * E);
     c->T = cfg->flush_interval > 0 ? cfg->flush_interval : 1;
@@ -604,6 +605,8 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.Rs = c->Rs;
     p.y = c->y;
     p.live = c->cur;
+    p.Dd = c->D;
+    p.mfrep = c->bf ? 1 : 0;
     p.Etot = c->cfg.instances;
     p.spin_log2 = c->spin_log2;
     p.test_drop = c->test_drop;

@@ -532,7 +532,44 @@ __device__ __forceinline__ bool certified_reject(const Block5& b, double ma, dou
     return (q - dq) > gate * gate * (1.0 + 1e-6) * (det + ddet);
 }
 
-// Certified rejection in fp32 (the first filter of the per-line gate; certified_reject in fp64
+// Certified cheap rejection (the first filter of the per-line gate: ≈35 fp64 operations, no
+// trigonometry). For a symmetric positive definite S, vᵀS⁻¹v ≥ v0²/S00 and vᵀS⁻¹v ≥ v1²/S11, so
+// the exact evaluation fails the gate (Robot.cpp:489) if either one-dimensional bound exceeds it:
+//  * S00 = H0·P5·H0ᵀ + R00 with the constant row H0 = (0, 0, −1, 1, 0): p22 − 2·p2a + daa + R00
+//    (innovation_cov's S[0]); the reference's normalizeRadian (Robot.cpp:62-71) and the 2π fold
+//    (:465-475) shift za − (ma − x_pre2) by multiples of 2π only, so |v0| ≥ its circular distance
+//    to 0;
+//  * S11 = H1·P5·H1ᵀ + R11 ≤ ‖H1‖²·tr(P5) + R11 with ‖H1‖² = 2 + h1l² ≤ 2 + (|x0| + |x1|)² (P5,
+//    a principal block of a covariance, is positive semidefinite); v1 = zr − (mr − (x0·cos ma +
+//    x1·sin ma)) bounded from below with the scan-start sin/cos of ma0 (|Δcos|, |Δsin| ≤ |ma − ma0|).
+// It needs R symmetric with R00, R11 large against the storage rounding of P5 (which could
+// otherwise make S indefinite: then it never rejects) and finite inputs (NaN never rejects).
+// Margins: 1e-6 relative on the gate plus absolute slack, far above the rounding of the bounds
+// and of the exact evaluation.
+__device__ __forceinline__ bool quick_reject(const Block5& b, double ma, double mr, double ma0, double s0,
+                                             double c0, const double xp[3], double za, double zr,
+                                             const double Rm[4], double gate)
+{
+    const double tr5 = b.p00 + b.p11 + b.p22 + b.daa + b.dbb;
+    const double X = fabs(xp[0]) + fabs(xp[1]);
+    const double H2 = 2.0 + X * X;   // ≥ ‖H1‖²
+    if (!(Rm[1] == Rm[2]) || !(tr5 >= 0.0) || !(Rm[0] > 1e-5 * 2.0 * tr5) || !(Rm[3] > 1e-5 * H2 * tr5))
+        return false;
+    const double g2 = gate * gate * (1.0 + 1e-6);
+    const double S00 = b.p22 - 2.0 * b.p2a + b.daa + Rm[0];
+    const double x = za - (ma - xp[2]);
+    const double cd = fabs(x - 2.0 * EKF_PI * rint(x * (0.5 / EKF_PI)));
+    if (S00 > 0.0 && cd - 1e-12 * (1.0 + fabs(x)) > 0.0) {
+        const double a0 = cd - 1e-12 * (1.0 + fabs(x));
+        if (a0 * a0 > g2 * S00) return true;
+    }
+    const double v1e = zr - (mr - (xp[0] * c0 + xp[1] * s0));
+    const double a1 = fabs(v1e) - X * fabs(ma - ma0) - 1e-12 * (1.0 + fabs(zr) + fabs(mr) + X);
+    const double S11u = H2 * tr5 * (1.0 + 1e-5) + Rm[3];
+    return a1 > 0.0 && a1 * a1 > g2 * S11u;
+}
+
+// Certified rejection in fp32 (the second filter of the per-line gate; certified_reject in fp64
 // and the exact evaluation run only where it cannot decide). Same bound structure as
 // certified_reject, with the fp32 roundings added to it: every input rounded to fp32 (relative
 // u = 2^-24), the short fp32 sums of S (≤ 12u of the sum of the absolute values of their terms,
@@ -721,21 +758,33 @@ __device__ __forceinline__ void publish_done(int* sync, int g, unsigned epoch, i
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ int lead_collect(int* sync, int G, unsigned epoch, int own_status, int spin)
+// Run by every thread of workgroup 0 (the words are polled in parallel, thread k word k); the
+// folded status of all G words (= commit_status) is returned to every thread.
+__device__ __forceinline__ int lead_collect(int* sync, int G, unsigned epoch, int own_status, int spin,
+                                            int tid, int* sh_red)
 {
-    int st = commit_fold(0, done_word(epoch, own_status), epoch);
-    int polls = 0;
-    bool late = (own_status & EKF_ST_TIMEOUT_BIT) != 0;
-    for (int k = 1; k < G; k++) {
+    int st = tid == 0 ? commit_fold(0, done_word(epoch, own_status), epoch) : 0;
+    const bool late0 = (own_status & EKF_ST_TIMEOUT_BIT) != 0;
+    for (int k = 1 + tid; k < G; k += SCAN_BLOCK) {
         const unsigned* w = reinterpret_cast<const unsigned*>(&sync[SYNC_WG0 + k]);
         unsigned v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int polls = 0;
+        bool late = late0;
         while ((v >> 8) != (epoch & 0xffffffu) && !late) {
             __builtin_amdgcn_s_sleep(1);
             if (++polls > (1 << spin)) late = true;
             v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        st = commit_fold(st, v, epoch);   // (= commit_status over the G words)
+        st = commit_fold(st, v, epoch);
     }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) st |= __shfl_xor(st, off, 64);
+    __syncthreads();
+    if ((tid & 63) == 0) sh_red[tid >> 6] = st;
+    __syncthreads();
+    st = 0;
+#pragma unroll
+    for (int w = 0; w < SCAN_BLOCK / 64; w++) st |= sh_red[w];
     return st;
 }
 
@@ -1201,6 +1250,60 @@ __device__ __forceinline__ void staged_pair_block(const PllView<T>& v, int wa, i
     }
 }
 
+// Split-bf16 contexts (ScanParams::mfrep): the pending steps' share of the blocks a scan reads,
+// ΔX = Σ_q V_q(rows)·V_q(cols)ᵀ over the active pending steps (amask: ks > 0; rolled-back steps
+// have ks = 0), by v_mfma_f32_16x16x32_bf16 on the operand planes the association kernels wrote
+// (V = hi + mid + lo exactly, the six part products of the flush). One instruction takes two
+// steps: k-groups 0/1 the even/odd k of step qa, 2/3 those of step qb (the same k permutation on
+// both operands). NB M-blocks of 16 rows: A row row_a(mb, r), B (16 columns) row row_b(c); a
+// negative or out-of-range row is a zero operand. Lane l holds ΔX[4·(l >> 4) + i][l & 15] of
+// M-block mb in acc[mb][i]. Not the fp32 chain of the flush (the split-bf16 flush is not one
+// either): held to the same parity bar.
+typedef __bf16 bf16x8r __attribute__((ext_vector_type(8)));
+template <int NB, typename RA, typename RB>
+__device__ __forceinline__ void plane_replay(const Slot* pend, int e, size_t inst_bf, int M, unsigned amask,
+                                             int lane, RA row_a, RB row_b, f32x4v (&acc)[NB])
+{
+#pragma unroll
+    for (int mb = 0; mb < NB; mb++) acc[mb] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    const int kg = lane >> 4, h = kg & 1, r16 = lane & 15;
+    typedef unsigned u32x4r __attribute__((ext_vector_type(4)));
+    const bf16x8r zero = __builtin_bit_cast(bf16x8r, u32x4r{0u, 0u, 0u, 0u});
+    const int rb_ = row_b(r16);
+    int ra_[NB];
+#pragma unroll
+    for (int mb = 0; mb < NB; mb++) ra_[mb] = row_a(mb, r16);
+    unsigned m = amask;
+    while (m) {
+        const int qa = __builtin_ctz(m);
+        m &= m - 1;
+        const int qb = m ? __builtin_ctz(m) : -1;
+        if (qb >= 0) m &= m - 1;
+        const unsigned short* pa = reinterpret_cast<const unsigned short*>(pend[qa].Bop) + (size_t)e * inst_bf;
+        const unsigned short* pb = qb >= 0 ? reinterpret_cast<const unsigned short*>(pend[qb].Bop) + (size_t)e * inst_bf : pa;
+        const unsigned short* pq = (kg >= 2) ? pb : pa;
+        const bool none = kg >= 2 && qb < 0;
+        bf16x8r B[3], A[NB][3];
+#pragma unroll
+        for (int pl = 0; pl < 3; pl++)
+            B[pl] = (!none && rb_ >= 0 && rb_ < M) ? *reinterpret_cast<const bf16x8r*>(pq + op_index_bf(rb_, h, pl)) : zero;
+#pragma unroll
+        for (int mb = 0; mb < NB; mb++)
+#pragma unroll
+            for (int pl = 0; pl < 3; pl++)
+                A[mb][pl] = (!none && ra_[mb] >= 0 && ra_[mb] < M)
+                                ? *reinterpret_cast<const bf16x8r*>(pq + op_index_bf(ra_[mb], h, pl)) : zero;
+#pragma unroll
+        for (int pp = 0; pp < 6; pp++) {
+            const int a = (0x102010 >> (4 * (5 - pp))) & 0xf;   // (mid, mid), (hi, lo), (lo, hi),
+            const int b = (0x120100 >> (4 * (5 - pp))) & 0xf;   // (hi, mid), (mid, hi), (hi, hi)
+#pragma unroll
+            for (int mb = 0; mb < NB; mb++)
+                acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mb][a], B[b], acc[mb], 0, 0, 0);
+        }
+    }
+}
+
 // Speculative association (lines <= SPEC_L, G <= SPEC_GMAX): every line's winner is guessed
 // from the pre-update state, the guesses' mutual data are exchanged once, every workgroup
 // replays the winners' part of the sequential chain to get all gain packages, then every thread
@@ -1232,13 +1335,16 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     const double* y = p.y + ((size_t)cb * p.Etot + e) * n;
     double* Rsw = p.Rs + ((size_t)(1 - cb) * p.Etot + e) * 3 * n;
     double* yw = p.y + ((size_t)(1 - cb) * p.Etot + e) * n;
+    // diagonal landmark blocks after the last committed step (split-bf16 contexts), same two copies
+    const double4* Ddr = p.mfrep ? reinterpret_cast<const double4*>(p.Dd) + ((size_t)cb * p.Etot + e) * d.N : nullptr;
+    double4* Ddw = p.mfrep ? reinterpret_cast<double4*>(p.Dd) + ((size_t)(1 - cb) * p.Etot + e) * d.N : nullptr;
     int* sync = p.sync + (size_t)e * p.sync_stride;
     double* mbox = p.mbox + (size_t)e * 2 * G * p.mbw;
     const bool lead = (g == 0 && tid == 0);
     if (p.test_drop == e + 1 && G > 1 && g == G - 1) return;   // test hook: a workgroup that never runs
 
     __shared__ double sh_pkg[MB_VH + 4 * EKF_MAX_LINES];
-    __shared__ int sh_red[SCAN_THREADS / 64];
+    __shared__ int sh_red[SCAN_BLOCK / 64];
     __shared__ int sh_best[MAX_GROUPS];
     __shared__ int sh_extra[EKF_MAX_LINES];
     __shared__ int4 sh_ctl[PMAX];
@@ -1257,6 +1363,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     __shared__ int sh_spec[SPEC_L];
     __shared__ int sh_flag;
     __shared__ int sh_ready;
+    __shared__ int sh_rwst;   // status bits of the replay wave (the winners' GSL_EDOM)
     __shared__ double sh_wd[SPEC_L * SPEC_WD];
     __shared__ double4 sh_wh[SPEC_L][SPEC_L][2];
     __shared__ double sh_pk[SPEC_L][PKW];
@@ -1336,11 +1443,13 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // the owned diagonal block as last flushed (the staged speculative path guesses from it),
     // issued with the owned-state loads: the scan's inputs arrive in one memory round trip
     typename Stor<T>::C dj0[4] = {0, 0, 0, 0};
+    double4 djb = make_double4(0, 0, 0, 0);   // the kept diagonal block (split-bf16 contexts)
     if (own && (p.phase & PHASE_UPDATE)) {
         PllView<T> v0;
         v0.X = reinterpret_cast<const T*>(p.Pread) + (size_t)e * d.ntiles * TILE_ELEMS;
         v0.nb = d.nb;
         load_block<T>(v0, 2 * j, 2 * j, dj0);
+        if (Ddr && p.npend > 0) djb = Ddr[j];
     }
     init_state();
     // the owned landmark's angle at the start of the scan and its sin/cos (sincos_near)
@@ -1355,14 +1464,13 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             *reinterpret_cast<double2*>(Rsw + n + b0) = rr1;
             *reinterpret_cast<double2*>(Rsw + 2 * n + b0) = rr2;
             *reinterpret_cast<double2*>(yw + b0) = yb;
+            if (Ddr) Ddw[j] = Ddr[j];
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0 && !lead) publish_done(sync, g, p.epoch, 0);
-        if (lead) {
-            const int st = lead_collect(sync, G, p.epoch, 0, p.spin_log2);
-            sync[SYNC_WG0] = (int)done_word(p.epoch, st);
-            if (!(st & EKF_ST_TIMEOUT_BIT)) {
+        if (tid == 0 && g != 0) publish_done(sync, g, p.epoch, 0);
+        if (g == 0) {
+            const int st = lead_collect(sync, G, p.epoch, 0, p.spin_log2, tid, sh_red);
+            if (lead) sync[SYNC_WG0] = (int)done_word(p.epoch, st);
+            if (lead && !(st & EKF_ST_TIMEOUT_BIT)) {
                 for (int a = 0; a < 9; a++) Rsw[(a / 3) * n + (a % 3)] = R33[a];
                 yw[0] = y[0]; yw[1] = y[1]; yw[2] = y[2];
                 p.xpre[3 * e + 0] = xp[0];
@@ -1424,14 +1532,26 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // speculative path with fp32 operands and few pending steps: the pending steps' rows of the
     // guessed columns are staged in LDS and one pass per step updates all owned blocks
     bool staged = false;
+    // split-bf16 contexts with plain pending steps (no reset, no augmented rows): the pending
+    // steps are applied by bf16 MFMA on the operand planes (plane_replay) and the diagonal blocks
+    // come from Dd (the last committed step's, exact); fp32 storage
+    bool mf = false;
+    unsigned amask = 0;   // pending steps with a downdate (ks > 0)
     if (spec_ok && sym && sizeof(typename Stor<T>::C) == 4 && p.npend <= SPEC_QMAX && d.kmax / 2 >= 8) {
         __syncthreads();   // sh_ctl
         staged = true;
         for (int q = 0; q < p.npend; q++) staged &= sh_ctl[q].y <= 8;
+        mf = staged && p.mfrep && std::is_same<T, float>::value;
+        for (int q = 0; q < p.npend; q++) {
+            mf &= !sh_ctl[q].x && sh_ctl[q].z == 0;
+            if (sh_ctl[q].y > 0) amask |= 1u << q;
+        }
     }
     double Dj[4] = {0, 0, 0, 0};   // owned diagonal block
     if (own && j < s) {
-        if (staged) {
+        if (mf && p.npend > 0) {
+            Dj[0] = djb.x; Dj[1] = djb.y; Dj[2] = djb.z; Dj[3] = djb.w;
+        } else if (staged) {
             // the guess only needs it approximately: the last flushed value (exact one below)
 #pragma unroll
             for (int a = 0; a < 4; a++) Dj[a] = from_domain<T>(dj0[a], pv.ex);
@@ -1676,7 +1796,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     sincos(qy.x, &r[12], &r[13]);
                 }
             }
-            if (staged) {
+            if (staged && !mf) {
                 // rows 2w, 2w+1 of U_q and V_q of every guessed column w, pending step q (4 row
                 // halves × 8 k each; the V side interleaved, stage_v_index): 16 pieces of 4 floats
                 const int kh = d.kmax / 2;
@@ -1702,9 +1822,41 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     }
                 }
             }
-            if (tid == SCAN_BLOCK - 1) sh_ready = 0;
+            if (tid == SCAN_BLOCK - 1) {
+                sh_ready = 0;
+                sh_rwst = 0;
+            }
             __syncthreads();
-            if (staged && tid >= SCAN_THREADS) {
+            if (mf && tid >= SCAN_THREADS) {
+              if constexpr (std::is_same<T, float>::value) {
+                // the winners' mutual blocks: X minus the pending steps' ΔX of the 16 winner rows
+                // against themselves (one M-block of plane_replay), by the replay wave itself
+                auto wrow = [&](int c) {
+                    const int t = c >> 1;
+                    const int w = t < L ? sh_spec[t] : -1;
+                    return w >= 0 ? 2 * w + (c & 1) : -1;
+                };
+                f32x4v dacc[1];
+                plane_replay<1>(p.pend, e, opstride * 3, M, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow, dacc);
+                float* scr = sh_stg;   // (not staged in this mode) 16 × 16 floats
+#pragma unroll
+                for (int i = 0; i < 4; i++) scr[(4 * (lane_r >> 4) + i) * 16 + (lane_r & 15)] = dacc[0][i];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                if (lane_r < L * (L + 1) / 2 && sh_spec[pu] >= 0 && sh_spec[pt] >= 0) {
+                    const bool swap = ((2 * sh_spec[pu]) >> 5) > ((2 * sh_spec[pt]) >> 5);
+                    const C xr[4] = {pacc[0], swap ? pacc[2] : pacc[1], swap ? pacc[1] : pacc[2], pacc[3]};
+                    double* r = sh_wd + pu * SPEC_WD + (pt == pu ? 6 : 14 + 4 * pt);
+#pragma unroll
+                    for (int a = 0; a < 4; a++)
+                        r[a] = from_domain<T>(xr[a], pv.ex) - (double)scr[(2 * pu + (a >> 1)) * 16 + 2 * pt + (a & 1)];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+              }
+            } else if (staged && tid >= SCAN_THREADS) {
                 // the winners' mutual blocks from the staged rows, by the replay wave itself
                 // (only it reads them): the landmark waves go straight on
                 if (lane_r < L * (L + 1) / 2 && sh_spec[pu] >= 0 && sh_spec[pt] >= 0) {
@@ -1758,6 +1910,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         sincos_near(wy.x, wma0, ws0, wc0, sn, cs);
                         eval_candidate(b5, wy.x, wy.y, sn, cs, xpl, ln.alpha, ln.r, Rm, p.gate, c);
                         bad |= c.pass ? 0 : 1;
+                        // GSL_EDOM of the winner (the reference evaluated it: Robot.cpp:454)
+                        if (c.singular) atomicOr(&sh_rwst, (int)EKF_ST_SINGULAR);
                         build_package(c, R33l, w0, w1, w2, pk);   // its V rows stay in sh_wh[t]
                         if (sym) {   // once per line for every landmark's operand stores
                             float F[3];
@@ -1802,7 +1956,53 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             } else {
                 // ---- (e) owned blocks of the guessed columns (Robot.cpp:560 operands), while the
                 // last wave runs (f) ----
-                if (own) {
+                if (mf) {
+                  if constexpr (std::is_same<T, float>::value) {
+                    // the owned rows' blocks of the guessed columns: X minus the pending steps' ΔX
+                    // of the wave's 128 rows (8 M-blocks) against the 16 winner rows, transposed
+                    // through this wave's part of sh_vpl (8 KB; the planes are staged there later)
+                    const int l = tid & 63;
+                    const int rbase = 2 * (g * SCAN_THREADS + (tid & ~63));
+                    auto wrow = [&](int c) {
+                        const int t = c >> 1;
+                        const int w = t < L ? sh_spec[t] : -1;
+                        return w >= 0 ? 2 * w + (c & 1) : -1;
+                    };
+                    f32x4v dacc[8];
+                    plane_replay<8>(p.pend, e, opstride * 3, M, amask, l,
+                                    [&](int mb, int r) { return rbase + 16 * mb + r; }, wrow, dacc);
+                    float* scr = sh_vpl + (tid & ~63) * 32;
+#pragma unroll
+                    for (int mb = 0; mb < 8; mb++)
+#pragma unroll
+                        for (int i = 0; i < 4; i++) scr[(mb * 16 + 4 * (l >> 4) + i) * 16 + (l & 15)] = dacc[mb][i];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    if (own) {
+                        const float* r0 = scr + ((l >> 3) * 16 + ((2 * l) & 15)) * 16;
+                        f32x4v d0[4], d1[4];
+#pragma unroll
+                        for (int k = 0; k < 4; k++) {
+                            d0[k] = *reinterpret_cast<const f32x4v*>(r0 + 4 * k);
+                            d1[k] = *reinterpret_cast<const f32x4v*>(r0 + 16 + 4 * k);
+                        }
+#pragma unroll
+                        for (int t = 0; t < SPEC_L; t++)
+                            if (t < L && sh_spec[t] >= 0) {
+                                const int c0 = 2 * t;
+                                sh_blk[t][tid] = make_float4(
+                                    (float)(from_domain<T>(srow[t][0], pv.ex) - (double)d0[c0 >> 2][c0 & 3]),
+                                    (float)(from_domain<T>(srow[t][1], pv.ex) - (double)d0[c0 >> 2][(c0 & 3) + 1]),
+                                    (float)(from_domain<T>(srow[t][2], pv.ex) - (double)d1[c0 >> 2][c0 & 3]),
+                                    (float)(from_domain<T>(srow[t][3], pv.ex) - (double)d1[c0 >> 2][(c0 & 3) + 1]));
+                            }
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                  }
+                } else if (own) {
                     if (staged) {
                         double blk[SPEC_L + 1][4];
                         staged_blocks<T>(pv, j, cols, sh_stg, srow, blk);
@@ -1847,16 +2047,19 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     double Rm[4];
                     line_R(ln, i, p.r_mode, Rm);
                     const int w = sh_spec[i];
-                    int deep = 0;   // diagnostics: 1 past the fp32 filter, 2 past the fp64 one
-                    if (own && j < s && !matched) {
+                    int deep = 0;   // diagnostics: 1 past the quick filter, 2 past the fp32 one, 3 past the fp64 one
+                    // the guessed winner itself (j == w) is evaluated exactly by the replay wave, which
+                    // flags a failed gate (sh_flag) and its GSL_EDOM (sh_rwst)
+                    if (own && j < s && !matched && j != w) {
                         Block5 b5;
                         fill_block5(b5, R33, rr0, rr1, rr2, Dj);
                         bool pass = false;
                         double sn = 0.0, cs = 1.0;
-                        if (!certified_reject_f32(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate) &&
-                            (deep = 1, sincos_near(yb.x, ma0, s0j, c0j, sn, cs),
+                        if (!quick_reject(b5, yb.x, yb.y, ma0, s0j, c0j, xp, ln.alpha, ln.r, Rm, p.gate) &&
+                            (deep = 1, !certified_reject_f32(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate)) &&
+                            (deep = 2, sincos_near(yb.x, ma0, s0j, c0j, sn, cs),
                              !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate))) {
-                            deep = 2;
+                            deep = 3;
                             Cand c;
                             eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, c);
                             // GSL_EDOM counts only for candidates the reference evaluates: the
@@ -1868,10 +2071,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         if (pass ? (w < 0 || j < w) : (j == w)) viol = 1;
                     }
                     if (p.dbg && g == 0) {   // waves of workgroup 0 whose lanes went deeper
-                        const bool d1 = __any(deep >= 1), d2 = __any(deep >= 2);
+                        const bool d1 = __any(deep >= 1), d2 = __any(deep >= 2), d3 = __any(deep >= 3);
                         if ((tid & 63) == 0) {
                             if (d1) atomicAdd(&sh_stamp[20], 1ull);
                             if (d2) atomicAdd(&sh_stamp[21], 1ull);
+                            if (d3) atomicAdd(&sh_stamp[23], 1ull);
                             atomicAdd(&sh_stamp[22], 1ull);
                         }
                     }
@@ -1921,6 +2125,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             }
             __syncthreads();
             viol |= sh_flag;
+            status |= sh_rwst;
             EKF_STAMP(14);
             // ---- (h) verdict (exchange 3, parity 0): any flag restarts on the sequential path ----
             const int wv = __any(viol) ? 1 : 0;
@@ -1973,7 +2178,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             fill_block5(b5, R33, rr0, rr1, rr2, Dj);
             double sn, cs;
             sincos_near(yb.x, ma0, s0j, c0j, sn, cs);
-            if (!certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate)) {
+            if (!quick_reject(b5, yb.x, yb.y, ma0, s0j, c0j, xp, ln.alpha, ln.r, Rm, p.gate) &&
+                !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate)) {
                 eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, c);
                 sing = c.singular;
                 if (c.pass) best = j;
@@ -2113,7 +2319,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 rr2 = make_double2(R33[8], ca * R33[2] + sa * R33[5]);
                 yb = make_double2(normalize_radian(alfa), r);
             }
-            if (lead) {
+            if (lead || j == sq) {
                 // P_ll = Gx·Prr·Gxᵀ + Gl·R·Glᵀ (Robot.cpp:813-847); Gx = [[0,0,1],[ca,sa,0]],
                 // Gl = [[1,0],[y1·ca − y0·sa, 1]]
                 const double Gx[6] = {0, 0, 1, ca, sa, 0};
@@ -2133,6 +2339,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         double gsum = 0.0;
                         for (int k = 0; k < 3; k++) gsum += GP[a * 3 + k] * Gx[b * 3 + k];
                         const double h = GlR[a * 2 + 0] * Gl[b * 2 + 0] + GlR[a * 2 + 1] * Gl[b * 2 + 1];
+                        if (j == sq) Dj[a * 2 + b] = gsum + h;   // the new landmark's kept diagonal block
+                        if (!lead) continue;
                         pdiag[q * 4 + a * 2 + b] = gsum + h;
                         // fp16 storage: the new landmark's variances bound its whole row and
                         // column (|P_ij| <= sqrt(P_ii P_jj)), and downdates only shrink them
@@ -2151,6 +2359,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         *reinterpret_cast<double2*>(Rsw + n + b0) = rr1;
         *reinterpret_cast<double2*>(Rsw + 2 * n + b0) = rr2;
         *reinterpret_cast<double2*>(yw + b0) = yb;
+        if (Ddw) Ddw[j] = reset || j >= s + nadd ? make_double4(0, 0, 0, 0) : make_double4(Dj[0], Dj[1], Dj[2], Dj[3]);
         if (sizeof(C) == 4) {
             // f32 operands: the k columns past the matches hold −0 (U) and +0 (V), so a flush
             // that runs every k-step unconditionally adds −0 there, which leaves every value as
@@ -2226,9 +2435,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // state and the step's result record — only if every workgroup completed without a timeout.
     // Otherwise the instance keeps its state from before the call, and the step's record applies
     // nothing (no downdate, rows or reset: the flush and later on-read replays skip it).
-    if (tid == 0 && !lead) publish_done(sync, g, p.epoch, wgst);
+    if (tid == 0 && g != 0) publish_done(sync, g, p.epoch, wgst);
+    if (g == 0) wgst = lead_collect(sync, G, p.epoch, wgst, p.spin_log2, tid, sh_red);
     if (lead) {
-        wgst = lead_collect(sync, G, p.epoch, wgst, p.spin_log2);
         sync[SYNC_WG0] = (int)done_word(p.epoch, wgst);
         const bool commit = !(wgst & EKF_ST_TIMEOUT_BIT);
         res[RES_NLINES] = L;
