@@ -91,6 +91,14 @@ def parse():
                     help="fp32 flush arithmetic (slam_ekf.h EKF_ARITH_*): exact = fp32 MFMA, the state "
                          "bit-identical for every T; bf16x6 = fp32 operands split exactly into three "
                          "bf16 parts, six bf16 MFMAs per product (f32 storage only)")
+    ap.add_argument("--dump-state", default="",
+                    help="directory: after all steps each rank writes its instances' final state "
+                         "(state_<global instance>.npz: P, y, saved, pose) for multi-rank checks")
+    ap.add_argument("--speculate", type=int, choices=[0, 1, 2], default=1,
+                    help="association path (EKF_SPECULATE): 1 speculative (default), 0 the "
+                         "sequential chain every scan, 2 every guess wrong (fallback cost)")
+    ap.add_argument("--world", choices=["bench", "survey"], default="bench",
+                    help="scan_gen parameter profile: bench (default) or SURVEY.md §8d literally")
     ap.add_argument("--traffic-json", default="",
                     help="HBM traffic file (default: the newest profiles/*/traffic.json)")
     return ap.parse_args()
@@ -168,7 +176,8 @@ def main():
     n = 3 + 2 * N
 
     world_map = G.make_world(N)
-    st = G.initial_state(world_map)
+    profile = None if args.world == "bench" else args.world
+    st = G.initial_state(world_map, profile=profile)
 
     arith = {"exact": ekf.ARITH_EXACT, "bf16x6": ekf.ARITH_BF16X6}[args.arith]
     if prec != ekf.PREC_F32:
@@ -176,6 +185,7 @@ def main():
     if args.flush_interval <= 0:
         args.flush_interval = {ekf.PREC_F64: 4, ekf.PREC_F16: 8}.get(
             prec, 12 if arith == ekf.ARITH_BF16X6 else 8)
+    os.environ["EKF_SPECULATE"] = str(args.speculate)
     ens = ekf.Ensemble(N, E, prec, max_lines=L_LINES, device=local, pipeline=bool(args.pipeline),
                       flush_interval=args.flush_interval, arith=arith)
     # one real stream for everything (torch's default stream has handle 0, which the C-ABI reads
@@ -195,7 +205,7 @@ def main():
     if rank == 0:
         host = np.zeros((steps_total, per_step))
         for s in range(steps_total):
-            enc, lines, _ = G.make_scan(world_map, s + 1, instances=E_total, lines=L_LINES)
+            enc, lines, _ = G.make_scan(world_map, s + 1, instances=E_total, lines=L_LINES, profile=profile)
             host[s] = D.pack(enc, lines)
         payload.copy_(torch.from_numpy(host))
     nlines = torch.full((E,), L_LINES, dtype=torch.int32, device=dev)
@@ -251,6 +261,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    if args.dump_state:
+        os.makedirs(args.dump_state, exist_ok=True)
+        for e in range(E):
+            P_, y_, s_, pose_ = ens.download_state(e)
+            np.savez(os.path.join(args.dump_state, f"state_{first + e}.npz"), P=P_, y=y_, saved=s_, pose=pose_)
+        del P_
     res = ens.read_results()
     # a step counts only if it committed a valid update: every line matched, no augmentation or
     # reset, and no status bit (a timed-out exchange rolls the call back, EKF_ST_SYNC_TIMEOUT)
@@ -312,6 +328,8 @@ def main():
                             f"broadcast of {B} scans per collective)") if world > 1 else "ensemble x1",
                 "pipeline": bool(args.pipeline), "flush_interval": args.flush_interval,
             "arith": "bf16x6" if arith == ekf.ARITH_BF16X6 else "exact",
+            "association": {0: "sequential", 1: "speculative", 2: "speculative, every guess wrong"}[args.speculate],
+            "world": args.world,
         },
         "clock_preroll_steps": PR,
         "roofline": {

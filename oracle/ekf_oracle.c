@@ -38,6 +38,8 @@ struct oracle_robot {
     int r_mode;
     int saved;      /* savedLineCount */
     int status;
+    double gate_margin; /* min |sqrt(|d²|) − MAHALANOBIS| over the candidates the last localize
+                           evaluated (test instrumentation: SURVEY §8d's gate-margin rejection) */
     double pose[3]; /* xPos, yPos, thetaPos */
     double* P;      /* P_t0, n*n */
     double* y;      /* y, n */
@@ -207,6 +209,7 @@ int oracle_n(const oracle_robot* o) { return o->n; }
 int oracle_capacity(const oracle_robot* o) { return o->N; }
 int oracle_saved(const oracle_robot* o) { return o->saved; }
 int oracle_status(const oracle_robot* o) { return o->status; }
+double oracle_gate_margin(const oracle_robot* o) { return o->gate_margin; }
 int oracle_threads(void)
 {
 #ifdef _OPENMP
@@ -328,6 +331,7 @@ int oracle_localize(oracle_robot* o, const oracle_line* lines, int L, const doub
     double* P_pre = o->P_pre;
     double* y = o->y;
     o->status = 0;
+    o->gate_margin = INFINITY;
 
     /* Robot.cpp:130-148 (SIMULATIONOFF branch; `rot` unused) */
     const double x_t0[3] = {o->pose[0], o->pose[1], o->pose[2]};
@@ -437,6 +441,7 @@ int oracle_localize(oracle_robot* o, const oracle_line* lines, int L, const doub
             oracle_dgemm(1, 0, 1, 2, 2, 1.0, z, 1, S_inv, 2, 0.0, vS, 2);
             oracle_dgemm(0, 0, 1, 1, 2, 1.0, vS, 2, z, 1, 0.0, &d2, 1);
 
+            if (fabs(sqrt(fabs(d2)) - MAHALANOBIS) < o->gate_margin) o->gate_margin = fabs(sqrt(fabs(d2)) - MAHALANOBIS);
             if (sqrt(fabs(d2)) > MAHALANOBIS) {                  /* Robot.cpp:489-498 */
                 if (j == s - 1) { extra[nextra++] = i; break; }
                 continue;

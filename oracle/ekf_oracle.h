@@ -61,6 +61,8 @@ int oracle_n(const oracle_robot* o);
 int oracle_capacity(const oracle_robot* o);
 int oracle_saved(const oracle_robot* o);
 int oracle_status(const oracle_robot* o);
+/* min |sqrt(|d²|) − 0.4| over the candidates the last localize evaluated (INFINITY: none) */
+double oracle_gate_margin(const oracle_robot* o);
 /* threads the O(n^2) loops run on: 1 in libekf_oracle.so, the OpenMP team in libekf_oracle_omp.so */
 int oracle_threads(void);   /* OR of GSL-like error codes seen in last call */
 void oracle_pose(const oracle_robot* o, double pose[3]);

@@ -64,6 +64,8 @@ def lib(omp: bool = False):
         L.oracle_normalize_radian.argtypes = [d]
         L.oracle_threads.restype = i
         L.oracle_threads.argtypes = []
+        L.oracle_gate_margin.restype = d
+        L.oracle_gate_margin.argtypes = [vp]
         _libs[omp] = L
     return _libs[omp]
 
@@ -176,6 +178,11 @@ class OracleRobot:
     @property
     def status(self) -> int:
         return self._lib.oracle_status(self._h)
+
+    @property
+    def gate_margin(self) -> float:
+        """min |sqrt(|d²|) − 0.4| over the candidates the last localize evaluated."""
+        return float(self._lib.oracle_gate_margin(self._h))
 
     def set_state(self, P=None, y=None, saved: int = 0, pose=None):
         Pc = None if P is None else np.ascontiguousarray(P, dtype=np.float64)

@@ -78,6 +78,7 @@ struct ekf_ctx {
     int spec;                 // speculative association (EKF_SPECULATE)
     int spin_log2;            // spin bound of the association kernel's waits (EKF_SPIN_LOG2, tests)
     int test_drop;            // test hook (EKF_TEST_DROP_WG = e): instance e's last workgroup never runs
+    int mfrep;                // split-bf16 contexts: MFMA replay of pending steps (EKF_MFREP=0: off, tests)
     int scan_batch;           // instances per association launch (co-residency bound)
     unsigned scan_epoch;      // association launches so far (mailbox tags)
     double* mbox;
@@ -364,6 +365,7 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     c->spec = getenv("EKF_SPECULATE") ? atoi(getenv("EKF_SPECULATE")) : 1;
     c->spin_log2 = getenv("EKF_SPIN_LOG2") ? std::max(8, std::min(24, atoi(getenv("EKF_SPIN_LOG2")))) : 24;
     c->test_drop = getenv("EKF_TEST_DROP_WG") ? atoi(getenv("EKF_TEST_DROP_WG")) + 1 : 0;
+    c->mfrep = (c->bf && !(getenv("EKF_MFREP") && atoi(getenv("EKF_MFREP")) == 0)) ? 1 : 0;
     ALLOC(c->mbox, sizeof(double) * 2 * c->G * c->mbw * E);
     c->sync_stride = ((ekf::SYNC_WG0 + c->G + 15) / 16) * 16;
     ALLOC(c->sync, sizeof(int) * c->sync_stride * E);
@@ -606,7 +608,7 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.y = c->y;
     p.live = c->cur;
     p.Dd = c->D;
-    p.mfrep = c->bf ? 1 : 0;
+    p.mfrep = c->mfrep;
     p.Etot = c->cfg.instances;
     p.spin_log2 = c->spin_log2;
     p.test_drop = c->test_drop;

@@ -11,6 +11,14 @@ Benchmark world (tuned so that association is robust):
     pose plus noise; each scan observes L distinct landmarks with small Gaussian noise and
     C_AR = diag(var_alpha, var_r) (off-diagonals zero, as lineFitting.cpp:446-448 forces).
 Instance k of an ensemble perturbs the encoder and the observations with its own stream.
+
+Two parameter profiles. "bench" (default, above): small noise, so that the association is
+unambiguous at the reference's 0.4 Mahalanobis gate. "survey": SURVEY.md §8d literally — P0 pose /
+heading / landmark variances 0.05 / 1e-3 / 1e-3 plus U·Uᵀ with U_ik ~ N(0, (1e-2/√32)²), 0.05 m and
+0.01 rad per step, encoder noise σ = 1e-3, observation noise σ_z = 1e-2, R = diag(9e-4, 9e-4)
+(LINENOISE² = 0.03², Robot.h:16). Under the survey profile a true match has sqrt(d²) ≈ σ_z·√2/0.03
+≈ 0.47 on average — above the 0.4 gate — so many lines are not matched and become new landmarks
+(DESIGN §5 reports what that does to the association and the throughput).
 """
 from __future__ import annotations
 
@@ -69,15 +77,31 @@ class InitialState:
         return P
 
 
+PROFILES = {
+    # P0 variances, U column sigma, step (m, rad), noise sigmas, line covariance
+    "bench": dict(pose_var=1e-4, heading_var=1e-5, landmark_var=1e-5, u_sigma=None, speed=1e-3,
+                  turn=None, enc_noise=1e-4, z_noise=5e-4, var_alpha=1e-4, var_r=1e-4),
+    "survey": dict(pose_var=0.05, heading_var=1e-3, landmark_var=1e-3, u_sigma=1e-2 / math.sqrt(32),
+                   speed=0.05, turn=0.01, enc_noise=1e-3, z_noise=1e-2, var_alpha=9e-4, var_r=9e-4),
+}
+
+
 def initial_state(world: World, seed: int = 43, rank: int = 32, pose_var: float = 1e-4,
-                  heading_var: float = 1e-5, landmark_var: float = 1e-5) -> InitialState:
+                  heading_var: float = 1e-5, landmark_var: float = 1e-5,
+                  profile: str | None = None) -> InitialState:
     n, s = world.n, world.active
     rng = np.random.default_rng(seed)
+    sigma = None
+    if profile is not None:
+        pr = PROFILES[profile]
+        pose_var, heading_var, landmark_var, sigma = (pr["pose_var"], pr["heading_var"],
+                                                      pr["landmark_var"], pr["u_sigma"])
     diag = np.zeros(n)
     diag[0] = diag[1] = pose_var
     diag[2] = heading_var
     diag[3:3 + 2 * s] = landmark_var
-    sigma = math.sqrt(0.5 * landmark_var / rank)
+    if sigma is None:
+        sigma = math.sqrt(0.5 * landmark_var / rank)
     U = rng.normal(0.0, sigma, size=(n, rank))
     U[3 + 2 * s:] = 0.0
     y = np.zeros(n)
@@ -86,8 +110,15 @@ def initial_state(world: World, seed: int = 43, rank: int = 32, pose_var: float 
     return InitialState(diag, U, y, s, np.zeros(3))
 
 
-def truth_pose(step: int, speed: float = 1e-3, wobble: float = 2e-4) -> np.ndarray:
-    return np.array([speed * step, 0.0, wobble * math.sin(step / 10.0)])
+def truth_pose(step: int, speed: float = 1e-3, wobble: float = 2e-4, turn: float | None = None) -> np.ndarray:
+    if turn is None:
+        return np.array([speed * step, 0.0, wobble * math.sin(step / 10.0)])
+    # constant speed and turn rate: a circle of radius speed / turn (0.05 m, 0.01 rad)
+    th = turn * step
+    if turn == 0.0:
+        return np.array([speed * step, 0.0, 0.0])
+    R = speed / turn
+    return np.array([R * math.sin(th), R * (1.0 - math.cos(th)), th])
 
 
 def _noise(rng: np.random.Generator, sigma: float, size, clip: float = 2.5) -> np.ndarray:
@@ -98,16 +129,23 @@ def _noise(rng: np.random.Generator, sigma: float, size, clip: float = 2.5) -> n
 
 def make_scan(world: World, step: int, instances: int = 1, lines: int = 8, seed: int = 7,
               z_noise: float = 5e-4, enc_noise: float = 1e-4, var_alpha: float = 1e-4,
-              var_r: float = 1e-4, first_instance: int = 0):
-    """Returns (encoder[E,3], lines[E,L,6], nlines[E]) for one scan of `instances` EKFs."""
+              var_r: float = 1e-4, first_instance: int = 0, profile: str | None = None,
+              redraw: int = 0):
+    """Returns (encoder[E,3], lines[E,L,6], nlines[E]) for one scan of `instances` EKFs.
+    redraw > 0 draws another scan for the same step (the gate-margin rejection of SURVEY §8d)."""
     s = world.active
     L = min(lines, s)
-    pick = np.random.default_rng(seed + step).choice(s, size=L, replace=False)
-    pose = truth_pose(step)
+    speed, turn = 1e-3, None
+    if profile is not None:
+        pr = PROFILES[profile]
+        z_noise, enc_noise, var_alpha, var_r = pr["z_noise"], pr["enc_noise"], pr["var_alpha"], pr["var_r"]
+        speed, turn = pr["speed"], pr["turn"]
+    pick = np.random.default_rng([seed + step, redraw] if redraw else seed + step).choice(s, size=L, replace=False)
+    pose = truth_pose(step, speed=speed, turn=turn)
     enc = np.zeros((instances, 3))
     out = np.zeros((instances, lines, LINE_FIELDS))
     for e in range(instances):
-        rng = np.random.default_rng([1000 + first_instance + e, step])
+        rng = np.random.default_rng([1000 + first_instance + e, step] + ([redraw] if redraw else []))
         enc[e] = pose + _noise(rng, enc_noise, 3) * np.array([1.0, 1.0, 0.1])
         a = world.alpha[pick]
         z_a = wrap_pi(a - pose[2] + _noise(rng, z_noise, L))

@@ -9,6 +9,7 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -38,3 +39,33 @@ def test_bench_two_ranks_one_gpu(bcast_every):
     assert r["all_lines_matched"] is True        # every instance of both ranks matched its 8 lines
     assert r["value"] > 0 and r["steps"] == 13
     assert f"broadcast of {bcast_every} scans" in r["config"]["parallelism"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arith", ["exact", "bf16x6"])
+def test_two_ranks_equal_one_rank(tmp_path, arith):
+    """Every instance's final state (P, y, savedLineCount, pose) after bench.py's whole schedule on
+    two ranks (two instances each) is bitwise the state a single-rank run of the same four global
+    instances ends in: the sharding, the grouped broadcast of the scan stream and the per-rank
+    contexts change nothing per instance (the arithmetic of an instance never depends on the
+    others in its launch)."""
+    common = ["--steps", "13", "--warmup", "3", "--preroll", "0", "--capacity", "256", "--no-cpu",
+              "--arith", arith, "--flush-interval", "8" if arith == "exact" else "12"]
+    env = dict(os.environ, BENCH_SAME_DEVICE="1", MASTER_ADDR="127.0.0.1")
+    two = tmp_path / "two"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--instances", "2", "--dist-backend", "gloo",
+           "--bcast-every", "3", "--dump-state", str(two)] + common
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr[-3000:]
+    one = tmp_path / "one"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--instances", "4",
+           "--dump-state", str(one)] + common
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr[-3000:]
+    for k in range(4):
+        a, b = np.load(two / f"state_{k}.npz"), np.load(one / f"state_{k}.npz")
+        for key in ("P", "y", "saved", "pose"):
+            assert np.array_equal(a[key], b[key]), (arith, k, key)
+        assert int(a["saved"]) == 246   # s = N − 10 kept: every line matched, no augmentation
