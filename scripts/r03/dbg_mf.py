@@ -29,9 +29,9 @@ for (N, T, lines, xe) in [(256, 16, 6, 7), (256, 16, 6, 0), (80, 16, 7, 0), (256
                 nl = np.full(E, ln.shape[1], dtype=np.int32)
             ra = a.localize(enc, ln, nl)
             rb = b.localize(enc, ln, nl)
-            ya = a.download_state(0, with_P=False)[1]; yb = b.download_state(0, with_P=False)[1]
-            out.append((step, rel(ya, yb), ra[0]["matches"], ra[0]["reset"], ra[0]["match"] == rb[0]["match"]))
+            out.append((step, float(np.abs(ra[0]["pose"] - rb[0]["pose"]).max()), ra[0]["matches"], ra[0]["reset"],
+                        ra[0]["match"] == rb[0]["match"]))
         Pa = a.download_state(0)[0]; Pb = b.download_state(0)[0]
         print(f"N={N} T={T} L={lines} xe={xe} mf={mf}: P {rel(Pa, Pb):.2e}", flush=True)
-        print("  y per step:", " ".join(f"{s}:{r:.1e}{'' if ok else '!'}" for s, r, m, rs, ok in out), flush=True)
+        print("  pose per step:", " ".join(f"{s}:{r:.1e}{'' if ok else '!'}" for s, r, m, rs, ok in out), flush=True)
         a.close(); b.close()

@@ -546,6 +546,9 @@ __device__ __forceinline__ bool certified_reject(const Block5& b, double ma, dou
 // otherwise make S indefinite: then it never rejects) and finite inputs (NaN never rejects).
 // Margins: 1e-6 relative on the gate plus absolute slack, far above the rounding of the bounds
 // and of the exact evaluation.
+// s0, c0: sin/cos of ma0 within QR_TRIG_EPS (the fp32 __sincosf of (float)ma0 for |ma0| <= 8:
+// argument rounding <= 8·2^-24 plus the instruction's own error, ≈1e-6 together).
+constexpr double QR_TRIG_EPS = 4e-6;
 __device__ __forceinline__ bool quick_reject(const Block5& b, double ma, double mr, double ma0, double s0,
                                              double c0, const double xp[3], double za, double zr,
                                              const double Rm[4], double gate)
@@ -553,7 +556,8 @@ __device__ __forceinline__ bool quick_reject(const Block5& b, double ma, double 
     const double tr5 = b.p00 + b.p11 + b.p22 + b.daa + b.dbb;
     const double X = fabs(xp[0]) + fabs(xp[1]);
     const double H2 = 2.0 + X * X;   // ≥ ‖H1‖²
-    if (!(Rm[1] == Rm[2]) || !(tr5 >= 0.0) || !(Rm[0] > 1e-5 * 2.0 * tr5) || !(Rm[3] > 1e-5 * H2 * tr5))
+    if (!(Rm[1] == Rm[2]) || !(tr5 >= 0.0) || !(Rm[0] > 1e-5 * 2.0 * tr5) || !(Rm[3] > 1e-5 * H2 * tr5) ||
+        !(fabs(ma0) <= 8.0))
         return false;
     const double g2 = gate * gate * (1.0 + 1e-6);
     const double S00 = b.p22 - 2.0 * b.p2a + b.daa + Rm[0];
@@ -564,7 +568,7 @@ __device__ __forceinline__ bool quick_reject(const Block5& b, double ma, double 
         if (a0 * a0 > g2 * S00) return true;
     }
     const double v1e = zr - (mr - (xp[0] * c0 + xp[1] * s0));
-    const double a1 = fabs(v1e) - X * fabs(ma - ma0) - 1e-12 * (1.0 + fabs(zr) + fabs(mr) + X);
+    const double a1 = fabs(v1e) - X * (fabs(ma - ma0) + QR_TRIG_EPS) - 1e-12 * (1.0 + fabs(zr) + fabs(mr) + X);
     const double S11u = H2 * tr5 * (1.0 + 1e-5) + Rm[3];
     return a1 > 0.0 && a1 * a1 > g2 * S11u;
 }
@@ -1364,6 +1368,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     __shared__ int sh_flag;
     __shared__ int sh_ready;
     __shared__ int sh_rwst;   // status bits of the replay wave (the winners' GSL_EDOM)
+    __shared__ int sh_first[SPEC_L];   // per line the first guessed candidate (speculative path)
+    if (tid < SPEC_L) sh_first[tid] = 0x7fffffff;
     __shared__ double sh_wd[SPEC_L * SPEC_WD];
     __shared__ double4 sh_wh[SPEC_L][SPEC_L][2];
     __shared__ double sh_pk[SPEC_L][PKW];
@@ -1451,10 +1457,39 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         load_block<T>(v0, 2 * j, 2 * j, dj0);
         if (Ddr && p.npend > 0) djb = Ddr[j];
     }
+    // the scan's other inputs, issued with the state loads (one memory round trip): the pending
+    // steps' control words, the line count, savedLineCount and the line words
+    int4 ctl_pre = make_int4(0, 0, 0, 0);
+    if ((p.phase & PHASE_UPDATE) && tid < p.npend) {
+        const int* r = p.pend[tid].res + (size_t)e * RES_STRIDE;
+        ctl_pre = make_int4(r[RES_RESET], r[RES_KSTEPS], r[RES_NADD], r[RES_SAVED_IN]);
+    }
+    const int L_pre = p.nlines[e];
+    const int s_pre = (p.phase & PHASE_UPDATE) ? p.saved[e] : 0;
+    constexpr int LW_PER = (EKF_MAX_LINES * 6 + SCAN_BLOCK - 1) / SCAN_BLOCK;
+    double lw_pre[LW_PER];
+    {
+        const double* src = reinterpret_cast<const double*>(p.lines + (size_t)e * d.max_lines);
+#pragma unroll
+        for (int k = 0; k < LW_PER; k++) {
+            const int idx = tid + k * SCAN_BLOCK;
+            lw_pre[k] = ((p.phase & PHASE_UPDATE) && idx < d.max_lines * 6) ? src[idx] : 0.0;
+        }
+    }
     init_state();
     // the owned landmark's angle at the start of the scan and its sin/cos (sincos_near)
+    // sin/cos of the owned landmark's scan-start angle: fp32 now (the quick filter's bound and the
+    // guess), the exact fp64 ones (sincos_near) only where a lane needs the exact evaluation
     double ma0 = yb.x, s0j = 0.0, c0j = 1.0;
-    if (own && (p.phase & PHASE_UPDATE)) sincos(ma0, &s0j, &c0j);
+    bool sc_exact = false;
+    float s0f = 0.f, c0f = 1.f;
+    if (own && (p.phase & PHASE_UPDATE)) __sincosf((float)ma0, &s0f, &c0f);
+    auto exact_sc = [&]() {
+        if (!sc_exact) {
+            sincos(ma0, &s0j, &c0j);
+            sc_exact = true;
+        }
+    };
 
     if (!(p.phase & PHASE_UPDATE)) {
         // predict only: the predicted robot strip (and the mean, unchanged) into the other copy,
@@ -1512,17 +1547,16 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     pv.npend = p.npend;
     pv.pend = p.pend;
     pv.ctl = sh_ctl;
-    if (tid < p.npend) {
-        const int* r = p.pend[tid].res + (size_t)e * RES_STRIDE;
-        sh_ctl[tid] = make_int4(r[RES_RESET], r[RES_KSTEPS], r[RES_NADD], r[RES_SAVED_IN]);
-    }
+    if (tid < p.npend) sh_ctl[tid] = ctl_pre;
 
-    int L = p.nlines[e];
+    int L = L_pre;
     L = L < 0 ? 0 : (L > d.max_lines ? d.max_lines : L);
-    const int s = p.saved[e];
-    const ekf_line* lines = p.lines + (size_t)e * d.max_lines;
-    for (int k = tid; k < L * 6; k += SCAN_BLOCK)
-        reinterpret_cast<double*>(sh_lines)[k] = reinterpret_cast<const double*>(lines)[k];
+    const int s = s_pre;
+#pragma unroll
+    for (int k = 0; k < LW_PER; k++) {
+        const int idx = tid + k * SCAN_BLOCK;
+        if (idx < L * 6) reinterpret_cast<double*>(sh_lines)[idx] = lw_pre[k];
+    }
     __syncthreads();   // sh_lines, sh_ctl
 
     const bool spec_ok = p.spec && L > 0 && L <= SPEC_L && s > 0 && G <= SPEC_GMAX;
@@ -1671,21 +1705,18 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         // instance's first guessed candidate (workgroups are in landmark order); if those are
         // distinct they are the winners. Otherwise, per line the first SPEC_K guessed candidates,
         // and in line order the first one not taken by an earlier line. ----
-        if (tid < 64) {
-            // lane t: the first workgroup (in landmark order) with a guessed candidate for line t
-            int c = 0x7fffffff;
-            if (tid < L) {
-                for (int gq = 0; gq < G; gq++) {
-                    const unsigned long long w = sh_lists[gq * SPEC_L + tid];
-                    if ((w >> LW_CNT) & 7) {
-                        c = gq * SCAN_THREADS + (int)(w & 255);
-                        break;
-                    }
-                }
-            }
+        // per line the first guessed candidate over all workgroups: one list word per thread, an LDS
+        // atomic minimum per line (sh_first, reset at the start of the kernel)
+        for (int k = tid; k < G * SPEC_L; k += SCAN_BLOCK) {
+            const int gq = k / SPEC_L, t = k - gq * SPEC_L;
+            const unsigned long long w = sh_lists[gq * SPEC_L + t];
+            if (t < L && ((w >> LW_CNT) & 7)) atomicMin(&sh_first[t], gq * SCAN_THREADS + (int)(w & 255));
+        }
+        __syncthreads();
+        {
             int first[SPEC_L];
 #pragma unroll
-            for (int t = 0; t < SPEC_L; t++) first[t] = __shfl(c, t, 64);
+            for (int t = 0; t < SPEC_L; t++) first[t] = sh_first[t];
             if (tid == 0) {
                 bool distinct = true;
 #pragma unroll
@@ -1792,8 +1823,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     if (p.phase & PHASE_PREDICT) predict_cols(F3, q0, q1, q2);
                     double* r = sh_wd + u * SPEC_WD;
                     r[0] = q0.x; r[1] = q0.y; r[2] = q1.x; r[3] = q1.y; r[4] = q2.x; r[5] = q2.y;
-                    r[10] = qy.x; r[11] = qy.y;
-                    sincos(qy.x, &r[12], &r[13]);
+                    r[10] = qy.x; r[11] = qy.y;   // (sin/cos of the angle: by the replay wave, after the barrier)
                 }
             }
             if (staged && !mf) {
@@ -1891,7 +1921,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     w0 = make_double2(r[0], r[1]); w1 = make_double2(r[2], r[3]);
                     w2 = make_double2(r[4], r[5]); wy = make_double2(r[10], r[11]);
                     wD[0] = r[6]; wD[1] = r[7]; wD[2] = r[8]; wD[3] = r[9];
-                    wma0 = r[10]; ws0 = r[12]; wc0 = r[13];
+                    wma0 = r[10];
+                    sincos(wma0, &ws0, &wc0);   // sincos_near's scan-start values (as the owner's)
                 }
                 int ml = 0, bad = 0;
                 const bool lst = p.dbg && g == 0 && u == 0;
@@ -2055,9 +2086,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         fill_block5(b5, R33, rr0, rr1, rr2, Dj);
                         bool pass = false;
                         double sn = 0.0, cs = 1.0;
-                        if (!quick_reject(b5, yb.x, yb.y, ma0, s0j, c0j, xp, ln.alpha, ln.r, Rm, p.gate) &&
+                        if (!quick_reject(b5, yb.x, yb.y, ma0, s0f, c0f, xp, ln.alpha, ln.r, Rm, p.gate) &&
                             (deep = 1, !certified_reject_f32(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate)) &&
-                            (deep = 2, sincos_near(yb.x, ma0, s0j, c0j, sn, cs),
+                            (deep = 2, exact_sc(), sincos_near(yb.x, ma0, s0j, c0j, sn, cs),
                              !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate))) {
                             deep = 3;
                             Cand c;
@@ -2177,9 +2208,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             Block5 b5;
             fill_block5(b5, R33, rr0, rr1, rr2, Dj);
             double sn, cs;
-            sincos_near(yb.x, ma0, s0j, c0j, sn, cs);
-            if (!quick_reject(b5, yb.x, yb.y, ma0, s0j, c0j, xp, ln.alpha, ln.r, Rm, p.gate) &&
-                !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate)) {
+            if (!quick_reject(b5, yb.x, yb.y, ma0, s0f, c0f, xp, ln.alpha, ln.r, Rm, p.gate) &&
+                (exact_sc(), sincos_near(yb.x, ma0, s0j, c0j, sn, cs),
+                 !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate))) {
                 eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, c);
                 sing = c.singular;
                 if (c.pass) best = j;

@@ -535,7 +535,13 @@ def test_bf16x6_flush_close_to_exact(ekf_mod, oracle_mod, N, T, lines, extra_eve
     state within the fp32 bar — P ≤ 1e-6 relative (BASELINE's bound), y ≤ 1e-8 — also against
     the fp64 restatement for instance 0."""
     E = 3
-    w = G.make_world(N, active=N - 14 if extra_every else N - 10)
+    # the trajectory stays clear of the capacity reset: after a reset the map is rebuilt from the
+    # observations and the reference's own fp64 dynamics double any perturbation every scan
+    # (measured with the restatement: 1e-16 → 6e-8 in 28 scans), so an uninterrupted trajectory
+    # across it compares chaos, not arithmetic. Resets inside deferred groups are covered by
+    # test_deferred_flush_equals_drained and the fp64 trajectories.
+    active = N - 12 - 2 * ((3 * T + 1) // extra_every) if extra_every else N - 10
+    w = G.make_world(N, active=active)
     st = G.initial_state(w)
     a = ekf_mod.Ensemble(N, E, 1, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
     b = ekf_mod.Ensemble(N, E, 1, max_lines=8)
@@ -562,6 +568,7 @@ def test_bf16x6_flush_close_to_exact(ekf_mod, oracle_mod, N, T, lines, extra_eve
         for e in range(E):
             assert ra[e]["match"] == rb[e]["match"], (step, e)
             assert ra[e]["status"] == 0, (step, e, ra[e]["status"])
+            assert not ra[e]["reset"], (step, e)
     k = 3 * T + 1
     meas = {}
     for e in range(E):
