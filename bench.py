@@ -180,11 +180,10 @@ def main():
     st = G.initial_state(world_map, profile=profile)
 
     arith = {"exact": ekf.ARITH_EXACT, "bf16x6": ekf.ARITH_BF16X6}[args.arith]
-    if prec != ekf.PREC_F32:
-        arith = ekf.ARITH_EXACT   # the split-bf16 flush serves fp32 storage only
+    if prec == ekf.PREC_F64:
+        arith = ekf.ARITH_EXACT   # the split-bf16 flush serves fp32 operands (fp32 and fp16 storage)
     if args.flush_interval <= 0:
-        args.flush_interval = {ekf.PREC_F64: 4, ekf.PREC_F16: 8}.get(
-            prec, 12 if arith == ekf.ARITH_BF16X6 else 8)
+        args.flush_interval = 4 if prec == ekf.PREC_F64 else (12 if arith == ekf.ARITH_BF16X6 else 8)
     os.environ["EKF_SPECULATE"] = str(args.speculate)
     ens = ekf.Ensemble(N, E, prec, max_lines=L_LINES, device=local, pipeline=bool(args.pipeline),
                       flush_interval=args.flush_interval, arith=arith)
@@ -293,7 +292,7 @@ def main():
     alg_bytes = E * n * (n + 1) * bpe   # one read + write of the packed block per flush
     alg_flops = steps_per_launch * E * 2 * L_LINES * n * (n + 1)
     mfma_peak = MFMA_F64_PEAK_TFS if prec == ekf.PREC_F64 else MFMA_F32_PEAK_TFS   # f16 storage: f32 MFMA
-    bf_form = bool(dom and dom["kernel"].endswith(", true>"))
+    bf_form = bool(dom and (dom["kernel"].endswith(", true>") or dom["kernel"].startswith("flush_bf24_kernel")))
     t_hbm = alg_bytes / (HBM_PEAK_GBS * 1e9)
     # split-bf16 flush: six bf16 MFMA products per fp32 product, at the dense bf16 rate
     t_mfma = (6 * alg_flops / (MFMA_BF16_PEAK_TFS * 1e12)) if bf_form else alg_flops / (mfma_peak * 1e12)

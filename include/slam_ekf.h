@@ -66,12 +66,14 @@ enum { EKF_R_INTENDED = 0, EKF_R_AS_WRITTEN = 1 };
  * EXACT: v_mfma_f32_32x32x2_f32; the flush's per-element chain is the ordered fp32 FMA chain the
  *   association kernel replays on read, so the state is bit-identical for every flush interval
  *   and schedule (default; the C++ drop-in uses it).
- * BF16X6: requires EKF_PREC_F32, EKF_R_INTENDED and max_lines <= 8; any other configuration is
- *   rejected by ekf_create with EKF_EINVAL. Every fp32 operand is split exactly into three bf16
- *   parts (hi + mid + lo), six v_mfma_f32_32x32x16_bf16 per product (all part products down to
- *   2^-16 relative; the dropped ones are below 2^-24), accumulated in fp32. Within fp32 rounding of
- *   EXACT (the 1e-6 bound of BASELINE holds) but no longer bit-identical across flush intervals:
- *   the on-read replay stays the fp32 chain. Groups of an even number of steps (2..16) without
+ * BF16X6: requires EKF_PREC_F32 or EKF_PREC_F16, EKF_R_INTENDED and max_lines <= 8; any other
+ *   configuration is rejected by ekf_create with EKF_EINVAL. Every fp32 operand is split exactly
+ *   into three bf16 parts (hi + mid + lo), six v_mfma_f32_32x32x16_bf16 per product (all part
+ *   products down to 2^-16 relative; the dropped ones are below 2^-24), accumulated in fp32; fp16
+ *   storage is scaled out of its exponent on load and rounded to fp16 once per group on store.
+ *   Within fp32 rounding of EXACT (the 1e-6 bound of BASELINE holds; fp16: its re-stated 1e-3) but
+ *   no longer bit-identical across flush intervals. The association kernel applies pending steps
+ *   by the same bf16 MFMAs on the planes and keeps the diagonal blocks in fp64. Groups of an even number of steps (2..16) without
  *   augmented rows or a reset take the split-bf16 flush; a group with augmentation or the reset,
  *   and an odd-sized group (a partial group flushed by a drain), take the EXACT forms
  *   (ekf_flush_kernel_name reports the form a group size runs). */

@@ -65,6 +65,8 @@ struct ekf_ctx {
     int nwt;
     ekf::WtEntry* wt64;
     int nwt64;
+    int* wt24;                // split-bf16 wave-tiles of 2 × 4 tiles (wr | wc << 16), panel order
+    int nwt24;
     double* d_enc;
     ekf_line* d_lines;
     int* d_nlines;
@@ -157,7 +159,7 @@ int ekf_abi_version(void) { return SLAM_EKF_ABI_VERSION; }
 static void free_all(ekf_ctx* c)
 {
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->cur, c->pose, c->xpre, c->saved, c->D,
-                               c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->pexp, c->sink, c->mbox,
+                               c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->wt24, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->pexp, c->sink, c->mbox,
                                c->sync, c->Ust, c->Vst};
     ptrs.push_back(c->ops_u);
     ptrs.push_back(c->ops_v);
@@ -280,7 +282,7 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         (cfg->arith != EKF_ARITH_EXACT && cfg->arith != EKF_ARITH_BF16X6) ||
         // the split-bf16 flush needs symmetric fp32 operands with kmax = 16 (slam_ekf.h)
         (cfg->arith == EKF_ARITH_BF16X6 &&
-         (cfg->precision != EKF_PREC_F32 || cfg->r_mode != EKF_R_INTENDED || cfg->max_lines > 8)))
+         (cfg->precision == EKF_PREC_F64 || cfg->r_mode != EKF_R_INTENDED || cfg->max_lines > 8)))
         return EKF_EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return EKF_EDEVICE;
@@ -332,7 +334,7 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     ALLOC(c->ops_u, (size_t)c->slot_bytes * c->ring.size());
     ALLOC(c->ops_v, (size_t)c->slot_bytes * c->ring.size());
     // split-bf16 flush: V's three bf16 planes per slot (written by the association kernel)
-    c->bf = cfg->arith == EKF_ARITH_BF16X6;   // (validated above: fp32, symmetric R, kmax 16)
+    c->bf = cfg->arith == EKF_ARITH_BF16X6;   // (validated above: fp32 / fp16, symmetric R, kmax 16)
     c->ops_b = nullptr;
     c->bslot_bytes = 0;
     if (c->bf) {
@@ -478,6 +480,18 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         if (hipMemcpy(c->wt64, w64.data(), sizeof(ekf::WtEntry) * w64.size(), hipMemcpyHostToDevice) !=
             hipSuccess)
             goto fail;
+        // the split-bf16 flush's 2 × 4 wave-tiles holding a stored tile (4wc + 3 >= 2wr), in panels of
+        // 8 wave-tile columns walked row by row (flush_bf24_kernel)
+        std::vector<int> w24;
+        const int nwr2 = (d.nb + 1) / 2, nwc4 = (d.nb + 3) / 4;
+        for (int pc = 0; pc < nwc4; pc += 8)
+            for (int wr = 0; wr < nwr2; wr++)
+                for (int wc = pc; wc < pc + 8 && wc < nwc4; wc++)
+                    if (4 * wc + 3 >= 2 * wr) w24.push_back(wr | (wc << 16));
+        c->nwt24 = (int)w24.size();
+        if (hipMalloc((void**)&c->wt24, sizeof(int) * w24.size()) != hipSuccess) goto fail;
+        if (hipMemcpy(c->wt24, w24.data(), sizeof(int) * w24.size(), hipMemcpyHostToDevice) != hipSuccess)
+            goto fail;
     }
     {
         hipDeviceProp_t prop;
@@ -489,7 +503,7 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         c->ncu = prop.multiProcessorCount;
         // test hook: force one of the bit-identical flush forms (tests/test_gpu_parity.py)
         c->dd_variant = getenv("EKF_FLUSH_VARIANT") ? atoi(getenv("EKF_FLUSH_VARIANT")) : 0;
-        if (c->dd_variant != 2 && c->dd_variant != 8) c->dd_variant = 0;
+        if (c->dd_variant != 2 && c->dd_variant != 4 && c->dd_variant != 8) c->dd_variant = 0;
         // all G workgroups of an instance must be co-resident (they exchange per line). A plain
         // launch gets the same residency as a cooperative one for the same grid
         // (cdna_hip_programming.md §1; the cooperative form only adds a launch-time check of the
@@ -673,6 +687,8 @@ static int enqueue_flush(ekf_ctx* c)
     dp.nwt = c->nwt;
     dp.wt64 = c->wt64;
     dp.nwt64 = c->nwt64;
+    dp.wt24 = c->wt24;
+    dp.nwt24 = c->nwt24;
     dp.pexp = c->pexp;
     dp.sink = c->sink;
     dp.ubase = c->ops_u;
@@ -1261,12 +1277,27 @@ extern "C" const char* ekf_flush_kernel_name(const ekf_ctx* c, int nsteps)
         return "downdate_f64_kernel";
     }
     const bool half = c->cfg.precision == EKF_PREC_F16;
+    if (c->bf && nsteps >= 2 && nsteps <= 16 && nsteps % 2 == 0 && c->dd_variant != 4) {
+        static const char* b24[2][9] = {
+            {"", "flush_bf24_kernel<float, 2>", "flush_bf24_kernel<float, 4>", "flush_bf24_kernel<float, 6>",
+             "flush_bf24_kernel<float, 8>", "flush_bf24_kernel<float, 10>", "flush_bf24_kernel<float, 12>",
+             "flush_bf24_kernel<float, 14>", "flush_bf24_kernel<float, 16>"},
+            {"", "flush_bf24_kernel<_Float16, 2>", "flush_bf24_kernel<_Float16, 4>", "flush_bf24_kernel<_Float16, 6>",
+             "flush_bf24_kernel<_Float16, 8>", "flush_bf24_kernel<_Float16, 10>", "flush_bf24_kernel<_Float16, 12>",
+             "flush_bf24_kernel<_Float16, 14>", "flush_bf24_kernel<_Float16, 16>"}};
+        return b24[half ? 1 : 0][nsteps / 2];
+    }
     if (c->bf && nsteps >= 2 && nsteps <= 16 && nsteps % 2 == 0) {
-        static const char* bfn[9] = {"", "flush_f32_wave_kernel<float, 2, true>", "flush_f32_wave_kernel<float, 4, true>",
-                                     "flush_f32_wave_kernel<float, 6, true>", "flush_f32_wave_kernel<float, 8, true>",
-                                     "flush_f32_wave_kernel<float, 10, true>", "flush_f32_wave_kernel<float, 12, true>",
-                                     "flush_f32_wave_kernel<float, 14, true>", "flush_f32_wave_kernel<float, 16, true>"};
-        return bfn[nsteps / 2];
+        static const char* bfn[2][9] = {
+            {"", "flush_f32_wave_kernel<float, 2, true>", "flush_f32_wave_kernel<float, 4, true>",
+             "flush_f32_wave_kernel<float, 6, true>", "flush_f32_wave_kernel<float, 8, true>",
+             "flush_f32_wave_kernel<float, 10, true>", "flush_f32_wave_kernel<float, 12, true>",
+             "flush_f32_wave_kernel<float, 14, true>", "flush_f32_wave_kernel<float, 16, true>"},
+            {"", "flush_f32_wave_kernel<_Float16, 2, true>", "flush_f32_wave_kernel<_Float16, 4, true>",
+             "flush_f32_wave_kernel<_Float16, 6, true>", "flush_f32_wave_kernel<_Float16, 8, true>",
+             "flush_f32_wave_kernel<_Float16, 10, true>", "flush_f32_wave_kernel<_Float16, 12, true>",
+             "flush_f32_wave_kernel<_Float16, 14, true>", "flush_f32_wave_kernel<_Float16, 16, true>"}};
+        return bfn[half ? 1 : 0][nsteps / 2];
     }
     const bool wave = nsteps >= 2 && nsteps <= 8 && nsteps % 2 == 0 && c->d.kmax <= 16 &&
                       (nsteps >= 6 || c->dd_variant == 8);

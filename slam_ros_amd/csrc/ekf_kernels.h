@@ -142,6 +142,8 @@ struct DowndateParams {
     const void* bbase;    // EKF_ARITH_BF16X6: bf16 operand planes of ring slot i at bbase + i·bslot_bytes
     long long bslot_bytes;
     int bf;               // 1: plain groups of 2, 4, 6 or 8 steps run the split-bf16 wave flush
+    const int* wt24;      // [nwt24] split-bf16 wave-tiles of 2 × 4 tiles (wr | wc << 16), panel order
+    int nwt24;
     Slot steps[PMAX];
 };
 

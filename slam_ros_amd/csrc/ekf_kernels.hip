@@ -118,8 +118,22 @@ __device__ __forceinline__ double normalize_radian(double rad)
     return rad;
 }
 
-// gsl_linalg_LU_decomp + LU_invert on 2x2 (Robot.cpp:449-457); false when U is singular
-// (GSL_EDOM), leaving Si untouched.
+// 1/a for a finite nonzero a of moderate exponent: v_rcp_f64 and two Newton steps (within an ulp;
+// the association chain's divisions, which sit on its critical path, take this instead of the
+// correctly rounded division)
+__device__ __forceinline__ double rcp_nr(double a)
+{
+    double r = __builtin_amdgcn_rcp(a);
+    double e = fma(-a, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-a, r, 1.0);
+    return fma(r, e, r);
+}
+
+// gsl_linalg_LU_decomp + LU_invert on 2x2 (Robot.cpp:449-457): partial pivoting, the elimination
+// and the two back substitutions of GSL, with the pivots' reciprocals (rcp_nr) in place of the
+// divisions (agrees with GSL within an ulp or two per entry); false when U is singular (GSL_EDOM),
+// leaving Si untouched.
 __device__ __forceinline__ bool lu_invert2(const double S[4], double Si[4])
 {
     double a0 = S[0], a1 = S[1], a2 = S[2], a3 = S[3];
@@ -130,19 +144,22 @@ __device__ __forceinline__ bool lu_invert2(const double S[4], double Si[4])
         a2 = t0; a3 = t1;
         p0 = 1; p1 = 0;
     }
+    double r0 = 0.0;
     if (a0 != 0.0) {
-        const double l = a2 / a0;
+        r0 = rcp_nr(a0);
+        const double l = a2 * r0;
         a2 = l;
         a3 -= l * a1;
     }
     if (a0 == 0.0 || a3 == 0.0) return false;
+    const double r3 = rcp_nr(a3);
 #pragma unroll
     for (int c = 0; c < 2; c++) {
         double b0 = (p0 == c) ? 1.0 : 0.0;
         double b1 = (p1 == c) ? 1.0 : 0.0;
         b1 = b1 - a2 * b0;
-        const double x1 = b1 / a3;
-        const double x0 = (b0 - a1 * x1) / a0;
+        const double x1 = b1 * r3;
+        const double x0 = (b0 - a1 * x1) * r0;
         Si[c] = x0;
         Si[2 + c] = x1;
     }
@@ -454,7 +471,14 @@ __device__ __forceinline__ void sincos_near(double ma, double ma0, double s0, do
                                             double& cs)
 {
     const double dl = ma - ma0;
-    if (fabs(dl) <= 0.015625) {
+    if (fabs(dl) <= 0.0009765625) {
+        // |δ| <= 2^-10: sin δ = δ − δ³/6 (next term ≤ 8e-18), 1 − cos δ = δ²/2 − δ⁴/24 (≤ 2e-21)
+        const double d2 = dl * dl;
+        const double sd = dl * (1.0 - d2 * (1.0 / 6.0));
+        const double cm = d2 * 0.5 * (1.0 - d2 * (1.0 / 12.0));
+        sn = s0 - (s0 * cm - c0 * sd);
+        cs = c0 - (c0 * cm + s0 * sd);
+    } else if (fabs(dl) <= 0.015625) {
         const double d2 = dl * dl;
         const double sd = dl * (1.0 - d2 * (1.0 / 6.0) * (1.0 - d2 * (1.0 / 20.0) * (1.0 - d2 * (1.0 / 42.0))));
         const double cm = d2 * 0.5 * (1.0 - d2 * (1.0 / 12.0) * (1.0 - d2 * (1.0 / 30.0) * (1.0 - d2 * (1.0 / 56.0))));
@@ -1377,7 +1401,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     __shared__ unsigned long long sh_stamp[EKF_NSTAMP];
     // EKF_ARITH_BF16X6 (fp32 storage): the owned rows' V values of this scan's matches (k-major
     // per row), split into bf16 planes and stored once at the end
-    __shared__ __attribute__((aligned(16))) float sh_vpl[std::is_same<T, float>::value ? SCAN_THREADS * 32 : 4];
+    // fp32 operand storage (fp32 and fp16 P): the split-bf16 planes, the MFMA replay
+    constexpr bool kPlanes = sizeof(typename Stor<T>::C) == 4;
+    __shared__ __attribute__((aligned(16))) float sh_vpl[kPlanes ? SCAN_THREADS * 32 : 4];
     unsigned long long* dbg = (p.dbg && lead) ? p.dbg + (size_t)e * EKF_NSTAMP : nullptr;
     if (p.dbg && tid < EKF_NSTAMP) sh_stamp[tid] = 0;
     unsigned long long t_last = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -1575,7 +1601,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         __syncthreads();   // sh_ctl
         staged = true;
         for (int q = 0; q < p.npend; q++) staged &= sh_ctl[q].y <= 8;
-        mf = staged && p.mfrep && std::is_same<T, float>::value;
+        mf = staged && p.mfrep && kPlanes;
         for (int q = 0; q < p.npend; q++) {
             mf &= !sh_ctl[q].x && sh_ctl[q].z == 0;
             if (sh_ctl[q].y > 0) amask |= 1u << q;
@@ -1623,7 +1649,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = to_domain<T>(-o1, pv.ex);
                 Vop[op_index_f32(lr, 2 * t, d.kmax)] = (C)v0;
                 Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (C)v1;
-                if constexpr (std::is_same<T, float>::value)
+                if constexpr (kPlanes)
                     if (Bop)
                         *reinterpret_cast<f32x2v*>(sh_vpl + tid * 32 + pp * 16 + 2 * t) = f32x2v{(float)v0, (float)v1};
             } else {
@@ -1858,7 +1884,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             }
             __syncthreads();
             if (mf && tid >= SCAN_THREADS) {
-              if constexpr (std::is_same<T, float>::value) {
+              if constexpr (kPlanes) {
                 // the winners' mutual blocks: X minus the pending steps' ΔX of the 16 winner rows
                 // against themselves (one M-block of plane_replay), by the replay wave itself
                 auto wrow = [&](int c) {
@@ -1943,29 +1969,33 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         bad |= c.pass ? 0 : 1;
                         // GSL_EDOM of the winner (the reference evaluated it: Robot.cpp:454)
                         if (c.singular) atomicOr(&sh_rwst, (int)EKF_ST_SINGULAR);
-                        build_package(c, R33l, w0, w1, w2, pk);   // its V rows stay in sh_wh[t]
+                        // the package in registers, the robot block after the line from it (for
+                        // every lane and every landmark wave), then all of it to LDS
+                        double pkl[PKW];
+                        build_package(c, R33l, w0, w1, w2, pkl);   // its V rows stay in sh_wh[t]
+                        robot_update(R33l, xpl, pkl);
+#pragma unroll
+                        for (int a = 0; a < 9; a++) pkl[PK_R33 + a] = R33l[a];
+                        pkl[PK_XP + 0] = xpl[0]; pkl[PK_XP + 1] = xpl[1]; pkl[PK_XP + 2] = xpl[2];
                         if (sym) {   // once per line for every landmark's operand stores
                             float F[3];
-                            sym_factor(pk, F);
-                            pk[PK_F + 0] = F[0]; pk[PK_F + 1] = F[1]; pk[PK_F + 2] = F[2];
+                            sym_factor(pkl, F);
+                            pkl[PK_F + 0] = F[0]; pkl[PK_F + 1] = F[1]; pkl[PK_F + 2] = F[2];
                         }
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    // the robot block after the line, once for every landmark wave
-                    robot_update(R33l, xpl, pk);
-                    if (u == 0) {
 #pragma unroll
-                        for (int a = 0; a < 9; a++) pk[PK_R33 + a] = R33l[a];
-                        pk[PK_XP + 0] = xpl[0]; pk[PK_XP + 1] = xpl[1]; pk[PK_XP + 2] = xpl[2];
+                        for (int a = MB_S; a < PKW; a++) pk[a] = pkl[a];
                     }
                     // the package is complete: to the other lanes of this wave, and to the
-                    // landmark waves (release of all lanes' LDS writes, then the line counter)
+                    // landmark waves (release of lane t's LDS writes, then the line counter)
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                     __builtin_amdgcn_wave_barrier();
                     if (u == 0) __hip_atomic_store(&sh_ready, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if (u != t) {   // (lane t has them)
+#pragma unroll
+                        for (int a = 0; a < 9; a++) R33l[a] = pk[PK_R33 + a];
+                        xpl[0] = pk[PK_XP + 0]; xpl[1] = pk[PK_XP + 1]; xpl[2] = pk[PK_XP + 2];
+                    }
                     if (lst) { const unsigned long long t2 = __builtin_amdgcn_s_memrealtime(); sh_stamp[3] += t2 - tl; tl = t2; }
                     if (act && u > t) {
                         const double* r = sh_wd + u * SPEC_WD + 14 + 4 * t;
@@ -1988,7 +2018,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 // ---- (e) owned blocks of the guessed columns (Robot.cpp:560 operands), while the
                 // last wave runs (f) ----
                 if (mf) {
-                  if constexpr (std::is_same<T, float>::value) {
+                  if constexpr (kPlanes) {
                     // the owned rows' blocks of the guessed columns: X minus the pending steps' ΔX
                     // of the wave's 128 rows (8 M-blocks) against the 16 winner rows, transposed
                     // through this wave's part of sh_vpl (8 KB; the planes are staged there later)
@@ -2423,7 +2453,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         __shared__ int sh_m;
         if (tid == 0) sh_m = m;   // the matches, as a landmark wave counted them
         __syncthreads();
-        if constexpr (std::is_same<T, float>::value)
+        if constexpr (kPlanes)
             if (Bop && own) {
                 // the owned rows' planes: per row and k parity h (k = 2s + h, s = 0..7) one
                 // 16-byte lane row per part; k past the matches +0
@@ -3059,6 +3089,107 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
     }
 }
 
+// One WT_R × WT_C wave-tile (instance e, table entry w) through a group of NS steps in order, operands
+// loaded in place: per step its reset, or the rank-2m downdate (v_mfma_f32_32x32x2_f32, the exact
+// k-ordered chain, fp16 rounding per step) and then its augmented rows (one tile at a time through
+// acc[0], rotating the accumulators). Tiles outside the triangle are stored to the sink tile. The
+// general path of the wave flushes (groups with a reset or new rows in some instance of the wave).
+template <typename TS, int NS>
+__device__ __forceinline__ void wt_general(const DowndateParams& p, int e, const WtEntry& w, int lane)
+{
+    const Dims d = p.d;
+    const int kh = d.kmax / 2;
+    const size_t opstride = (size_t)d.nb * 64 * kh;
+    const size_t inst_elems = (size_t)d.ntiles * TILE_ELEMS;
+    const TS* Pin = reinterpret_cast<const TS*>(p.Pin);
+    TS* Pout = reinterpret_cast<TS*>(p.Pout);
+    TS* sink = reinterpret_cast<TS*>(p.sink);
+    const int lofs = lane * kh;
+    auto op_row = [&](int side, int k) { return (w.rows[side] >> (16 * k)) & 0xffff; };
+    f32x16 acc[WT_N];
+#pragma unroll
+    for (int i = 0; i < WT_N; i++) {
+        const TS* tl = Pin + (size_t)e * inst_elems + (size_t)w.tile[i] * TILE_ELEMS;
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) {
+            const f32x4 v = tile_ld(tl, lane, qq);
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = v[j];
+        }
+    }
+    const int wr = w.rc & 0xffff, wc = w.rc >> 16;
+    for (int q = 0; q < NS; q++) {
+        const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
+        const int reset = sload(r + RES_RESET);
+        const int kc = reset ? 0 : sload(r + RES_KSTEPS);
+        if (kc > 0) {
+            const float* U = reinterpret_cast<const float*>(p.steps[q].Uop) + e * opstride + lofs;
+            const float* V = reinterpret_cast<const float*>(p.steps[q].Vop) + e * opstride + lofs;
+            f32x4 a[WT_R][2], b[WT_C][2];
+#pragma unroll
+            for (int rr = 0; rr < WT_R; rr++) {
+                const float* src = U + (size_t)op_row(0, rr) * 64 * kh;
+                a[rr][0] = *reinterpret_cast<const f32x4*>(src);
+                a[rr][1] = *reinterpret_cast<const f32x4*>(src + 4);
+            }
+#pragma unroll
+            for (int c = 0; c < WT_C; c++) {
+                const float* src = V + (size_t)op_row(1, c) * 64 * kh;
+                b[c][0] = *reinterpret_cast<const f32x4*>(src);
+                b[c][1] = *reinterpret_cast<const f32x4*>(src + 4);
+            }
+#pragma unroll
+            for (int s = 0; s < SBK; s++)
+                if (s < kc) {
+#pragma unroll
+                    for (int rr = 0; rr < WT_R; rr++)
+#pragma unroll
+                        for (int c = 0; c < WT_C; c++)
+                            acc[rr * WT_C + c] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                                a[rr][s >> 2][s & 3], b[c][s >> 2][s & 3], acc[rr * WT_C + c], 0, 0, 0);
+                }
+#pragma unroll
+            for (int i = 0; i < WT_N; i++) round_acc<TS>(acc[i]);
+        }
+        if (reset) {
+#pragma unroll
+            for (int i = 0; i < WT_N; i++)
+#pragma unroll
+                for (int k = 0; k < 16; k++) acc[i][k] = 0.f;
+            continue;
+        }
+        const int nadd = sload(r + RES_NADD), s0 = sload(r + RES_SAVED_IN);
+        if (nadd <= 0 || (wc + 1) * WT_C * 16 <= s0 || wc * WT_C * 16 >= s0 + nadd) continue;
+        const double* prw0 = p.steps[q].patch + (size_t)e * d.max_lines * 2 * d.M;
+        const double* pdg = p.steps[q].patch_diag + (size_t)e * d.max_lines * 4;
+        const int ex = storage_exp<TS>(p.pexp, e);
+#pragma nounroll
+        for (int i = 0; i < WT_N; i++) {
+            const int bi = wr * WT_R + i / WT_C, bj = wc * WT_C + i % WT_C;
+            if (((w.valid >> i) & 1) && bj * 16 + 15 >= s0 && bj * 16 < s0 + nadd) {
+                const int col = bj * 32 + (lane & 31);
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
+                    const int hi = max(row >> 1, col >> 1);
+                    if (hi >= s0 && hi < s0 + nadd)
+                        acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s0, row, col), ex));
+                }
+            }
+            const f32x16 t0 = acc[0];
+#pragma unroll
+            for (int j = 0; j < WT_N - 1; j++) acc[j] = acc[j + 1];
+            acc[WT_N - 1] = t0;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < WT_N; i++) {
+        TS* tl = ((w.valid >> i) & 1) ? Pout + (size_t)e * inst_elems + (size_t)w.tile[i] * TILE_ELEMS : sink;
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) tile_st(tl, lane, qq, acc[i]);
+    }
+}
+
 // f32/f16 flush, barrier-free per-wave form for groups of an even number of steps NS (2..8,
 // kmax <= 16). One wave per SIMD, each working alone (no LDS, no barriers) through a sequence of
 // wave-tiles of WT_R × WT_C tiles (four 32×32 accumulators). Software pipeline, one wave-tile
@@ -3086,7 +3217,6 @@ template <typename TS, int NS, bool BF = false>
 __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_wave_kernel(DowndateParams p)
 {
     static_assert(NS >= 2 && NS % 2 == 0 && NS <= PMAX, "even step count");
-    static_assert(!BF || sizeof(TS) == 4, "split-bf16 flush: fp32 storage");
     static_assert(BF || NS <= 8, "fp32 wave flush: at most 8 steps (operands of every step in registers)");
     constexpr bool HALF = sizeof(TS) == 2;
     constexpr bool AM = HALF;   // fp16 storage: pair-major step order (below)
@@ -3195,26 +3325,44 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
                 return reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(p.bbase) +
                                                        (size_t)sl * (size_t)p.bslot_bytes);
             };
-            f32x4 pref[WT_N][4];
+            // raw tile words in flight (fp16 storage: converted when the wave-tile starts)
+            using Raw = typename std::conditional<HALF, f16x4, f32x4>::type;
+            Raw pref[WT_N][4];
             f32x16 acc[WT_N];
             bf16x8 R[RD][WT_R + WT_C][3];
             // step q of wave-tile t into ring set r: A row blocks, then B row blocks, three planes
             auto load_ops = [&](int r, const Item& t, int q) __attribute__((always_inline)) {
                 const bf16x8* b = pl_base(q) + t.e * pstride + lane;
+#ifdef EKF_XP_BF_HALF_OPS   // timing experiment (results invalid): A planes only, reused as B
+#pragma unroll
+                for (int i = 0; i < WT_R; i++) {
+                    const bf16x8* rb = b + (size_t)op_row(t, 0, i) * 3 * 64;
+#pragma unroll
+                    for (int pl = 0; pl < 3; pl++) R[r][i][pl] = R[r][WT_R + i][pl] = rb[pl * 64];
+                }
+#else
 #pragma unroll
                 for (int i = 0; i < WT_R + WT_C; i++) {
                     const bf16x8* rb = b + (size_t)(i < WT_R ? op_row(t, 0, i) : op_row(t, 1, i - WT_R)) * 3 * 64;
 #pragma unroll
                     for (int pl = 0; pl < 3; pl++) R[r][i][pl] = rb[pl * 64];
                 }
+#endif
             };
             auto load_tiles = [&](const Item& t) __attribute__((always_inline)) {
 #pragma unroll
                 for (int i = 0; i < WT_N; i++) {
-                    const f32x4* tl = reinterpret_cast<const f32x4*>(Pin + tile_ptr(t, i));
+                    const Raw* tl = reinterpret_cast<const Raw*>(Pin + tile_ptr(t, i));
 #pragma unroll
                     for (int qq = 0; qq < 4; qq++) pref[i][qq] = __builtin_nontemporal_load(tl + lane + qq * 64);
                 }
+            };
+            // the accumulators hold −P: fp32 storage −X; fp16 storage −2^−x·X (X = fp16(2^x·P), the
+            // instance's exponent; power-of-two scalings, exact), so that both operands are the
+            // unscaled V planes; the store scales back and rounds to fp16 once per group
+            auto in_scale = [&](const Item& t) __attribute__((always_inline)) {
+                if constexpr (HALF) return -ldexpf(1.0f, -sload(p.pexp + t.e));
+                else return -1.0f;
             };
             Item cur, nxt, nxt2;
             first_item(cur);
@@ -3239,12 +3387,13 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
                 const bool more = g + K < g_end;
                 next_item(nxt, nxt2);
                 const Item ldi = more ? nxt : cur;   // the last wave-tile re-reads its own rows
+                const float isc = in_scale(cur);
 #pragma unroll
                 for (int i = 0; i < WT_N; i++)
 #pragma unroll
                     for (int qq = 0; qq < 4; qq++)
 #pragma unroll
-                        for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = -pref[i][qq][j];
+                        for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = (float)pref[i][qq][j] * isc;
 #ifndef EKF_XP_BF_NO_TILES   // timing experiment (results invalid): no tile stream after the first
                 if (more) load_tiles(nxt);
 #endif
@@ -3284,10 +3433,11 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
 #ifdef EKF_XP_FLUSH_STAMPS
                 const unsigned long long xt2 = __builtin_amdgcn_s_memtime();
 #endif
+                const float osc = 1.0f / isc;   // (−1, or −2^x: exact)
 #pragma unroll
                 for (int i = 0; i < WT_N; i++)
 #pragma unroll
-                    for (int k = 0; k < 16; k++) acc[i][k] = -acc[i][k];
+                    for (int k = 0; k < 16; k++) acc[i][k] = acc[i][k] * osc;
 #ifdef EKF_XP_BF_NO_TILES
                 if (acc[0][0] == 1234.5f && acc[3][15] == -1234.5f)   // (never true: keeps the MFMAs live)
 #endif
@@ -3506,8 +3656,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
     }
 
     // general loop: per wave-tile, every step in order with its operands loaded in place, then
-    // the step's reset or rows (one tile at a time through acc[0], rotating the accumulators)
-    f32x16 acc[WT_N];
+    // the step's reset or rows (wt_general)
     Item t;
     first_item(t);
     for (int g = g0; g < g_end; g += K) {
@@ -3516,83 +3665,206 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
             next_item(t, n);
             t = n;
         }
+        wt_general<TS, NS>(p, t.e, t.w, lane);
+    }
+}
+
+// Split-bf16 flush on wave-tiles of 2 × 4 tiles (EKF_ARITH_BF16X6; the default form for its groups).
+// The 2 × 2 form of flush_f32_wave_kernel<TS, NS, true> streams 12 KB of operand planes per step
+// through a CU's vector memory path per wave (3 KB per tile and step: 62 B per clock for the four
+// waves at the MFMA rate) beside its tile stream, and every operand wait of a wave also waits for
+// its older tile loads (one in-order vmcnt). Measured at N = 4096, E = 8, T = 12 (timing builds):
+// MFMA alone 0.36 ms, + operand planes 0.46, + tiles 0.41, both 0.63. A 2 × 4 wave-tile needs 18 KB
+// per step for twice the MFMAs (2.25 KB per tile and step) and amortises each wave-tile's
+// boundary and tile-stream waits over twice the MFMA time. Registers: 8 accumulators (128), the
+// next wave-tile's tiles (128 fp32 / 64 fp16), a ring of 2 operand step-sets (144). Otherwise the
+// 2 × 2 form's scheme: one 4-wave workgroup per CU, barrier-free waves, XCD-ranged K-strided walk
+// of a panel-ordered table (p.wt24: 8 wave-tile columns per panel), tile prefetch one wave-tile
+// ahead, operand ring one step ahead across wave-tile boundaries, −P in the accumulators (fp16:
+// scaled out of the storage exponent), invalid slots stored to the sink. Groups in which some
+// instance of the wave resets or adds rows run wt_general on the two 2 × 2 halves.
+constexpr int W4_R = 2, W4_C = 4, W4_N = W4_R * W4_C;
+template <typename TS, int NS>
+__global__ __launch_bounds__(DD_THREADS, 1) void flush_bf24_kernel(DowndateParams p)
+{
+    static_assert(NS >= 2 && NS % 2 == 0 && NS <= PMAX, "even step count");
+    constexpr bool HALF = sizeof(TS) == 2;
+    constexpr int RD = 2;   // operand ring depth (divides NS)
+    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    using Raw = typename std::conditional<HALF, f16x4, f32x4>::type;
+    const Dims d = p.d;
+    const int nwt = p.nwt24;
+    const int total = p.E * nwt;
+    const int per = (total + 7) / 8;
+    const int xcd = blockIdx.x & 7;
+    const int K = (int)(gridDim.x >> 3) * (DD_THREADS / 64);     // waves per XCD
+    const int g_end = min(total, (xcd + 1) * per);
+    const int g0 = __builtin_amdgcn_readfirstlane(
+        xcd * per + (int)(blockIdx.x >> 3) * (DD_THREADS / 64) + (int)(threadIdx.x >> 6));
+    if (g0 >= g_end) return;
+    const int lane = threadIdx.x & 63;
+    const int nb = d.nb;
+    const size_t inst_elems = (size_t)d.ntiles * TILE_ELEMS;
+    const TS* Pin = reinterpret_cast<const TS*>(p.Pin);
+    TS* Pout = reinterpret_cast<TS*>(p.Pout);
+    TS* sink = reinterpret_cast<TS*>(p.sink);
+
+    bool fast = true;
+    {
+        const int e_lo = g0 / nwt, e_hi = (g_end - 1) / nwt;
+        for (int e = e_lo; e <= e_hi; e++)
 #pragma unroll
-        for (int i = 0; i < WT_N; i++) {
-            const TS* tl = Pin + tile_ptr(t, i);
+            for (int q = 0; q < NS; q++) {
+                const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
+                fast = fast && !sload(r + RES_RESET) && sload(r + RES_NADD) == 0 && !sload(r + RES_ROLLBACK);
+            }
+    }
+    struct Item {
+        int e, li, wr, wc;
+    };
+    auto load_item = [&](int e, int li, Item& t) __attribute__((always_inline)) {
+        t.e = e;
+        t.li = li;
+        const int v = sload(p.wt24 + (e < p.E ? li : 0));
+        t.wr = v & 0xffff;
+        t.wc = v >> 16;
+    };
+    auto next_item = [&](const Item& c, Item& t) __attribute__((always_inline)) {
+        int li = c.li + K, e = c.e;
+        while (li >= nwt) {
+            li -= nwt;
+            e++;
+        }
+        load_item(e, li, t);
+    };
+    // slot (r, c): tile (2wr + r, 4wc + c) if stored, else a stored tile of the wave-tile
+    auto slot_tile = [&](const Item& t, int i, bool& valid) __attribute__((always_inline)) {
+        const int bi = W4_R * t.wr + i / W4_C, bj = W4_C * t.wc + i % W4_C;
+        valid = bi < nb && bj < nb && bi <= bj;
+        return valid ? tile_index(bi, bj, nb) : tile_index(W4_R * t.wr, min(W4_C * t.wc + W4_C - 1, nb - 1), nb);
+    };
+    auto op_rowA = [&](const Item& t, int r) __attribute__((always_inline)) { return min(W4_R * t.wr + r, nb - 1); };
+    auto op_rowB = [&](const Item& t, int c) __attribute__((always_inline)) { return min(W4_C * t.wc + c, nb - 1); };
+
+    if (!fast) {
+        Item t;
+        load_item(g0 / nwt, g0 - (g0 / nwt) * nwt, t);
+        for (int g = g0; g < g_end; g += K) {
+            if (g != g0) {
+                Item n;
+                next_item(t, n);
+                t = n;
+            }
+#pragma unroll 1
+            for (int h = 0; h < 2; h++) {
+                WtEntry w;
+                w.valid = 0;
 #pragma unroll
-            for (int qq = 0; qq < 4; qq++) {
-                const f32x4 v = tile_ld(tl, lane, qq);
-#pragma unroll
-                for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = v[j];
+                for (int i = 0; i < WT_N; i++) {
+                    bool v;
+                    w.tile[i] = (int)slot_tile(t, (i / WT_C) * W4_C + 2 * h + i % WT_C, v);
+                    w.valid |= (v ? 1 : 0) << i;
+                }
+                w.rows[0] = op_rowA(t, 0) | (op_rowA(t, 1) << 16);
+                w.rows[1] = op_rowB(t, 2 * h) | (op_rowB(t, 2 * h + 1) << 16);
+                w.rc = t.wr | ((2 * t.wc + h) << 16);
+                wt_general<TS, NS>(p, t.e, w, lane);
             }
         }
-        const int wr = t.w.rc & 0xffff, wc = t.w.rc >> 16;
+        return;
+    }
+
+    const size_t pstride = (size_t)nb * 3 * 64;   // bf16x8 per instance
+    auto pl_base = [&](int q) __attribute__((always_inline)) {
+        int sl = p.slot0 + q;
+        if (sl >= p.nslots) sl -= p.nslots;
+        return reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(p.bbase) + (size_t)sl * (size_t)p.bslot_bytes);
+    };
+    Raw pref[W4_N][4];
+    f32x16 acc[W4_N];
+    bf16x8 R[RD][W4_R + W4_C][3];
+    auto load_ops = [&](int r, const Item& t, int q) __attribute__((always_inline)) {
+        const bf16x8* b = pl_base(q) + t.e * pstride + lane;
+#pragma unroll
+        for (int i = 0; i < W4_R + W4_C; i++) {
+            const bf16x8* rb = b + (size_t)(i < W4_R ? op_rowA(t, i) : op_rowB(t, i - W4_R)) * 3 * 64;
+#pragma unroll
+            for (int pl = 0; pl < 3; pl++) R[r][i][pl] = rb[pl * 64];
+        }
+    };
+    auto load_tiles = [&](const Item& t) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < W4_N; i++) {
+            bool v;
+            const Raw* tl = reinterpret_cast<const Raw*>(Pin + (size_t)t.e * inst_elems + (size_t)slot_tile(t, i, v) * TILE_ELEMS);
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) pref[i][qq] = __builtin_nontemporal_load(tl + lane + qq * 64);
+        }
+    };
+    auto in_scale = [&](const Item& t) __attribute__((always_inline)) {
+        if constexpr (HALF) return -ldexpf(1.0f, -sload(p.pexp + t.e));
+        else return -1.0f;
+    };
+    Item cur, nxt, nxt2;
+    load_item(g0 / nwt, g0 - (g0 / nwt) * nwt, cur);
+    next_item(cur, nxt);
+    load_tiles(cur);
+#pragma unroll
+    for (int q = 0; q < RD - 1; q++) load_ops(q, cur, q);
+    int g = g0;
+    while (true) {
+        const bool more = g + K < g_end;
+        next_item(nxt, nxt2);
+        const Item ldi = more ? nxt : cur;   // the last wave-tile re-reads its own rows
+        const float isc = in_scale(cur);
+#pragma unroll
+        for (int i = 0; i < W4_N; i++)
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = (float)pref[i][qq][j] * isc;
+        if (more) load_tiles(nxt);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < NS; q++) {
-            const int* r = p.steps[q].res + (size_t)t.e * RES_STRIDE;
-            const int reset = sload(r + RES_RESET);
-            const int kc = reset ? 0 : sload(r + RES_KSTEPS);
-            if (kc > 0) {
-                const float* U = reinterpret_cast<const float*>(p.steps[q].Uop) + t.e * opstride + lofs;
-                const float* V = reinterpret_cast<const float*>(p.steps[q].Vop) + t.e * opstride + lofs;
-                f32x4 a[WT_R][2], b[WT_C][2];
+            const int ql = q + RD - 1;
+            if (ql < NS) load_ops(ql % RD, cur, ql);
+            else load_ops(ql % RD, ldi, ql - NS);
+            const int r = q % RD;
+            // part products smallest first: (mid, mid), (hi, lo), (lo, hi), (hi, mid), (mid, hi), (hi, hi)
 #pragma unroll
-                for (int rr = 0; rr < WT_R; rr++) {
-                    const float* src = U + (size_t)op_row(t, 0, rr) * 64 * kh;
-                    a[rr][0] = *reinterpret_cast<const f32x4*>(src);
-                    a[rr][1] = *reinterpret_cast<const f32x4*>(src + 4);
-                }
+            for (int pp = 0; pp < 6; pp++) {
+                const int pa = (0x102010 >> (4 * (5 - pp))) & 0xf;
+                const int pb = (0x120100 >> (4 * (5 - pp))) & 0xf;
 #pragma unroll
-                for (int c = 0; c < WT_C; c++) {
-                    const float* src = V + (size_t)op_row(t, 1, c) * 64 * kh;
-                    b[c][0] = *reinterpret_cast<const f32x4*>(src);
-                    b[c][1] = *reinterpret_cast<const f32x4*>(src + 4);
-                }
+                for (int rr = 0; rr < W4_R; rr++)
 #pragma unroll
-                for (int s = 0; s < SBK; s++)
-                    if (s < kc) {
-#pragma unroll
-                        for (int rr = 0; rr < WT_R; rr++)
-#pragma unroll
-                            for (int c = 0; c < WT_C; c++)
-                                acc[rr * WT_C + c] = __builtin_amdgcn_mfma_f32_32x32x2f32(
-                                    a[rr][s >> 2][s & 3], b[c][s >> 2][s & 3], acc[rr * WT_C + c], 0, 0, 0);
-                    }
-#pragma unroll
-                for (int i = 0; i < WT_N; i++) round_acc<TS>(acc[i]);
+                    for (int c = 0; c < W4_C; c++)
+                        acc[rr * W4_C + c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                            R[r][rr][pa], R[r][W4_R + c][pb], acc[rr * W4_C + c], 0, 0, 0);
             }
-            if (reset) {
 #pragma unroll
-                for (int i = 0; i < WT_N; i++)
-#pragma unroll
-                    for (int k = 0; k < 16; k++) acc[i][k] = 0.f;
-                continue;
+            for (int i = 0; i < 6; i++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);   // VMEM read
             }
-            const int nadd = sload(r + RES_NADD), s0 = sload(r + RES_SAVED_IN);
-            if (nadd <= 0 || (wc + 1) * WT_C * 16 <= s0 || wc * WT_C * 16 >= s0 + nadd) continue;
-            const double* prw0 = p.steps[q].patch + (size_t)t.e * d.max_lines * 2 * d.M;
-            const double* pdg = p.steps[q].patch_diag + (size_t)t.e * d.max_lines * 4;
-            const int ex = storage_exp<TS>(p.pexp, t.e);
-#pragma nounroll
-            for (int i = 0; i < WT_N; i++) {
-                const int bi = wr * WT_R + i / WT_C, bj = wc * WT_C + i % WT_C;
-                if (((t.w.valid >> i) & 1) && bj * 16 + 15 >= s0 && bj * 16 < s0 + nadd) {
-                    const int col = bj * 32 + (lane & 31);
-#pragma unroll
-                    for (int k = 0; k < 16; k++) {
-                        const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
-                        const int hi = max(row >> 1, col >> 1);
-                        if (hi >= s0 && hi < s0 + nadd)
-                            acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s0, row, col), ex));
-                    }
-                }
-                const f32x16 t0 = acc[0];
-#pragma unroll
-                for (int j = 0; j < WT_N - 1; j++) acc[j] = acc[j + 1];
-                acc[WT_N - 1] = t0;
-            }
+            __builtin_amdgcn_sched_barrier(0);
         }
-        store_tiles(t, acc);
+        const float osc = 1.0f / isc;   // (−1, or −2^x: exact)
+#pragma unroll
+        for (int i = 0; i < W4_N; i++) {
+            bool v;
+            const size_t ti = slot_tile(cur, i, v);
+            TS* tl = v ? Pout + (size_t)cur.e * inst_elems + ti * TILE_ELEMS : sink;
+#pragma unroll
+            for (int k = 0; k < 16; k++) acc[i][k] = acc[i][k] * osc;
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) tile_st(tl, lane, qq, acc[i]);
+        }
+        if (!more) break;
+        g += K;
+        cur = nxt;
+        nxt = nxt2;
     }
 }
 
@@ -4076,12 +4348,37 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     const bool wave_ok = wave_shape && (p.nsteps >= 6 || p.variant == 8);
     const bool bf_shape = p.nsteps >= 2 && p.nsteps <= 16 && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
                           p.nwt > 0 && p.wt != nullptr;
-    if (p.bf && !half && bf_shape) {   // EKF_ARITH_BF16X6: split-bf16 wave flush, groups of 2-16 steps (even)
+    if (p.bf && bf_shape && p.variant != 4 && p.nwt24 > 0 && p.wt24 != nullptr) {
+        // EKF_ARITH_BF16X6: the 2 × 4 split-bf16 wave flush (EKF_FLUSH_VARIANT=4: the 2 × 2 form)
+        const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
+#define EKF_BF24_CASE(NSV)                                                                              \
+    case NSV:                                                                                           \
+        if (half) hipExtLaunchKernelGGL((flush_bf24_kernel<_Float16, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, \
+                                        ev_a, ev_b, 0, p);                                              \
+        else hipExtLaunchKernelGGL((flush_bf24_kernel<float, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, \
+                                   ev_b, 0, p);                                                         \
+        break;
+        switch (p.nsteps) {
+            EKF_BF24_CASE(2)
+            EKF_BF24_CASE(4)
+            EKF_BF24_CASE(6)
+            EKF_BF24_CASE(8)
+            EKF_BF24_CASE(10)
+            EKF_BF24_CASE(12)
+            EKF_BF24_CASE(14)
+            EKF_BF24_CASE(16)
+        }
+#undef EKF_BF24_CASE
+        return hipGetLastError();
+    }
+    if (p.bf && bf_shape) {   // EKF_ARITH_BF16X6: split-bf16 wave flush, groups of 2-16 steps (even)
         const unsigned wgrid = (unsigned)(8 * EKF_BF_WAVES * ((p.ncu + 7) / 8));   // EKF_BF_WAVES workgroups per CU
 #define EKF_BF_CASE(NSV)                                                                                \
     case NSV:                                                                                           \
-        hipExtLaunchKernelGGL((flush_f32_wave_kernel<float, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, st, \
-                              ev_a, ev_b, 0, p);                                                        \
+        if (half) hipExtLaunchKernelGGL((flush_f32_wave_kernel<_Float16, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, \
+                                        st, ev_a, ev_b, 0, p);                                          \
+        else hipExtLaunchKernelGGL((flush_f32_wave_kernel<float, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, st, \
+                                   ev_a, ev_b, 0, p);                                                   \
         break;
         switch (p.nsteps) {
             EKF_BF_CASE(2)

@@ -145,3 +145,17 @@ def test_bench_config_fp32_t12_bf16x6(ekf_mod, oracle_mod):
 def test_bench_config_fp32_t16_bf16x6(ekf_mod, oracle_mod):
     out = run_config(ekf_mod, oracle_mod, 1, 16, 20, arith=ekf_mod.ARITH_BF16X6)
     record("f32_T16_N4096_E8_bf16x6", out)
+
+
+def test_bench_config_fp16_t12_bf16x6(ekf_mod, oracle_mod):
+    """fp16 storage (BASELINE config 5) with the split-bf16 flush (flush_f32_wave_kernel<_Float16,
+    NS, true>: tiles scaled out of the storage exponent on load, rounded to fp16 once per group)
+    and the MFMA replay of the pending steps, T = 12 over 20 scans: P within the re-stated 1e-3 at
+    every group end, y within 1e-8, association identical."""
+    out = run_config(ekf_mod, oracle_mod, 2, 12, 20, arith=ekf_mod.ARITH_BF16X6)
+    record("f16_T12_N4096_E8_bf16x6", out)
+
+
+def test_bench_config_fp16_t8_bf16x6(ekf_mod, oracle_mod):
+    out = run_config(ekf_mod, oracle_mod, 2, 8, 20, arith=ekf_mod.ARITH_BF16X6)
+    record("f16_T8_N4096_E8_bf16x6", out)

@@ -27,6 +27,11 @@ def rel(a, b):
     return np.linalg.norm(a - b) / (nb if nb > 0 else 1.0)
 
 
+def is_bf_form(name):
+    """A split-bf16 flush form: the 2 × 4 kernel (default) or the 2 × 2 wave form's <.., true>."""
+    return name.startswith("flush_bf24_kernel") or name.endswith(", true>")
+
+
 def make_pair(ekf, oracle, N, prec, state=None, r_mode=0, max_lines=16, mode=None,
               reset_margin=10):
     ens = ekf.Ensemble(N, 1, prec, max_lines=max_lines, r_mode=r_mode, reset_margin=reset_margin)
@@ -546,8 +551,8 @@ def test_bf16x6_flush_close_to_exact(ekf_mod, oracle_mod, N, T, lines, extra_eve
     a = ekf_mod.Ensemble(N, E, 1, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
     b = ekf_mod.Ensemble(N, E, 1, max_lines=8)
     if T % 2 == 0:
-        assert a.flush_kernel_name(T).endswith(", true>"), a.flush_kernel_name(T)
-    assert not b.flush_kernel_name(8).endswith(", true>")
+        assert is_bf_form(a.flush_kernel_name(T)), a.flush_kernel_name(T)
+    assert not is_bf_form(b.flush_kernel_name(8))
     for ens in (a, b):
         for e in range(E):
             ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
@@ -589,6 +594,38 @@ def test_bf16x6_flush_close_to_exact(ekf_mod, oracle_mod, N, T, lines, extra_eve
     # kmax > 16 (max_lines 16) can never take the split-bf16 flush: rejected, no silent fallback
     with pytest.raises(ekf_mod.EkfError):
         ekf_mod.Ensemble(N, 1, 1, max_lines=16, flush_interval=8, arith=ekf_mod.ARITH_BF16X6)
+
+
+@pytest.mark.parametrize("N,T,extra_every", [(256, 8, 0), (256, 12, 5), (80, 16, 0), (1024, 6, 4)])
+def test_bf16x6_fp16_storage(ekf_mod, oracle_mod, N, T, extra_every):
+    """fp16 storage with EKF_ARITH_BF16X6 (split-bf16 flush on the fp16 tiles, rounded once per
+    group; MFMA replay of plain pending steps, the VALU replay after augmented rows) against the
+    fp64 restatement, never re-synchronised: association identical, P within the re-stated 1e-3
+    (fp16 rounding ≈3e-4 per materialisation), y within 1e-8, at the end and after every drain."""
+    E = 2
+    active = N - 12 - 2 * ((3 * T + 1) // extra_every) if extra_every else N - 10
+    w = G.make_world(N, active=active)
+    st = G.initial_state(w)
+    a = ekf_mod.Ensemble(N, E, 2, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
+    assert a.flush_kernel_name(T if T % 2 == 0 else T - 1).startswith("flush_bf24_kernel<_Float16")
+    for e in range(E):
+        a.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+    ref = oracle_mod.OracleRobot(N)
+    ref.set_state(*a.download_state(0))
+    rng = np.random.default_rng(11)
+    for step in range(1, 3 * T + 2):
+        enc, ln, nl = G.make_scan(w, step, instances=E, lines=6 if extra_every else 8)
+        if extra_every and step % extra_every == 0:
+            ex = G.random_lines(rng, 2)[None].repeat(E, axis=0)
+            ln = np.concatenate([ln, ex], axis=1)
+            nl = np.full(E, ln.shape[1], dtype=np.int32)
+        r = a.localize(enc, ln, nl)
+        m = ref.localize(ln[0], enc[0])
+        assert r[0]["match"] == m and r[0]["status"] == 0, (step, r[0], m)
+    P, y, saved, pose = a.download_state(0)
+    assert saved == ref.savedLineCount
+    assert rel(P, ref.P_t0) <= 1e-3, rel(P, ref.P_t0)
+    assert rel(y, ref.y) <= 1e-8, rel(y, ref.y)
 
 
 @pytest.mark.parametrize("N,T,lines,extra_every", [(80, 4, 8, 0), (80, 4, 6, 3), (64, 3, 6, 2), (100, 2, 8, 0),
@@ -658,3 +695,39 @@ def test_singular_status_counts_only_evaluated_candidates(ekf_mod, oracle_mod, m
         assert ref.status & 1 == want
         assert res["status"] & ekf_mod.ST_SINGULAR_S == want, (target, res["status"])
         ens.close()
+
+
+@pytest.mark.parametrize("prec,N,T,extra_every", [(1, 1024, 12, 0), (1, 200, 8, 3), (2, 512, 10, 0), (1, 100, 16, 0)])
+def test_bf16_2x4_flush_equals_2x2(ekf_mod, monkeypatch, prec, N, T, extra_every):
+    """The split-bf16 flush on 2 × 4 wave-tiles (flush_bf24_kernel, default) and on 2 × 2 wave-tiles
+    (flush_f32_wave_kernel<.., true>, EKF_FLUSH_VARIANT=4) run the same MFMA sequence per element
+    (same part products in the same order, bf16 MFMA deterministic): bit-identical state, fast
+    groups and groups with augmented rows (general path on the two 2 × 2 halves) alike, fp32 and
+    fp16 storage, block sizes that are not multiples of the wave-tile."""
+    E = 3
+    active = N - 12 - 2 * ((3 * T + 1) // extra_every) if extra_every else N - 10
+    w = G.make_world(N, active=active)
+    st = G.initial_state(w)
+    a = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
+    monkeypatch.setenv("EKF_FLUSH_VARIANT", "4")
+    b = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
+    monkeypatch.delenv("EKF_FLUSH_VARIANT")
+    assert a.flush_kernel_name(T).startswith("flush_bf24_kernel"), a.flush_kernel_name(T)
+    assert b.flush_kernel_name(T).endswith(", true>"), b.flush_kernel_name(T)
+    for ens in (a, b):
+        for e in range(E):
+            ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+    rng = np.random.default_rng(3)
+    for step in range(1, 3 * T + 2):
+        enc, ln, nl = G.make_scan(w, step, instances=E, lines=6 if extra_every else 8)
+        if extra_every and step % extra_every == 0:
+            ex = G.random_lines(rng, 2)[None].repeat(E, axis=0)
+            ln = np.concatenate([ln, ex], axis=1)
+            nl = np.full(E, ln.shape[1], dtype=np.int32)
+        ra, rb = a.localize(enc, ln, nl), b.localize(enc, ln, nl)
+        for e in range(E):
+            assert ra[e]["match"] == rb[e]["match"], (step, e)
+    for e in range(E):
+        Pa, ya, sa, pa = a.download_state(e)
+        Pb, yb, sb, pb = b.download_state(e)
+        assert np.array_equal(Pa, Pb) and np.array_equal(ya, yb) and sa == sb, e
