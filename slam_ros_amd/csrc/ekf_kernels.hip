@@ -1589,6 +1589,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // symmetric downdate operands (sym_factor): fp32 operand storage, every mode but the
     // reference's asymmetric R
     const bool sym = p.r_mode != 1 && sizeof(typename Stor<T>::C) == 4;
+    // symmetric fp32 operands with kmax = 16: staged in LDS (sh_vpl) and written at the end
+    const bool stage_ops = sym && d.kmax == 16;
     // speculative path with fp32 operands and few pending steps: the pending steps' rows of the
     // guessed columns are staged in LDS and one pass per step updates all owned blocks
     bool staged = false;
@@ -1645,13 +1647,17 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     o0 = (double)(float)v0;
                     o1 = (double)(float)v1;
                 }
-                Uop[op_index_f32(lr, 2 * t, d.kmax)] = to_domain<T>(-o0, pv.ex);
-                Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = to_domain<T>(-o1, pv.ex);
-                Vop[op_index_f32(lr, 2 * t, d.kmax)] = (C)v0;
-                Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (C)v1;
-                if constexpr (kPlanes)
-                    if (Bop)
+                if (stage_ops) {
+                    // staged in LDS: the operand rows (U, V, the bf16 planes) go out once at the end
+                    // of the scan as whole 16-byte lane rows
+                    if constexpr (kPlanes)
                         *reinterpret_cast<f32x2v*>(sh_vpl + tid * 32 + pp * 16 + 2 * t) = f32x2v{(float)v0, (float)v1};
+                } else {
+                    Uop[op_index_f32(lr, 2 * t, d.kmax)] = to_domain<T>(-o0, pv.ex);
+                    Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = to_domain<T>(-o1, pv.ex);
+                    Vop[op_index_f32(lr, 2 * t, d.kmax)] = (C)v0;
+                    Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (C)v1;
+                }
             } else {
                 Uop[op_index_f64(lr, 2 * t, d.kmax)] = (C)(-uu[2 * pp]);
                 Uop[op_index_f64(lr, 2 * t + 1, d.kmax)] = (C)(-uu[2 * pp + 1]);
@@ -2421,7 +2427,36 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         *reinterpret_cast<double2*>(Rsw + 2 * n + b0) = rr2;
         *reinterpret_cast<double2*>(yw + b0) = yb;
         if (Ddw) Ddw[j] = reset || j >= s + nadd ? make_double4(0, 0, 0, 0) : make_double4(Dj[0], Dj[1], Dj[2], Dj[3]);
-        if (sizeof(C) == 4) {
+        if (stage_ops) {
+            if constexpr (kPlanes) {
+                // symmetric operands from their LDS stage: per owned row the even-k and the odd-k
+                // halves of V (two 32-byte lane rows each) and U = −2^x·V (exact); k past the
+                // matches +0 (V) and −0 (U), so that a flush running every k-step leaves every value
+                // as it is (flush_f32_wave_kernel; the other forms and the on-read replay stop at ks)
+                const float us = -ldexpf(1.0f, pv.ex);
+#pragma unroll
+                for (int pp = 0; pp < 2; pp++) {
+                    const f32x4v* src = reinterpret_cast<const f32x4v*>(sh_vpl + tid * 32 + pp * 16);
+                    float v[16];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const f32x4v x = src[i];
+#pragma unroll
+                        for (int u = 0; u < 4; u++) v[4 * i + u] = (4 * i + u) < 2 * m ? x[u] : 0.f;
+                    }
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const size_t o = op_index_f32(2 * j + pp, h, d.kmax);   // k = h: s = 0
+                        const f32x4v v0 = {v[h], v[2 + h], v[4 + h], v[6 + h]};
+                        const f32x4v v1 = {v[8 + h], v[10 + h], v[12 + h], v[14 + h]};
+                        *reinterpret_cast<f32x4v*>(Vop + o) = v0;
+                        *reinterpret_cast<f32x4v*>(Vop + o + 4) = v1;
+                        *reinterpret_cast<f32x4v*>(Uop + o) = v0 * us;
+                        *reinterpret_cast<f32x4v*>(Uop + o + 4) = v1 * us;
+                    }
+                }
+            }
+        } else if (sizeof(C) == 4) {
             // f32 operands: the k columns past the matches hold −0 (U) and +0 (V), so a flush
             // that runs every k-step unconditionally adds −0 there, which leaves every value as
             // it is (flush_f32_wave_kernel; the other forms and the on-read replay stop at ks)
