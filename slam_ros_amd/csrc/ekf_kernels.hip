@@ -3126,7 +3126,7 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
 
 // One WT_R × WT_C wave-tile (instance e, table entry w) through a group of NS steps in order, operands
 // loaded in place: per step its reset, or the rank-2m downdate (v_mfma_f32_32x32x2_f32, the exact
-// k-ordered chain, fp16 rounding per step) and then its augmented rows (one tile at a time through
+// k-ordered chain, fp16 rounding per step; once per group, at the store, under p.bf) and then its augmented rows (one tile at a time through
 // acc[0], rotating the accumulators). Tiles outside the triangle are stored to the sink tile. The
 // general path of the wave flushes (groups with a reset or new rows in some instance of the wave).
 template <typename TS, int NS>
@@ -3183,8 +3183,10 @@ __device__ __forceinline__ void wt_general(const DowndateParams& p, int e, const
                             acc[rr * WT_C + c] = __builtin_amdgcn_mfma_f32_32x32x2f32(
                                 a[rr][s >> 2][s & 3], b[c][s >> 2][s & 3], acc[rr * WT_C + c], 0, 0, 0);
                 }
+            if (!p.bf) {   // split-bf16 flushes round fp16 storage once per group (at the store)
 #pragma unroll
-            for (int i = 0; i < WT_N; i++) round_acc<TS>(acc[i]);
+                for (int i = 0; i < WT_N; i++) round_acc<TS>(acc[i]);
+            }
         }
         if (reset) {
 #pragma unroll
@@ -3207,8 +3209,10 @@ __device__ __forceinline__ void wt_general(const DowndateParams& p, int e, const
                 for (int k = 0; k < 16; k++) {
                     const int row = bi * 32 + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
                     const int hi = max(row >> 1, col >> 1);
-                    if (hi >= s0 && hi < s0 + nadd)
-                        acc[0][k] = round_step<TS>(to_domain<TS>(patched_value(prw0, pdg, d.M, s0, row, col), ex));
+                    if (hi >= s0 && hi < s0 + nadd) {
+                        const float v = to_domain<TS>(patched_value(prw0, pdg, d.M, s0, row, col), ex);
+                        acc[0][k] = p.bf ? v : round_step<TS>(v);
+                    }
                 }
             }
             const f32x16 t0 = acc[0];
