@@ -623,6 +623,7 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.live = c->cur;
     p.Dd = c->D;
     p.mfrep = c->mfrep;
+    p.bf = c->bf ? 1 : 0;
     p.Etot = c->cfg.instances;
     p.spin_log2 = c->spin_log2;
     p.test_drop = c->test_drop;

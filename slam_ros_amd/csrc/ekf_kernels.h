@@ -99,6 +99,8 @@ struct ScanParams {
                           // (copy live[e] read, the other written and committed with Rs / y)
     int mfrep;            // split-bf16 context: pending steps replayed on read by bf16 MFMA from
                           // the operand planes, diagonal blocks kept in Dd
+    int bf;               // split-bf16 context: fp16 storage rounded once per flush group, also in
+                          // the on-read replay
     double* pose;         // [E][3]
     double* xpre;         // [E][3]
     int* saved;           // [E]

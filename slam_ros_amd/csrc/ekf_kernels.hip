@@ -179,7 +179,16 @@ struct PllView {
     int npend;        // pending steps (oldest first)
     const Slot* pend;
     const int4* ctl;  // per pending step {reset, ks, nadd, s0} of instance e (LDS copy)
+    int rnd;          // fp16: round after every pending step, as the exact flush does (0 under
+                      // the split-bf16 flush, which rounds once per group)
 };
+
+// fp16 rounding of a replayed element (identity for fp32 / fp64 storage)
+template <typename T>
+__device__ __forceinline__ typename Stor<T>::C vround(const PllView<T>& v, typename Stor<T>::C x)
+{
+    return v.rnd ? round_step<T>(x) : x;
+}
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
@@ -259,11 +268,11 @@ __device__ __forceinline__ void patch_block(const PllView<T>& v, const Slot& sq,
             raw[2] = prw[i0 + 1]; raw[3] = prw[v.M + i0 + 1];
         }
         if (swap) {
-            acc[0] = round_step<T>(to_domain<T>(raw[0], v.ex)); acc[1] = round_step<T>(to_domain<T>(raw[2], v.ex));
-            acc[2] = round_step<T>(to_domain<T>(raw[1], v.ex)); acc[3] = round_step<T>(to_domain<T>(raw[3], v.ex));
+            acc[0] = vround<T>(v, to_domain<T>(raw[0], v.ex)); acc[1] = vround<T>(v, to_domain<T>(raw[2], v.ex));
+            acc[2] = vround<T>(v, to_domain<T>(raw[1], v.ex)); acc[3] = vround<T>(v, to_domain<T>(raw[3], v.ex));
         } else {
-            acc[0] = round_step<T>(to_domain<T>(raw[0], v.ex)); acc[1] = round_step<T>(to_domain<T>(raw[1], v.ex));
-            acc[2] = round_step<T>(to_domain<T>(raw[2], v.ex)); acc[3] = round_step<T>(to_domain<T>(raw[3], v.ex));
+            acc[0] = vround<T>(v, to_domain<T>(raw[0], v.ex)); acc[1] = vround<T>(v, to_domain<T>(raw[1], v.ex));
+            acc[2] = vround<T>(v, to_domain<T>(raw[2], v.ex)); acc[3] = vround<T>(v, to_domain<T>(raw[3], v.ex));
         }
     }
 }
@@ -363,7 +372,7 @@ __device__ __forceinline__ void pll_blocks(const PllView<T>& v, int i0, const in
 #pragma unroll
             for (int b = 0; b < B; b++)
 #pragma unroll
-                for (int k = 0; k < 4; k++) acc[b][k] = round_step<T>(acc[b][k]);
+                for (int k = 0; k < 4; k++) acc[b][k] = vround<T>(v, acc[b][k]);
         }
         if (cw.z > 0) {
 #pragma unroll
@@ -1161,8 +1170,8 @@ __device__ __forceinline__ void staged_blocks(const PllView<T>& v, int j, const 
                     r23 = __builtin_elementwise_fma(f32x2v{U[1][h][s4], U[1][h][s4]}, x01, r23);
                     r23 = __builtin_elementwise_fma(f32x2v{U[3][h][s4], U[3][h][s4]}, x23, r23);
                 }
-                r[b][0] = round_step<T>(r01[0]); r[b][1] = round_step<T>(r01[1]);
-                r[b][2] = round_step<T>(r23[0]); r[b][3] = round_step<T>(r23[1]);
+                r[b][0] = vround<T>(v, r01[0]); r[b][1] = vround<T>(v, r01[1]);
+                r[b][2] = vround<T>(v, r23[0]); r[b][3] = vround<T>(v, r23[1]);
                 // one block at a time (bounds the staged rows in registers)
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -1265,7 +1274,7 @@ __device__ __forceinline__ void staged_pair_block(const PllView<T>& v, int wa, i
                 }
             }
 #pragma unroll
-            for (int k = 0; k < 4; k++) acc[k] = round_step<T>(acc[k]);
+            for (int k = 0; k < 4; k++) acc[k] = vround<T>(v, acc[k]);
         }
         if (cw.z > 0) patch_block<T>(v, v.pend[q], cw, i0, jb, swap, acc);
     }
@@ -1480,6 +1489,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         PllView<T> v0;
         v0.X = reinterpret_cast<const T*>(p.Pread) + (size_t)e * d.ntiles * TILE_ELEMS;
         v0.nb = d.nb;
+        v0.rnd = 1;
         load_block<T>(v0, 2 * j, 2 * j, dj0);
         if (Ddr && p.npend > 0) djb = Ddr[j];
     }
@@ -1573,6 +1583,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     pv.npend = p.npend;
     pv.pend = p.pend;
     pv.ctl = sh_ctl;
+    pv.rnd = !p.bf;
     if (tid < p.npend) sh_ctl[tid] = ctl_pre;
 
     int L = L_pre;

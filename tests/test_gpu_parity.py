@@ -599,7 +599,8 @@ def test_bf16x6_flush_close_to_exact(ekf_mod, oracle_mod, N, T, lines, extra_eve
 @pytest.mark.parametrize("N,T,extra_every", [(256, 8, 0), (256, 12, 5), (80, 16, 0), (1024, 6, 4)])
 def test_bf16x6_fp16_storage(ekf_mod, oracle_mod, N, T, extra_every):
     """fp16 storage with EKF_ARITH_BF16X6 (split-bf16 flush on the fp16 tiles, rounded once per
-    group; MFMA replay of plain pending steps, the VALU replay after augmented rows) against the
+    group — the general path of groups with augmented rows and the on-read replay too; MFMA replay
+    of plain pending steps, the VALU replay after augmented rows) against the
     fp64 restatement, never re-synchronised: association identical, P within the re-stated 1e-3
     (fp16 rounding ≈3e-4 per materialisation), y within 1e-8, at the end and after every drain."""
     E = 2
