@@ -1,6 +1,7 @@
 """Association-kernel phase timers (EKF_SCAN_STAMPS=1; thread 0 of workgroup 0 of each instance,
 s_memrealtime, 100 MHz), µs per launch averaged over instances, at the bench's shapes
-(f32, E = 8, L = m = 8). usage: python scripts/assoc_probe.py [N:T ...]"""
+(f32, E = 8, L = m = 8; the bench's split-bf16 arithmetic, PROBE_ARITH=exact for the exact one).
+usage: python scripts/assoc_probe.py [N:T ...]"""
 import json
 import os
 import sys
@@ -12,14 +13,16 @@ from slam_ros_amd import ekf, scan_gen as G  # noqa: E402
 NAMES = {0: "predict+state", 1: "diag+ctl", 5: "guess", 2: "exchange1", 10: "resolve",
          12: "records+stage", 11: "staged_replay(w0)", 13: "replay_wave_total", 3: "rw_eval+publish",
          4: "rw_gain+robot", 16: "lw_gate", 17: "lw_wait_pkg", 18: "lw_gain+store", 19: "lw_robot",
-         14: "landmark_total", 6: "verdict", 7: "commit", 8: "total", 15: "fallbacks"}
+         14: "landmark_total", 6: "verdict", 27: "commit:augment", 28: "commit:state", 24: "commit:operands", 25: "commit:planes", 26: "commit:collect",
+         7: "commit:record", 8: "total", 15: "fallbacks"}
 E = 8
 cfgs = sys.argv[1:] or ["4096:8", "4096:1", "1024:8"]
 for c in cfgs:
     N, T = (int(x) for x in c.split(":"))
     w = G.make_world(N)
     st = G.initial_state(w)
-    ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8, flush_interval=T)
+    arith = ekf.ARITH_EXACT if os.environ.get("PROBE_ARITH") == "exact" else ekf.ARITH_BF16X6
+    ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8, flush_interval=T, arith=arith)
     for e in range(E):
         ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
     base = ens.scan_stamps()
@@ -36,5 +39,5 @@ for c in cfgs:
     out["past_quick_filter"] = stp[20]           # ... with a lane past the quick certified filter
     out["past_f32_filter"] = stp[21]             # ... past the fp32 certified filter
     out["past_f64_filter"] = stp[23]             # ... and past the fp64 one (exact evaluation)
-    print(json.dumps({"N": N, "T": T, "E": E, "launches_x_instances": stp[9], "us": out}), flush=True)
+    print(json.dumps({"N": N, "T": T, "E": E, "arith": "exact" if arith == ekf.ARITH_EXACT else "bf16x6", "launches_x_instances": stp[9], "us": out}), flush=True)
     ens.close()

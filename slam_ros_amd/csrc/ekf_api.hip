@@ -503,7 +503,7 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         c->ncu = prop.multiProcessorCount;
         // test hook: force one of the bit-identical flush forms (tests/test_gpu_parity.py)
         c->dd_variant = getenv("EKF_FLUSH_VARIANT") ? atoi(getenv("EKF_FLUSH_VARIANT")) : 0;
-        if (c->dd_variant != 2 && c->dd_variant != 4 && c->dd_variant != 8) c->dd_variant = 0;
+        if (c->dd_variant != 2 && c->dd_variant != 8 && c->dd_variant != 24) c->dd_variant = 0;
         // all G workgroups of an instance must be co-resident (they exchange per line). A plain
         // launch gets the same residency as a cooperative one for the same grid
         // (cdna_hip_programming.md §1; the cooperative form only adds a launch-time check of the
@@ -1278,7 +1278,7 @@ extern "C" const char* ekf_flush_kernel_name(const ekf_ctx* c, int nsteps)
         return "downdate_f64_kernel";
     }
     const bool half = c->cfg.precision == EKF_PREC_F16;
-    if (c->bf && nsteps >= 2 && nsteps <= 16 && nsteps % 2 == 0 && c->dd_variant != 4) {
+    if (c->bf && nsteps >= 2 && nsteps <= 16 && nsteps % 2 == 0 && c->dd_variant == 24) {
         static const char* b24[2][9] = {
             {"", "flush_bf24_kernel<float, 2>", "flush_bf24_kernel<float, 4>", "flush_bf24_kernel<float, 6>",
              "flush_bf24_kernel<float, 8>", "flush_bf24_kernel<float, 10>", "flush_bf24_kernel<float, 12>",

@@ -1297,47 +1297,109 @@ __device__ __forceinline__ void staged_pair_block(const PllView<T>& v, int wa, i
 // M-block mb in acc[mb][i]. Not the fp32 chain of the flush (the split-bf16 flush is not one
 // either): held to the same parity bar.
 typedef __bf16 bf16x8r __attribute__((ext_vector_type(8)));
+// One pair of pending steps' operands of plane_replay: NB A M-blocks and the B block, three parts each
+template <int NB>
+struct PlaneSet {
+    bf16x8r A[NB][3];
+    bf16x8r B[3];
+};
+
+// Lane geometry of plane_replay: rows of the lane's A M-blocks and B column; the step pairs are
+// the set bits of amask taken two at a time (the odd step out pairs with nothing).
+template <int NB>
+struct PlanePlan {
+    int kg, h, rb;
+    int ra[NB];
+    unsigned amask;   // (wave-uniform)
+    int np;
+};
+
 template <int NB, typename RA, typename RB>
-__device__ __forceinline__ void plane_replay(const Slot* pend, int e, size_t inst_bf, int M, unsigned amask,
-                                             int lane, RA row_a, RB row_b, f32x4v (&acc)[NB])
+__device__ __forceinline__ void plane_plan(PlanePlan<NB>& pl, unsigned amask, int lane, RA row_a, RB row_b)
+{
+    pl.kg = lane >> 4;
+    pl.h = pl.kg & 1;
+    const int r16 = lane & 15;
+    pl.rb = row_b(r16);
+#pragma unroll
+    for (int mb = 0; mb < NB; mb++) pl.ra[mb] = row_a(mb, r16);
+    pl.amask = __builtin_amdgcn_readfirstlane(amask);
+    pl.np = (__builtin_popcount(pl.amask) + 1) >> 1;
+}
+
+// Issue the loads of pair i (clamped to the last pair: a load past the end re-reads it, so that
+// every set is loaded unconditionally and the wait counts stay exact)
+template <int NB>
+__device__ __forceinline__ void plane_load(PlaneSet<NB>& S, const PlanePlan<NB>& pl, int i, const Slot* pend, int e,
+                                           size_t inst_bf, int M)
+{
+    typedef unsigned u32x4r __attribute__((ext_vector_type(4)));
+    const bf16x8r zero = __builtin_bit_cast(bf16x8r, u32x4r{0u, 0u, 0u, 0u});
+    const int ii = i < pl.np ? i : pl.np - 1;
+    unsigned m = pl.amask;   // pair ii: the steps of set bits 2ii and 2ii + 1
+    for (int k = 0; k < 2 * ii; k++) m &= m - 1;
+    const int qa = __builtin_ctz(m);
+    m &= m - 1;
+    const int qb = m ? __builtin_ctz(m) : -1;
+    const unsigned short* pa = reinterpret_cast<const unsigned short*>(pend[qa].Bop) + (size_t)e * inst_bf;
+    const unsigned short* pb = qb >= 0 ? reinterpret_cast<const unsigned short*>(pend[qb].Bop) + (size_t)e * inst_bf : pa;
+    const unsigned short* pq = (pl.kg >= 2) ? pb : pa;
+    const bool none = pl.kg >= 2 && qb < 0;
+#pragma unroll
+    for (int p3 = 0; p3 < 3; p3++)
+        S.B[p3] = (!none && pl.rb >= 0 && pl.rb < M) ? *reinterpret_cast<const bf16x8r*>(pq + op_index_bf(pl.rb, pl.h, p3)) : zero;
+#pragma unroll
+    for (int mb = 0; mb < NB; mb++)
+#pragma unroll
+        for (int p3 = 0; p3 < 3; p3++)
+            S.A[mb][p3] = (!none && pl.ra[mb] >= 0 && pl.ra[mb] < M)
+                              ? *reinterpret_cast<const bf16x8r*>(pq + op_index_bf(pl.ra[mb], pl.h, p3)) : zero;
+}
+
+template <int NB>
+__device__ __forceinline__ void plane_mfma(const PlaneSet<NB>& S, f32x4v (&acc)[NB])
+{
+#pragma unroll
+    for (int pp = 0; pp < 6; pp++) {
+        const int a = (0x102010 >> (4 * (5 - pp))) & 0xf;   // (mid, mid), (hi, lo), (lo, hi),
+        const int b = (0x120100 >> (4 * (5 - pp))) & 0xf;   // (hi, mid), (mid, hi), (hi, hi)
+#pragma unroll
+        for (int mb = 0; mb < NB; mb++)
+            acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(S.A[mb][a], S.B[b], acc[mb], 0, 0, 0);
+    }
+}
+
+// Split-bf16 contexts (ScanParams::mfrep): the pending steps' share of the blocks a scan reads,
+// ΔX = Σ_q V_q(rows)·V_q(cols)ᵀ over the active pending steps (amask: ks > 0; rolled-back steps
+// have ks = 0), by v_mfma_f32_16x16x32_bf16 on the operand planes the association kernels wrote
+// (V = hi + mid + lo exactly, the six part products of the flush). One instruction takes two
+// steps: k-groups 0/1 the even/odd k of step qa, 2/3 those of step qb (the same k permutation on
+// both operands). NB M-blocks of 16 rows: A row row_a(mb, r), B (16 columns) row row_b(c); a
+// negative or out-of-range row is a zero operand. Lane l holds ΔX[4·(l >> 4) + i][l & 15] of
+// M-block mb in acc[mb][i]. Not the fp32 chain of the flush (the split-bf16 flush is not one
+// either): held to the same parity bar. Two operand sets in flight: pair i + 1 loads during pair
+// i's MFMAs, and the caller issues pair 0 (`first`, plane_load(.., 0, ..)) with its own loads.
+template <int NB>
+__device__ __forceinline__ void plane_replay(const PlanePlan<NB>& pl, PlaneSet<NB>& first, const Slot* pend, int e,
+                                             size_t inst_bf, int M, f32x4v (&acc)[NB])
 {
 #pragma unroll
     for (int mb = 0; mb < NB; mb++) acc[mb] = f32x4v{0.f, 0.f, 0.f, 0.f};
-    const int kg = lane >> 4, h = kg & 1, r16 = lane & 15;
-    typedef unsigned u32x4r __attribute__((ext_vector_type(4)));
-    const bf16x8r zero = __builtin_bit_cast(bf16x8r, u32x4r{0u, 0u, 0u, 0u});
-    const int rb_ = row_b(r16);
-    int ra_[NB];
-#pragma unroll
-    for (int mb = 0; mb < NB; mb++) ra_[mb] = row_a(mb, r16);
-    unsigned m = amask;
-    while (m) {
-        const int qa = __builtin_ctz(m);
-        m &= m - 1;
-        const int qb = m ? __builtin_ctz(m) : -1;
-        if (qb >= 0) m &= m - 1;
-        const unsigned short* pa = reinterpret_cast<const unsigned short*>(pend[qa].Bop) + (size_t)e * inst_bf;
-        const unsigned short* pb = qb >= 0 ? reinterpret_cast<const unsigned short*>(pend[qb].Bop) + (size_t)e * inst_bf : pa;
-        const unsigned short* pq = (kg >= 2) ? pb : pa;
-        const bool none = kg >= 2 && qb < 0;
-        bf16x8r B[3], A[NB][3];
-#pragma unroll
-        for (int pl = 0; pl < 3; pl++)
-            B[pl] = (!none && rb_ >= 0 && rb_ < M) ? *reinterpret_cast<const bf16x8r*>(pq + op_index_bf(rb_, h, pl)) : zero;
-#pragma unroll
-        for (int mb = 0; mb < NB; mb++)
-#pragma unroll
-            for (int pl = 0; pl < 3; pl++)
-                A[mb][pl] = (!none && ra_[mb] >= 0 && ra_[mb] < M)
-                                ? *reinterpret_cast<const bf16x8r*>(pq + op_index_bf(ra_[mb], h, pl)) : zero;
-#pragma unroll
-        for (int pp = 0; pp < 6; pp++) {
-            const int a = (0x102010 >> (4 * (5 - pp))) & 0xf;   // (mid, mid), (hi, lo), (lo, hi),
-            const int b = (0x120100 >> (4 * (5 - pp))) & 0xf;   // (hi, mid), (mid, hi), (hi, hi)
-#pragma unroll
-            for (int mb = 0; mb < NB; mb++)
-                acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mb][a], B[b], acc[mb], 0, 0, 0);
-        }
+    if (pl.np == 0) return;
+    PlaneSet<NB> second;
+    int i = 0;
+    for (; i + 2 < pl.np; i += 2) {   // straight-line body: every load unconditional
+        plane_load(second, pl, i + 1, pend, e, inst_bf, M);
+        plane_mfma(first, acc);
+        plane_load(first, pl, i + 2, pend, e, inst_bf, M);
+        plane_mfma(second, acc);
+    }
+    if (i + 1 < pl.np) {
+        plane_load(second, pl, i + 1, pend, e, inst_bf, M);
+        plane_mfma(first, acc);
+        plane_mfma(second, acc);
+    } else {
+        plane_mfma(first, acc);
     }
 }
 
@@ -1895,6 +1957,30 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     }
                 }
             }
+            // split-bf16 replay: the first pair of pending steps' operand planes, issued with the
+            // records (landmark waves: their 128 rows × the 16 winner rows; the replay wave: the
+            // winner rows against themselves)
+            PlanePlan<8> plL;
+            PlaneSet<8> setL;
+            PlanePlan<1> plR;
+            PlaneSet<1> setR;
+            if constexpr (kPlanes) {
+                if (mf) {
+                    auto wrow = [&](int c) {
+                        const int t = c >> 1;
+                        const int w = t < L ? sh_spec[t] : -1;
+                        return w >= 0 ? 2 * w + (c & 1) : -1;
+                    };
+                    if (tid < SCAN_THREADS) {
+                        const int rbase = 2 * (g * SCAN_THREADS + (tid & ~63));
+                        plane_plan<8>(plL, amask, tid & 63, [&](int mb, int r) { return rbase + 16 * mb + r; }, wrow);
+                        if (plL.np) plane_load(setL, plL, 0, p.pend, e, opstride * 3, M);
+                    } else {
+                        plane_plan<1>(plR, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow);
+                        if (plR.np) plane_load(setR, plR, 0, p.pend, e, opstride * 3, M);
+                    }
+                }
+            }
             if (tid == SCAN_BLOCK - 1) {
                 sh_ready = 0;
                 sh_rwst = 0;
@@ -1904,13 +1990,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
               if constexpr (kPlanes) {
                 // the winners' mutual blocks: X minus the pending steps' ΔX of the 16 winner rows
                 // against themselves (one M-block of plane_replay), by the replay wave itself
-                auto wrow = [&](int c) {
-                    const int t = c >> 1;
-                    const int w = t < L ? sh_spec[t] : -1;
-                    return w >= 0 ? 2 * w + (c & 1) : -1;
-                };
                 f32x4v dacc[1];
-                plane_replay<1>(p.pend, e, opstride * 3, M, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow, dacc);
+                plane_replay<1>(plR, setR, p.pend, e, opstride * 3, M, dacc);
                 float* scr = sh_stg;   // (not staged in this mode) 16 × 16 floats
 #pragma unroll
                 for (int i = 0; i < 4; i++) scr[(4 * (lane_r >> 4) + i) * 16 + (lane_r & 15)] = dacc[0][i];
@@ -2040,15 +2121,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     // of the wave's 128 rows (8 M-blocks) against the 16 winner rows, transposed
                     // through this wave's part of sh_vpl (8 KB; the planes are staged there later)
                     const int l = tid & 63;
-                    const int rbase = 2 * (g * SCAN_THREADS + (tid & ~63));
-                    auto wrow = [&](int c) {
-                        const int t = c >> 1;
-                        const int w = t < L ? sh_spec[t] : -1;
-                        return w >= 0 ? 2 * w + (c & 1) : -1;
-                    };
                     f32x4v dacc[8];
-                    plane_replay<8>(p.pend, e, opstride * 3, M, amask, l,
-                                    [&](int mb, int r) { return rbase + 16 * mb + r; }, wrow, dacc);
+                    plane_replay<8>(plL, setL, p.pend, e, opstride * 3, M, dacc);
                     float* scr = sh_vpl + (tid & ~63) * 32;
 #pragma unroll
                     for (int mb = 0; mb < 8; mb++)
@@ -2428,6 +2502,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             }
         }
     }
+    EKF_STAMP(27);
     // write back the owned state (reset: Robot.cpp:893-904 zeroes landmark entries of y and P)
     if (own) {
         if (reset) {
@@ -2438,6 +2513,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         *reinterpret_cast<double2*>(Rsw + 2 * n + b0) = rr2;
         *reinterpret_cast<double2*>(yw + b0) = yb;
         if (Ddw) Ddw[j] = reset || j >= s + nadd ? make_double4(0, 0, 0, 0) : make_double4(Dj[0], Dj[1], Dj[2], Dj[3]);
+    }
+    EKF_STAMP(28);
+    if (own) {
         if (stage_ops) {
             if constexpr (kPlanes) {
                 // symmetric operands from their LDS stage: per owned row the even-k and the odd-k
@@ -2490,6 +2568,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 }
         }
     }
+    EKF_STAMP(24);
     // status bits seen by this workgroup's threads → its status word (read by ekf_read_results)
     int wgst = 0;
     {
@@ -2542,8 +2621,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // state and the step's result record — only if every workgroup completed without a timeout.
     // Otherwise the instance keeps its state from before the call, and the step's record applies
     // nothing (no downdate, rows or reset: the flush and later on-read replays skip it).
+    EKF_STAMP(25);
     if (tid == 0 && g != 0) publish_done(sync, g, p.epoch, wgst);
     if (g == 0) wgst = lead_collect(sync, G, p.epoch, wgst, p.spin_log2, tid, sh_red);
+    EKF_STAMP(26);
     if (lead) {
         sync[SYNC_WG0] = (int)done_word(p.epoch, wgst);
         const bool commit = !(wgst & EKF_ST_TIMEOUT_BIT);
@@ -4398,8 +4479,9 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     const bool wave_ok = wave_shape && (p.nsteps >= 6 || p.variant == 8);
     const bool bf_shape = p.nsteps >= 2 && p.nsteps <= 16 && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
                           p.nwt > 0 && p.wt != nullptr;
-    if (p.bf && bf_shape && p.variant != 4 && p.nwt24 > 0 && p.wt24 != nullptr) {
-        // EKF_ARITH_BF16X6: the 2 × 4 split-bf16 wave flush (EKF_FLUSH_VARIANT=4: the 2 × 2 form)
+    if (p.bf && bf_shape && p.variant == 24 && p.nwt24 > 0 && p.wt24 != nullptr) {
+        // EKF_ARITH_BF16X6, EKF_FLUSH_VARIANT=24: the 2 × 4 split-bf16 wave flush (measured 7 %
+        // slower than the 2 × 2 form below at T = 12; kept as an option, bit-identical)
         const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
 #define EKF_BF24_CASE(NSV)                                                                              \
     case NSV:                                                                                           \

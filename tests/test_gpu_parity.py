@@ -28,7 +28,7 @@ def rel(a, b):
 
 
 def is_bf_form(name):
-    """A split-bf16 flush form: the 2 × 4 kernel (default) or the 2 × 2 wave form's <.., true>."""
+    """A split-bf16 flush form: the 2 × 2 wave form's <.., true> (default) or the 2 × 4 kernel."""
     return name.startswith("flush_bf24_kernel") or name.endswith(", true>")
 
 
@@ -608,7 +608,7 @@ def test_bf16x6_fp16_storage(ekf_mod, oracle_mod, N, T, extra_every):
     w = G.make_world(N, active=active)
     st = G.initial_state(w)
     a = ekf_mod.Ensemble(N, E, 2, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
-    assert a.flush_kernel_name(T if T % 2 == 0 else T - 1).startswith("flush_bf24_kernel<_Float16")
+    assert a.flush_kernel_name(T if T % 2 == 0 else T - 1).startswith("flush_f32_wave_kernel<_Float16")
     for e in range(E):
         a.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
     ref = oracle_mod.OracleRobot(N)
@@ -700,8 +700,8 @@ def test_singular_status_counts_only_evaluated_candidates(ekf_mod, oracle_mod, m
 
 @pytest.mark.parametrize("prec,N,T,extra_every", [(1, 1024, 12, 0), (1, 200, 8, 3), (2, 512, 10, 0), (1, 100, 16, 0)])
 def test_bf16_2x4_flush_equals_2x2(ekf_mod, monkeypatch, prec, N, T, extra_every):
-    """The split-bf16 flush on 2 × 4 wave-tiles (flush_bf24_kernel, default) and on 2 × 2 wave-tiles
-    (flush_f32_wave_kernel<.., true>, EKF_FLUSH_VARIANT=4) run the same MFMA sequence per element
+    """The split-bf16 flush on 2 × 4 wave-tiles (flush_bf24_kernel, EKF_FLUSH_VARIANT=24) and on 2 × 2
+    wave-tiles (flush_f32_wave_kernel<.., true>, default) run the same MFMA sequence per element
     (same part products in the same order, bf16 MFMA deterministic): bit-identical state, fast
     groups and groups with augmented rows (general path on the two 2 × 2 halves) alike, fp32 and
     fp16 storage, block sizes that are not multiples of the wave-tile."""
@@ -709,10 +709,10 @@ def test_bf16_2x4_flush_equals_2x2(ekf_mod, monkeypatch, prec, N, T, extra_every
     active = N - 12 - 2 * ((3 * T + 1) // extra_every) if extra_every else N - 10
     w = G.make_world(N, active=active)
     st = G.initial_state(w)
+    monkeypatch.setenv("EKF_FLUSH_VARIANT", "24")
     a = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
-    monkeypatch.setenv("EKF_FLUSH_VARIANT", "4")
-    b = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
     monkeypatch.delenv("EKF_FLUSH_VARIANT")
+    b = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
     assert a.flush_kernel_name(T).startswith("flush_bf24_kernel"), a.flush_kernel_name(T)
     assert b.flush_kernel_name(T).endswith(", true>"), b.flush_kernel_name(T)
     for ens in (a, b):
