@@ -1957,30 +1957,18 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     }
                 }
             }
-            // split-bf16 replay: the first pair of pending steps' operand planes, issued with the
-            // records (landmark waves: their 128 rows × the 16 winner rows; the replay wave: the
-            // winner rows against themselves)
+            // split-bf16 replay plans (landmark waves: their 128 rows × the 16 winner rows; the
+            // replay wave: the winner rows against themselves). The first pair's planes are loaded
+            // after the barrier: issued with the records they doubled the records' round trip
+            // (≈14 MB over all instances at T = 12, from the MALL/HBM: L2 does not survive the
+            // kernel boundary)
             PlanePlan<8> plL;
-            PlaneSet<8> setL;
             PlanePlan<1> plR;
-            PlaneSet<1> setR;
-            if constexpr (kPlanes) {
-                if (mf) {
-                    auto wrow = [&](int c) {
-                        const int t = c >> 1;
-                        const int w = t < L ? sh_spec[t] : -1;
-                        return w >= 0 ? 2 * w + (c & 1) : -1;
-                    };
-                    if (tid < SCAN_THREADS) {
-                        const int rbase = 2 * (g * SCAN_THREADS + (tid & ~63));
-                        plane_plan<8>(plL, amask, tid & 63, [&](int mb, int r) { return rbase + 16 * mb + r; }, wrow);
-                        if (plL.np) plane_load(setL, plL, 0, p.pend, e, opstride * 3, M);
-                    } else {
-                        plane_plan<1>(plR, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow);
-                        if (plR.np) plane_load(setR, plR, 0, p.pend, e, opstride * 3, M);
-                    }
-                }
-            }
+            auto wrow = [&](int c) {
+                const int t = c >> 1;
+                const int w = t < L ? sh_spec[t] : -1;
+                return w >= 0 ? 2 * w + (c & 1) : -1;
+            };
             if (tid == SCAN_BLOCK - 1) {
                 sh_ready = 0;
                 sh_rwst = 0;
@@ -1991,6 +1979,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 // the winners' mutual blocks: X minus the pending steps' ΔX of the 16 winner rows
                 // against themselves (one M-block of plane_replay), by the replay wave itself
                 f32x4v dacc[1];
+                PlaneSet<1> setR;
+                plane_plan<1>(plR, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow);
+                if (plR.np) plane_load(setR, plR, 0, p.pend, e, opstride * 3, M);
                 plane_replay<1>(plR, setR, p.pend, e, opstride * 3, M, dacc);
                 float* scr = sh_stg;   // (not staged in this mode) 16 × 16 floats
 #pragma unroll
@@ -2122,6 +2113,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     // through this wave's part of sh_vpl (8 KB; the planes are staged there later)
                     const int l = tid & 63;
                     f32x4v dacc[8];
+                    PlaneSet<8> setL;
+                    const int rbase = 2 * (g * SCAN_THREADS + (tid & ~63));
+                    plane_plan<8>(plL, amask, l, [&](int mb, int r) { return rbase + 16 * mb + r; }, wrow);
+                    if (plL.np) plane_load(setL, plL, 0, p.pend, e, opstride * 3, M);
                     plane_replay<8>(plL, setL, p.pend, e, opstride * 3, M, dacc);
                     float* scr = sh_vpl + (tid & ~63) * 32;
 #pragma unroll
