@@ -851,6 +851,69 @@ __device__ __forceinline__ void line_R(const ekf_line& ln, int i, int r_mode, do
     }
 }
 
+// Drift-certified rejection (the speculative path's first per-line filter, before quick_reject):
+// quick_reject's two bounds evaluated from the owned landmark's values at the start of the line
+// loop and a bound on how far its mean can have moved since, so that it needs nothing from the
+// landmark's own gain rows of the earlier lines (it runs beside them, one line ahead).
+//  * P only decreases within a scan (every line subtracts K·S·Kᵀ, positive semidefinite), so
+//    S00 = H0·P5·H0ᵀ + R00 and tr(P5) at line i are at most their line-loop-start values.
+//  * The mean of landmark row r moves at line q by (K·v)_r = W_r,0·u0 + W_r,1·u1, u = S⁻¹·v
+//    (gain_rows), and |W_r,c| = |e_rᵀ·P·h_c| ≤ sqrt(P_rr)·sqrt(h_cᵀ·P·h_c) (P positive
+//    semidefinite) ≤ sqrt(D_rr)·sqrt(|S_cc| + |R_cc|), D the line-loop-start diagonal block. So
+//    |Δ mean_r| ≤ sqrt(D_rr)·G with G = Σ_q g_q, g_q = Σ_c sqrt(|S_cc| + |R_cc|)·|u_c| — one
+//    uniform value per line (drift_g).
+//  * The circular distance of v0 and the one-sided bound on |v1| are 1-Lipschitz in the means
+//    (|Δcos|, |Δsin| ≤ |Δ angle|); the robot pose after the earlier lines is the package's, exact.
+// Margins: the bounds are inflated by 1e-6 relative plus absolute slack, far above the roundings
+// of the chain; NaN never rejects.
+struct DriftBase {
+    double ma0, mr0, sDa, sDb, S00b, tr5;
+};
+
+__device__ __forceinline__ void drift_base(DriftBase& d, const double R33[9], double2 rr2, const double Dj[4],
+                                           double2 yb)
+{
+    d.ma0 = yb.x;
+    d.mr0 = yb.y;
+    d.sDa = sqrt(fmax(Dj[0], 0.0)) * (1.0 + 1e-6);
+    d.sDb = sqrt(fmax(Dj[3], 0.0)) * (1.0 + 1e-6);
+    d.S00b = R33[8] - 2.0 * rr2.x + Dj[0];   // quick_reject's S00 less R00: p22 − 2·p2a + daa
+    d.tr5 = R33[0] + R33[4] + R33[8] + Dj[0] + Dj[3];
+}
+
+// g_q of one match from its package and the line's R (uniform)
+__device__ __forceinline__ double drift_g(const double* pk, const double Rm[4])
+{
+    const double v0 = pk[MB_V], v1 = pk[MB_V + 1];
+    const double u0 = pk[MB_SI] * v0 + pk[MB_SI + 1] * v1;
+    const double u1 = pk[MB_SI + 2] * v0 + pk[MB_SI + 3] * v1;
+    const double g = sqrt(fabs(pk[MB_S]) + fabs(Rm[0])) * fabs(u0) + sqrt(fabs(pk[MB_S + 3]) + fabs(Rm[3])) * fabs(u1);
+    return g * (1.0 + 1e-6);
+}
+
+// s0, c0: sin/cos of ma0 within QR_TRIG_EPS (as quick_reject); G: Σ g_q over the earlier lines
+__device__ __forceinline__ bool drift_reject(const DriftBase& d, double za, double zr, const double Rm[4],
+                                             const double xp[3], double G, double s0, double c0, double gate)
+{
+    const double X = fabs(xp[0]) + fabs(xp[1]);
+    const double H2 = 2.0 + X * X;
+    if (!(Rm[1] == Rm[2]) || !(d.tr5 >= 0.0) || !(Rm[0] > 1e-5 * 2.0 * d.tr5) || !(Rm[3] > 1e-5 * H2 * d.tr5) ||
+        !(fabs(d.ma0) <= 8.0) || !(G >= 0.0))
+        return false;
+    const double g2 = gate * gate * (1.0 + 1e-6);
+    const double Dma = d.sDa * G * (1.0 + 1e-6) + 1e-15;
+    const double Dmr = d.sDb * G * (1.0 + 1e-6) + 1e-15;
+    const double S00 = d.S00b + Rm[0];
+    const double x = za - (d.ma0 - xp[2]);
+    const double cd = fabs(x - 2.0 * EKF_PI * rint(x * (0.5 / EKF_PI)));
+    const double a0 = cd - Dma - 1e-12 * (1.0 + fabs(x));
+    if (S00 > 0.0 && a0 > 0.0 && a0 * a0 > g2 * S00) return true;
+    const double v1e = zr - (d.mr0 - (xp[0] * c0 + xp[1] * s0));
+    const double a1 = fabs(v1e) - Dmr - X * (Dma + QR_TRIG_EPS) - 1e-12 * (1.0 + fabs(zr) + fabs(d.mr0) + X);
+    const double S11u = H2 * d.tr5 * (1.0 + 1e-5) + Rm[3];
+    return a1 > 0.0 && a1 * a1 > g2 * S11u;
+}
+
 __device__ __forceinline__ void fill_block5(Block5& b5, const double R33[9], double2 rr0, double2 rr1,
                                             double2 rr2, const double Dj[4])
 {
@@ -1334,7 +1397,6 @@ __device__ __forceinline__ void plane_load(PlaneSet<NB>& S, const PlanePlan<NB>&
                                            size_t inst_bf, int M)
 {
     typedef unsigned u32x4r __attribute__((ext_vector_type(4)));
-    const bf16x8r zero = __builtin_bit_cast(bf16x8r, u32x4r{0u, 0u, 0u, 0u});
     const int ii = i < pl.np ? i : pl.np - 1;
     unsigned m = pl.amask;   // pair ii: the steps of set bits 2ii and 2ii + 1
     for (int k = 0; k < 2 * ii; k++) m &= m - 1;
@@ -1345,15 +1407,27 @@ __device__ __forceinline__ void plane_load(PlaneSet<NB>& S, const PlanePlan<NB>&
     const unsigned short* pb = qb >= 0 ? reinterpret_cast<const unsigned short*>(pend[qb].Bop) + (size_t)e * inst_bf : pa;
     const unsigned short* pq = (pl.kg >= 2) ? pb : pa;
     const bool none = pl.kg >= 2 && qb < 0;
+    // branch-free: a zero operand loads row 0 and is masked (per-load branches serialised the
+    // loads and forced a full vmcnt(0) wait before the MFMAs)
+    const bool okB = !none && pl.rb >= 0 && pl.rb < M;
+    const unsigned mB = okB ? ~0u : 0u;
+    const int rB = okB ? pl.rb : 0;
 #pragma unroll
-    for (int p3 = 0; p3 < 3; p3++)
-        S.B[p3] = (!none && pl.rb >= 0 && pl.rb < M) ? *reinterpret_cast<const bf16x8r*>(pq + op_index_bf(pl.rb, pl.h, p3)) : zero;
+    for (int p3 = 0; p3 < 3; p3++) {
+        const u32x4r x = *reinterpret_cast<const u32x4r*>(pq + op_index_bf(rB, pl.h, p3));
+        S.B[p3] = __builtin_bit_cast(bf16x8r, x & mB);
+    }
 #pragma unroll
-    for (int mb = 0; mb < NB; mb++)
+    for (int mb = 0; mb < NB; mb++) {
+        const bool ok = !none && pl.ra[mb] >= 0 && pl.ra[mb] < M;
+        const unsigned mA = ok ? ~0u : 0u;
+        const int rA = ok ? pl.ra[mb] : 0;
 #pragma unroll
-        for (int p3 = 0; p3 < 3; p3++)
-            S.A[mb][p3] = (!none && pl.ra[mb] >= 0 && pl.ra[mb] < M)
-                              ? *reinterpret_cast<const bf16x8r*>(pq + op_index_bf(pl.ra[mb], pl.h, p3)) : zero;
+        for (int p3 = 0; p3 < 3; p3++) {
+            const u32x4r x = *reinterpret_cast<const u32x4r*>(pq + op_index_bf(rA, pl.h, p3));
+            S.A[mb][p3] = __builtin_bit_cast(bf16x8r, x & mA);
+        }
+    }
 }
 
 template <int NB>
@@ -2189,6 +2263,20 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         tq = t2;
                     }
                 };
+                // drift_reject: the owned landmark's bases at the start of the line loop, the
+                // uniform drift sum G, and the verdict for the next line (computed one line ahead,
+                // beside the gain rows it does not depend on)
+                DriftBase db;
+                drift_base(db, R33, rr2, Dj, yb);
+                double Gd = 0.0;
+                auto drift_next = [&](int i1, const double xq[3], double G) -> bool {
+                    if (!(own && j < s && i1 < L)) return false;
+                    const ekf_line l1 = sh_lines[i1];
+                    double R1[4];
+                    line_R(l1, i1, p.r_mode, R1);
+                    return drift_reject(db, l1.alpha, l1.r, R1, xq, G, s0f, c0f, p.gate);
+                };
+                bool drej = drift_next(0, xp, 0.0);
                 for (int i = 0; i < L && !viol; ++i) {
                     const ekf_line ln = sh_lines[i];
                     double Rm[4];
@@ -2197,7 +2285,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     int deep = 0;   // diagnostics: 1 past the quick filter, 2 past the fp32 one, 3 past the fp64 one
                     // the guessed winner itself (j == w) is evaluated exactly by the replay wave, which
                     // flags a failed gate (sh_flag) and its GSL_EDOM (sh_rwst)
-                    if (own && j < s && !matched && j != w) {
+                    if (own && j < s && !matched && j != w && !drej) {
                         Block5 b5;
                         fill_block5(b5, R33, rr0, rr1, rr2, Dj);
                         bool pass = false;
@@ -2218,8 +2306,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         if (pass ? (w < 0 || j < w) : (j == w)) viol = 1;
                     }
                     if (p.dbg && g == 0) {   // waves of workgroup 0 whose lanes went deeper
+                        const bool d0 = __any(own && j < s && !matched && j != w && !drej);
                         const bool d1 = __any(deep >= 1), d2 = __any(deep >= 2), d3 = __any(deep >= 3);
                         if ((tid & 63) == 0) {
+                            if (d0) atomicAdd(&sh_stamp[29], 1ull);
                             if (d1) atomicAdd(&sh_stamp[20], 1ull);
                             if (d2) atomicAdd(&sh_stamp[21], 1ull);
                             if (d3) atomicAdd(&sh_stamp[23], 1ull);
@@ -2235,6 +2325,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         }
                         if (tid == 0) sh_extra[nextra] = i;
                         nextra++;
+                        drej = drift_next(i + 1, xp, Gd);   // state unchanged
                         continue;
                     }
                     int polls = 0;
@@ -2245,6 +2336,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     sub(17);
                     const double* pk = sh_pk[i];
                     if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
+                    // the next line's drift verdict: robot pose after this line from the package
+                    const double xpn[3] = {pk[PK_XP + 0], pk[PK_XP + 1], pk[PK_XP + 2]};
+                    Gd += drift_g(pk, Rm);
+                    drej = drift_next(i + 1, xpn, Gd);
                     if (own) {
                         double blk[4];
                         if constexpr (sizeof(typename Stor<T>::C) == 4) {
