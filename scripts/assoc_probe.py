@@ -35,9 +35,9 @@ for c in cfgs:
     n = stp[9] or 1
     out = {v: round(stp[k] * 10e-3 / n, 2) for k, v in NAMES.items()}
     out["fallbacks"] = stp[15]
+    out["rw_replay_done_after_records"] = round((stp[30] - stp[31]) * 10e-3 / n, 2)   # replay wave's ΔX ready, relative to stamp 12
     out["gate_waves"] = stp[22]                  # (wave, line) gate evaluations, workgroup 0
-    out["past_drift_filter"] = stp[29]           # ... with a lane past the drift-certified filter
-    out["past_quick_filter"] = stp[20]           # ... past the quick certified filter
+    out["past_quick_filter"] = stp[20]           # ... with a lane past the quick certified filter
     out["past_f32_filter"] = stp[21]             # ... past the fp32 certified filter
     out["past_f64_filter"] = stp[23]             # ... and past the fp64 one (exact evaluation)
     print(json.dumps({"N": N, "T": T, "E": E, "arith": "exact" if arith == ekf.ARITH_EXACT else "bf16x6", "launches_x_instances": stp[9], "us": out}), flush=True)

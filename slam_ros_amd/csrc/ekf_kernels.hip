@@ -851,69 +851,6 @@ __device__ __forceinline__ void line_R(const ekf_line& ln, int i, int r_mode, do
     }
 }
 
-// Drift-certified rejection (the speculative path's first per-line filter, before quick_reject):
-// quick_reject's two bounds evaluated from the owned landmark's values at the start of the line
-// loop and a bound on how far its mean can have moved since, so that it needs nothing from the
-// landmark's own gain rows of the earlier lines (it runs beside them, one line ahead).
-//  * P only decreases within a scan (every line subtracts K·S·Kᵀ, positive semidefinite), so
-//    S00 = H0·P5·H0ᵀ + R00 and tr(P5) at line i are at most their line-loop-start values.
-//  * The mean of landmark row r moves at line q by (K·v)_r = W_r,0·u0 + W_r,1·u1, u = S⁻¹·v
-//    (gain_rows), and |W_r,c| = |e_rᵀ·P·h_c| ≤ sqrt(P_rr)·sqrt(h_cᵀ·P·h_c) (P positive
-//    semidefinite) ≤ sqrt(D_rr)·sqrt(|S_cc| + |R_cc|), D the line-loop-start diagonal block. So
-//    |Δ mean_r| ≤ sqrt(D_rr)·G with G = Σ_q g_q, g_q = Σ_c sqrt(|S_cc| + |R_cc|)·|u_c| — one
-//    uniform value per line (drift_g).
-//  * The circular distance of v0 and the one-sided bound on |v1| are 1-Lipschitz in the means
-//    (|Δcos|, |Δsin| ≤ |Δ angle|); the robot pose after the earlier lines is the package's, exact.
-// Margins: the bounds are inflated by 1e-6 relative plus absolute slack, far above the roundings
-// of the chain; NaN never rejects.
-struct DriftBase {
-    double ma0, mr0, sDa, sDb, S00b, tr5;
-};
-
-__device__ __forceinline__ void drift_base(DriftBase& d, const double R33[9], double2 rr2, const double Dj[4],
-                                           double2 yb)
-{
-    d.ma0 = yb.x;
-    d.mr0 = yb.y;
-    d.sDa = sqrt(fmax(Dj[0], 0.0)) * (1.0 + 1e-6);
-    d.sDb = sqrt(fmax(Dj[3], 0.0)) * (1.0 + 1e-6);
-    d.S00b = R33[8] - 2.0 * rr2.x + Dj[0];   // quick_reject's S00 less R00: p22 − 2·p2a + daa
-    d.tr5 = R33[0] + R33[4] + R33[8] + Dj[0] + Dj[3];
-}
-
-// g_q of one match from its package and the line's R (uniform)
-__device__ __forceinline__ double drift_g(const double* pk, const double Rm[4])
-{
-    const double v0 = pk[MB_V], v1 = pk[MB_V + 1];
-    const double u0 = pk[MB_SI] * v0 + pk[MB_SI + 1] * v1;
-    const double u1 = pk[MB_SI + 2] * v0 + pk[MB_SI + 3] * v1;
-    const double g = sqrt(fabs(pk[MB_S]) + fabs(Rm[0])) * fabs(u0) + sqrt(fabs(pk[MB_S + 3]) + fabs(Rm[3])) * fabs(u1);
-    return g * (1.0 + 1e-6);
-}
-
-// s0, c0: sin/cos of ma0 within QR_TRIG_EPS (as quick_reject); G: Σ g_q over the earlier lines
-__device__ __forceinline__ bool drift_reject(const DriftBase& d, double za, double zr, const double Rm[4],
-                                             const double xp[3], double G, double s0, double c0, double gate)
-{
-    const double X = fabs(xp[0]) + fabs(xp[1]);
-    const double H2 = 2.0 + X * X;
-    if (!(Rm[1] == Rm[2]) || !(d.tr5 >= 0.0) || !(Rm[0] > 1e-5 * 2.0 * d.tr5) || !(Rm[3] > 1e-5 * H2 * d.tr5) ||
-        !(fabs(d.ma0) <= 8.0) || !(G >= 0.0))
-        return false;
-    const double g2 = gate * gate * (1.0 + 1e-6);
-    const double Dma = d.sDa * G * (1.0 + 1e-6) + 1e-15;
-    const double Dmr = d.sDb * G * (1.0 + 1e-6) + 1e-15;
-    const double S00 = d.S00b + Rm[0];
-    const double x = za - (d.ma0 - xp[2]);
-    const double cd = fabs(x - 2.0 * EKF_PI * rint(x * (0.5 / EKF_PI)));
-    const double a0 = cd - Dma - 1e-12 * (1.0 + fabs(x));
-    if (S00 > 0.0 && a0 > 0.0 && a0 * a0 > g2 * S00) return true;
-    const double v1e = zr - (d.mr0 - (xp[0] * c0 + xp[1] * s0));
-    const double a1 = fabs(v1e) - Dmr - X * (Dma + QR_TRIG_EPS) - 1e-12 * (1.0 + fabs(zr) + fabs(d.mr0) + X);
-    const double S11u = H2 * d.tr5 * (1.0 + 1e-5) + Rm[3];
-    return a1 > 0.0 && a1 * a1 > g2 * S11u;
-}
-
 __device__ __forceinline__ void fill_block5(Block5& b5, const double R33[9], double2 rr0, double2 rr1,
                                             double2 rr2, const double Dj[4])
 {
@@ -1360,120 +1297,47 @@ __device__ __forceinline__ void staged_pair_block(const PllView<T>& v, int wa, i
 // M-block mb in acc[mb][i]. Not the fp32 chain of the flush (the split-bf16 flush is not one
 // either): held to the same parity bar.
 typedef __bf16 bf16x8r __attribute__((ext_vector_type(8)));
-// One pair of pending steps' operands of plane_replay: NB A M-blocks and the B block, three parts each
-template <int NB>
-struct PlaneSet {
-    bf16x8r A[NB][3];
-    bf16x8r B[3];
-};
-
-// Lane geometry of plane_replay: rows of the lane's A M-blocks and B column; the step pairs are
-// the set bits of amask taken two at a time (the odd step out pairs with nothing).
-template <int NB>
-struct PlanePlan {
-    int kg, h, rb;
-    int ra[NB];
-    unsigned amask;   // (wave-uniform)
-    int np;
-};
-
 template <int NB, typename RA, typename RB>
-__device__ __forceinline__ void plane_plan(PlanePlan<NB>& pl, unsigned amask, int lane, RA row_a, RB row_b)
-{
-    pl.kg = lane >> 4;
-    pl.h = pl.kg & 1;
-    const int r16 = lane & 15;
-    pl.rb = row_b(r16);
-#pragma unroll
-    for (int mb = 0; mb < NB; mb++) pl.ra[mb] = row_a(mb, r16);
-    pl.amask = __builtin_amdgcn_readfirstlane(amask);
-    pl.np = (__builtin_popcount(pl.amask) + 1) >> 1;
-}
-
-// Issue the loads of pair i (clamped to the last pair: a load past the end re-reads it, so that
-// every set is loaded unconditionally and the wait counts stay exact)
-template <int NB>
-__device__ __forceinline__ void plane_load(PlaneSet<NB>& S, const PlanePlan<NB>& pl, int i, const Slot* pend, int e,
-                                           size_t inst_bf, int M)
-{
-    typedef unsigned u32x4r __attribute__((ext_vector_type(4)));
-    const int ii = i < pl.np ? i : pl.np - 1;
-    unsigned m = pl.amask;   // pair ii: the steps of set bits 2ii and 2ii + 1
-    for (int k = 0; k < 2 * ii; k++) m &= m - 1;
-    const int qa = __builtin_ctz(m);
-    m &= m - 1;
-    const int qb = m ? __builtin_ctz(m) : -1;
-    const unsigned short* pa = reinterpret_cast<const unsigned short*>(pend[qa].Bop) + (size_t)e * inst_bf;
-    const unsigned short* pb = qb >= 0 ? reinterpret_cast<const unsigned short*>(pend[qb].Bop) + (size_t)e * inst_bf : pa;
-    const unsigned short* pq = (pl.kg >= 2) ? pb : pa;
-    const bool none = pl.kg >= 2 && qb < 0;
-    // branch-free: a zero operand loads row 0 and is masked (per-load branches serialised the
-    // loads and forced a full vmcnt(0) wait before the MFMAs)
-    const bool okB = !none && pl.rb >= 0 && pl.rb < M;
-    const unsigned mB = okB ? ~0u : 0u;
-    const int rB = okB ? pl.rb : 0;
-#pragma unroll
-    for (int p3 = 0; p3 < 3; p3++) {
-        const u32x4r x = *reinterpret_cast<const u32x4r*>(pq + op_index_bf(rB, pl.h, p3));
-        S.B[p3] = __builtin_bit_cast(bf16x8r, x & mB);
-    }
-#pragma unroll
-    for (int mb = 0; mb < NB; mb++) {
-        const bool ok = !none && pl.ra[mb] >= 0 && pl.ra[mb] < M;
-        const unsigned mA = ok ? ~0u : 0u;
-        const int rA = ok ? pl.ra[mb] : 0;
-#pragma unroll
-        for (int p3 = 0; p3 < 3; p3++) {
-            const u32x4r x = *reinterpret_cast<const u32x4r*>(pq + op_index_bf(rA, pl.h, p3));
-            S.A[mb][p3] = __builtin_bit_cast(bf16x8r, x & mA);
-        }
-    }
-}
-
-template <int NB>
-__device__ __forceinline__ void plane_mfma(const PlaneSet<NB>& S, f32x4v (&acc)[NB])
-{
-#pragma unroll
-    for (int pp = 0; pp < 6; pp++) {
-        const int a = (0x102010 >> (4 * (5 - pp))) & 0xf;   // (mid, mid), (hi, lo), (lo, hi),
-        const int b = (0x120100 >> (4 * (5 - pp))) & 0xf;   // (hi, mid), (mid, hi), (hi, hi)
-#pragma unroll
-        for (int mb = 0; mb < NB; mb++)
-            acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(S.A[mb][a], S.B[b], acc[mb], 0, 0, 0);
-    }
-}
-
-// Split-bf16 contexts (ScanParams::mfrep): the pending steps' share of the blocks a scan reads,
-// ΔX = Σ_q V_q(rows)·V_q(cols)ᵀ over the active pending steps (amask: ks > 0; rolled-back steps
-// have ks = 0), by v_mfma_f32_16x16x32_bf16 on the operand planes the association kernels wrote
-// (V = hi + mid + lo exactly, the six part products of the flush). One instruction takes two
-// steps: k-groups 0/1 the even/odd k of step qa, 2/3 those of step qb (the same k permutation on
-// both operands). NB M-blocks of 16 rows: A row row_a(mb, r), B (16 columns) row row_b(c); a
-// negative or out-of-range row is a zero operand. Lane l holds ΔX[4·(l >> 4) + i][l & 15] of
-// M-block mb in acc[mb][i]. Not the fp32 chain of the flush (the split-bf16 flush is not one
-// either): held to the same parity bar. Two operand sets in flight: pair i + 1 loads during pair
-// i's MFMAs, and the caller issues pair 0 (`first`, plane_load(.., 0, ..)) with its own loads.
-template <int NB>
-__device__ __forceinline__ void plane_replay(const PlanePlan<NB>& pl, PlaneSet<NB>& first, const Slot* pend, int e,
-                                             size_t inst_bf, int M, f32x4v (&acc)[NB])
+__device__ __forceinline__ void plane_replay(const Slot* pend, int e, size_t inst_bf, int M, unsigned amask,
+                                             int lane, RA row_a, RB row_b, f32x4v (&acc)[NB])
 {
 #pragma unroll
     for (int mb = 0; mb < NB; mb++) acc[mb] = f32x4v{0.f, 0.f, 0.f, 0.f};
-    if (pl.np == 0) return;
-    PlaneSet<NB> second;
-    int i = 0;
-    for (; i + 2 < pl.np; i += 2) {   // straight-line body: every load unconditional
-        plane_load(second, pl, i + 1, pend, e, inst_bf, M);
-        plane_mfma(first, acc);
-        plane_load(first, pl, i + 2, pend, e, inst_bf, M);
-        plane_mfma(second, acc);
-    }
-    if (i + 1 < pl.np) {
-        plane_load(second, pl, i + 1, pend, e, inst_bf, M);
-        plane_mfma(first, acc);
-        plane_mfma(second, acc);
-    } else {
-        plane_mfma(first, acc);
+    const int kg = lane >> 4, h = kg & 1, r16 = lane & 15;
+    typedef unsigned u32x4r __attribute__((ext_vector_type(4)));
+    const bf16x8r zero = __builtin_bit_cast(bf16x8r, u32x4r{0u, 0u, 0u, 0u});
+    const int rb_ = row_b(r16);
+    int ra_[NB];
+#pragma unroll
+    for (int mb = 0; mb < NB; mb++) ra_[mb] = row_a(mb, r16);
+    unsigned m = amask;
+    while (m) {
+        const int qa = __builtin_ctz(m);
+        m &= m - 1;
+        const int qb = m ? __builtin_ctz(m) : -1;
+        if (qb >= 0) m &= m - 1;
+        const unsigned short* pa = reinterpret_cast<const unsigned short*>(pend[qa].Bop) + (size_t)e * inst_bf;
+        const unsigned short* pb = qb >= 0 ? reinterpret_cast<const unsigned short*>(pend[qb].Bop) + (size_t)e * inst_bf : pa;
+        const unsigned short* pq = (kg >= 2) ? pb : pa;
+        const bool none = kg >= 2 && qb < 0;
+        bf16x8r B[3], A[NB][3];
+#pragma unroll
+        for (int pl = 0; pl < 3; pl++)
+            B[pl] = (!none && rb_ >= 0 && rb_ < M) ? *reinterpret_cast<const bf16x8r*>(pq + op_index_bf(rb_, h, pl)) : zero;
+#pragma unroll
+        for (int mb = 0; mb < NB; mb++)
+#pragma unroll
+            for (int pl = 0; pl < 3; pl++)
+                A[mb][pl] = (!none && ra_[mb] >= 0 && ra_[mb] < M)
+                                ? *reinterpret_cast<const bf16x8r*>(pq + op_index_bf(ra_[mb], h, pl)) : zero;
+#pragma unroll
+        for (int pp = 0; pp < 6; pp++) {
+            const int a = (0x102010 >> (4 * (5 - pp))) & 0xf;   // (mid, mid), (hi, lo), (lo, hi),
+            const int b = (0x120100 >> (4 * (5 - pp))) & 0xf;   // (hi, mid), (mid, hi), (hi, hi)
+#pragma unroll
+            for (int mb = 0; mb < NB; mb++)
+                acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mb][a], B[b], acc[mb], 0, 0, 0);
+        }
     }
 }
 
@@ -2031,18 +1895,38 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     }
                 }
             }
-            // split-bf16 replay plans (landmark waves: their 128 rows × the 16 winner rows; the
-            // replay wave: the winner rows against themselves). The first pair's planes are loaded
-            // after the barrier: issued with the records they doubled the records' round trip
-            // (≈14 MB over all instances at T = 12, from the MALL/HBM: L2 does not survive the
-            // kernel boundary)
-            PlanePlan<8> plL;
-            PlanePlan<1> plR;
-            auto wrow = [&](int c) {
-                const int t = c >> 1;
-                const int w = t < L ? sh_spec[t] : -1;
-                return w >= 0 ? 2 * w + (c & 1) : -1;
-            };
+            // the replay wave's share of the pending steps (the winners' mutual blocks, split-bf16
+            // contexts): the 16 winner rows' planes of every pending pair, issued with the records
+            // (12 registers per pair; the replay wave's chain starts right after the barrier)
+            constexpr int MPAIRS = (SPEC_QMAX + 1) / 2;
+            bf16x8r mpl[MPAIRS][3];
+            if constexpr (kPlanes) {
+                if (mf && tid >= SCAN_THREADS) {
+                    typedef unsigned u32x4r __attribute__((ext_vector_type(4)));
+                    const bf16x8r zero = __builtin_bit_cast(bf16x8r, u32x4r{0u, 0u, 0u, 0u});
+                    const int kg = lane_r >> 4, h = kg & 1, c = lane_r & 15;
+                    const int tw = c >> 1;
+                    const int ww = tw < L ? sh_spec[tw] : -1;
+                    const int row = ww >= 0 ? 2 * ww + (c & 1) : -1;
+                    unsigned mm = amask;
+#pragma unroll
+                    for (int pi = 0; pi < MPAIRS; pi++) {
+                        mpl[pi][0] = mpl[pi][1] = mpl[pi][2] = zero;
+                        if (mm) {
+                            const int qa = __builtin_ctz(mm);
+                            mm &= mm - 1;
+                            const int qb = mm ? __builtin_ctz(mm) : -1;
+                            if (qb >= 0) mm &= mm - 1;
+                            const int q = kg >= 2 ? qb : qa;
+                            if (q >= 0 && row >= 0 && row < M) {
+                                const unsigned short* pq = reinterpret_cast<const unsigned short*>(p.pend[q].Bop) + (size_t)e * opstride * 3;
+#pragma unroll
+                                for (int pl = 0; pl < 3; pl++) mpl[pi][pl] = *reinterpret_cast<const bf16x8r*>(pq + op_index_bf(row, h, pl));
+                            }
+                        }
+                    }
+                }
+            }
             if (tid == SCAN_BLOCK - 1) {
                 sh_ready = 0;
                 sh_rwst = 0;
@@ -2051,12 +1935,20 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             if (mf && tid >= SCAN_THREADS) {
               if constexpr (kPlanes) {
                 // the winners' mutual blocks: X minus the pending steps' ΔX of the 16 winner rows
-                // against themselves (one M-block of plane_replay), by the replay wave itself
-                f32x4v dacc[1];
-                PlaneSet<1> setR;
-                plane_plan<1>(plR, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow);
-                if (plR.np) plane_load(setR, plR, 0, p.pend, e, opstride * 3, M);
-                plane_replay<1>(plR, setR, p.pend, e, opstride * 3, M, dacc);
+                // against themselves (plane_replay's products on the planes loaded above; A and B
+                // are the same rows), by the replay wave itself
+                f32x4v dacc[1] = {f32x4v{0.f, 0.f, 0.f, 0.f}};
+                const int npairs = (__builtin_popcount(amask) + 1) >> 1;
+#pragma unroll
+                for (int pi = 0; pi < MPAIRS; pi++)
+                    if (pi < npairs)
+#pragma unroll
+                        for (int pp = 0; pp < 6; pp++) {
+                            const int a = (0x102010 >> (4 * (5 - pp))) & 0xf;
+                            const int b = (0x120100 >> (4 * (5 - pp))) & 0xf;
+                            dacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mpl[pi][a], mpl[pi][b], dacc[0], 0, 0, 0);
+                        }
+                if (p.dbg && g == 0 && lane_r == 0) sh_stamp[30] += __builtin_amdgcn_s_memrealtime();   // absolute (diagnostics)
                 float* scr = sh_stg;   // (not staged in this mode) 16 × 16 floats
 #pragma unroll
                 for (int i = 0; i < 4; i++) scr[(4 * (lane_r >> 4) + i) * 16 + (lane_r & 15)] = dacc[0][i];
@@ -2089,6 +1981,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             }
             EKF_STAMP(12);
+            if (dbg) sh_stamp[31] += t_last;   // absolute: slot 30 minus slot 31 = the replay wave's ΔX after the records
             // ---- (f) the winners' part of the sequential chain, in the last wave (lane u carries
             // winner u's rows): per line the winner's lane evaluates it and writes the package,
             // then the later winners' lanes apply their gain rows. Meanwhile (g) the landmark
@@ -2186,12 +2079,15 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     // of the wave's 128 rows (8 M-blocks) against the 16 winner rows, transposed
                     // through this wave's part of sh_vpl (8 KB; the planes are staged there later)
                     const int l = tid & 63;
-                    f32x4v dacc[8];
-                    PlaneSet<8> setL;
                     const int rbase = 2 * (g * SCAN_THREADS + (tid & ~63));
-                    plane_plan<8>(plL, amask, l, [&](int mb, int r) { return rbase + 16 * mb + r; }, wrow);
-                    if (plL.np) plane_load(setL, plL, 0, p.pend, e, opstride * 3, M);
-                    plane_replay<8>(plL, setL, p.pend, e, opstride * 3, M, dacc);
+                    auto wrow = [&](int c) {
+                        const int t = c >> 1;
+                        const int w = t < L ? sh_spec[t] : -1;
+                        return w >= 0 ? 2 * w + (c & 1) : -1;
+                    };
+                    f32x4v dacc[8];
+                    plane_replay<8>(p.pend, e, opstride * 3, M, amask, l,
+                                    [&](int mb, int r) { return rbase + 16 * mb + r; }, wrow, dacc);
                     float* scr = sh_vpl + (tid & ~63) * 32;
 #pragma unroll
                     for (int mb = 0; mb < 8; mb++)
@@ -2263,53 +2159,72 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         tq = t2;
                     }
                 };
-                // drift_reject: the owned landmark's bases at the start of the line loop, the
-                // uniform drift sum G, and the verdict for the next line (computed one line ahead,
-                // beside the gain rows it does not depend on)
-                DriftBase db;
-                drift_base(db, R33, rr2, Dj, yb);
-                double Gd = 0.0;
-                auto drift_next = [&](int i1, const double xq[3], double G) -> bool {
-                    if (!(own && j < s && i1 < L)) return false;
-                    const ekf_line l1 = sh_lines[i1];
-                    double R1[4];
-                    line_R(l1, i1, p.r_mode, R1);
-                    return drift_reject(db, l1.alpha, l1.r, R1, xq, G, s0f, c0f, p.gate);
-                };
-                bool drej = drift_next(0, xp, 0.0);
                 for (int i = 0; i < L && !viol; ++i) {
                     const ekf_line ln = sh_lines[i];
                     double Rm[4];
                     line_R(ln, i, p.r_mode, Rm);
                     const int w = sh_spec[i];
                     int deep = 0;   // diagnostics: 1 past the quick filter, 2 past the fp32 one, 3 past the fp64 one
-                    // the guessed winner itself (j == w) is evaluated exactly by the replay wave, which
-                    // flags a failed gate (sh_flag) and its GSL_EDOM (sh_rwst)
-                    if (own && j < s && !matched && j != w && !drej) {
-                        Block5 b5;
-                        fill_block5(b5, R33, rr0, rr1, rr2, Dj);
+                    // the gate of line i on the state before it (the guessed winner itself, j == w, is
+                    // evaluated exactly by the replay wave, which flags a failed gate (sh_flag) and its
+                    // GSL_EDOM (sh_rwst)). Its first filter runs in one block with the line's gain rows,
+                    // which do not depend on it: two independent chains for the scheduler to interleave
+                    const bool cand = own && j < s && !matched && j != w;
+                    Block5 b5;
+                    fill_block5(b5, R33, rr0, rr1, rr2, Dj);
+                    const double ybx = yb.x, yby = yb.y;
+                    const double xpg[3] = {xp[0], xp[1], xp[2]};
+                    bool deeper = false;
+                    const double* pk = nullptr;
+                    if (w >= 0) {
+                        int polls = 0;
+                        while (__hip_atomic_load(&sh_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= i) {
+                            __builtin_amdgcn_s_sleep(1);
+                            if ((tstatus & EKF_ST_TIMEOUT_BIT) || ++polls > (1 << p.spin_log2)) { tstatus |= EKF_ST_TIMEOUT_BIT; viol = 1; break; }
+                        }
+                        sub(17);
+                        pk = sh_pk[i];
+                        if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
+                        if (own) {
+                            deeper = cand && !quick_reject(b5, ybx, yby, ma0, s0f, c0f, xpg, ln.alpha, ln.r, Rm, p.gate);
+                            double blk[4];
+                            if constexpr (sizeof(typename Stor<T>::C) == 4) {
+                                const float4 bk = sh_blk[i][tid];
+                                blk[0] = bk.x; blk[1] = bk.y; blk[2] = bk.z; blk[3] = bk.w;
+                            } else {
+                                pll_block(pv, 2 * j, 2 * w, blk);   // fp64 operands: read in the loop
+                            }
+                            double kk[4], uu[4];
+                            gain_rows<SPEC_L>(pk, m, uq_owned, [&](int q) { return sh_wh[i][q][1]; }, blk, rr0, rr1,
+                                              rr2, yb, Dj, kk, uu);
+                            const float F[3] = {(float)pk[PK_F], (float)pk[PK_F + 1], (float)pk[PK_F + 2]};
+                            store_rows(m, kk, uu, false, F);
+                        }
+                        sub(18);
+                    } else {
+                        deeper = cand && !quick_reject(b5, ybx, yby, ma0, s0f, c0f, xpg, ln.alpha, ln.r, Rm, p.gate);
+                    }
+                    if (deeper) {   // rare: the certified fp32 and fp64 filters, then the exact evaluation
+                        deep = 1;
                         bool pass = false;
                         double sn = 0.0, cs = 1.0;
-                        if (!quick_reject(b5, yb.x, yb.y, ma0, s0f, c0f, xp, ln.alpha, ln.r, Rm, p.gate) &&
-                            (deep = 1, !certified_reject_f32(b5, yb.x, yb.y, xp, ln.alpha, ln.r, Rm, p.gate)) &&
-                            (deep = 2, exact_sc(), sincos_near(yb.x, ma0, s0j, c0j, sn, cs),
-                             !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate))) {
+                        if (!certified_reject_f32(b5, ybx, yby, xpg, ln.alpha, ln.r, Rm, p.gate) &&
+                            (deep = 2, exact_sc(), sincos_near(ybx, ma0, s0j, c0j, sn, cs),
+                             !certified_reject(b5, ybx, yby, sn, cs, xpg, ln.alpha, ln.r, Rm, p.gate))) {
                             deep = 3;
                             Cand c;
-                            eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, c);
+                            eval_candidate(b5, ybx, yby, sn, cs, xpg, ln.alpha, ln.r, Rm, p.gate, c);
                             // GSL_EDOM counts only for candidates the reference evaluates: the
                             // unmatched ones up to the winner (Robot.cpp:313-498 stops there)
                             if (c.singular && (w < 0 || j <= w)) status |= EKF_ST_SINGULAR;
                             pass = c.pass;
                         }
                         // the guess must be the first passing unmatched landmark
-                        if (pass ? (w < 0 || j < w) : (j == w)) viol = 1;
+                        if (pass && (w < 0 || j < w)) viol = 1;
                     }
                     if (p.dbg && g == 0) {   // waves of workgroup 0 whose lanes went deeper
-                        const bool d0 = __any(own && j < s && !matched && j != w && !drej);
                         const bool d1 = __any(deep >= 1), d2 = __any(deep >= 2), d3 = __any(deep >= 3);
                         if ((tid & 63) == 0) {
-                            if (d0) atomicAdd(&sh_stamp[29], 1ull);
                             if (d1) atomicAdd(&sh_stamp[20], 1ull);
                             if (d2) atomicAdd(&sh_stamp[21], 1ull);
                             if (d3) atomicAdd(&sh_stamp[23], 1ull);
@@ -2325,36 +2240,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         }
                         if (tid == 0) sh_extra[nextra] = i;
                         nextra++;
-                        drej = drift_next(i + 1, xp, Gd);   // state unchanged
                         continue;
                     }
-                    int polls = 0;
-                    while (__hip_atomic_load(&sh_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= i) {
-                        __builtin_amdgcn_s_sleep(1);
-                        if ((tstatus & EKF_ST_TIMEOUT_BIT) || ++polls > (1 << p.spin_log2)) { tstatus |= EKF_ST_TIMEOUT_BIT; viol = 1; break; }
-                    }
-                    sub(17);
-                    const double* pk = sh_pk[i];
-                    if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
-                    // the next line's drift verdict: robot pose after this line from the package
-                    const double xpn[3] = {pk[PK_XP + 0], pk[PK_XP + 1], pk[PK_XP + 2]};
-                    Gd += drift_g(pk, Rm);
-                    drej = drift_next(i + 1, xpn, Gd);
-                    if (own) {
-                        double blk[4];
-                        if constexpr (sizeof(typename Stor<T>::C) == 4) {
-                            const float4 bk = sh_blk[i][tid];
-                            blk[0] = bk.x; blk[1] = bk.y; blk[2] = bk.z; blk[3] = bk.w;
-                        } else {
-                            pll_block(pv, 2 * j, 2 * w, blk);   // fp64 operands: read in the loop
-                        }
-                        double kk[4], uu[4];
-                        gain_rows<SPEC_L>(pk, m, uq_owned, [&](int q) { return sh_wh[i][q][1]; }, blk, rr0, rr1,
-                                          rr2, yb, Dj, kk, uu);
-                        const float F[3] = {(float)pk[PK_F], (float)pk[PK_F + 1], (float)pk[PK_F + 2]};
-                        store_rows(m, kk, uu, false, F);
-                    }
-                    sub(18);
                     // = robot_update(R33, xp, pk), computed by the replay wave
 #pragma unroll
                     for (int a = 0; a < 9; a++) R33[a] = pk[PK_R33 + a];
@@ -2711,9 +2598,13 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // state and the step's result record — only if every workgroup completed without a timeout.
     // Otherwise the instance keeps its state from before the call, and the step's record applies
     // nothing (no downdate, rows or reset: the flush and later on-read replays skip it).
+    // After a passed speculative verdict the lead needs no collection: every workgroup published
+    // its verdict word after its last wait (a workgroup that timed out, or never ran, makes the
+    // verdict fail or the lead's own verdict poll time out), and none waits on anything after it.
+    // The done words still carry every workgroup's status bits to ekf_read_results.
     EKF_STAMP(25);
     if (tid == 0 && g != 0) publish_done(sync, g, p.epoch, wgst);
-    if (g == 0) wgst = lead_collect(sync, G, p.epoch, wgst, p.spin_log2, tid, sh_red);
+    if (g == 0 && sequential) wgst = lead_collect(sync, G, p.epoch, wgst, p.spin_log2, tid, sh_red);
     EKF_STAMP(26);
     if (lead) {
         sync[SYNC_WG0] = (int)done_word(p.epoch, wgst);
