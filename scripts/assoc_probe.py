@@ -35,7 +35,6 @@ for c in cfgs:
     n = stp[9] or 1
     out = {v: round(stp[k] * 10e-3 / n, 2) for k, v in NAMES.items()}
     out["fallbacks"] = stp[15]
-    out["rw_replay_done_after_records"] = round((stp[30] - stp[31]) * 10e-3 / n, 2)   # replay wave's ΔX ready, relative to stamp 12
     out["gate_waves"] = stp[22]                  # (wave, line) gate evaluations, workgroup 0
     out["past_quick_filter"] = stp[20]           # ... with a lane past the quick certified filter
     out["past_f32_filter"] = stp[21]             # ... past the fp32 certified filter

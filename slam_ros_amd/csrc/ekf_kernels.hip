@@ -1895,38 +1895,6 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     }
                 }
             }
-            // the replay wave's share of the pending steps (the winners' mutual blocks, split-bf16
-            // contexts): the 16 winner rows' planes of every pending pair, issued with the records
-            // (12 registers per pair; the replay wave's chain starts right after the barrier)
-            constexpr int MPAIRS = (SPEC_QMAX + 1) / 2;
-            bf16x8r mpl[MPAIRS][3];
-            if constexpr (kPlanes) {
-                if (mf && tid >= SCAN_THREADS) {
-                    typedef unsigned u32x4r __attribute__((ext_vector_type(4)));
-                    const bf16x8r zero = __builtin_bit_cast(bf16x8r, u32x4r{0u, 0u, 0u, 0u});
-                    const int kg = lane_r >> 4, h = kg & 1, c = lane_r & 15;
-                    const int tw = c >> 1;
-                    const int ww = tw < L ? sh_spec[tw] : -1;
-                    const int row = ww >= 0 ? 2 * ww + (c & 1) : -1;
-                    unsigned mm = amask;
-#pragma unroll
-                    for (int pi = 0; pi < MPAIRS; pi++) {
-                        mpl[pi][0] = mpl[pi][1] = mpl[pi][2] = zero;
-                        if (mm) {
-                            const int qa = __builtin_ctz(mm);
-                            mm &= mm - 1;
-                            const int qb = mm ? __builtin_ctz(mm) : -1;
-                            if (qb >= 0) mm &= mm - 1;
-                            const int q = kg >= 2 ? qb : qa;
-                            if (q >= 0 && row >= 0 && row < M) {
-                                const unsigned short* pq = reinterpret_cast<const unsigned short*>(p.pend[q].Bop) + (size_t)e * opstride * 3;
-#pragma unroll
-                                for (int pl = 0; pl < 3; pl++) mpl[pi][pl] = *reinterpret_cast<const bf16x8r*>(pq + op_index_bf(row, h, pl));
-                            }
-                        }
-                    }
-                }
-            }
             if (tid == SCAN_BLOCK - 1) {
                 sh_ready = 0;
                 sh_rwst = 0;
@@ -1935,20 +1903,14 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             if (mf && tid >= SCAN_THREADS) {
               if constexpr (kPlanes) {
                 // the winners' mutual blocks: X minus the pending steps' ΔX of the 16 winner rows
-                // against themselves (plane_replay's products on the planes loaded above; A and B
-                // are the same rows), by the replay wave itself
-                f32x4v dacc[1] = {f32x4v{0.f, 0.f, 0.f, 0.f}};
-                const int npairs = (__builtin_popcount(amask) + 1) >> 1;
-#pragma unroll
-                for (int pi = 0; pi < MPAIRS; pi++)
-                    if (pi < npairs)
-#pragma unroll
-                        for (int pp = 0; pp < 6; pp++) {
-                            const int a = (0x102010 >> (4 * (5 - pp))) & 0xf;
-                            const int b = (0x120100 >> (4 * (5 - pp))) & 0xf;
-                            dacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mpl[pi][a], mpl[pi][b], dacc[0], 0, 0, 0);
-                        }
-                if (p.dbg && g == 0 && lane_r == 0) sh_stamp[30] += __builtin_amdgcn_s_memrealtime();   // absolute (diagnostics)
+                // against themselves (one M-block of plane_replay), by the replay wave itself
+                auto wrow = [&](int c) {
+                    const int t = c >> 1;
+                    const int w = t < L ? sh_spec[t] : -1;
+                    return w >= 0 ? 2 * w + (c & 1) : -1;
+                };
+                f32x4v dacc[1];
+                plane_replay<1>(p.pend, e, opstride * 3, M, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow, dacc);
                 float* scr = sh_stg;   // (not staged in this mode) 16 × 16 floats
 #pragma unroll
                 for (int i = 0; i < 4; i++) scr[(4 * (lane_r >> 4) + i) * 16 + (lane_r & 15)] = dacc[0][i];
@@ -1981,7 +1943,6 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             }
             EKF_STAMP(12);
-            if (dbg) sh_stamp[31] += t_last;   // absolute: slot 30 minus slot 31 = the replay wave's ΔX after the records
             // ---- (f) the winners' part of the sequential chain, in the last wave (lane u carries
             // winner u's rows): per line the winner's lane evaluates it and writes the package,
             // then the later winners' lanes apply their gain rows. Meanwhile (g) the landmark
