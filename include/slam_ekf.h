@@ -181,7 +181,10 @@ int ekf_get_pose_cov(ekf_ctx* ctx, int e, double P33[9]);
 int ekf_get_ellipse(ekf_ctx* ctx, int e, float axii[2], float* angle);
 /* The same computation on a given 2x2 block P22 = {P00, P01, P10, P11} (host only, no device):
  * gsl_eigen_nonsymmv + GSL_EIGEN_SORT_ABS_ASC restated (sign convention included). Returns 1,
- * 0 for a non-finite block or a complex eigenvalue pair, negative on API error. */
+ * 0 for a non-finite block or a complex eigenvalue pair, negative on API error. Divergence: for a
+ * complex pair (only a non-symmetric block has one; P's pose block is symmetric) the reference's
+ * nonsymmv succeeds and it publishes |Re λ| and an angle from the real parts of the complex
+ * eigenvector; that branch of GSL is not restated here, axii and angle are left untouched. */
 int ekf_ellipse_of_block(const double P22[4], float axii[2], float* angle);
 
 /* Introspection for the benchmark's roofline accounting. */

@@ -49,6 +49,7 @@ struct ekf_ctx {
     double* Rs;               // [2][E][3][n] robot strip, two copies (the association kernel reads
     double* y;                // [2][E][n]    copy cur[e] and writes the other; the lead commits it)
     int* cur;                 // [E] committed copy per instance (device; read back when needed)
+    double* dense = nullptr;   // n × n fp64 scratch of upload / download / rescale (allocated on first use, kept)
     double* pose;
     double* xpre;
     int* saved;
@@ -160,7 +161,7 @@ static void free_all(ekf_ctx* c)
 {
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->cur, c->pose, c->xpre, c->saved, c->D,
                                c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->wt24, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->pexp, c->sink, c->mbox,
-                               c->sync, c->Ust, c->Vst};
+                               c->sync, c->Ust, c->Vst, c->dense};
     ptrs.push_back(c->ops_u);
     ptrs.push_back(c->ops_v);
     ptrs.push_back(c->ops_b);
@@ -855,6 +856,21 @@ extern "C" int ekf_update(ekf_ctx* c, const ekf_line* lines, const int32_t* nlin
     return ekf_read_results(c, out);
 }
 
+// The dense n × n fp64 scratch of the state transfers: allocated on first use and kept, so that a
+// caller mirroring P after every scan (the drop-in's full mirror) does not allocate per call
+static hipError_t dense_scratch(ekf_ctx* c, double** out)
+{
+    if (!c->dense) {
+        const hipError_t err = hipMalloc((void**)&c->dense, sizeof(double) * c->d.n * c->d.n);
+        if (err != hipSuccess) {
+            c->dense = nullptr;
+            return err;
+        }
+    }
+    *out = c->dense;
+    return hipSuccess;
+}
+
 extern "C" int ekf_upload_state(ekf_ctx* c, int e, const double* P, const double* y, int saved,
                                 const double pose[3])
 {
@@ -874,7 +890,7 @@ extern "C" int ekf_upload_state(ekf_ctx* c, int e, const double* P, const double
         rc = set_exponent(c, e, choose_exponent(c, vmax));
         if (rc) return rc;
         double* tmp = nullptr;
-        HIP_TRY(hipMalloc((void**)&tmp, sizeof(double) * d.n * d.n));
+        HIP_TRY(dense_scratch(c, &tmp));
         hipError_t err = hipMemcpyAsync(tmp, P, sizeof(double) * d.n * d.n, hipMemcpyHostToDevice,
                                         c->stream);
         if (err == hipSuccess)
@@ -882,7 +898,6 @@ extern "C" int ekf_upload_state(ekf_ctx* c, int e, const double* P, const double
                                    (char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem,
                                    strip_of(c, cb, e), c->tile_rc, c->pexp_h[e], c->stream);
         if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
-        (void)hipFree(tmp);
         HIP_TRY(err);
     }
     if (y)
@@ -912,7 +927,7 @@ extern "C" int ekf_download_state(ekf_ctx* c, int e, double* P, double* y, int* 
     if (rc) return rc;
     if (P) {
         double* tmp = nullptr;
-        HIP_TRY(hipMalloc((void**)&tmp, sizeof(double) * d.n * d.n));
+        HIP_TRY(dense_scratch(c, &tmp));
         hipError_t err = ekf::launch_unpack(d, c->cfg.precision, tmp,
                                             (const char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem,
                                             strip_of(c, cb, e), c->pexp_h[e], c->stream);
@@ -920,7 +935,6 @@ extern "C" int ekf_download_state(ekf_ctx* c, int e, double* P, double* y, int* 
             err = hipMemcpyAsync(P, tmp, sizeof(double) * d.n * d.n, hipMemcpyDeviceToHost,
                                  c->stream);
         if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
-        (void)hipFree(tmp);
         HIP_TRY(err);
     }
     if (y)
@@ -995,7 +1009,7 @@ extern "C" int ekf_rescale(ekf_ctx* c, int e, int ex)
     void* X = (char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem;
     double* Rs = strip_of(c, cb, e);
     double* tmp = nullptr;
-    HIP_TRY(hipMalloc((void**)&tmp, sizeof(double) * d.n * d.n));
+    HIP_TRY(dense_scratch(c, &tmp));
     std::vector<double> dg(d.n);
     hipError_t err = ekf::launch_unpack(d, c->cfg.precision, tmp, X, Rs, c->pexp_h[e], c->stream);
     if (err == hipSuccess)   // the diagonal of the dense copy (stride n + 1)
@@ -1011,7 +1025,6 @@ extern "C" int ekf_rescale(ekf_ctx* c, int e, int ex)
             if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
         }
     }
-    (void)hipFree(tmp);
     HIP_TRY(err);
     return rc;
 }

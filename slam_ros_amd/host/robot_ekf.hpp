@@ -10,7 +10,9 @@
 // mirror. Mirror policy (setMirror): kFull (default) refreshes all of P_t0 after every call, as
 // the reference's member always holds the full P; kPoseBlock refreshes only [0:3, 0:3] (what
 // getEllipse reads, Robot.cpp:75-77) and leaves the rest as of the last downloadP() — for large
-// capacities, where the full download costs O(n²) per scan.
+// capacities, where the full download costs O(n²) per scan. The per-call cost of kFull: a drain
+// of the deferred flush (so the flush interval has no effect), an unpack into the context's
+// persistent n × n device scratch and an n² × 8-byte device-to-host copy.
 //
 // The types are template parameters so that the core compiles without ROS or GSL:
 //   Line         needs .alfa, .r, .C_AR (pointer to a 2x2 matrix with .data and .tda, the

@@ -76,3 +76,16 @@ def test_sign_convention_examples(oracle_mod):
     # a' (here the larger one) is (cs, sn) with a positive first component
     ok, axii, angle = oracle_mod.gsl_ellipse((0.04, 0.01, 0.01, 0.02))
     assert ok and 0.0 < angle < math.pi
+
+
+def test_complex_pair_is_reported(ekf_mod, oracle_mod):
+    """A non-symmetric block with a complex eigenvalue pair: both restatements return 0 and leave
+    the outputs alone (documented divergence, slam_ekf.h ekf_ellipse_of_block: the reference's
+    gsl_eigen_nonsymmv succeeds there and publishes |Re λ| and the real parts' angle)."""
+    for blk in [(0.03, 0.02, -0.02, 0.03), (1e-3, -5e-4, 6e-4, 2e-3), (0.0, 1.0, -1.0, 0.0)]:
+        S = np.array(blk).reshape(2, 2)
+        assert np.iscomplexobj(np.linalg.eigvals(S)) and abs(np.linalg.eigvals(S)[0].imag) > 0
+        ok_l, ax_l, an_l = ekf_mod.ellipse_of_block(blk)
+        ok_o, _, _ = oracle_mod.gsl_ellipse(blk)
+        assert not ok_l, (blk, ok_l)
+        assert not ok_o
