@@ -62,7 +62,7 @@ def main(tag):
             return True
         if k.startswith("_Z"):   # still mangled: Itanium template arguments
             args = [a.strip() for a in kern[kern.index("<") + 1:-1].split(",")]
-            code = {"float": "f", "double": "d", "_Float16": "DF16_"}
+            code = {"float": "f", "double": "d", "_Float16": "DF16_", "true": "Lb1E", "false": "Lb0E"}
             want = "I" + "".join(code.get(a, "Li%sE" % a) for a in args) + "E"
             return want in k
         return False
