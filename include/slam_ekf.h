@@ -187,6 +187,37 @@ int ekf_get_ellipse(ekf_ctx* ctx, int e, float axii[2], float* angle);
  * eigenvector; that branch of GSL is not restated here, axii and angle are left untouched. */
 int ekf_ellipse_of_block(const double P22[4], float axii[2], float* angle);
 
+/* One instance row-sharded across ranks: each rank's context holds
+ * instance 0 (instances = 1, EKF_ARITH_EXACT, fp32 or fp64, no pipeline) and owns the landmarks
+ * [first, end); the reference's sequential localize (Robot.cpp:298-641) runs as phases, the caller
+ * doing the per-line exchanges between them (no reference member maps to these; they replace the
+ * single call Robot::localize, Robot.h:34, for a map sharded over processes):
+ *   ekf_shard_begin(enc, lines)              predict; the owned landmarks' scan state
+ *   for each line i:
+ *     ekf_shard_gate(i, &j)                  first passing owned unmatched landmark (INT_MAX: none)
+ *     j* = MIN over ranks                     (the reference takes the first in index order)
+ *     ekf_shard_package(i, j*, pkg)          on j*'s owner: S, S^-1, v, H, K/U robot rows, V history
+ *     broadcast pkg from the owner
+ *     ekf_shard_apply(i, j* or -1, pkg)      gain rows of the owned landmarks, robot update
+ *   ekf_shard_end()                          commit (a scan that would add landmarks or reset the
+ *                                            map is refused with EKF_EINVAL: not sharded)
+ *   ekf_shard_operands(U, V, 0) / all-gather the owned rows / ekf_shard_operands(U, V, 1)
+ *   ekf_shard_commit()                       the step joins the deferred flush, which runs on the
+ *                                            wave-tiles holding an owned row block only
+ * With the same inputs the owned rows of P, the owned mean entries, the robot block and the pose
+ * are bit-identical to a single context's (exact arithmetic). */
+int ekf_shard_init(ekf_ctx* ctx, int first, int end);
+int ekf_shard_begin(ekf_ctx* ctx, const double enc[3], const ekf_line* lines, int nlines);
+int ekf_shard_gate(ekf_ctx* ctx, int line, int* first_pass);
+int ekf_shard_package_words(const ekf_ctx* ctx);   /* doubles in a package */
+int ekf_shard_package(ekf_ctx* ctx, int line, int jstar, double* pkg);
+int ekf_shard_apply(ekf_ctx* ctx, int line, int jstar, const double* pkg);
+int ekf_shard_end(ekf_ctx* ctx);
+size_t ekf_shard_operand_bytes(const ekf_ctx* ctx);   /* bytes of each of U and V */
+int ekf_shard_operands(ekf_ctx* ctx, void* U, void* V, int upload);
+int ekf_shard_commit(ekf_ctx* ctx);
+int ekf_shard_status(ekf_ctx* ctx, int* status);   /* status bits of the scan (GSL_EDOM, NSYM) */
+
 /* Introspection for the benchmark's roofline accounting. */
 size_t ekf_landmark_block_bytes(const ekf_ctx* ctx); /* stored bytes of P_ll per instance */
 int ekf_state_dim(const ekf_ctx* ctx);                /* n */

@@ -50,6 +50,17 @@ struct ekf_ctx {
     double* y;                // [2][E][n]    copy cur[e] and writes the other; the lead commits it)
     int* cur;                 // [E] committed copy per instance (device; read back when needed)
     double* dense = nullptr;   // n × n fp64 scratch of upload / download / rescale (allocated on first use, kept)
+    // row shard (ekf_shard_*): owned landmarks [sh_a, sh_b) of instance 0, the running scan's state
+    int sh_a = -1, sh_b = -1;
+    double* sh_rob = nullptr;
+    double* sh_rec = nullptr;
+    double* sh_hist = nullptr;
+    double* sh_pkg = nullptr;
+    int* sh_flags = nullptr;
+    int* sh_out = nullptr;
+    int* sh_match = nullptr;
+    int sh_line = -1, sh_m = 0, sh_L = 0, sh_s = 0, sh_nextra = 0, sh_open = 0;
+    std::vector<int> sh_match_h;
     double* pose;
     double* xpre;
     int* saved;
@@ -161,7 +172,8 @@ static void free_all(ekf_ctx* c)
 {
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->cur, c->pose, c->xpre, c->saved, c->D,
                                c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->wt24, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->pexp, c->sink, c->mbox,
-                               c->sync, c->Ust, c->Vst, c->dense};
+                               c->sync, c->Ust, c->Vst, c->dense,
+                               c->sh_rob, c->sh_rec, c->sh_hist, c->sh_pkg, c->sh_flags, c->sh_out, c->sh_match};
     ptrs.push_back(c->ops_u);
     ptrs.push_back(c->ops_v);
     ptrs.push_back(c->ops_b);
@@ -1228,6 +1240,238 @@ extern "C" size_t ekf_landmark_block_bytes(const ekf_ctx* c)
 }
 
 extern "C" int ekf_state_dim(const ekf_ctx* c) { return c ? c->d.n : 0; }
+
+// ---------------------------------------------------------------------------------------
+// One instance row-sharded across ranks: this context keeps the
+// landmarks [first, end) of instance 0. The scan runs as host-driven phases of the scan kernel's
+// sequential association (ekf::shard_kernel); between them the caller exchanges, per line, the
+// first passing landmark (MIN over ranks) and the winner's package, and at the end of the scan
+// the operand rows (all-gather). The flush runs the product kernels on the wave-tiles that touch
+// the owned rows only.
+
+static ekf::ShardParams shard_params(ekf_ctx* c, int phase)
+{
+    ekf::ShardParams p;
+    memset(&p, 0, sizeof(p));
+    p.d = c->d;
+    p.a = c->sh_a;
+    p.b = c->sh_b;
+    p.phase = phase;
+    p.line = c->sh_line;
+    p.jstar = -1;
+    p.m = c->sh_m;
+    p.L = c->sh_L;
+    p.s = c->sh_s;
+    p.nextra = c->sh_nextra;
+    p.r_mode = c->cfg.r_mode;
+    p.gate = c->cfg.mahalanobis;
+    p.enc_noise = c->cfg.encoder_noise;
+    const int np = (int)(c->nsteps - c->pend0);
+    p.npend = np;
+    p.Pread = c->X[c->base];
+    for (int q = 0; q < np; q++) p.pend[q] = slot_of(c, c->pend0 + q);
+    p.cur = slot_of(c, c->nsteps);
+    p.Rs = strip_of(c, 0, 0);
+    p.y = mean_of(c, 0, 0);
+    p.pose = c->pose;
+    p.saved = c->saved;
+    p.rob = c->sh_rob;
+    p.rec = c->sh_rec;
+    p.hist = c->sh_hist;
+    p.flags = c->sh_flags;
+    p.pkg = c->sh_pkg;
+    p.out = c->sh_out;
+    p.enc = c->d_enc;
+    p.lines = c->d_lines;
+    p.pexp = c->pexp;
+    p.match = c->sh_match;
+    return p;
+}
+
+static int shard_words(const ekf_ctx* c) { return ekf::MB_WORDS_FIXED + 4 * c->d.max_lines; }
+
+extern "C" int ekf_shard_init(ekf_ctx* c, int first, int end)
+{
+    if (!c) return EKF_EINVAL;
+    if (c->cfg.instances != 1 || c->cfg.pipeline || c->bf || c->cfg.arith != EKF_ARITH_EXACT ||
+        c->cfg.precision == EKF_PREC_F16 || c->sh_a >= 0)
+        return EKF_EINVAL;
+    if (first < 0 || end > c->d.N || first >= end) return EKF_ERANGE;
+    int rc = drain(c);
+    if (rc) return rc;
+    int cb = 0;
+    rc = strip_copy(c, 0, &cb);
+    if (rc) return rc;
+    if (cb != 0) {   // the shard phases keep the committed strip and mean in copy 0
+        HIP_TRY(hipMemcpyAsync(strip_of(c, 0, 0), strip_of(c, 1, 0), sizeof(double) * 3 * c->d.n,
+                               hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(mean_of(c, 0, 0), mean_of(c, 1, 0), sizeof(double) * c->d.n,
+                               hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipMemsetAsync(c->cur, 0, sizeof(int), c->stream));
+    }
+    const size_t N = (size_t)c->d.N;
+    HIP_TRY(hipMalloc((void**)&c->sh_rob, sizeof(double) * 12));
+    HIP_TRY(hipMalloc((void**)&c->sh_rec, sizeof(double) * N * ekf::SH_REC));
+    HIP_TRY(hipMalloc((void**)&c->sh_hist, sizeof(double) * N * c->d.max_lines * 8));
+    HIP_TRY(hipMalloc((void**)&c->sh_pkg, sizeof(double) * shard_words(c)));
+    HIP_TRY(hipMalloc((void**)&c->sh_flags, sizeof(int) * N));
+    HIP_TRY(hipMalloc((void**)&c->sh_out, sizeof(int) * 2));
+    HIP_TRY(hipMalloc((void**)&c->sh_match, sizeof(int) * c->d.max_lines));
+    c->sh_match_h.assign(c->d.max_lines, -1);
+    // the flush's wave-tiles restricted to those holding a tile of an owned row block (a tile of
+    // two ranks' rows is kept by both, identically); groups of 2 and 4 steps take the wave form too
+    const int rb0 = (2 * first) / ekf::TILE, rb1 = (2 * end - 1) / ekf::TILE;
+    auto owned = [&](int blk) { return blk >= rb0 && blk <= rb1; };
+    auto restrict_table = [&](ekf::WtEntry* dev, int& cnt, int nr, int nc) -> int {
+        if (!dev || cnt <= 0) return EKF_OK;
+        std::vector<ekf::WtEntry> all(cnt), keep;
+        HIP_TRY(hipMemcpy(all.data(), dev, sizeof(ekf::WtEntry) * cnt, hipMemcpyDeviceToHost));
+        for (const auto& w : all) {
+            bool k = false;
+            for (int r = 0; r < nr; r++)
+                for (int q = 0; q < nc; q++) {
+                    if (!((w.valid >> (r * nc + q)) & 1)) continue;
+                    const int bi = (w.rows[0] >> (16 * r)) & 0xffff, bj = (w.rows[1] >> (16 * q)) & 0xffff;
+                    k |= owned(bi) || owned(bj);
+                }
+            if (k) keep.push_back(w);
+        }
+        if (!keep.empty())
+            HIP_TRY(hipMemcpy(dev, keep.data(), sizeof(ekf::WtEntry) * keep.size(), hipMemcpyHostToDevice));
+        cnt = (int)keep.size();
+        return EKF_OK;
+    };
+    rc = restrict_table(c->wt, c->nwt, ekf::WT_R, ekf::WT_C);
+    if (rc) return rc;
+    rc = restrict_table(c->wt64, c->nwt64, 1, ekf::WT64_C);
+    if (rc) return rc;
+    c->dd_variant = 8;
+    c->sh_a = first;
+    c->sh_b = end;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return EKF_OK;
+}
+
+extern "C" int ekf_shard_begin(ekf_ctx* c, const double enc[3], const ekf_line* lines, int nlines)
+{
+    if (!c || c->sh_a < 0 || !enc || (nlines > 0 && !lines)) return EKF_EINVAL;
+    if (nlines < 0 || nlines > c->d.max_lines) return EKF_ERANGE;
+    if (c->sh_open) return EKF_EINVAL;
+    std::vector<ekf_line> pad(c->d.max_lines);
+    memset(pad.data(), 0, sizeof(ekf_line) * pad.size());
+    for (int i = 0; i < nlines; i++) pad[i] = lines[i];
+    int rc = stage_inputs(c, enc, pad.data(), &nlines);
+    if (rc) return rc;
+    int s = 0;
+    HIP_TRY(hipMemcpyAsync(&s, c->saved, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->sh_line = -1;
+    c->sh_m = 0;
+    c->sh_L = nlines;
+    c->sh_s = s;
+    c->sh_nextra = 0;
+    c->sh_match_h.assign(c->d.max_lines, -1);
+    HIP_TRY(hipMemsetAsync(c->sh_out, 0, sizeof(int) * 2, c->stream));
+    HIP_TRY(ekf::launch_shard(shard_params(c, ekf::SH_BEGIN), c->cfg.precision, c->stream));
+    c->sh_open = 1;
+    return EKF_OK;
+}
+
+extern "C" int ekf_shard_gate(ekf_ctx* c, int line, int* first_pass)
+{
+    if (!c || !c->sh_open || !first_pass) return EKF_EINVAL;
+    if (line < 0 || line >= c->sh_L) return EKF_ERANGE;
+    c->sh_line = line;
+    const int init[2] = {0x7fffffff, 0};
+    HIP_TRY(hipMemcpyAsync(c->sh_out, init, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(ekf::launch_shard(shard_params(c, ekf::SH_GATE), c->cfg.precision, c->stream));
+    HIP_TRY(hipMemcpyAsync(first_pass, c->sh_out, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return EKF_OK;
+}
+
+extern "C" int ekf_shard_package_words(const ekf_ctx* c) { return c ? shard_words(c) : 0; }
+
+extern "C" int ekf_shard_package(ekf_ctx* c, int line, int jstar, double* pkg)
+{
+    if (!c || !c->sh_open || !pkg || line != c->sh_line) return EKF_EINVAL;
+    if (jstar < c->sh_a || jstar >= c->sh_b) return EKF_ERANGE;
+    ekf::ShardParams p = shard_params(c, ekf::SH_PACKAGE);
+    p.jstar = jstar;
+    HIP_TRY(hipMemsetAsync(c->sh_pkg, 0, sizeof(double) * shard_words(c), c->stream));
+    HIP_TRY(ekf::launch_shard(p, c->cfg.precision, c->stream));
+    HIP_TRY(hipMemcpyAsync(pkg, c->sh_pkg, sizeof(double) * shard_words(c), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return EKF_OK;
+}
+
+extern "C" int ekf_shard_apply(ekf_ctx* c, int line, int jstar, const double* pkg)
+{
+    if (!c || !c->sh_open || line != c->sh_line || (jstar >= 0 && !pkg)) return EKF_EINVAL;
+    if (jstar >= c->d.N) return EKF_ERANGE;
+    ekf::ShardParams p = shard_params(c, ekf::SH_APPLY);
+    p.jstar = jstar;
+    if (jstar >= 0)
+        HIP_TRY(hipMemcpyAsync(c->sh_pkg, pkg, sizeof(double) * shard_words(c), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(ekf::launch_shard(p, c->cfg.precision, c->stream));
+    if (jstar >= 0) {
+        // the robot block after the match (Robot.cpp:560-602), the same on every rank
+        HIP_TRY(ekf::launch_shard(shard_params(c, ekf::SH_ROBOT), c->cfg.precision, c->stream));
+        c->sh_match_h[line] = jstar;
+        c->sh_m++;
+    } else {
+        c->sh_nextra++;
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return EKF_OK;
+}
+
+extern "C" size_t ekf_shard_operand_bytes(const ekf_ctx* c) { return c ? c->op_inst * c->op_elem : 0; }
+
+extern "C" int ekf_shard_operands(ekf_ctx* c, void* U, void* V, int upload)
+{
+    if (!c || !c->sh_open || !U || !V) return EKF_EINVAL;
+    const ekf::Slot& cur = slot_of(c, c->nsteps);
+    const size_t bytes = c->op_inst * c->op_elem;
+    const hipMemcpyKind k = upload ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+    HIP_TRY(hipMemcpyAsync(upload ? cur.Uop : U, upload ? U : cur.Uop, bytes, k, c->stream));
+    HIP_TRY(hipMemcpyAsync(upload ? cur.Vop : V, upload ? V : cur.Vop, bytes, k, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return EKF_OK;
+}
+
+// Closes the scan: the owned strip columns and mean, the robot block, pose and the step's record,
+// then (ekf_shard_commit, after the operand all-gather) the step joins the flush schedule.
+extern "C" int ekf_shard_end(ekf_ctx* c)
+{
+    if (!c || !c->sh_open) return EKF_EINVAL;
+    // augmentation and the capacity reset need the whole robot strip on the new landmark's owner:
+    // not sharded; such scans are refused before anything is committed
+    const int nadd = std::min(c->sh_nextra, c->d.N - c->sh_s);
+    if (nadd > 0 || c->sh_s + nadd > c->d.N - c->cfg.reset_margin) return EKF_EINVAL;
+    HIP_TRY(hipMemcpyAsync(c->sh_match, c->sh_match_h.data(), sizeof(int) * c->d.max_lines,
+                           hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(ekf::launch_shard(shard_params(c, ekf::SH_END), c->cfg.precision, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return EKF_OK;
+}
+
+extern "C" int ekf_shard_commit(ekf_ctx* c)
+{
+    if (!c || !c->sh_open) return EKF_EINVAL;
+    c->sh_open = 0;
+    c->nsteps++;
+    if (c->nsteps - c->unflushed0 >= c->T) return enqueue_flush(c);
+    return EKF_OK;
+}
+
+extern "C" int ekf_shard_status(ekf_ctx* c, int* status)
+{
+    if (!c || !status) return EKF_EINVAL;
+    HIP_TRY(hipMemcpyAsync(status, c->sh_out + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return EKF_OK;
+}
 
 extern "C" int ekf_profile_enable(ekf_ctx* c, int enable)
 {

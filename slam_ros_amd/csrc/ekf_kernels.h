@@ -115,6 +115,40 @@ struct ScanParams {
     unsigned long long* dbg;  // optional [E][16] phase timers (s_memrealtime ticks, 100 MHz)
 };
 
+// One instance row-sharded across ranks: the sequential association
+// of the scan kernel (Robot.cpp:298-641) as host-driven phases over the rank's landmarks [a, b),
+// the per-line exchanges (MIN of the first passing landmark, the winner's package) done by the
+// caller between launches. Per-landmark running state lives in `rec` between the phases.
+enum { SH_BEGIN = 0, SH_GATE = 1, SH_PACKAGE = 2, SH_APPLY = 3, SH_END = 4, SH_ROBOT = 5 };
+constexpr int SH_REC = 20;   // doubles per landmark: rr0..2 (6), yb (2), Dj (4), ma0, s0j, c0j, s0f, c0f, spare
+struct ShardParams {
+    Dims d;
+    int a, b;             // owned landmarks
+    int phase;
+    int line, jstar, m, L, s, nextra;
+    int r_mode;
+    double gate, enc_noise;
+    int npend;
+    const void* Pread;    // [ntiles][1024] (instance 0)
+    Slot cur;
+    Slot pend[PMAX];
+    double* Rs;           // [3][n] robot strip (the committed copy)
+    double* y;            // [n]
+    double* pose;         // [3]
+    int* saved;           // [1]
+    double* rob;          // [12] R33 and x_pre of the running scan (the same on every rank)
+    double* rec;          // [N][SH_REC]
+    double* hist;         // [N][max_lines][8] U rows and V rows of each match of the scan
+    int* flags;           // [N] bit 0 matched, bit 1 singular at this line
+    double* pkg;          // [MB words + 4·max_lines] the line's gain package
+    int* out;             // [2] first passing landmark (atomic min), status bits (atomic or)
+    const double* enc;    // [3]
+    const ekf_line* lines;// [max_lines]
+    const int* pexp;
+    const int* match;     // [max_lines] the lines' winners (SH_END)
+};
+hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st);
+
 // One pass over the landmark block applying nsteps steps in order (each: reset, or rank-2m
 // downdate then its augmented rows). Pout may equal Pin (in place).
 struct DowndateParams {

@@ -2614,6 +2614,279 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// One instance row-sharded across ranks (ShardParams): the scan kernel's
+// sequential association path phase by phase over the rank's landmarks [a, b), one thread per
+// landmark, every expression the scan kernel's (the same inline functions in this contract(on)
+// region), so that a sharded run is bit-identical to a single-context one. Between phases the
+// caller exchanges the first passing landmark (MIN over ranks) and the winner's package.
+// Predict (Robot.cpp:130-286) as the scan kernel's init_state: F3, x_pre and the 3×3 block
+__device__ __forceinline__ void shard_predict(const double pose[3], const double enc[3], double enc_noise,
+                                              double F3[9], double R33[9], double xp[3])
+{
+    const double x0 = pose[0], y0 = pose[1], t0 = pose[2];
+    const double u2 = t0 - enc[2];
+    const double dx = x0 - enc[0], dy = y0 - enc[1];
+    const double u0 = sqrt(dx * dx + dy * dy);
+    const double c = u2 / 2.0 + t0;
+    double sc, cc;
+    sincos(c, &sc, &cc);
+    F3[2] = -u0 * sc;
+    F3[5] = u0 * cc;
+    xp[0] = x0 + u0 * cc;
+    xp[1] = y0 + u0 * sc;
+    xp[2] = t0 + u2;
+    const double Fu3[9] = {cc, 0, -u0 * sc / 2.0, sc, 1, u0 * cc / 2.0, 0, 0, 1};
+    const double qs = (-1.0 / (1 + fabs(u0)) + 1);
+    const double Q[9] = {enc_noise * qs, 0, 0, 0, 2 * enc_noise * qs, 0, 0, 0, enc_noise * qs};
+    double FP[9], FuQ[9];
+    for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) {
+            double s = 0.0, t = 0.0;
+            for (int k = 0; k < 3; k++) {
+                s += F3[a * 3 + k] * R33[k * 3 + b];
+                t += Fu3[a * 3 + k] * Q[k * 3 + b];
+            }
+            FP[a * 3 + b] = s;
+            FuQ[a * 3 + b] = t;
+        }
+    for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) {
+            double s = 0.0, t = 0.0;
+            for (int k = 0; k < 3; k++) {
+                s += FP[a * 3 + k] * F3[b * 3 + k];
+                t += FuQ[a * 3 + k] * Fu3[b * 3 + k];
+            }
+            R33[a * 3 + b] = s + t;
+        }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
+{
+    using C = typename Stor<T>::C;
+    const Dims d = p.d;
+    const int n = d.n;
+    const int gid = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int j = p.a + gid;
+    const bool own = j < p.b;
+    __shared__ int4 sh_ctl[PMAX];
+    if ((int)threadIdx.x < p.npend) {
+        const int* r = p.pend[threadIdx.x].res;
+        sh_ctl[threadIdx.x] = make_int4(r[RES_RESET], r[RES_KSTEPS], r[RES_NADD], r[RES_SAVED_IN]);
+    }
+    __syncthreads();
+    PllView<T> pv;
+    pv.X = reinterpret_cast<const T*>(p.Pread);
+    pv.nb = d.nb;
+    pv.kmax = d.kmax;
+    pv.M = d.M;
+    pv.max_lines = d.max_lines;
+    pv.e = 0;
+    pv.ex = storage_exp<T>(p.pexp, 0);
+    pv.opstride = (size_t)d.nb * 64 * (d.kmax / 2);
+    pv.npend = p.npend;
+    pv.pend = p.pend;
+    pv.ctl = sh_ctl;
+    pv.rnd = 1;
+    const bool sym = p.r_mode != 1 && sizeof(C) == 4;
+    const int b0 = 3 + 2 * j;
+    double* rc = p.rec + (size_t)j * SH_REC;
+    double R33[9], xp[3];
+    if (p.phase != SH_BEGIN) {
+#pragma unroll
+        for (int a = 0; a < 9; a++) R33[a] = p.rob[a];
+        xp[0] = p.rob[9]; xp[1] = p.rob[10]; xp[2] = p.rob[11];
+    }
+    if (p.phase == SH_ROBOT) {
+        // the robot block and x_pre after the line's match (Robot.cpp:560-602), one thread
+        if (gid == 0) {
+            robot_update(R33, xp, p.pkg);
+#pragma unroll
+            for (int a = 0; a < 9; a++) p.rob[a] = R33[a];
+            p.rob[9] = xp[0]; p.rob[10] = xp[1]; p.rob[11] = xp[2];
+        }
+        return;
+    }
+
+    if (p.phase == SH_BEGIN) {
+        // the committed robot block and pose, predicted (every thread the same), the owned strip
+        // columns predicted (Robot.cpp:242), the diagonal block with the pending steps applied
+#pragma unroll
+        for (int a = 0; a < 9; a++) R33[a] = p.Rs[(a / 3) * n + (a % 3)];
+        double F3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        shard_predict(p.pose, p.enc, p.enc_noise, F3, R33, xp);
+        if (gid == 0) {
+#pragma unroll
+            for (int a = 0; a < 9; a++) p.rob[a] = R33[a];
+            p.rob[9] = xp[0]; p.rob[10] = xp[1]; p.rob[11] = xp[2];
+        }
+        if (!own) return;
+        double2 rr0 = *reinterpret_cast<const double2*>(p.Rs + b0);
+        double2 rr1 = *reinterpret_cast<const double2*>(p.Rs + n + b0);
+        double2 rr2 = *reinterpret_cast<const double2*>(p.Rs + 2 * n + b0);
+        const double2 yb = *reinterpret_cast<const double2*>(p.y + b0);
+        predict_cols(F3, rr0, rr1, rr2);
+        double Dj[4] = {0, 0, 0, 0};
+        if (j < p.s) pll_block(pv, 2 * j, 2 * j, Dj);
+        double s0j, c0j;
+        sincos(yb.x, &s0j, &c0j);
+        float s0f, c0f;
+        __sincosf((float)yb.x, &s0f, &c0f);
+        const double v[SH_REC] = {rr0.x, rr0.y, rr1.x, rr1.y, rr2.x, rr2.y, yb.x, yb.y, Dj[0], Dj[1], Dj[2], Dj[3],
+                                  yb.x, s0j, c0j, (double)s0f, (double)c0f, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < SH_REC; k++) rc[k] = v[k];
+        p.flags[j] = 0;
+        return;
+    }
+    if (!own) return;
+    double2 rr0 = make_double2(rc[0], rc[1]), rr1 = make_double2(rc[2], rc[3]), rr2 = make_double2(rc[4], rc[5]);
+    double2 yb = make_double2(rc[6], rc[7]);
+    double Dj[4] = {rc[8], rc[9], rc[10], rc[11]};
+    const double ma0 = rc[12], s0j = rc[13], c0j = rc[14];
+    const double s0f = rc[15], c0f = rc[16];
+    int fl = p.flags[j];
+    const ekf_line ln = p.lines[p.line < 0 ? 0 : p.line];
+    double Rm[4];
+    line_R(ln, p.line, p.r_mode, Rm);
+
+    if (p.phase == SH_GATE || p.phase == SH_PACKAGE) {
+        // gating of the owned candidate (Robot.cpp:313-498) exactly as the sequential path
+        if (p.phase == SH_PACKAGE && j != p.jstar) return;
+        if (!(j < p.s) || (fl & 1)) {
+            if (p.phase == SH_GATE) p.flags[j] = fl & 1;
+            return;
+        }
+        Block5 b5;
+        fill_block5(b5, R33, rr0, rr1, rr2, Dj);
+        double sn, cs;
+        Cand c;
+        bool pass = false, sing = false;
+        if (!quick_reject(b5, yb.x, yb.y, ma0, s0f, c0f, xp, ln.alpha, ln.r, Rm, p.gate) &&
+            (sincos_near(yb.x, ma0, s0j, c0j, sn, cs),
+             !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate))) {
+            eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, c);
+            sing = c.singular;
+            pass = c.pass;
+        }
+        if (p.phase == SH_GATE) {
+            p.flags[j] = (fl & 1) | (sing ? 2 : 0);
+            if (pass) atomicMin(p.out, j);
+            return;
+        }
+        // the winner's package and its V rows of the earlier matches (Robot.cpp:560-568)
+        build_package(c, R33, rr0, rr1, rr2, p.pkg);
+        for (int q = 0; q < p.m; q++) {
+            const double* h = p.hist + ((size_t)j * d.max_lines + q) * 8 + 4;
+            p.pkg[MB_VH + 4 * q + 0] = h[0];
+            p.pkg[MB_VH + 4 * q + 1] = h[1];
+            p.pkg[MB_VH + 4 * q + 2] = h[2];
+            p.pkg[MB_VH + 4 * q + 3] = h[3];
+        }
+        return;
+    }
+
+    if (p.phase == SH_APPLY) {
+        // GSL_EDOM counts only for the candidates the reference evaluates (up to the winner)
+        int st = (fl & 2) && j <= (p.jstar < 0 ? 0x7fffffff : p.jstar) ? (int)EKF_ST_SINGULAR : 0;
+        if (p.r_mode == 1 && (p.line == 1 || p.line == 2)) st |= EKF_ST_NSYM;
+        if (st) atomicOr(p.out + 1, st);
+        if (p.jstar < 0) return;
+        double blk[4];
+        pll_block(pv, 2 * j, 2 * p.jstar, blk);
+        const double* pk = p.pkg;
+        const int m = p.m;
+        double kk[4], uu[4];
+        gain_rows<0>(pk, m,
+                     [&](int q) {
+                         const double* h = p.hist + ((size_t)j * d.max_lines + q) * 8;
+                         return make_double4(h[0], h[1], h[2], h[3]);
+                     },
+                     [&](int q) {
+                         const double* vh = pk + MB_VH + 4 * q;
+                         return make_double4(vh[0], vh[1], vh[2], vh[3]);
+                     },
+                     blk, rr0, rr1, rr2, yb, Dj, kk, uu);
+        float F[3] = {0.f, 0.f, 0.f};
+        if (sym) sym_factor(pk, F);
+        // store_rows (the scan kernel's non-staged form: the same values)
+        double* h = p.hist + ((size_t)j * d.max_lines + m) * 8;
+        h[0] = uu[0]; h[1] = uu[1]; h[2] = uu[2]; h[3] = uu[3];
+        h[4] = kk[0]; h[5] = kk[1]; h[6] = kk[2]; h[7] = kk[3];
+        C* Uop = reinterpret_cast<C*>(p.cur.Uop);
+        C* Vop = reinterpret_cast<C*>(p.cur.Vop);
+#pragma unroll
+        for (int pp = 0; pp < 2; pp++) {
+            const int lr = 2 * j + pp;
+            if constexpr (sizeof(C) == 4) {
+                double o0 = uu[2 * pp], o1 = uu[2 * pp + 1], v0 = kk[2 * pp], v1 = kk[2 * pp + 1];
+                if (sym) {
+                    v0 = kk[2 * pp] * (double)F[0] + kk[2 * pp + 1] * (double)F[1];
+                    v1 = kk[2 * pp + 1] * (double)F[2];
+                    o0 = (double)(float)v0;
+                    o1 = (double)(float)v1;
+                }
+                Uop[op_index_f32(lr, 2 * m, d.kmax)] = to_domain<T>(-o0, pv.ex);
+                Uop[op_index_f32(lr, 2 * m + 1, d.kmax)] = to_domain<T>(-o1, pv.ex);
+                Vop[op_index_f32(lr, 2 * m, d.kmax)] = (C)v0;
+                Vop[op_index_f32(lr, 2 * m + 1, d.kmax)] = (C)v1;
+            } else {
+                Uop[op_index_f64(lr, 2 * m, d.kmax)] = (C)(-uu[2 * pp]);
+                Uop[op_index_f64(lr, 2 * m + 1, d.kmax)] = (C)(-uu[2 * pp + 1]);
+                Vop[op_index_f64(lr, 2 * m, d.kmax)] = (C)kk[2 * pp];
+                Vop[op_index_f64(lr, 2 * m + 1, d.kmax)] = (C)kk[2 * pp + 1];
+            }
+        }
+        if (j == p.jstar) fl |= 1;
+        p.flags[j] = fl & 1;
+        const double v[12] = {rr0.x, rr0.y, rr1.x, rr1.y, rr2.x, rr2.y, yb.x, yb.y, Dj[0], Dj[1], Dj[2], Dj[3]};
+#pragma unroll
+        for (int k = 0; k < 12; k++) rc[k] = v[k];
+        return;
+    }
+
+    // SH_END: the owned strip columns and mean, the operand padding past the matches
+    *reinterpret_cast<double2*>(p.Rs + b0) = rr0;
+    *reinterpret_cast<double2*>(p.Rs + n + b0) = rr1;
+    *reinterpret_cast<double2*>(p.Rs + 2 * n + b0) = rr2;
+    *reinterpret_cast<double2*>(p.y + b0) = yb;
+    C* Uop = reinterpret_cast<C*>(p.cur.Uop);
+    C* Vop = reinterpret_cast<C*>(p.cur.Vop);
+    for (int k = 2 * p.m; k < d.kmax; k++)
+#pragma unroll
+        for (int pp = 0; pp < 2; pp++) {
+            if constexpr (sizeof(C) == 4) {
+                Uop[op_index_f32(2 * j + pp, k, d.kmax)] = (C)(-0.0f);
+                Vop[op_index_f32(2 * j + pp, k, d.kmax)] = (C)0.0f;
+            } else {
+                Uop[op_index_f64(2 * j + pp, k, d.kmax)] = (C)(-0.0);
+                Vop[op_index_f64(2 * j + pp, k, d.kmax)] = (C)0.0;
+            }
+        }
+    if (gid == 0) {
+        // commit (Robot.cpp:702-716), no augmentation or reset (the host refuses those scans)
+        double pose[3] = {xp[0], xp[1], xp[2]};
+        if (p.L == 0 || p.m == 0) pose[2] = normalize_radian(xp[2]);
+        for (int a = 0; a < 9; a++) p.Rs[(a / 3) * n + (a % 3)] = R33[a];
+        p.y[0] = xp[0]; p.y[1] = xp[1]; p.y[2] = xp[2];
+        p.pose[0] = pose[0]; p.pose[1] = pose[1]; p.pose[2] = pose[2];
+        int* res = p.cur.res;
+        res[RES_NLINES] = p.L;
+        res[RES_SAVED_IN] = p.s;
+        res[RES_DBG] = 16;
+        res[RES_STATUS] = 0;
+        res[RES_M] = p.m;
+        res[RES_NEXTRA] = 0;
+        res[RES_SAVED] = p.s;
+        res[RES_RESET] = 0;
+        res[RES_NADD] = 0;
+        res[RES_KSTEPS] = (sizeof(C) == 4) ? p.m : (p.m + 1) / 2;
+        res[RES_ROLLBACK] = 0;
+        for (int i = 0; i < p.L; i++) res[RES_MATCH + i] = p.match[i];
+    }
+}
+
 #pragma clang fp contract(fast)
 
 // ---------------------------------------------------------------------------------------
@@ -4383,6 +4656,16 @@ size_t scan_lds_bytes(int precision)
         : (precision == EKF_PREC_F16) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<_Float16>))
         : hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<float>));
     return err == hipSuccess ? a.sharedSizeBytes : 0;
+}
+
+hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st)
+{
+    const int cnt = p.b - p.a;
+    const unsigned grid = (unsigned)((cnt + 255) / 256 > 0 ? (cnt + 255) / 256 : 1);
+    if (precision == EKF_PREC_F64) hipLaunchKernelGGL(shard_kernel<double>, dim3(grid), dim3(256), 0, st, p);
+    else if (precision == EKF_PREC_F32) hipLaunchKernelGGL(shard_kernel<float>, dim3(grid), dim3(256), 0, st, p);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
 }
 
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)

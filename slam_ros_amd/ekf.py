@@ -36,6 +36,9 @@ EXPORTED = [
     "ekf_landmark_block_bytes",
     "ekf_state_dim", "ekf_profile_enable", "ekf_profile_read", "ekf_profile_flushes",
     "ekf_flush_kernel_name", "ekf_debug_scan_stamps", "ekf_debug_result_words",
+    "ekf_shard_init", "ekf_shard_begin", "ekf_shard_gate", "ekf_shard_package_words", "ekf_shard_package",
+    "ekf_shard_apply", "ekf_shard_end", "ekf_shard_operand_bytes", "ekf_shard_operands", "ekf_shard_commit",
+    "ekf_shard_status",
 ]
 
 
@@ -118,6 +121,17 @@ def load_library(path: str = ""):
         "ekf_flush_kernel_name": (ctypes.c_char_p, [vp, ctypes.c_int]),
         "ekf_debug_scan_stamps": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_ulonglong)]),
         "ekf_debug_result_words": (ctypes.c_int, [vp, ctypes.c_int, ip]),
+        "ekf_shard_init": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int]),
+        "ekf_shard_begin": (ctypes.c_int, [vp, dp, vp, ctypes.c_int]),
+        "ekf_shard_gate": (ctypes.c_int, [vp, ctypes.c_int, ip]),
+        "ekf_shard_package_words": (ctypes.c_int, [vp]),
+        "ekf_shard_package": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, dp]),
+        "ekf_shard_apply": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, dp]),
+        "ekf_shard_end": (ctypes.c_int, [vp]),
+        "ekf_shard_operand_bytes": (sz, [vp]),
+        "ekf_shard_operands": (ctypes.c_int, [vp, vp, vp, ctypes.c_int]),
+        "ekf_shard_commit": (ctypes.c_int, [vp]),
+        "ekf_shard_status": (ctypes.c_int, [vp, ip]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
