@@ -199,9 +199,12 @@ int ekf_ellipse_of_block(const double P22[4], float axii[2], float* angle);
  *     ekf_shard_package(i, j*, pkg)          on j*'s owner: S, S^-1, v, H, K/U robot rows, V history
  *     broadcast pkg from the owner
  *     ekf_shard_apply(i, j* or -1, pkg)      gain rows of the owned landmarks, robot update
- *   ekf_shard_end()                          commit (a scan that would add landmarks or reset the
- *                                            map is refused with EKF_EINVAL: not sharded)
+ *   ekf_shard_end()                          commit; augmentation (Robot.cpp:776-866): each rank
+ *                                            writes its columns of the new landmarks' rows, the
+ *                                            owner of a new landmark its strip columns and mean;
+ *                                            the capacity reset (Robot.cpp:893-904)
  *   ekf_shard_operands(U, V, 0) / all-gather the owned rows / ekf_shard_operands(U, V, 1)
+ *   ekf_shard_patch(rows, 0) / all-gather the owned columns / ekf_shard_patch(rows, 1)
  *   ekf_shard_commit()                       the step joins the deferred flush, which runs on the
  *                                            wave-tiles holding an owned row block only
  * With the same inputs the owned rows of P, the owned mean entries, the robot block and the pose
@@ -215,6 +218,8 @@ int ekf_shard_apply(ekf_ctx* ctx, int line, int jstar, const double* pkg);
 int ekf_shard_end(ekf_ctx* ctx);
 size_t ekf_shard_operand_bytes(const ekf_ctx* ctx);   /* bytes of each of U and V */
 int ekf_shard_operands(ekf_ctx* ctx, void* U, void* V, int upload);
+size_t ekf_shard_patch_bytes(const ekf_ctx* ctx);   /* bytes of the new-landmark rows [max_lines][2][2N] */
+int ekf_shard_patch(ekf_ctx* ctx, double* rows, int upload);
 int ekf_shard_commit(ekf_ctx* ctx);
 int ekf_shard_status(ekf_ctx* ctx, int* status);   /* status bits of the scan (GSL_EDOM, NSYM) */
 

@@ -1285,6 +1285,7 @@ static ekf::ShardParams shard_params(ekf_ctx* c, int phase)
     p.lines = c->d_lines;
     p.pexp = c->pexp;
     p.match = c->sh_match;
+    p.reset_margin = c->cfg.reset_margin;
     return p;
 }
 
@@ -1316,8 +1317,8 @@ extern "C" int ekf_shard_init(ekf_ctx* c, int first, int end)
     HIP_TRY(hipMalloc((void**)&c->sh_pkg, sizeof(double) * shard_words(c)));
     HIP_TRY(hipMalloc((void**)&c->sh_flags, sizeof(int) * N));
     HIP_TRY(hipMalloc((void**)&c->sh_out, sizeof(int) * 2));
-    HIP_TRY(hipMalloc((void**)&c->sh_match, sizeof(int) * c->d.max_lines));
-    c->sh_match_h.assign(c->d.max_lines, -1);
+    HIP_TRY(hipMalloc((void**)&c->sh_match, sizeof(int) * 2 * c->d.max_lines));
+    c->sh_match_h.assign(2 * c->d.max_lines, -1);
     // the flush's wave-tiles restricted to those holding a tile of an owned row block (a tile of
     // two ranks' rows is kept by both, identically); groups of 2 and 4 steps take the wave form too
     const int rb0 = (2 * first) / ekf::TILE, rb1 = (2 * end - 1) / ekf::TILE;
@@ -1370,7 +1371,7 @@ extern "C" int ekf_shard_begin(ekf_ctx* c, const double enc[3], const ekf_line* 
     c->sh_L = nlines;
     c->sh_s = s;
     c->sh_nextra = 0;
-    c->sh_match_h.assign(c->d.max_lines, -1);
+    c->sh_match_h.assign(2 * c->d.max_lines, -1);
     HIP_TRY(hipMemsetAsync(c->sh_out, 0, sizeof(int) * 2, c->stream));
     HIP_TRY(ekf::launch_shard(shard_params(c, ekf::SH_BEGIN), c->cfg.precision, c->stream));
     c->sh_open = 1;
@@ -1420,6 +1421,7 @@ extern "C" int ekf_shard_apply(ekf_ctx* c, int line, int jstar, const double* pk
         c->sh_match_h[line] = jstar;
         c->sh_m++;
     } else {
+        c->sh_match_h[c->d.max_lines + c->sh_nextra] = line;
         c->sh_nextra++;
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1445,13 +1447,27 @@ extern "C" int ekf_shard_operands(ekf_ctx* c, void* U, void* V, int upload)
 extern "C" int ekf_shard_end(ekf_ctx* c)
 {
     if (!c || !c->sh_open) return EKF_EINVAL;
-    // augmentation and the capacity reset need the whole robot strip on the new landmark's owner:
-    // not sharded; such scans are refused before anything is committed
-    const int nadd = std::min(c->sh_nextra, c->d.N - c->sh_s);
-    if (nadd > 0 || c->sh_s + nadd > c->d.N - c->cfg.reset_margin) return EKF_EINVAL;
-    HIP_TRY(hipMemcpyAsync(c->sh_match, c->sh_match_h.data(), sizeof(int) * c->d.max_lines,
+    HIP_TRY(hipMemcpyAsync(c->sh_match, c->sh_match_h.data(), sizeof(int) * 2 * c->d.max_lines,
                            hipMemcpyHostToDevice, c->stream));
     HIP_TRY(ekf::launch_shard(shard_params(c, ekf::SH_END), c->cfg.precision, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return EKF_OK;
+}
+
+extern "C" size_t ekf_shard_patch_bytes(const ekf_ctx* c)
+{
+    return c ? sizeof(double) * c->d.max_lines * 2 * c->d.M : 0;
+}
+
+// The step's new-landmark rows (patch buffer, [max_lines][2][M]): each rank writes the columns of
+// its landmarks; the caller all-gathers them like the operand rows (upload = 1 sets them)
+extern "C" int ekf_shard_patch(ekf_ctx* c, double* rows, int upload)
+{
+    if (!c || !c->sh_open || !rows) return EKF_EINVAL;
+    const ekf::Slot& cur = slot_of(c, c->nsteps);
+    const size_t bytes = ekf_shard_patch_bytes(c);
+    HIP_TRY(hipMemcpyAsync(upload ? (void*)cur.patch : (void*)rows, upload ? (const void*)rows : (const void*)cur.patch,
+                           bytes, upload ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return EKF_OK;
 }

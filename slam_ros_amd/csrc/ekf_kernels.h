@@ -145,7 +145,8 @@ struct ShardParams {
     const double* enc;    // [3]
     const ekf_line* lines;// [max_lines]
     const int* pexp;
-    const int* match;     // [max_lines] the lines' winners (SH_END)
+    const int* match;     // [2][max_lines] the lines' winners, then the unmatched lines in order (SH_END)
+    int reset_margin;
 };
 hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st);
 

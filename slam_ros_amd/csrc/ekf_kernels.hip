@@ -2846,7 +2846,65 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
         return;
     }
 
-    // SH_END: the owned strip columns and mean, the operand padding past the matches
+    // SH_END: augmentation (Robot.cpp:776-866) as the scan kernel's commit: the new landmarks'
+    // rows (this rank's columns of them to the step's patch buffer, all-gathered by the caller),
+    // the new landmark's strip columns and mean on its owner, the 2×2 diagonal blocks on every
+    // rank; the capacity reset (Robot.cpp:893-904)
+    double pose[3] = {xp[0], xp[1], xp[2]};
+    if (p.L == 0 || p.m == 0) pose[2] = normalize_radian(xp[2]);
+    const int N = d.N, M = d.M;
+    const int nadd = min(p.nextra, N - p.s);
+    const int reset = (p.s + nadd > N - p.reset_margin) ? 1 : 0;
+    double* patch = p.cur.patch;
+    double* pdiag = p.cur.patch_diag;
+    if (!reset) {
+        for (int q = 0; q < nadd; q++) {
+            const ekf_line lq = p.lines[p.match[d.max_lines + q]];
+            const int sq = p.s + q;
+            double alfa = lq.alpha;
+            const double r = lq.r + (pose[0] * cos(alfa) + pose[1] * sin(alfa));
+            alfa += pose[2];
+            double sa, ca;
+            sincos(alfa, &sa, &ca);
+            if (j < sq) {
+                double* prow = patch + (size_t)(q * 2) * M;
+                *reinterpret_cast<double2*>(prow + 2 * j) = rr2;
+                double2 gx;
+                gx.x = ca * rr0.x + sa * rr1.x;
+                gx.y = ca * rr0.y + sa * rr1.y;
+                *reinterpret_cast<double2*>(prow + M + 2 * j) = gx;
+            }
+            if (j == sq) {
+                rr0 = make_double2(R33[6], ca * R33[0] + sa * R33[3]);
+                rr1 = make_double2(R33[7], ca * R33[1] + sa * R33[4]);
+                rr2 = make_double2(R33[8], ca * R33[2] + sa * R33[5]);
+                yb = make_double2(normalize_radian(alfa), r);
+            }
+            if (gid == 0) {
+                const double Gx[6] = {0, 0, 1, ca, sa, 0};
+                const double Gl[4] = {1.0, 0, xp[1] * ca - xp[0] * sa, 1};
+                double GP[6], GlR[4];
+                for (int a = 0; a < 2; a++)
+                    for (int b = 0; b < 3; b++) {
+                        double acc = 0.0;
+                        for (int k = 0; k < 3; k++) acc += Gx[a * 3 + k] * R33[k * 3 + b];
+                        GP[a * 3 + b] = acc;
+                    }
+                for (int a = 0; a < 2; a++)
+                    for (int b = 0; b < 2; b++)
+                        GlR[a * 2 + b] = Gl[a * 2 + 0] * lq.R[0 * 2 + b] + Gl[a * 2 + 1] * lq.R[1 * 2 + b];
+                for (int a = 0; a < 2; a++)
+                    for (int b = 0; b < 2; b++) {
+                        double gsum = 0.0;
+                        for (int k = 0; k < 3; k++) gsum += GP[a * 3 + k] * Gx[b * 3 + k];
+                        const double hh = GlR[a * 2 + 0] * Gl[b * 2 + 0] + GlR[a * 2 + 1] * Gl[b * 2 + 1];
+                        pdiag[q * 4 + a * 2 + b] = gsum + hh;
+                    }
+            }
+        }
+    }
+    if (reset) rr0 = rr1 = rr2 = yb = make_double2(0.0, 0.0);
+    // the owned strip columns and mean, the operand padding past the matches
     *reinterpret_cast<double2*>(p.Rs + b0) = rr0;
     *reinterpret_cast<double2*>(p.Rs + n + b0) = rr1;
     *reinterpret_cast<double2*>(p.Rs + 2 * n + b0) = rr2;
@@ -2865,9 +2923,7 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
             }
         }
     if (gid == 0) {
-        // commit (Robot.cpp:702-716), no augmentation or reset (the host refuses those scans)
-        double pose[3] = {xp[0], xp[1], xp[2]};
-        if (p.L == 0 || p.m == 0) pose[2] = normalize_radian(xp[2]);
+        // commit (Robot.cpp:702-716)
         for (int a = 0; a < 9; a++) p.Rs[(a / 3) * n + (a % 3)] = R33[a];
         p.y[0] = xp[0]; p.y[1] = xp[1]; p.y[2] = xp[2];
         p.pose[0] = pose[0]; p.pose[1] = pose[1]; p.pose[2] = pose[2];
@@ -2875,15 +2931,17 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
         res[RES_NLINES] = p.L;
         res[RES_SAVED_IN] = p.s;
         res[RES_DBG] = 16;
-        res[RES_STATUS] = 0;
+        res[RES_STATUS] = (p.nextra > nadd) ? EKF_ST_CAP : 0;
         res[RES_M] = p.m;
-        res[RES_NEXTRA] = 0;
-        res[RES_SAVED] = p.s;
-        res[RES_RESET] = 0;
-        res[RES_NADD] = 0;
+        res[RES_NEXTRA] = p.nextra;
+        res[RES_SAVED] = reset ? 0 : p.s + nadd;
+        res[RES_RESET] = reset;
+        res[RES_NADD] = reset ? 0 : nadd;
         res[RES_KSTEPS] = (sizeof(C) == 4) ? p.m : (p.m + 1) / 2;
         res[RES_ROLLBACK] = 0;
         for (int i = 0; i < p.L; i++) res[RES_MATCH + i] = p.match[i];
+        for (int q = 0; q < p.nextra; q++) res[RES_EXTRA + q] = p.match[d.max_lines + q];
+        p.saved[0] = reset ? 0 : p.s + nadd;
     }
 }
 

@@ -37,7 +37,8 @@ EXPORTED = [
     "ekf_state_dim", "ekf_profile_enable", "ekf_profile_read", "ekf_profile_flushes",
     "ekf_flush_kernel_name", "ekf_debug_scan_stamps", "ekf_debug_result_words",
     "ekf_shard_init", "ekf_shard_begin", "ekf_shard_gate", "ekf_shard_package_words", "ekf_shard_package",
-    "ekf_shard_apply", "ekf_shard_end", "ekf_shard_operand_bytes", "ekf_shard_operands", "ekf_shard_commit",
+    "ekf_shard_apply", "ekf_shard_end", "ekf_shard_operand_bytes", "ekf_shard_operands", "ekf_shard_patch_bytes",
+    "ekf_shard_patch", "ekf_shard_commit",
     "ekf_shard_status",
 ]
 
@@ -130,6 +131,8 @@ def load_library(path: str = ""):
         "ekf_shard_end": (ctypes.c_int, [vp]),
         "ekf_shard_operand_bytes": (sz, [vp]),
         "ekf_shard_operands": (ctypes.c_int, [vp, vp, vp, ctypes.c_int]),
+        "ekf_shard_patch_bytes": (sz, [vp]),
+        "ekf_shard_patch": (ctypes.c_int, [vp, dp, ctypes.c_int]),
         "ekf_shard_commit": (ctypes.c_int, [vp]),
         "ekf_shard_status": (ctypes.c_int, [vp, ip]),
     }

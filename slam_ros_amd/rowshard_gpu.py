@@ -12,15 +12,16 @@ Robot.cpp:126-904, sequential association):
     ekf_shard_package (owner)      S, S⁻¹, v, H row, K·S and K robot rows, the winner's V history
     broadcast from the owner
     ekf_shard_apply                gain rows of the owned landmarks (Robot.cpp:522-602), robot update
-  ekf_shard_end                    commit (Robot.cpp:702-716)
+  ekf_shard_end                    commit (Robot.cpp:702-716), augmentation (Robot.cpp:776-866): each
+                                   rank its columns of the new landmarks' rows, the new landmark's
+                                   owner its strip columns and mean; the reset (Robot.cpp:893-904)
   all-gather of the operand rows   the step's U/V rows: the flush of a tile needs the rows of both
-                                   its row and its column block (the n×2m exchange of rowshard.py)
+                                   its row and its column block (the n×2m exchange of rowshard.py),
+  and of the new-landmark rows     and the new rows' columns of every rank
   ekf_shard_commit                 the step joins the flush schedule
 
 The collectives go through torch.distributed (gloo: host-staged, as the tests run two ranks on one
-GPU; on an 8-GPU node the same calls run over RCCL on device tensors). Scans that would add
-landmarks or reset the map are refused (EKF_EINVAL): augmentation needs the whole robot strip on
-the new landmark's owner, which this form does not exchange (rowshard.py specifies it).
+GPU; on an 8-GPU node the same calls run over RCCL on device tensors).
 """
 from __future__ import annotations
 
@@ -91,6 +92,10 @@ class ShardedInstance:
         rows = operand_rows(nb, kmax, self.f64)
         self.mask = [(rows >= 2 * a) & (rows < 2 * b) for a, b in self.ranges]
         self.dtype = dt
+        # the patch buffer [max_lines][2][2N]: column c belongs to landmark c // 2
+        self.pwords = self.lib.ekf_shard_patch_bytes(self.h) // 8
+        cols = np.tile(np.arange(2 * capacity), self.pwords // (2 * capacity))
+        self.pmask = [(cols >= 2 * a) & (cols < 2 * b) for a, b in self.ranges]
 
     # state: every rank starts from the same full state, then keeps its rows
     def init_lowrank(self, diag, U, y, saved, pose):
@@ -153,6 +158,15 @@ class ShardedInstance:
             Vc[m] = gv[r].numpy()[m]
         E._check(lib.ekf_shard_operands(h, Uc.ctypes.data_as(ctypes.c_void_p), Vc.ctypes.data_as(ctypes.c_void_p), 1),
                  "ekf_shard_operands")
+        if out.count(-1):   # new landmarks: their rows' columns from every rank
+            pr = np.empty(self.pwords)
+            E._check(lib.ekf_shard_patch(h, E._dp(pr), 0), "ekf_shard_patch")
+            gp = [torch.empty(pr.shape, dtype=torch.float64) for _ in range(self.world)]
+            dist.all_gather(gp, torch.from_numpy(pr), group=self.group)
+            pc = pr.copy()
+            for r in range(self.world):
+                pc[self.pmask[r]] = gp[r].numpy()[self.pmask[r]]
+            E._check(lib.ekf_shard_patch(h, E._dp(pc), 1), "ekf_shard_patch")
         E._check(lib.ekf_shard_commit(h), "ekf_shard_commit")
         return out
 

@@ -4,7 +4,8 @@ two gloo ranks on the one GPU of the test box, each a context owning half of the
 the owned rows of P (all columns), the robot block and strip columns of the owned landmarks, the
 owned entries of the mean, the pose and every association are bit-identical (the phases run the
 scan kernel's sequential-path expressions; the flush is the product wave kernel on the wave-tiles
-that hold an owned row block, with the all-gathered operand rows)."""
+that hold an owned row block, with the all-gathered operand rows), augmentation and the capacity
+reset included."""
 import os
 import socket
 import subprocess
@@ -25,24 +26,39 @@ def free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("prec,N,T,scans", [(1, 1024, 4, 9), (1, 1000, 6, 8), (0, 512, 4, 6)])
-def test_two_rank_shard_equals_single_context(ekf_mod, tmp_path, prec, N, T, scans):
-    w = G.make_world(N)
+@pytest.mark.parametrize("prec,N,T,scans,active,extra_every",
+                         [(1, 1024, 4, 9, 0, 0), (1, 1000, 6, 8, 0, 0), (0, 512, 4, 6, 0, 0),
+                          (1, 1024, 4, 9, 1000, 3), (1, 256, 4, 6, 0, 3), (0, 480, 4, 7, 400, 2)])
+def test_two_rank_shard_equals_single_context(ekf_mod, tmp_path, prec, N, T, scans, active, extra_every):
+    """(active, extra_every): every extra_every-th scan carries two unmatched lines — augmented
+    landmarks landing on either rank, and (active = N − 10) the capacity reset."""
+    w = G.make_world(N, active=active or N - 10)
     st = G.initial_state(w)
     one = ekf_mod.Ensemble(N, 1, prec, max_lines=8, flush_interval=T)
     one.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
-    ref_matches = []
+    ref_matches, resets, added = [], 0, 0
+    rng = np.random.default_rng(11)
     for step in range(1, scans + 1):
-        enc, lines, nl = G.make_scan(w, step, instances=1)
-        r = one.localize(enc, lines, nl)
-        ref_matches.append(r[0]["match"][:nl[0]])
+        enc, lines, nl = G.make_scan(w, step, instances=1, lines=6 if extra_every else 8)
+        ln = lines[0, :nl[0]]
+        if extra_every and step % extra_every == 0:
+            ln = np.concatenate([ln, G.random_lines(rng, 2)])
+        la = np.zeros((1, 8, 6))
+        la[0, :len(ln)] = ln
+        r = one.localize(enc, la, np.array([len(ln)], dtype=np.int32))
+        ref_matches.append(list(r[0]["match"][:len(ln)]) + [-2] * (8 - len(ln)))
+        resets += r[0]["reset"]
+        added += r[0]["new_landmarks"]
     P, y, saved, pose = one.download_state(0)
     one.close()
+    if extra_every:
+        assert added > 0 or resets > 0
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "tests", "rowshard_gpu_worker.py"), "--out", str(tmp_path), "--N", str(N),
-           "--T", str(T), "--scans", str(scans), "--precision", str(prec)]
+           "--T", str(T), "--scans", str(scans), "--precision", str(prec), "--active", str(active),
+           "--extra-every", str(extra_every)]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-3000:]
     covered = 0
@@ -50,32 +66,12 @@ def test_two_rank_shard_equals_single_context(ekf_mod, tmp_path, prec, N, T, sca
         d = np.load(tmp_path / f"rank{r}.npz")
         idx = d["rows"]
         covered += len(idx)
-        assert [list(m) for m in d["matches"]] == [list(m) for m in ref_matches], r
-        assert all(len(m) == 8 and min(m) >= 0 for m in ref_matches)   # the sharded form needs no augmentation
+        assert [list(m) for m in d["matches"]] == ref_matches, r
         np.testing.assert_array_equal(d["P_rows"], P[idx])            # owned rows, every column
         np.testing.assert_array_equal(d["P_robot"][:, :3], P[:3, :3])
         np.testing.assert_array_equal(d["P_robot"][:, idx], P[:3, idx])
         np.testing.assert_array_equal(d["y"][idx], y[idx])
         np.testing.assert_array_equal(d["y"][:3], y[:3])
         np.testing.assert_array_equal(d["pose"], pose)
-        assert int(d["saved"]) == saved and int(d["status"]) == 0
+        assert int(d["saved"]) == saved
     assert covered == 2 * N
-
-
-def test_shard_refuses_augmentation(ekf_mod):
-    """A scan with an unmatched line (a new landmark) is refused before anything is committed."""
-    import torch.distributed as dist
-    from slam_ros_amd import rowshard_gpu as R
-    if not dist.is_initialized():
-        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
-    N = 256
-    w = G.make_world(N)
-    st = G.initial_state(w)
-    inst = R.ShardedInstance(N, 1, max_lines=8, flush_interval=4)
-    inst.init_lowrank(st.diag, st.U, st.y, st.saved, st.pose)
-    enc, lines, nl = G.make_scan(w, 1, instances=1)
-    extra = G.random_lines(np.random.default_rng(2), 1)
-    with pytest.raises(ekf_mod.EkfError):
-        inst.localize(np.concatenate([lines[0, :7], extra]), enc[0])
-    inst.close()
-    dist.destroy_process_group()
