@@ -35,6 +35,9 @@ for c in cfgs:
     n = stp[9] or 1
     out = {v: round(stp[k] * 10e-3 / n, 2) for k, v in NAMES.items()}
     out["fallbacks"] = stp[15]
+    out["after_records:rw_start"] = round(stp[29] * 10e-3 / n, 2)   # replay wave's chain starts
+    out["after_records:rw_end"] = round(stp[30] * 10e-3 / n, 2)     # ... ends
+    out["after_records:lw0_end"] = round(stp[31] * 10e-3 / n, 2)    # landmark wave 0 done
     out["gate_waves"] = stp[22]                  # (wave, line) gate evaluations, workgroup 0
     out["past_quick_filter"] = stp[20]           # ... with a lane past the quick certified filter
     out["past_f32_filter"] = stp[21]             # ... past the fp32 certified filter

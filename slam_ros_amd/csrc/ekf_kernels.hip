@@ -1943,6 +1943,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             }
             EKF_STAMP(12);
+            __shared__ unsigned long long sh_trec;   // diagnostics: the records' end (thread 0, WG 0)
+            if (dbg) sh_trec = t_last;
             // ---- (f) the winners' part of the sequential chain, in the last wave (lane u carries
             // winner u's rows): per line the winner's lane evaluates it and writes the package,
             // then the later winners' lanes apply their gain rows. Meanwhile (g) the landmark
@@ -2029,7 +2031,12 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 bad = __any(bad) ? 1 : 0;
                 if (u == 0) {
                     sh_flag = bad;
-                    if (p.dbg && g == 0) sh_stamp[13] += __builtin_amdgcn_s_memrealtime() - t_l0;
+                    if (p.dbg && g == 0) {
+                        const unsigned long long te = __builtin_amdgcn_s_memrealtime();
+                        sh_stamp[13] += te - t_l0;
+                        sh_stamp[29] += t_l0 - sh_trec;   // the replay wave's chain starts ...
+                        sh_stamp[30] += te - sh_trec;     // ... and ends, after the records
+                    }
                 }
             } else {
                 // ---- (e) owned blocks of the guessed columns (Robot.cpp:560 operands), while the
@@ -2213,6 +2220,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     m++;
                 }
             }
+            if (dbg) sh_stamp[31] += __builtin_amdgcn_s_memrealtime() - sh_trec;   // landmark wave 0 done
             __syncthreads();
             viol |= sh_flag;
             status |= sh_rwst;
