@@ -1348,7 +1348,7 @@ __device__ __forceinline__ void plane_replay(const Slot* pend, int e, size_t ins
 // whose exact first passing candidate differs from the guess. Three exchanges per scan instead
 // of one per line; on a flag the scan restarts on the sequential path (identical results).
 
-template <typename T>
+template <typename T, bool ST>
 __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
 {
     const Dims d = p.d;
@@ -1413,8 +1413,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // fp32 operand storage (fp32 and fp16 P): the split-bf16 planes, the MFMA replay
     constexpr bool kPlanes = sizeof(typename Stor<T>::C) == 4;
     __shared__ __attribute__((aligned(16))) float sh_vpl[kPlanes ? SCAN_THREADS * 32 : 4];
-    unsigned long long* dbg = (p.dbg && lead) ? p.dbg + (size_t)e * EKF_NSTAMP : nullptr;
-    if (p.dbg && tid < EKF_NSTAMP) sh_stamp[tid] = 0;
+    // phase timers only in the ST instantiation (EKF_SCAN_STAMPS=1): the product kernel carries
+    // no timer code at all (its uniform branches and registers cost ≈2 µs per scan)
+    unsigned long long* const pdbg = ST ? p.dbg : nullptr;
+    unsigned long long* dbg = (pdbg && lead) ? pdbg + (size_t)e * EKF_NSTAMP : nullptr;
+    if (pdbg && tid < EKF_NSTAMP) sh_stamp[tid] = 0;
     unsigned long long t_last = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const unsigned long long t_first = t_last;
 
@@ -1970,7 +1973,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     sincos(wma0, &ws0, &wc0);   // sincos_near's scan-start values (as the owner's)
                 }
                 int ml = 0, bad = 0;
-                const bool lst = p.dbg && g == 0 && u == 0;
+                const bool lst = pdbg && g == 0 && u == 0;
                 unsigned long long tl = lst ? __builtin_amdgcn_s_memrealtime() : 0ull;
                 for (int t = 0; t < L; t++) {
                     if (sh_spec[t] < 0) continue;
@@ -2031,7 +2034,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 bad = __any(bad) ? 1 : 0;
                 if (u == 0) {
                     sh_flag = bad;
-                    if (p.dbg && g == 0) {
+                    if (pdbg && g == 0) {
                         const unsigned long long te = __builtin_amdgcn_s_memrealtime();
                         sh_stamp[13] += te - t_l0;
                         sh_stamp[29] += t_l0 - sh_trec;   // the replay wave's chain starts ...
@@ -2190,7 +2193,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         // the guess must be the first passing unmatched landmark
                         if (pass && (w < 0 || j < w)) viol = 1;
                     }
-                    if (p.dbg && g == 0) {   // waves of workgroup 0 whose lanes went deeper
+                    if (pdbg && g == 0) {   // waves of workgroup 0 whose lanes went deeper
                         const bool d1 = __any(deep >= 1), d2 = __any(deep >= 2), d3 = __any(deep >= 3);
                         if ((tid & 63) == 0) {
                             if (d1) atomicAdd(&sh_stamp[20], 1ull);
@@ -4708,9 +4711,9 @@ int scan_blocks_per_cu(int precision)
 {
     int nb = 0;
     hipError_t err =
-        (precision == EKF_PREC_F64) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<double>, SCAN_BLOCK, 0)
-        : (precision == EKF_PREC_F16) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<_Float16>, SCAN_BLOCK, 0)
-        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<float>, SCAN_BLOCK, 0);
+        (precision == EKF_PREC_F64) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<double, false>, SCAN_BLOCK, 0)
+        : (precision == EKF_PREC_F16) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<_Float16, false>, SCAN_BLOCK, 0)
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<float, false>, SCAN_BLOCK, 0);
     return err == hipSuccess ? nb : 0;
 }
 
@@ -4718,9 +4721,9 @@ size_t scan_lds_bytes(int precision)
 {
     hipFuncAttributes a;
     hipError_t err =
-        (precision == EKF_PREC_F64) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<double>))
-        : (precision == EKF_PREC_F16) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<_Float16>))
-        : hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<float>));
+        (precision == EKF_PREC_F64) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<double, false>))
+        : (precision == EKF_PREC_F16) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<_Float16, false>))
+        : hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<float, false>));
     return err == hipSuccess ? a.sharedSizeBytes : 0;
 }
 
@@ -4736,12 +4739,16 @@ hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st)
 
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 {
-    if (precision == EKF_PREC_F64)
-        hipLaunchKernelGGL(scan_kernel<double>, dim3(p.G * p.E), dim3(SCAN_BLOCK), 0, st, p);
-    else if (precision == EKF_PREC_F16)
-        hipLaunchKernelGGL(scan_kernel<_Float16>, dim3(p.G * p.E), dim3(SCAN_BLOCK), 0, st, p);
-    else
-        hipLaunchKernelGGL(scan_kernel<float>, dim3(p.G * p.E), dim3(SCAN_BLOCK), 0, st, p);
+    const dim3 grid(p.G * p.E), block(SCAN_BLOCK);
+    if (p.dbg) {   // phase timers (EKF_SCAN_STAMPS=1): the instrumented instantiation
+        if (precision == EKF_PREC_F64) hipLaunchKernelGGL((scan_kernel<double, true>), grid, block, 0, st, p);
+        else if (precision == EKF_PREC_F16) hipLaunchKernelGGL((scan_kernel<_Float16, true>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((scan_kernel<float, true>), grid, block, 0, st, p);
+    } else {
+        if (precision == EKF_PREC_F64) hipLaunchKernelGGL((scan_kernel<double, false>), grid, block, 0, st, p);
+        else if (precision == EKF_PREC_F16) hipLaunchKernelGGL((scan_kernel<_Float16, false>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((scan_kernel<float, false>), grid, block, 0, st, p);
+    }
     return hipGetLastError();
 }
 
