@@ -136,21 +136,16 @@ __device__ __forceinline__ double rcp_nr(double a)
 // leaving Si untouched.
 __device__ __forceinline__ bool lu_invert2(const double S[4], double Si[4])
 {
-    double a0 = S[0], a1 = S[1], a2 = S[2], a3 = S[3];
-    int p0 = 0, p1 = 1;
-    if (fabs(a2) > fabs(a0)) {
-        double t0 = a0, t1 = a1;
-        a0 = a2; a1 = a3;
-        a2 = t0; a3 = t1;
-        p0 = 1; p1 = 0;
-    }
-    double r0 = 0.0;
-    if (a0 != 0.0) {
-        r0 = rcp_nr(a0);
-        const double l = a2 * r0;
-        a2 = l;
-        a3 -= l * a1;
-    }
+    // the row swap by selects and the elimination unconditionally (a zero pivot makes r0 infinite,
+    // and the function then returns before using anything derived from it): the same values as
+    // the branching form, without exec-mask branches on the association's serial chain
+    const bool sw = fabs(S[2]) > fabs(S[0]);
+    double a0 = sw ? S[2] : S[0], a1 = sw ? S[3] : S[1], a2 = sw ? S[0] : S[2], a3 = sw ? S[1] : S[3];
+    const int p0 = sw ? 1 : 0, p1 = sw ? 0 : 1;
+    const double r0 = rcp_nr(a0);
+    const double l = a2 * r0;
+    a2 = l;
+    a3 -= l * a1;
     if (a0 == 0.0 || a3 == 0.0) return false;
     const double r3 = rcp_nr(a3);
 #pragma unroll
@@ -586,24 +581,24 @@ __device__ __forceinline__ bool quick_reject(const Block5& b, double ma, double 
                                              double c0, const double xp[3], double za, double zr,
                                              const double Rm[4], double gate)
 {
+    // every bound evaluated, the tests combined without branches (bitwise on bools): the same
+    // values as the early-exit form, fewer exec-mask instructions on the per-line chain
     const double tr5 = b.p00 + b.p11 + b.p22 + b.daa + b.dbb;
     const double X = fabs(xp[0]) + fabs(xp[1]);
     const double H2 = 2.0 + X * X;   // ≥ ‖H1‖²
-    if (!(Rm[1] == Rm[2]) || !(tr5 >= 0.0) || !(Rm[0] > 1e-5 * 2.0 * tr5) || !(Rm[3] > 1e-5 * H2 * tr5) ||
-        !(fabs(ma0) <= 8.0))
-        return false;
+    const bool ok = (Rm[1] == Rm[2]) & (tr5 >= 0.0) & (Rm[0] > 1e-5 * 2.0 * tr5) & (Rm[3] > 1e-5 * H2 * tr5) &
+                    (fabs(ma0) <= 8.0);
     const double g2 = gate * gate * (1.0 + 1e-6);
     const double S00 = b.p22 - 2.0 * b.p2a + b.daa + Rm[0];
     const double x = za - (ma - xp[2]);
     const double cd = fabs(x - 2.0 * EKF_PI * rint(x * (0.5 / EKF_PI)));
-    if (S00 > 0.0 && cd - 1e-12 * (1.0 + fabs(x)) > 0.0) {
-        const double a0 = cd - 1e-12 * (1.0 + fabs(x));
-        if (a0 * a0 > g2 * S00) return true;
-    }
+    const double a0 = cd - 1e-12 * (1.0 + fabs(x));
+    const bool r0 = (S00 > 0.0) & (a0 > 0.0) & (a0 * a0 > g2 * S00);
     const double v1e = zr - (mr - (xp[0] * c0 + xp[1] * s0));
     const double a1 = fabs(v1e) - X * (fabs(ma - ma0) + QR_TRIG_EPS) - 1e-12 * (1.0 + fabs(zr) + fabs(mr) + X);
     const double S11u = H2 * tr5 * (1.0 + 1e-5) + Rm[3];
-    return a1 > 0.0 && a1 * a1 > g2 * S11u;
+    const bool r1 = (a1 > 0.0) & (a1 * a1 > g2 * S11u);
+    return ok & (r0 | r1);
 }
 
 // Certified rejection in fp32 (the second filter of the per-line gate; certified_reject in fp64
@@ -1975,11 +1970,16 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 int ml = 0, bad = 0;
                 const bool lst = pdbg && g == 0 && u == 0;
                 unsigned long long tl = lst ? __builtin_amdgcn_s_memrealtime() : 0ull;
+                // lane u evaluates line u: its line in registers, and the lines with a winner as a
+                // wave-uniform mask (no LDS read on the chain)
+                ekf_line lnu = {};
+                if (u < L) lnu = sh_lines[u];
+                const unsigned long long wmask = __ballot(act);
                 for (int t = 0; t < L; t++) {
-                    if (sh_spec[t] < 0) continue;
+                    if (!((wmask >> t) & 1ull)) continue;
                     double* pk = sh_pk[t];
                     if (u == t) {
-                        const ekf_line ln = sh_lines[t];
+                        const ekf_line ln = lnu;
                         double Rm[4];
                         line_R(ln, t, p.r_mode, Rm);
                         Block5 b5;
@@ -2004,8 +2004,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                             sym_factor(pkl, F);
                             pkl[PK_F + 0] = F[0]; pkl[PK_F + 1] = F[1]; pkl[PK_F + 2] = F[2];
                         }
+                        // (the robot rows of K stay in registers: only robot_update, here, reads them)
 #pragma unroll
-                        for (int a = MB_S; a < PKW; a++) pk[a] = pkl[a];
+                        for (int a = MB_S; a < PKW; a++)
+                            if (a < MB_KR || a >= MB_KR + 6) pk[a] = pkl[a];
                     }
                     // the package is complete: to the other lanes of this wave, and to the
                     // landmark waves (release of lane t's LDS writes, then the line counter)
