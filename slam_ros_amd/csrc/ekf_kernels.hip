@@ -1343,10 +1343,14 @@ __device__ __forceinline__ void plane_replay(const Slot* pend, int e, size_t ins
 // whose exact first passing candidate differs from the guess. Three exchanges per scan instead
 // of one per line; on a flag the scan restarts on the sequential path (identical results).
 
-template <typename T, bool ST>
+// ST: phase timers (EKF_SCAN_STAMPS=1). HOT: the launch guarantees symmetric fp32 operands with
+// kmax = 16 (the bench and every EKF_R_SYMMETRIC fp32/fp16 context with max_lines <= 8): the
+// per-line loops then carry no code for the other operand forms
+template <typename T, bool ST, bool HOT>
 __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
 {
     const Dims d = p.d;
+    const int r_mode = HOT ? (int)EKF_R_INTENDED : p.r_mode;   // (HOT: the launch checked it)
     // 1-D grid, instance-minor: block b is workgroup b / E of instance b % E. Workgroups are
     // dealt round-robin over the 8 XCDs, so with 8 instances per launch each instance's
     // workgroups share one XCD (and its L2) in every launch; correctness never depends on it
@@ -1597,9 +1601,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     const bool spec_ok = p.spec && L > 0 && L <= SPEC_L && s > 0 && G <= SPEC_GMAX;
     // symmetric downdate operands (sym_factor): fp32 operand storage, every mode but the
     // reference's asymmetric R
-    const bool sym = p.r_mode != 1 && sizeof(typename Stor<T>::C) == 4;
+    const bool sym = HOT || (r_mode != 1 && sizeof(typename Stor<T>::C) == 4);
     // symmetric fp32 operands with kmax = 16: staged in LDS (sh_vpl) and written at the end
-    const bool stage_ops = sym && d.kmax == 16;
+    const bool stage_ops = HOT || (sym && d.kmax == 16);
     // speculative path with fp32 operands and few pending steps: the pending steps' rows of the
     // guessed columns are staged in LDS and one pass per step updates all owned blocks
     bool staged = false;
@@ -1698,7 +1702,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 if (t >= L) break;
                 const ekf_line ln = sh_lines[t];
                 double Rm[4];
-                line_R(ln, t, p.r_mode, Rm);
+                line_R(ln, t, r_mode, Rm);
                 if (guess_pass(gs, ln.alpha, ln.r, Rm, p.gate)) gp |= 1u << t;
             }
             if (p.spec == 2 && L > 1)   // test hook: every guess taken from the next line
@@ -1981,7 +1985,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     if (u == t) {
                         const ekf_line ln = lnu;
                         double Rm[4];
-                        line_R(ln, t, p.r_mode, Rm);
+                        line_R(ln, t, r_mode, Rm);
                         Block5 b5;
                         fill_block5(b5, R33l, w0, w1, w2, wD);
                         Cand c;
@@ -2135,7 +2139,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 for (int i = 0; i < L && !viol; ++i) {
                     const ekf_line ln = sh_lines[i];
                     double Rm[4];
-                    line_R(ln, i, p.r_mode, Rm);
+                    line_R(ln, i, r_mode, Rm);
                     const int w = sh_spec[i];
                     int deep = 0;   // diagnostics: 1 past the quick filter, 2 past the fp32 one, 3 past the fp64 one
                     // the gate of line i on the state before it (the guessed winner itself, j == w, is
@@ -2157,7 +2161,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         }
                         sub(17);
                         pk = sh_pk[i];
-                        if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
+                        if (r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
                         if (own) {
                             deeper = cand && !quick_reject(b5, ybx, yby, ma0, s0f, c0f, xpg, ln.alpha, ln.r, Rm, p.gate);
                             double blk[4];
@@ -2271,7 +2275,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     for (int i = 0; sequential && i < L; ++i) {
         const ekf_line ln = sh_lines[i];
         double Rm[4];
-        line_R(ln, i, p.r_mode, Rm);
+        line_R(ln, i, r_mode, Rm);
         // gating of the owned candidate (Robot.cpp:313-498); the first passing unmatched j wins
         int best = 0x7fffffff;
         bool sing = false;
@@ -2367,7 +2371,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         } else if (own) {
             pll_block(pv, 2 * j, 2 * jstar, blk);
         }
-        if (p.r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
+        if (r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
         if (own) {
             double kk[4], uu[4];
             gain_rows<0>(sh_pkg, m, uq_owned,
@@ -4713,9 +4717,9 @@ int scan_blocks_per_cu(int precision)
 {
     int nb = 0;
     hipError_t err =
-        (precision == EKF_PREC_F64) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<double, false>, SCAN_BLOCK, 0)
-        : (precision == EKF_PREC_F16) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<_Float16, false>, SCAN_BLOCK, 0)
-        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<float, false>, SCAN_BLOCK, 0);
+        (precision == EKF_PREC_F64) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<double, false, false>, SCAN_BLOCK, 0)
+        : (precision == EKF_PREC_F16) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<_Float16, false, false>, SCAN_BLOCK, 0)
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<float, false, false>, SCAN_BLOCK, 0);
     return err == hipSuccess ? nb : 0;
 }
 
@@ -4723,9 +4727,9 @@ size_t scan_lds_bytes(int precision)
 {
     hipFuncAttributes a;
     hipError_t err =
-        (precision == EKF_PREC_F64) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<double, false>))
-        : (precision == EKF_PREC_F16) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<_Float16, false>))
-        : hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<float, false>));
+        (precision == EKF_PREC_F64) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<double, false, false>))
+        : (precision == EKF_PREC_F16) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<_Float16, false, false>))
+        : hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<float, false, false>));
     return err == hipSuccess ? a.sharedSizeBytes : 0;
 }
 
@@ -4743,13 +4747,16 @@ hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 {
     const dim3 grid(p.G * p.E), block(SCAN_BLOCK);
     if (p.dbg) {   // phase timers (EKF_SCAN_STAMPS=1): the instrumented instantiation
-        if (precision == EKF_PREC_F64) hipLaunchKernelGGL((scan_kernel<double, true>), grid, block, 0, st, p);
-        else if (precision == EKF_PREC_F16) hipLaunchKernelGGL((scan_kernel<_Float16, true>), grid, block, 0, st, p);
-        else hipLaunchKernelGGL((scan_kernel<float, true>), grid, block, 0, st, p);
+        if (precision == EKF_PREC_F64) hipLaunchKernelGGL((scan_kernel<double, true, false>), grid, block, 0, st, p);
+        else if (precision == EKF_PREC_F16) hipLaunchKernelGGL((scan_kernel<_Float16, true, false>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((scan_kernel<float, true, false>), grid, block, 0, st, p);
+    } else if (precision != EKF_PREC_F64 && p.r_mode != 1 && p.d.kmax == 16) {
+        if (precision == EKF_PREC_F16) hipLaunchKernelGGL((scan_kernel<_Float16, false, true>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((scan_kernel<float, false, true>), grid, block, 0, st, p);
     } else {
-        if (precision == EKF_PREC_F64) hipLaunchKernelGGL((scan_kernel<double, false>), grid, block, 0, st, p);
-        else if (precision == EKF_PREC_F16) hipLaunchKernelGGL((scan_kernel<_Float16, false>), grid, block, 0, st, p);
-        else hipLaunchKernelGGL((scan_kernel<float, false>), grid, block, 0, st, p);
+        if (precision == EKF_PREC_F64) hipLaunchKernelGGL((scan_kernel<double, false, false>), grid, block, 0, st, p);
+        else if (precision == EKF_PREC_F16) hipLaunchKernelGGL((scan_kernel<_Float16, false, false>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((scan_kernel<float, false, false>), grid, block, 0, st, p);
     }
     return hipGetLastError();
 }
