@@ -1682,6 +1682,36 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     auto uq_owned = [&](int q) -> double4 {
         return q < HIST_LDS ? sh_uhist[q][tid] : *reinterpret_cast<const double4*>(Ust + ((size_t)q * n + b0) * 2);
     };
+    // symmetric operands from their LDS stage (stage_ops): per owned row and k parity h one 16-byte
+    // half of the 32-byte lane row, half 0 = k slots 0..3 (matches 0..3), half 1 = slots 4..7; V and
+    // U = −2^x·V (exact); k past the matches +0 (V) and −0 (U), so that a flush running every
+    // k-step leaves every value as it is (flush_f32_wave_kernel; the other forms and the on-read
+    // replay stop at ks). Half 0 is final after the fourth match: the speculative path stores it
+    // then, during the later lines (the commit's stores are issue-bound, ≈10 B/clk per CU)
+    int ops_early = 0;
+    auto store_ops_half = [&](int half, int mm) {   // mm: the matches
+        if constexpr (kPlanes) {
+            const float us = -ldexpf(1.0f, pv.ex);
+#pragma unroll
+            for (int pp = 0; pp < 2; pp++) {
+                const f32x4v* src = reinterpret_cast<const f32x4v*>(sh_vpl + tid * 32 + pp * 16) + 2 * half;
+                float v[8];
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    const f32x4v x = src[i];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) v[4 * i + u] = (8 * half + 4 * i + u) < 2 * mm ? x[u] : 0.f;
+                }
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const size_t o = op_index_f32(2 * j + pp, h, d.kmax) + 4 * half;   // k = h: s = 0
+                    const f32x4v vh = {v[h], v[2 + h], v[4 + h], v[6 + h]};
+                    *reinterpret_cast<f32x4v*>(Vop + o) = vh;
+                    *reinterpret_cast<f32x4v*>(Uop + o) = vh * us;
+                }
+            }
+        }
+    };
 
     bool matched = false;
     int m = 0, nextra = 0, status = 0, tstatus = 0;
@@ -2227,6 +2257,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     if (j == w) matched = true;
                     if (lead) res[RES_MATCH + i] = w;
                     m++;
+                    if (stage_ops && own && m == 4) {
+                        store_ops_half(0, m);
+                        ops_early = 1;
+                    }
                 }
             }
             if (dbg) sh_stamp[31] += __builtin_amdgcn_s_memrealtime() - sh_trec;   // landmark wave 0 done
@@ -2262,6 +2296,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 if (own && j < s) pll_block(pv, 2 * j, 2 * j, Dj);
                 matched = false;
                 m = nextra = status = 0;
+                ops_early = 0;   // (the sequential path rewrites every operand row)
                 __syncthreads();   // sh_extra, sh_vhist reuse
             }
         } else {
@@ -2472,34 +2507,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     EKF_STAMP(28);
     if (own) {
         if (stage_ops) {
-            if constexpr (kPlanes) {
-                // symmetric operands from their LDS stage: per owned row the even-k and the odd-k
-                // halves of V (two 32-byte lane rows each) and U = −2^x·V (exact); k past the
-                // matches +0 (V) and −0 (U), so that a flush running every k-step leaves every value
-                // as it is (flush_f32_wave_kernel; the other forms and the on-read replay stop at ks)
-                const float us = -ldexpf(1.0f, pv.ex);
-#pragma unroll
-                for (int pp = 0; pp < 2; pp++) {
-                    const f32x4v* src = reinterpret_cast<const f32x4v*>(sh_vpl + tid * 32 + pp * 16);
-                    float v[16];
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const f32x4v x = src[i];
-#pragma unroll
-                        for (int u = 0; u < 4; u++) v[4 * i + u] = (4 * i + u) < 2 * m ? x[u] : 0.f;
-                    }
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const size_t o = op_index_f32(2 * j + pp, h, d.kmax);   // k = h: s = 0
-                        const f32x4v v0 = {v[h], v[2 + h], v[4 + h], v[6 + h]};
-                        const f32x4v v1 = {v[8 + h], v[10 + h], v[12 + h], v[14 + h]};
-                        *reinterpret_cast<f32x4v*>(Vop + o) = v0;
-                        *reinterpret_cast<f32x4v*>(Vop + o + 4) = v1;
-                        *reinterpret_cast<f32x4v*>(Uop + o) = v0 * us;
-                        *reinterpret_cast<f32x4v*>(Uop + o + 4) = v1 * us;
-                    }
-                }
-            }
+            if (!ops_early) store_ops_half(0, m);
+            store_ops_half(1, m);
         } else if (sizeof(C) == 4) {
             // f32 operands: the k columns past the matches hold −0 (U) and +0 (V), so a flush
             // that runs every k-step unconditionally adds −0 there, which leaves every value as
@@ -2536,7 +2545,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         if constexpr (kPlanes)
             if (Bop && own) {
                 // the owned rows' planes: per row and k parity h (k = 2s + h, s = 0..7) one
-                // 16-byte lane row per part; k past the matches +0
+                // 16-byte lane row per part; k past the matches +0 (stored early, as the U and V
+                // halves are, their split arithmetic lands on the per-line chain: scan +0.8 µs)
                 const int m = sh_m;
                 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
 #pragma unroll
