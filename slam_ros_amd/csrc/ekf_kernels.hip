@@ -110,6 +110,7 @@ __device__ __forceinline__ int storage_exp(const int* pexp, int e)
 __device__ __forceinline__ double normalize_radian(double rad)
 {
     // Robot.cpp:62-71
+    if (fabs(rad) <= EKF_PI) return rad;   // (the common case, one test)
     if (rad > EKF_PI) {
         rad = rad - (2.0 * EKF_PI + floor(rad / (2.0 * EKF_PI)) * 2.0 * EKF_PI);
     } else if (rad < -EKF_PI) {
@@ -514,7 +515,13 @@ __device__ __forceinline__ void eval_candidate(const Block5& b, double ma, doubl
     const double vs0 = v0 * c.Si[0] + v1 * c.Si[2];
     const double vs1 = v0 * c.Si[1] + v1 * c.Si[3];
     const double d2 = vs0 * v0 + vs1 * v1;
-    c.pass = !(sqrt(fabs(d2)) > gate);
+    // sqrt(|d2|) > gate decided without the square root where |d2| is more than 2^-40 (relative)
+    // away from gate²: sqrt is correctly rounded and monotonic, so such a |d2| gives the same
+    // answer; near the gate, and for NaN (which passes), the reference's expression itself
+    const double a = fabs(d2), g2 = gate * gate;
+    if (a < g2 * (1.0 - 0x1p-40)) c.pass = 1;
+    else if (a > g2 * (1.0 + 0x1p-40)) c.pass = 0;
+    else c.pass = !(sqrt(a) > gate);
 }
 
 // Certified rejection: true only if the exact evaluation is guaranteed to fail the gate. It
