@@ -3835,6 +3835,9 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
 #ifndef EKF_XP_BF_NO_TILES   // timing experiment (results invalid): no tile stream after the first
                 if (more) load_tiles(nxt);
 #endif
+#ifdef EKF_XP_TILE_WAIT   // timing experiment: wait for the next wave-tile's tiles right away
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
                 __builtin_amdgcn_sched_barrier(0);
 #ifdef EKF_XP_FLUSH_STAMPS
                 const unsigned long long xt1 = __builtin_amdgcn_s_memtime();

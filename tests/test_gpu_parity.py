@@ -490,6 +490,47 @@ def test_speculative_association_identical(ekf_mod, oracle_mod, monkeypatch, pre
 
 
 @pytest.mark.parametrize("prec", [1, 2])
+@pytest.mark.parametrize("arith", [0, 1])
+def test_hot_scan_kernel_equals_generic(ekf_mod, monkeypatch, prec, arith):
+    """The association kernel's HOT instantiation (symmetric fp32 operands, kmax 16: the product
+    launch of every EKF_R_INTENDED fp32/fp16 context with max_lines <= 8) and the generic
+    instrumented one (EKF_SCAN_STAMPS=1, `scan_kernel<T, true, false>`) give bit-identical state
+    and results — on the speculative path (with the early U/V operand stores after the fourth
+    match) and when every guess is wrong (the restart after those stores), in both flush
+    arithmetics (Robot.cpp:313-641)."""
+    N, T = 1024, 8
+    w = G.make_world(N, active=N - 30)
+    st = G.initial_state(w)
+    scans = _spec_scans(w, np.random.default_rng(5), 10)
+    runs = {}
+    for stamps in ("0", "1"):
+        for spec in ("1", "2"):
+            monkeypatch.setenv("EKF_SCAN_STAMPS", stamps)
+            monkeypatch.setenv("EKF_SPECULATE", spec)
+            ens = ekf_mod.Ensemble(N, 1, prec, max_lines=8, flush_interval=T, arith=arith)
+            ens.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
+            results = []
+            for enc, ln in scans:
+                r = ens.localize(enc, ln[None], [len(ln)])[0]
+                results.append((r["match"], r["matches"], r["new_landmarks"], r["status"]))
+            runs[(stamps, spec)] = (results, ens.download_state(0))
+            ens.close()
+    for spec in ("1", "2"):
+        hot, gen = runs[("0", spec)], runs[("1", spec)]
+        assert hot[0] == gen[0], spec
+        P, y, s, pose = hot[1]
+        P0, y0, s0, pose0 = gen[1]
+        bad = np.argwhere(P != P0)
+        assert bad.size == 0, (spec, bad[:8].tolist(), rel(P, P0))
+        np.testing.assert_array_equal(y, y0)
+        np.testing.assert_array_equal(pose, pose0)
+        assert s == s0
+    if arith == 0:   # exact arithmetic: the restart is the sequential chain, bit for bit
+        assert runs[("0", "2")][0] == runs[("0", "1")][0]
+        np.testing.assert_array_equal(runs[("0", "2")][1][0], runs[("0", "1")][1][0])
+
+
+@pytest.mark.parametrize("prec", [1, 2])
 @pytest.mark.parametrize("N,T,lines,extra_every", [(80, 8, 6, 3), (80, 2, 8, 0), (64, 6, 6, 4),
                                                   (1024, 8, 8, 0), (1024, 4, 6, 5)])
 def test_wave_flush_equals_drained(ekf_mod, monkeypatch, prec, N, T, lines, extra_every):
