@@ -11,8 +11,15 @@
  *
  * Errors: every call returns an int status (EKF_OK == 0). The reference's localize() returns
  * void and only prints GSL error codes (Robot.cpp:128, 909-917); per-instance numeric
- * conditions (singular S, capacity overflow) are reported in ekf_result.status instead, and
- * the state is always committed, as in the reference.
+ * conditions (singular S, capacity overflow, fp16 range) are reported in ekf_result.status
+ * instead and the state is committed, as in the reference. One condition the reference cannot
+ * have is handled differently: EKF_ST_SYNC_TIMEOUT (an instance spread over G > 1 cooperating
+ * workgroups lost one of them) rolls that instance's call back instead of committing it. A
+ * context whose instances fit one workgroup (N <= 192, e.g. the drop-in's N = 100) cannot time
+ * out, so there every call commits.
+ *
+ * The library reads no environment variables: diagnostics and test hooks are per-context
+ * options (ekf_set_option), all off by default.
  */
 #ifndef SLAM_EKF_H
 #define SLAM_EKF_H
@@ -26,8 +33,11 @@ extern "C" {
 
 /* 2: ekf_debug_scan_stamps fills 32 slots (was 16); ekf_config.arith (formerly reserved) selects
  *    the fp32 flush arithmetic and EKF_ARITH_BF16X6 is rejected (EKF_EINVAL) for configurations
- *    that can never use it; EKF_ST_SYNC_TIMEOUT rolls the call back instead of committing it. */
-#define SLAM_EKF_ABI_VERSION 2
+ *    that can never use it; EKF_ST_SYNC_TIMEOUT rolls the call back instead of committing it.
+ * 3: ekf_set_option / ekf_get_option replace the environment variables the library used to read
+ *    (EKF_SPECULATE, EKF_SPIN_LOG2, EKF_TEST_DROP_WG, EKF_MFREP, EKF_SCAN_STAMPS,
+ *    EKF_DD_BLOCKS_PER_CU, EKF_FLUSH_VARIANT); ekf_shard_abort. */
+#define SLAM_EKF_ABI_VERSION 3
 #define EKF_MAX_LINES 64 /* lines per scan per instance; main.cpp:99 reserves 20 */
 
 /* status codes */
@@ -135,6 +145,39 @@ int ekf_destroy(ekf_ctx* ctx);
 int ekf_set_stream(ekf_ctx* ctx, void* hip_stream);
 int ekf_sync(ekf_ctx* ctx);
 
+/* Per-context options: diagnostics, alternative (result-identical or parity-equivalent) kernel
+ * forms and test hooks. A new context has every option at its default; nothing is read from the
+ * environment. ekf_set_option drains the context first (the option applies from the next call)
+ * and returns EKF_EINVAL for an unknown option, EKF_ERANGE for a value out of range. */
+enum {
+    /* association path: 1 speculative (default), 0 the sequential chain on every scan (one
+     * cross-workgroup exchange per line), 2 test hook: every guess wrong (the speculative path,
+     * a failed verdict and the sequential restart on every scan). Identical results. */
+    EKF_OPT_SPECULATE = 1,
+    /* spin bound of the association's cross-workgroup waits: 2^v polls, 8 <= v <= 24 (24) */
+    EKF_OPT_SPIN_LOG2 = 2,
+    /* fp32 / fp16 flush form, all bit-identical within an arithmetic: 0 automatic (default),
+     * 2 the super-tile form for every group, 8 the wave form also for groups of 2 and 4 steps,
+     * 24 the split-bf16 flush on 2 x 4 wave-tiles */
+    EKF_OPT_FLUSH_FORM = 3,
+    /* workgroups per CU of the grid-strided flush forms, 1..16 (8) */
+    EKF_OPT_FLUSH_BLOCKS_PER_CU = 4,
+    /* split-bf16 contexts: pending steps applied on read by MFMA on the operand planes (1,
+     * default) or by the exact staged replay (0) */
+    EKF_OPT_MFMA_REPLAY = 5,
+    /* 1: the association kernel's instrumented instantiation with phase timers
+     * (ekf_debug_scan_stamps); 0 (default) the product kernel */
+    EKF_OPT_SCAN_STAMPS = 6,
+    /* test hook: e + 1 = the last association workgroup of instance e never runs (its exchanges
+     * time out and the instance's calls roll back); 0 off (default) */
+    EKF_OPT_TEST_DROP_WG = 7,
+    /* test hook: e + 1 = on the speculative path, association workgroup 1 of instance e treats
+     * its verdict poll as timed out while every other workgroup completes; 0 off (default) */
+    EKF_OPT_TEST_VERDICT_TIMEOUT = 8,
+};
+int ekf_set_option(ekf_ctx* ctx, int option, int value);
+int ekf_get_option(const ekf_ctx* ctx, int option, int* value);
+
 /* Robot::Robot(x, y, theta) on one instance (e < 0: all instances). */
 int ekf_reset_instance(ekf_ctx* ctx, int e, double x, double y, double theta);
 
@@ -222,6 +265,11 @@ size_t ekf_shard_patch_bytes(const ekf_ctx* ctx);   /* bytes of the new-landmark
 int ekf_shard_patch(ekf_ctx* ctx, double* rows, int upload);
 int ekf_shard_commit(ekf_ctx* ctx);
 int ekf_shard_status(ekf_ctx* ctx, int* status);   /* status bits of the scan (GSL_EDOM, NSYM) */
+/* Abandons the open scan (between ekf_shard_begin and ekf_shard_end: nothing of the committed state
+ * has been written yet), e.g. after a failed exchange; a phase that fails abandons it too. A
+ * sharded context rejects the whole-instance entry points (ekf_localize, ekf_localize_device,
+ * ekf_predict, ekf_update) with EKF_EINVAL. */
+int ekf_shard_abort(ekf_ctx* ctx);
 
 /* Introspection for the benchmark's roofline accounting. */
 size_t ekf_landmark_block_bytes(const ekf_ctx* ctx); /* stored bytes of P_ll per instance */
@@ -240,7 +288,7 @@ int ekf_profile_read(ekf_ctx* ctx, double* scan_ms, double* downdate_ms, double*
 int ekf_profile_flushes(ekf_ctx* ctx, int cap, int* nsteps, float* ms);
 const char* ekf_flush_kernel_name(const ekf_ctx* ctx, int nsteps);
 /* Diagnostic: association-kernel phase timers (sum over instances, 100 MHz ticks), collected
- * only when the environment had EKF_SCAN_STAMPS=1 at ekf_create. 32 slots (ABI 2; ABI 1 had 16):
+ * only while EKF_OPT_SCAN_STAMPS is 1. 32 slots (ABI 2; ABI 1 had 16):
  * 0 predict, 1 diagonal gather + barrier, 2 gating, 3 min-reduction barrier, 4 winner package,
  * 5 broadcast barrier, 6 gain rows, 7 commit/augmentation, 8 total, 9 launches; 16-19 per-line
  * phases of the first landmark wave (gate, wait for the package, gain rows, robot update);

@@ -38,11 +38,10 @@ N, E, T = args.n, args.e, args.t
 for case in args.cases:
     spec = {"spec0": "0", "spec2": "2"}.get(case, "1")
     profile = "survey" if case.startswith("survey") else None
-    os.environ["EKF_SPECULATE"] = spec
     w = G.make_world(N)
     st = G.initial_state(w, profile=profile)
-    ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8, flush_interval=T, arith=ekf.ARITH_BF16X6)
-    os.environ["EKF_SPECULATE"] = "1"
+    ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8, flush_interval=T, arith=ekf.ARITH_BF16X6,
+                       options={"speculate": int(spec)})
     for e in range(E):
         ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
     ref = None

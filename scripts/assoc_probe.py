@@ -1,4 +1,4 @@
-"""Association-kernel phase timers (EKF_SCAN_STAMPS=1; thread 0 of workgroup 0 of each instance,
+"""Association-kernel phase timers (EKF_OPT_SCAN_STAMPS = 1; thread 0 of workgroup 0 of each instance,
 s_memrealtime, 100 MHz), µs per launch averaged over instances, at the bench's shapes
 (f32, E = 8, L = m = 8; the bench's split-bf16 arithmetic, PROBE_ARITH=exact for the exact one).
 usage: python scripts/assoc_probe.py [N:T ...]"""
@@ -6,7 +6,6 @@ import json
 import os
 import sys
 
-os.environ["EKF_SCAN_STAMPS"] = "1"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from slam_ros_amd import ekf, scan_gen as G  # noqa: E402
 
@@ -22,7 +21,8 @@ for c in cfgs:
     w = G.make_world(N)
     st = G.initial_state(w)
     arith = ekf.ARITH_EXACT if os.environ.get("PROBE_ARITH") == "exact" else ekf.ARITH_BF16X6
-    ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8, flush_interval=T, arith=arith)
+    ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8, flush_interval=T, arith=arith,
+                       options={"scan_stamps": 1})
     for e in range(E):
         ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
     base = ens.scan_stamps()

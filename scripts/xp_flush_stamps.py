@@ -1,12 +1,11 @@
 """Flush timing experiment (build with -DEKF_XP_FLUSH_STAMPS, SLAM_EKF_LIB): shader cycles per
 wave-tile in the wave flush's boundary (entry, tile copy, next tiles issued), MFMA steps, and
-tile stores, summed over waves (EKF_SCAN_STAMPS=1 provides the buffer; instance 0's slots
+tile stores, summed over waves (EKF_OPT_SCAN_STAMPS = 1 provides the buffer; instance 0's slots
 24..27). usage: SLAM_EKF_LIB=... python scripts/xp_flush_stamps.py"""
 import json
 import os
 import sys
 
-os.environ["EKF_SCAN_STAMPS"] = "1"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from slam_ros_amd import ekf, scan_gen as G  # noqa: E402
 
@@ -16,7 +15,7 @@ T = int(os.environ.get("XP_T", "12" if BF else "8"))
 w = G.make_world(N)
 st = G.initial_state(w)
 ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8, flush_interval=T,
-                   arith=ekf.ARITH_BF16X6 if BF else ekf.ARITH_EXACT)
+                   arith=ekf.ARITH_BF16X6 if BF else ekf.ARITH_EXACT, options={"scan_stamps": 1})
 for e in range(E):
     ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
 for s in range(1, T * 6 + 1):

@@ -85,20 +85,23 @@ struct ekf_ctx {
     int* h_res;
     double* h_pose;
     int dd_grid;
-    int dd_variant;           // f32 flush kernel form (EKF_FLUSH_VARIANT)
+    int dd_per_cu;            // flush workgroups per CU of the grid-strided forms (EKF_OPT_FLUSH_BLOCKS_PER_CU)
+    int dd_variant;           // f32 flush kernel form (EKF_OPT_FLUSH_FORM)
     int ncu;
     int G;                    // association workgroups per instance
     int mbw;                  // mailbox words per workgroup slot
-    int spec;                 // speculative association (EKF_SPECULATE)
-    int spin_log2;            // spin bound of the association kernel's waits (EKF_SPIN_LOG2, tests)
-    int test_drop;            // test hook (EKF_TEST_DROP_WG = e): instance e's last workgroup never runs
-    int mfrep;                // split-bf16 contexts: MFMA replay of pending steps (EKF_MFREP=0: off, tests)
+    int spec;                 // speculative association (EKF_OPT_SPECULATE)
+    int spin_log2;            // spin bound of the association kernel's waits (EKF_OPT_SPIN_LOG2)
+    int test_drop;            // test hook (EKF_OPT_TEST_DROP_WG = e + 1): instance e's last workgroup never runs
+    int test_verdict;         // test hook (EKF_OPT_TEST_VERDICT_TIMEOUT = e + 1)
+    int mfrep_opt;            // EKF_OPT_MFMA_REPLAY
+    int mfrep;                // split-bf16 contexts: MFMA replay of pending steps (bf && mfrep_opt)
     int scan_batch;           // instances per association launch (co-residency bound)
     unsigned scan_epoch;      // association launches so far (mailbox tags)
     double* mbox;
     int* sync;
     int sync_stride;
-    unsigned long long* dbg;  // association-kernel phase timers (EKF_SCAN_STAMPS=1)
+    unsigned long long* dbg;  // association-kernel phase timers (EKF_OPT_SCAN_STAMPS = 1, else null)
     int* pexp;                // [E] fp16 storage exponents (device), host copy below
     void* sink;               // scratch tile for the wave flushes (DowndateParams::sink)
     void* ops_u;              // operand rows of every ring slot (U), slot_bytes apart
@@ -377,15 +380,17 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     c->pexp_h.assign(E, 0);
     // whole 128-B lines: the package words, then 16 words for the speculative list words
     c->mbw = ((ekf::MB_WORDS_FIXED + 4 * d.max_lines + 15) / 16) * 16 + 16;
-    c->spec = getenv("EKF_SPECULATE") ? atoi(getenv("EKF_SPECULATE")) : 1;
-    c->spin_log2 = getenv("EKF_SPIN_LOG2") ? std::max(8, std::min(24, atoi(getenv("EKF_SPIN_LOG2")))) : 24;
-    c->test_drop = getenv("EKF_TEST_DROP_WG") ? atoi(getenv("EKF_TEST_DROP_WG")) + 1 : 0;
-    c->mfrep = (c->bf && !(getenv("EKF_MFREP") && atoi(getenv("EKF_MFREP")) == 0)) ? 1 : 0;
+    // options (ekf_set_option): defaults, nothing from the environment
+    c->spec = 1;
+    c->spin_log2 = 24;
+    c->test_drop = 0;
+    c->test_verdict = 0;
+    c->mfrep_opt = 1;
+    c->mfrep = c->bf ? 1 : 0;
+    c->dbg = nullptr;
     ALLOC(c->mbox, sizeof(double) * 2 * c->G * c->mbw * E);
     c->sync_stride = ((ekf::SYNC_WG0 + c->G + 15) / 16) * 16;
     ALLOC(c->sync, sizeof(int) * c->sync_stride * E);
-    if (getenv("EKF_SCAN_STAMPS") && atoi(getenv("EKF_SCAN_STAMPS")))
-        ALLOC(c->dbg, sizeof(unsigned long long) * 32 * E);
 #undef ALLOC
     if (hipHostMalloc((void**)&c->h_res, sizeof(int) * ekf::RES_STRIDE * E) != hipSuccess) goto fail;
     if (hipHostMalloc((void**)&c->h_pose, sizeof(double) * 3 * E) != hipSuccess) goto fail;
@@ -509,14 +514,10 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) goto fail;
-        int dd_per_cu = 8;   // downdate workgroups per CU (4 waves each)
-        if (getenv("EKF_DD_BLOCKS_PER_CU")) dd_per_cu = atoi(getenv("EKF_DD_BLOCKS_PER_CU"));
-        if (dd_per_cu < 1) dd_per_cu = 1;
-        c->dd_grid = prop.multiProcessorCount * dd_per_cu;
+        c->dd_per_cu = 8;   // downdate workgroups per CU (4 waves each; EKF_OPT_FLUSH_BLOCKS_PER_CU)
+        c->dd_grid = prop.multiProcessorCount * c->dd_per_cu;
         c->ncu = prop.multiProcessorCount;
-        // test hook: force one of the bit-identical flush forms (tests/test_gpu_parity.py)
-        c->dd_variant = getenv("EKF_FLUSH_VARIANT") ? atoi(getenv("EKF_FLUSH_VARIANT")) : 0;
-        if (c->dd_variant != 2 && c->dd_variant != 8 && c->dd_variant != 24) c->dd_variant = 0;
+        c->dd_variant = 0;   // automatic flush form (EKF_OPT_FLUSH_FORM)
         // all G workgroups of an instance must be co-resident (they exchange per line). A plain
         // launch gets the same residency as a cooperative one for the same grid
         // (cdna_hip_programming.md §1; the cooperative form only adds a launch-time check of the
@@ -577,6 +578,71 @@ extern "C" int ekf_sync(ekf_ctx* c)
 {
     if (!c) return EKF_EINVAL;
     return drain(c);
+}
+
+extern "C" int ekf_set_option(ekf_ctx* c, int opt, int v)
+{
+    if (!c) return EKF_EINVAL;
+    const int E = c->cfg.instances;
+    switch (opt) {
+    case EKF_OPT_SPECULATE: if (v < 0 || v > 2) return EKF_ERANGE; break;
+    case EKF_OPT_SPIN_LOG2: if (v < 8 || v > 24) return EKF_ERANGE; break;
+    case EKF_OPT_FLUSH_FORM: if (v != 0 && v != 2 && v != 8 && v != 24) return EKF_ERANGE; break;
+    case EKF_OPT_FLUSH_BLOCKS_PER_CU: if (v < 1 || v > 16) return EKF_ERANGE; break;
+    case EKF_OPT_MFMA_REPLAY:
+    case EKF_OPT_SCAN_STAMPS: if (v < 0 || v > 1) return EKF_ERANGE; break;
+    case EKF_OPT_TEST_DROP_WG:
+    case EKF_OPT_TEST_VERDICT_TIMEOUT: if (v < 0 || v > E) return EKF_ERANGE; break;
+    default: return EKF_EINVAL;
+    }
+    int rc = drain(c);
+    if (rc) return rc;
+    switch (opt) {
+    case EKF_OPT_SPECULATE: c->spec = v; break;
+    case EKF_OPT_SPIN_LOG2: c->spin_log2 = v; break;
+    case EKF_OPT_FLUSH_FORM: c->dd_variant = v; break;
+    case EKF_OPT_FLUSH_BLOCKS_PER_CU:
+        c->dd_per_cu = v;
+        c->dd_grid = c->ncu * v;
+        break;
+    case EKF_OPT_MFMA_REPLAY:
+        c->mfrep_opt = v;
+        c->mfrep = (c->bf && v) ? 1 : 0;
+        break;
+    case EKF_OPT_SCAN_STAMPS:
+        if (v && !c->dbg) {
+            const size_t bytes = sizeof(unsigned long long) * 32 * E;
+            if (hipMalloc((void**)&c->dbg, bytes) != hipSuccess) {
+                c->dbg = nullptr;
+                return EKF_ENOMEM;
+            }
+            HIP_TRY(hipMemset(c->dbg, 0, bytes));
+        } else if (!v && c->dbg) {
+            HIP_TRY(hipFree(c->dbg));
+            c->dbg = nullptr;
+        }
+        break;
+    case EKF_OPT_TEST_DROP_WG: c->test_drop = v; break;
+    case EKF_OPT_TEST_VERDICT_TIMEOUT: c->test_verdict = v; break;
+    }
+    return EKF_OK;
+}
+
+extern "C" int ekf_get_option(const ekf_ctx* c, int opt, int* v)
+{
+    if (!c || !v) return EKF_EINVAL;
+    switch (opt) {
+    case EKF_OPT_SPECULATE: *v = c->spec; break;
+    case EKF_OPT_SPIN_LOG2: *v = c->spin_log2; break;
+    case EKF_OPT_FLUSH_FORM: *v = c->dd_variant; break;
+    case EKF_OPT_FLUSH_BLOCKS_PER_CU: *v = c->dd_per_cu; break;
+    case EKF_OPT_MFMA_REPLAY: *v = c->mfrep_opt; break;
+    case EKF_OPT_SCAN_STAMPS: *v = c->dbg ? 1 : 0; break;
+    case EKF_OPT_TEST_DROP_WG: *v = c->test_drop; break;
+    case EKF_OPT_TEST_VERDICT_TIMEOUT: *v = c->test_verdict; break;
+    default: return EKF_EINVAL;
+    }
+    return EKF_OK;
 }
 
 extern "C" int ekf_reset_instance(ekf_ctx* c, int e, double x, double y, double th)
@@ -640,6 +706,7 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.Etot = c->cfg.instances;
     p.spin_log2 = c->spin_log2;
     p.test_drop = c->test_drop;
+    p.test_verdict = c->test_verdict;
     p.pose = c->pose;
     p.xpre = c->xpre;
     p.saved = c->saved;
@@ -745,6 +812,9 @@ static int enqueue_flush(ekf_ctx* c)
 static int enqueue(ekf_ctx* c, int phase, const double* enc, const ekf_line* lines,
                    const int* nlines)
 {
+    // a row-sharded context keeps only its own rows current: the whole-instance scan would read
+    // stale ones (slam_ekf.h ekf_shard_abort)
+    if (c->sh_a >= 0) return EKF_EINVAL;
     ekf::ScanParams sp = scan_params(c, phase, enc, lines, nlines);
     if (!(phase & ekf::PHASE_UPDATE)) {
         EvPair* pr = prof_begin(c, 0, c->stream);
@@ -807,10 +877,17 @@ extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
     HIP_TRY(hipMemcpyAsync(hs.data(), c->sync, sizeof(int) * hs.size(), hipMemcpyDeviceToHost,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    for (int e = 0; e < E; e++)
-        for (int gq = 0; gq < c->G; gq++)
-            c->h_res[(size_t)e * ekf::RES_STRIDE + ekf::RES_STATUS] |=
-                hs[(size_t)e * c->sync_stride + ekf::SYNC_WG0 + gq] & 0xff;   // done_word: status bits
+    // every workgroup's completion word of the last association launch (commit_fold: a word of
+    // another launch — a workgroup that never ran or never finished — reads as a timeout, not as
+    // the status bits an earlier launch left in it)
+    if (c->scan_epoch > 0)
+        for (int e = 0; e < E; e++) {
+            int st = 0;
+            for (int gq = 0; gq < c->G; gq++)
+                st = ekf::commit_fold(st, (unsigned)hs[(size_t)e * c->sync_stride + ekf::SYNC_WG0 + gq],
+                                      c->scan_epoch);
+            c->h_res[(size_t)e * ekf::RES_STRIDE + ekf::RES_STATUS] |= st;
+        }
     if (!out) return EKF_OK;
     for (int e = 0; e < E; e++) {
         const int* r = c->h_res + (size_t)e * ekf::RES_STRIDE;
@@ -834,7 +911,7 @@ extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
 extern "C" int ekf_localize(ekf_ctx* c, const double* enc, const ekf_line* lines,
                             const int32_t* nlines, ekf_result* out)
 {
-    if (!c || !enc || !lines || !nlines) return EKF_EINVAL;
+    if (!c || !enc || !lines || !nlines || c->sh_a >= 0) return EKF_EINVAL;
     int rc = stage_inputs(c, enc, lines, nlines);
     if (rc) return rc;
     rc = enqueue(c, ekf::PHASE_BOTH, c->d_enc, c->d_lines, c->d_nlines);
@@ -851,7 +928,7 @@ extern "C" int ekf_localize_device(ekf_ctx* c, const double* d_enc, const ekf_li
 
 extern "C" int ekf_predict(ekf_ctx* c, const double* enc)
 {
-    if (!c || !enc) return EKF_EINVAL;
+    if (!c || !enc || c->sh_a >= 0) return EKF_EINVAL;
     int rc = stage_inputs(c, enc, nullptr, nullptr);
     if (rc) return rc;
     return enqueue(c, ekf::PHASE_PREDICT, c->d_enc, c->d_lines, c->d_nlines);
@@ -860,7 +937,7 @@ extern "C" int ekf_predict(ekf_ctx* c, const double* enc)
 extern "C" int ekf_update(ekf_ctx* c, const ekf_line* lines, const int32_t* nlines,
                           ekf_result* out)
 {
-    if (!c || !lines || !nlines) return EKF_EINVAL;
+    if (!c || !lines || !nlines || c->sh_a >= 0) return EKF_EINVAL;
     int rc = stage_inputs(c, nullptr, lines, nlines);
     if (rc) return rc;
     rc = enqueue(c, ekf::PHASE_UPDATE, c->d_enc, c->d_lines, c->d_nlines);
@@ -1291,6 +1368,17 @@ static ekf::ShardParams shard_params(ekf_ctx* c, int phase)
 
 static int shard_words(const ekf_ctx* c) { return ekf::MB_WORDS_FIXED + 4 * c->d.max_lines; }
 
+// a HIP failure inside a shard phase abandons the open scan (slam_ekf.h ekf_shard_abort)
+#define SH_TRY(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess) {                                                             \
+            fprintf(stderr, "slam_ekf: %s failed: %s\n", #expr, hipGetErrorString(_e));     \
+            c->sh_open = 0;                                                                 \
+            return EKF_EDEVICE;                                                             \
+        }                                                                                   \
+    } while (0)
+
 extern "C" int ekf_shard_init(ekf_ctx* c, int first, int end)
 {
     if (!c) return EKF_EINVAL;
@@ -1311,13 +1399,24 @@ extern "C" int ekf_shard_init(ekf_ctx* c, int first, int end)
         HIP_TRY(hipMemsetAsync(c->cur, 0, sizeof(int), c->stream));
     }
     const size_t N = (size_t)c->d.N;
-    HIP_TRY(hipMalloc((void**)&c->sh_rob, sizeof(double) * 12));
-    HIP_TRY(hipMalloc((void**)&c->sh_rec, sizeof(double) * N * ekf::SH_REC));
-    HIP_TRY(hipMalloc((void**)&c->sh_hist, sizeof(double) * N * c->d.max_lines * 8));
-    HIP_TRY(hipMalloc((void**)&c->sh_pkg, sizeof(double) * shard_words(c)));
-    HIP_TRY(hipMalloc((void**)&c->sh_flags, sizeof(int) * N));
-    HIP_TRY(hipMalloc((void**)&c->sh_out, sizeof(int) * 2));
-    HIP_TRY(hipMalloc((void**)&c->sh_match, sizeof(int) * 2 * c->d.max_lines));
+    {
+        // every scratch buffer or none: a failure frees what was allocated, so a retry neither
+        // leaks nor finds half-initialised pointers
+        void** bufs[7] = {(void**)&c->sh_rob, (void**)&c->sh_rec, (void**)&c->sh_hist, (void**)&c->sh_pkg,
+                          (void**)&c->sh_flags, (void**)&c->sh_out, (void**)&c->sh_match};
+        const size_t bytes[7] = {sizeof(double) * 12, sizeof(double) * N * ekf::SH_REC,
+                                 sizeof(double) * N * c->d.max_lines * 8, sizeof(double) * shard_words(c),
+                                 sizeof(int) * N, sizeof(int) * 2, sizeof(int) * 2 * c->d.max_lines};
+        for (int k = 0; k < 7; k++) {
+            if (*bufs[k] == nullptr && hipMalloc(bufs[k], bytes[k]) != hipSuccess) {
+                for (int q = 0; q < 7; q++) {
+                    if (*bufs[q]) (void)hipFree(*bufs[q]);
+                    *bufs[q] = nullptr;
+                }
+                return EKF_ENOMEM;
+            }
+        }
+    }
     c->sh_match_h.assign(2 * c->d.max_lines, -1);
     // the flush's wave-tiles restricted to those holding a tile of an owned row block (a tile of
     // two ranks' rows is kept by both, identically); groups of 2 and 4 steps take the wave form too
@@ -1384,10 +1483,10 @@ extern "C" int ekf_shard_gate(ekf_ctx* c, int line, int* first_pass)
     if (line < 0 || line >= c->sh_L) return EKF_ERANGE;
     c->sh_line = line;
     const int init[2] = {0x7fffffff, 0};
-    HIP_TRY(hipMemcpyAsync(c->sh_out, init, sizeof(int), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(ekf::launch_shard(shard_params(c, ekf::SH_GATE), c->cfg.precision, c->stream));
-    HIP_TRY(hipMemcpyAsync(first_pass, c->sh_out, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    SH_TRY(hipMemcpyAsync(c->sh_out, init, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_GATE), c->cfg.precision, c->stream));
+    SH_TRY(hipMemcpyAsync(first_pass, c->sh_out, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    SH_TRY(hipStreamSynchronize(c->stream));
     return EKF_OK;
 }
 
@@ -1399,10 +1498,10 @@ extern "C" int ekf_shard_package(ekf_ctx* c, int line, int jstar, double* pkg)
     if (jstar < c->sh_a || jstar >= c->sh_b) return EKF_ERANGE;
     ekf::ShardParams p = shard_params(c, ekf::SH_PACKAGE);
     p.jstar = jstar;
-    HIP_TRY(hipMemsetAsync(c->sh_pkg, 0, sizeof(double) * shard_words(c), c->stream));
-    HIP_TRY(ekf::launch_shard(p, c->cfg.precision, c->stream));
-    HIP_TRY(hipMemcpyAsync(pkg, c->sh_pkg, sizeof(double) * shard_words(c), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    SH_TRY(hipMemsetAsync(c->sh_pkg, 0, sizeof(double) * shard_words(c), c->stream));
+    SH_TRY(ekf::launch_shard(p, c->cfg.precision, c->stream));
+    SH_TRY(hipMemcpyAsync(pkg, c->sh_pkg, sizeof(double) * shard_words(c), hipMemcpyDeviceToHost, c->stream));
+    SH_TRY(hipStreamSynchronize(c->stream));
     return EKF_OK;
 }
 
@@ -1413,18 +1512,18 @@ extern "C" int ekf_shard_apply(ekf_ctx* c, int line, int jstar, const double* pk
     ekf::ShardParams p = shard_params(c, ekf::SH_APPLY);
     p.jstar = jstar;
     if (jstar >= 0)
-        HIP_TRY(hipMemcpyAsync(c->sh_pkg, pkg, sizeof(double) * shard_words(c), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(ekf::launch_shard(p, c->cfg.precision, c->stream));
+        SH_TRY(hipMemcpyAsync(c->sh_pkg, pkg, sizeof(double) * shard_words(c), hipMemcpyHostToDevice, c->stream));
+    SH_TRY(ekf::launch_shard(p, c->cfg.precision, c->stream));
     if (jstar >= 0) {
         // the robot block after the match (Robot.cpp:560-602), the same on every rank
-        HIP_TRY(ekf::launch_shard(shard_params(c, ekf::SH_ROBOT), c->cfg.precision, c->stream));
+        SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_ROBOT), c->cfg.precision, c->stream));
         c->sh_match_h[line] = jstar;
         c->sh_m++;
     } else {
         c->sh_match_h[c->d.max_lines + c->sh_nextra] = line;
         c->sh_nextra++;
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    SH_TRY(hipStreamSynchronize(c->stream));
     return EKF_OK;
 }
 
@@ -1436,9 +1535,9 @@ extern "C" int ekf_shard_operands(ekf_ctx* c, void* U, void* V, int upload)
     const ekf::Slot& cur = slot_of(c, c->nsteps);
     const size_t bytes = c->op_inst * c->op_elem;
     const hipMemcpyKind k = upload ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
-    HIP_TRY(hipMemcpyAsync(upload ? cur.Uop : U, upload ? U : cur.Uop, bytes, k, c->stream));
-    HIP_TRY(hipMemcpyAsync(upload ? cur.Vop : V, upload ? V : cur.Vop, bytes, k, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    SH_TRY(hipMemcpyAsync(upload ? cur.Uop : U, upload ? U : cur.Uop, bytes, k, c->stream));
+    SH_TRY(hipMemcpyAsync(upload ? cur.Vop : V, upload ? V : cur.Vop, bytes, k, c->stream));
+    SH_TRY(hipStreamSynchronize(c->stream));
     return EKF_OK;
 }
 
@@ -1447,10 +1546,10 @@ extern "C" int ekf_shard_operands(ekf_ctx* c, void* U, void* V, int upload)
 extern "C" int ekf_shard_end(ekf_ctx* c)
 {
     if (!c || !c->sh_open) return EKF_EINVAL;
-    HIP_TRY(hipMemcpyAsync(c->sh_match, c->sh_match_h.data(), sizeof(int) * 2 * c->d.max_lines,
+    SH_TRY(hipMemcpyAsync(c->sh_match, c->sh_match_h.data(), sizeof(int) * 2 * c->d.max_lines,
                            hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(ekf::launch_shard(shard_params(c, ekf::SH_END), c->cfg.precision, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_END), c->cfg.precision, c->stream));
+    SH_TRY(hipStreamSynchronize(c->stream));
     return EKF_OK;
 }
 
@@ -1466,9 +1565,9 @@ extern "C" int ekf_shard_patch(ekf_ctx* c, double* rows, int upload)
     if (!c || !c->sh_open || !rows) return EKF_EINVAL;
     const ekf::Slot& cur = slot_of(c, c->nsteps);
     const size_t bytes = ekf_shard_patch_bytes(c);
-    HIP_TRY(hipMemcpyAsync(upload ? (void*)cur.patch : (void*)rows, upload ? (const void*)rows : (const void*)cur.patch,
+    SH_TRY(hipMemcpyAsync(upload ? (void*)cur.patch : (void*)rows, upload ? (const void*)rows : (const void*)cur.patch,
                            bytes, upload ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    SH_TRY(hipStreamSynchronize(c->stream));
     return EKF_OK;
 }
 
@@ -1478,6 +1577,16 @@ extern "C" int ekf_shard_commit(ekf_ctx* c)
     c->sh_open = 0;
     c->nsteps++;
     if (c->nsteps - c->unflushed0 >= c->T) return enqueue_flush(c);
+    return EKF_OK;
+}
+
+extern "C" int ekf_shard_abort(ekf_ctx* c)
+{
+    // before ekf_shard_end nothing of the committed state is written (the phases use the scan's
+    // scratch and the current ring slot, which only ekf_shard_commit adds to the schedule)
+    if (!c || c->sh_a < 0) return EKF_EINVAL;
+    c->sh_open = 0;
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return EKF_OK;
 }
 

@@ -95,6 +95,7 @@ struct ScanParams {
     int Etot;             // instances of the context
     int spin_log2;        // spin bound of every wait: 2^spin_log2 polls (24; tests lower it)
     int test_drop;        // test hook: e + 1 = the last workgroup of instance e never runs (0: off)
+    int test_verdict;     // test hook: e + 1 = workgroup 1 of instance e sees its verdict poll time out
     double* Dd;           // [2][Etot][N][4] diagonal landmark blocks after the last committed step
                           // (copy live[e] read, the other written and committed with Rs / y)
     int mfrep;            // split-bf16 context: pending steps replayed on read by bf16 MFMA from

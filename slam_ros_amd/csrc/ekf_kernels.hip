@@ -1407,6 +1407,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     __shared__ int sh_flag;
     __shared__ int sh_ready;
     __shared__ int sh_rwst;   // status bits of the replay wave (the winners' GSL_EDOM)
+    __shared__ int sh_vto;    // a verdict poll of this workgroup timed out
     __shared__ int sh_first[SPEC_L];   // per line the first guessed candidate (speculative path)
     if (tid < SPEC_L) sh_first[tid] = 0x7fffffff;
     __shared__ double sh_wd[SPEC_L * SPEC_WD];
@@ -1937,6 +1938,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             if (tid == SCAN_BLOCK - 1) {
                 sh_ready = 0;
                 sh_rwst = 0;
+                sh_vto = 0;
             }
             __syncthreads();
             if (mf && tid >= SCAN_THREADS) {
@@ -2286,11 +2288,24 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             if (G > 1) {
                 if (tid == 0) mb_tag(mbox + (size_t)g * p.mbw, p.epoch, TAG_SPEC_VERDICT, (unsigned)any);
                 if (tid < G) {
-                    const int v = mb_poll(mbox, 0, G, tid, p.mbw, p.epoch, TAG_SPEC_VERDICT, tstatus, p.spin_log2);
+                    int v = mb_poll(mbox, 0, G, tid, p.mbw, p.epoch, TAG_SPEC_VERDICT, tstatus, p.spin_log2);
+                    if (p.test_verdict == e + 1 && g == 1 && tid == 0) {   // test hook: this poll timed out
+                        tstatus |= EKF_ST_TIMEOUT_BIT;
+                        v = -1;
+                    }
                     sh_best[tid] = v != 0;
+                    if (v < 0) sh_vto = 1;
                 }
                 __syncthreads();
                 for (int k = 0; k < G; k++) any |= sh_best[k];
+                if (sh_vto) {
+                    // a verdict that never arrived: this workgroup does not restart (its peers
+                    // may have committed their halves already); it finishes with the timeout bit
+                    // in its completion word, and the lead, which collects every word, rolls the
+                    // instance's call back
+                    tstatus |= EKF_ST_TIMEOUT_BIT;
+                    any = 0;
+                }
             }
             EKF_STAMP(6);
             if (any) {
@@ -2593,13 +2608,12 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // state and the step's result record — only if every workgroup completed without a timeout.
     // Otherwise the instance keeps its state from before the call, and the step's record applies
     // nothing (no downdate, rows or reset: the flush and later on-read replays skip it).
-    // After a passed speculative verdict the lead needs no collection: every workgroup published
-    // its verdict word after its last wait (a workgroup that timed out, or never ran, makes the
-    // verdict fail or the lead's own verdict poll time out), and none waits on anything after it.
-    // The done words still carry every workgroup's status bits to ekf_read_results.
+    // The lead collects on the speculative path too: a workgroup's own verdict poll can time out
+    // while the lead's succeeds (the two polls race the spin bound), and that workgroup then
+    // finishes with the timeout bit (above); only its completion word tells the lead.
     EKF_STAMP(25);
     if (tid == 0 && g != 0) publish_done(sync, g, p.epoch, wgst);
-    if (g == 0 && sequential) wgst = lead_collect(sync, G, p.epoch, wgst, p.spin_log2, tid, sh_red);
+    if (g == 0 && (sequential || G > 1)) wgst = lead_collect(sync, G, p.epoch, wgst, p.spin_log2, tid, sh_red);
     EKF_STAMP(26);
     if (lead) {
         sync[SYNC_WG0] = (int)done_word(p.epoch, wgst);

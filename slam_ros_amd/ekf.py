@@ -24,13 +24,20 @@ R_INTENDED, R_AS_WRITTEN = 0, 1
 ARITH_EXACT, ARITH_BF16X6 = 0, 1   # fp32 flush arithmetic (slam_ekf.h EKF_ARITH_*)
 ST_SINGULAR_S, ST_CAPACITY, ST_NONSYM, ST_SYNC_TIMEOUT, ST_RANGE = 1, 2, 4, 8, 16
 EXP_AUTO = -1000
+# per-context options (slam_ekf.h EKF_OPT_*, ekf_set_option)
+OPT_SPECULATE, OPT_SPIN_LOG2, OPT_FLUSH_FORM, OPT_FLUSH_BLOCKS_PER_CU = 1, 2, 3, 4
+OPT_MFMA_REPLAY, OPT_SCAN_STAMPS, OPT_TEST_DROP_WG, OPT_TEST_VERDICT_TIMEOUT = 5, 6, 7, 8
+OPTIONS = {"speculate": OPT_SPECULATE, "spin_log2": OPT_SPIN_LOG2, "flush_form": OPT_FLUSH_FORM,
+           "flush_blocks_per_cu": OPT_FLUSH_BLOCKS_PER_CU, "mfma_replay": OPT_MFMA_REPLAY,
+           "scan_stamps": OPT_SCAN_STAMPS, "test_drop_wg": OPT_TEST_DROP_WG,
+           "test_verdict_timeout": OPT_TEST_VERDICT_TIMEOUT}
 
 LIB_PATH = _build.LIB_PATH
 
 # symbols declared by include/slam_ekf.h (checked by tests/test_abi.py)
 EXPORTED = [
     "ekf_config_init", "ekf_strerror", "ekf_abi_version", "ekf_create", "ekf_destroy",
-    "ekf_set_stream", "ekf_sync", "ekf_reset_instance", "ekf_localize", "ekf_localize_device",
+    "ekf_set_stream", "ekf_sync", "ekf_set_option", "ekf_get_option", "ekf_reset_instance", "ekf_localize", "ekf_localize_device",
     "ekf_predict", "ekf_update", "ekf_read_results", "ekf_upload_state", "ekf_download_state",
     "ekf_init_lowrank", "ekf_storage_exponent", "ekf_rescale", "ekf_get_pose_cov", "ekf_get_ellipse", "ekf_ellipse_of_block",
     "ekf_landmark_block_bytes",
@@ -39,7 +46,7 @@ EXPORTED = [
     "ekf_shard_init", "ekf_shard_begin", "ekf_shard_gate", "ekf_shard_package_words", "ekf_shard_package",
     "ekf_shard_apply", "ekf_shard_end", "ekf_shard_operand_bytes", "ekf_shard_operands", "ekf_shard_patch_bytes",
     "ekf_shard_patch", "ekf_shard_commit",
-    "ekf_shard_status",
+    "ekf_shard_status", "ekf_shard_abort",
 ]
 
 
@@ -97,6 +104,8 @@ def load_library(path: str = ""):
         "ekf_destroy": (ctypes.c_int, [vp]),
         "ekf_set_stream": (ctypes.c_int, [vp, vp]),
         "ekf_sync": (ctypes.c_int, [vp]),
+        "ekf_set_option": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int]),
+        "ekf_get_option": (ctypes.c_int, [vp, ctypes.c_int, ip]),
         "ekf_reset_instance": (ctypes.c_int, [vp, ctypes.c_int, d, d, d]),
         "ekf_localize": (ctypes.c_int, [vp, dp, vp, ip, vp]),
         "ekf_localize_device": (ctypes.c_int, [vp, vp, vp, vp]),
@@ -135,6 +144,7 @@ def load_library(path: str = ""):
         "ekf_shard_patch": (ctypes.c_int, [vp, dp, ctypes.c_int]),
         "ekf_shard_commit": (ctypes.c_int, [vp]),
         "ekf_shard_status": (ctypes.c_int, [vp, ip]),
+        "ekf_shard_abort": (ctypes.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -183,7 +193,8 @@ class Ensemble:
     def __init__(self, capacity: int, instances: int = 1, precision: int = PREC_F64,
                  max_lines: int = 20, device: int = -1, r_mode: int = R_INTENDED,
                  reset_margin: int = 10, mahalanobis: float = 0.4, encoder_noise: float = 0.024,
-                 pipeline: bool = False, flush_interval: int = 1, arith: int = ARITH_EXACT):
+                 pipeline: bool = False, flush_interval: int = 1, arith: int = ARITH_EXACT,
+                 options: dict | None = None):
         self._lib = load_library()
         cfg = EkfConfig()
         self._lib.ekf_config_init(ctypes.byref(cfg))
@@ -201,6 +212,8 @@ class Ensemble:
         self.arith = int(arith)
         self.n = self._lib.ekf_state_dim(h)
         self._res = (EkfResult * instances)()
+        for k, v in (options or {}).items():
+            self.set_option(k, v)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -222,6 +235,17 @@ class Ensemble:
 
     def sync(self):
         _check(self._lib.ekf_sync(self._h), "ekf_sync")
+
+    def set_option(self, option, value: int):
+        """ekf_set_option: option is an OPT_* number or an OPTIONS name (e.g. "speculate")."""
+        opt = OPTIONS[option] if isinstance(option, str) else int(option)
+        _check(self._lib.ekf_set_option(self._h, opt, int(value)), f"ekf_set_option({option}, {value})")
+
+    def get_option(self, option) -> int:
+        opt = OPTIONS[option] if isinstance(option, str) else int(option)
+        v = ctypes.c_int32()
+        _check(self._lib.ekf_get_option(self._h, opt, ctypes.byref(v)), f"ekf_get_option({option})")
+        return v.value
 
     def reset(self, e: int = -1, x: float = 0.0, y: float = 0.0, theta: float = 0.0):
         _check(self._lib.ekf_reset_instance(self._h, e, x, y, theta), "ekf_reset_instance")

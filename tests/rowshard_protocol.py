@@ -1,5 +1,8 @@
-"""One EKF instance row-sharded across ranks: the protocol
-for N ≫ 4096, where a single landmark block outgrows what one GPU should rewrite per scan.
+"""TEST INFRASTRUCTURE (not product code; only tests/test_rowshard_gloo.py imports it). One EKF
+instance row-sharded across ranks: the protocol for
+N ≫ 4096, where a single landmark block outgrows what one GPU should rewrite per scan, as an
+executable specification on host arrays. The product form is slam_ros_amd/rowshard_gpu.py over
+the library's ekf_shard_* kernels.
 
 Partition: rank r owns the landmarks [a_r, b_r) (contiguous, sizes differing by at most one,
 `dist.shard`), i.e. the full rows 3+2a_r … 3+2b_r−1 of P (all n columns). Every rank keeps a
@@ -33,8 +36,8 @@ This module is the protocol's executable specification on host arrays (float64 n
 operation order of the CPU restatement's fast mode, oracle/ekf_oracle.c, so that the sharded run
 is bit-identical to the single-process one: tests/test_rowshard_gloo.py, world_size 2 over
 gloo). On MI355X ranks the owned rows live in HBM in the packed tile layout of one instance and
-the local steps are the association kernel's per-workgroup phases; the
-collectives are the same calls over RCCL. It is not on the benchmark path (the ensemble is).
+the local steps are the library's shard phases. It is not on the benchmark path
+(the ensemble is).
 """
 from __future__ import annotations
 
@@ -42,7 +45,7 @@ import math
 
 import numpy as np
 
-from .dist import shard
+from slam_ros_amd.dist import shard
 
 MAHALANOBIS = 0.4          # Robot.h:15
 ENCODERNOISE = 0.024       # Robot.h:17

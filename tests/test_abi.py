@@ -42,7 +42,12 @@ def test_library_is_gfx950_code_object(ekf_mod):
 
 def test_cpu_only_calls(ekf_mod):
     lib = ekf_mod.load_library()
-    assert lib.ekf_abi_version() == 2   # ABI 2: 32 stamp slots, arith validated, rollback
+    assert lib.ekf_abi_version() == 3   # ABI 3: options instead of environment variables
+    # no context: every option call is EKF_EINVAL before any HIP call
+    v = ctypes.c_int32()
+    assert lib.ekf_set_option(None, ekf_mod.OPT_SPECULATE, 1) == 1
+    assert lib.ekf_get_option(None, ekf_mod.OPT_SPECULATE, ctypes.byref(v)) == 1
+    assert lib.ekf_shard_abort(None) == 1
     assert lib.ekf_strerror(0) == b"ok"
     cfg = ekf_mod.EkfConfig()
     lib.ekf_config_init(ctypes.byref(cfg))
@@ -66,6 +71,21 @@ def test_cpu_only_calls(ekf_mod):
         bad.precision, bad.max_lines, bad.arith = ekf_mod.PREC_F32, 8, ekf_mod.ARITH_BF16X6
         setattr(bad, field, val)
         assert lib.ekf_create(ctypes.byref(bad), ctypes.byref(h)) == 1, field
+
+
+def test_library_reads_no_environment(ekf_mod):
+    """The product library reads no environment variables (a stray EKF_TEST_DROP_WG
+    made an instance time out on every scan): no getenv import in the shared object, and the
+    former knobs are per-context options (slam_ekf.h EKF_OPT_*)."""
+    out = subprocess.run(["nm", "-D", "--undefined-only", ekf_mod.LIB_PATH], capture_output=True, text=True)
+    assert out.returncode == 0
+    assert not re.search(r"\b(secure_)?getenv\b", out.stdout), out.stdout
+    src = open(HEADER).read()
+    for name in ("EKF_OPT_SPECULATE", "EKF_OPT_SPIN_LOG2", "EKF_OPT_FLUSH_FORM", "EKF_OPT_FLUSH_BLOCKS_PER_CU",
+                 "EKF_OPT_MFMA_REPLAY", "EKF_OPT_SCAN_STAMPS", "EKF_OPT_TEST_DROP_WG",
+                 "EKF_OPT_TEST_VERDICT_TIMEOUT"):
+        assert name in src
+        assert getattr(ekf_mod, name[4:]) == int(re.search(name + r" = (\d+)", src).group(1))
 
 
 def test_struct_layouts_match_header():

@@ -50,7 +50,7 @@ def record(key, value):
     json.dump(data, open(path, "w"), indent=1)
 
 
-def run_config(ekf_mod, oracle_mod, prec, T, scans, pipeline=False, arith=0):
+def run_config(ekf_mod, oracle_mod, prec, T, scans, pipeline=False, arith=0, N=N):
     from tests.hipmem import DeviceArray
     world = G.make_world(N)
     st = G.initial_state(world)
@@ -135,11 +135,14 @@ def test_bench_config_fp32_t8_bf16x6_pipelined(ekf_mod, oracle_mod):
     record("f32_T8_N4096_E8_bf16x6_pipelined", out)
 
 
-def test_bench_config_fp32_t12_bf16x6(ekf_mod, oracle_mod):
-    """bench.py's default line: EKF_ARITH_BF16X6 at T = 12 over its 20 timed steps (a group of 12,
-    then 8 flushed by ekf_sync); up to 11 pending steps replayed on read (staged in LDS)."""
-    out = run_config(ekf_mod, oracle_mod, 1, 12, 20, arith=ekf_mod.ARITH_BF16X6)
-    record("f32_T12_N4096_E8_bf16x6", out)
+@pytest.mark.parametrize("n_cap", [256, 1024, 4096])
+def test_bench_config_fp32_t12_bf16x6(ekf_mod, oracle_mod, n_cap):
+    """bench.py's default schedule at every capacity BASELINE names (configs 2, 3 and 4's per-GPU
+    slice): EKF_ARITH_BF16X6 at T = 12, E = 8, over the driver's 20 timed steps (a group of 12, then
+    8 flushed by ekf_sync), no intermediate drains; up to 11 pending steps replayed on read by MFMA
+    on the operand planes. Instances 0 and 7 against the restatement, never re-synchronised."""
+    out = run_config(ekf_mod, oracle_mod, 1, 12, 20, arith=ekf_mod.ARITH_BF16X6, N=n_cap)
+    record(f"f32_T12_N{n_cap}_E8_bf16x6", out)
 
 
 def test_bench_config_fp32_t16_bf16x6(ekf_mod, oracle_mod):

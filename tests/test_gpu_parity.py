@@ -453,16 +453,15 @@ def _spec_scans(w, rng, steps, L=8):
 def test_speculative_association_identical(ekf_mod, oracle_mod, monkeypatch, prec, N, T):
     """The speculative association (guessed winners, three exchanges per scan, exact local
     re-check) gives bit-identical state and results to the per-line sequential exchange, also
-    when every guess is wrong (EKF_SPECULATE=2: every scan falls back); association vs the
+    when every guess is wrong (EKF_OPT_SPECULATE = 2: every scan falls back); association vs the
     restatement."""
     w = G.make_world(N, active=N - 30)
     st = G.initial_state(w)
     scans = _spec_scans(w, np.random.default_rng(3), 8)
     runs = {}
-    monkeypatch.setenv("EKF_SCAN_STAMPS", "1")
     for mode in (0, 1, 2):
-        monkeypatch.setenv("EKF_SPECULATE", str(mode))
-        ens = ekf_mod.Ensemble(N, 1, prec, max_lines=8, flush_interval=T)
+        ens = ekf_mod.Ensemble(N, 1, prec, max_lines=8, flush_interval=T,
+                               options={"scan_stamps": 1, "speculate": mode})
         ens.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
         if mode == 1:
             ref = oracle_mod.OracleRobot(N)
@@ -494,7 +493,7 @@ def test_speculative_association_identical(ekf_mod, oracle_mod, monkeypatch, pre
 def test_hot_scan_kernel_equals_generic(ekf_mod, monkeypatch, prec, arith):
     """The association kernel's HOT instantiation (symmetric fp32 operands, kmax 16: the product
     launch of every EKF_R_INTENDED fp32/fp16 context with max_lines <= 8) and the generic
-    instrumented one (EKF_SCAN_STAMPS=1, `scan_kernel<T, true, false>`) give bit-identical state
+    instrumented one (EKF_OPT_SCAN_STAMPS = 1, `scan_kernel<T, true, false>`) give bit-identical state
     and results — on the speculative path (with the early U/V operand stores after the fourth
     match) and when every guess is wrong (the restart after those stores), in both flush
     arithmetics (Robot.cpp:313-641)."""
@@ -505,9 +504,8 @@ def test_hot_scan_kernel_equals_generic(ekf_mod, monkeypatch, prec, arith):
     runs = {}
     for stamps in ("0", "1"):
         for spec in ("1", "2"):
-            monkeypatch.setenv("EKF_SCAN_STAMPS", stamps)
-            monkeypatch.setenv("EKF_SPECULATE", spec)
-            ens = ekf_mod.Ensemble(N, 1, prec, max_lines=8, flush_interval=T, arith=arith)
+            ens = ekf_mod.Ensemble(N, 1, prec, max_lines=8, flush_interval=T, arith=arith,
+                                   options={"scan_stamps": int(stamps), "speculate": int(spec)})
             ens.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
             results = []
             for enc, ln in scans:
@@ -535,17 +533,14 @@ def test_hot_scan_kernel_equals_generic(ekf_mod, monkeypatch, prec, arith):
                                                   (1024, 8, 8, 0), (1024, 4, 6, 5)])
 def test_wave_flush_equals_drained(ekf_mod, monkeypatch, prec, N, T, lines, extra_every):
     """The barrier-free per-wave flush (2 × 2-tile wave-tiles, software-pipelined operand ring;
-    forced with EKF_FLUSH_VARIANT=8) gives bit-identical state to one in-place flush per scan:
+    forced with EKF_OPT_FLUSH_FORM = 8) gives bit-identical state to one in-place flush per scan:
     full groups in its pipelined loop (8 matches, or partial downdates predicated), groups with
     augmentation rows or the capacity reset in its general loop, odd tile counts (N = 80: 5 tile
     rows, a wave-tile column past the block) and several instances per XCD range."""
-    # EKF_WAVE_TEST_VARIANT=83 checks the fp32 group-major form the same way
-    monkeypatch.setenv("EKF_FLUSH_VARIANT", os.environ.get("EKF_WAVE_TEST_VARIANT", "8"))
     E = 3
     w = G.make_world(N, active=N - 14 if extra_every else N - 10)
     st = G.initial_state(w)
-    a = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T)
-    monkeypatch.delenv("EKF_FLUSH_VARIANT")
+    a = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, options={"flush_form": 8})
     b = ekf_mod.Ensemble(N, E, prec, max_lines=8)
     for ens in (a, b):
         for e in range(E):
@@ -675,15 +670,13 @@ def test_bf16x6_fp16_storage(ekf_mod, oracle_mod, N, T, extra_every):
 def test_f64_wave_flush_equals_tile_kernel(ekf_mod, monkeypatch, N, T, lines, extra_every):
     """fp64 storage: the wave flush (1 × 2-tile wave-tiles, every k-step run over the −0·(+0)
     operand padding; default for groups of ≤ 4 steps) gives bit-identical state to the per-tile
-    downdate_f64_kernel (EKF_FLUSH_VARIANT=2) flushed after every scan — fast loop, predicated
+    downdate_f64_kernel (EKF_OPT_FLUSH_FORM = 2) flushed after every scan — fast loop, predicated
     partial downdates, and the general loop for groups with augmentation rows or the reset."""
     E = 3
     w = G.make_world(N, active=N - 14 if extra_every else N - 10)
     st = G.initial_state(w)
     a = ekf_mod.Ensemble(N, E, 0, max_lines=8, flush_interval=T)
-    monkeypatch.setenv("EKF_FLUSH_VARIANT", "2")
-    b = ekf_mod.Ensemble(N, E, 0, max_lines=8)
-    monkeypatch.delenv("EKF_FLUSH_VARIANT")
+    b = ekf_mod.Ensemble(N, E, 0, max_lines=8, options={"flush_form": 2})
     for ens in (a, b):
         for e in range(E):
             ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
@@ -717,7 +710,6 @@ def test_singular_status_counts_only_evaluated_candidates(ekf_mod, oracle_mod, m
     one). Landmark 1 has a zero covariance and the lines an exact R = 0, so its S is singular;
     observing landmark 0 never evaluates it, observing landmark 1 does (after landmark 0 fails).
     Speculative and sequential association paths."""
-    monkeypatch.setenv("EKF_SPECULATE", spec)
     N = 16
     n = 3 + 2 * N
     P = np.zeros((n, n))
@@ -726,7 +718,7 @@ def test_singular_status_counts_only_evaluated_candidates(ekf_mod, oracle_mod, m
     y[3:5] = (0.5, 2.0)
     y[5:7] = (1.2, 3.0)
     for target, want in ((0, 0), (1, 1)):
-        ens = ekf_mod.Ensemble(N, 1, prec, max_lines=8)
+        ens = ekf_mod.Ensemble(N, 1, prec, max_lines=8, options={"speculate": int(spec)})
         ens.upload_state(0, P, y, 2, [0.0, 0.0, 0.0])
         ref = oracle_mod.OracleRobot(N)
         ref.set_state(*ens.download_state(0))
@@ -741,7 +733,7 @@ def test_singular_status_counts_only_evaluated_candidates(ekf_mod, oracle_mod, m
 
 @pytest.mark.parametrize("prec,N,T,extra_every", [(1, 1024, 12, 0), (1, 200, 8, 3), (2, 512, 10, 0), (1, 100, 16, 0)])
 def test_bf16_2x4_flush_equals_2x2(ekf_mod, monkeypatch, prec, N, T, extra_every):
-    """The split-bf16 flush on 2 × 4 wave-tiles (flush_bf24_kernel, EKF_FLUSH_VARIANT=24) and on 2 × 2
+    """The split-bf16 flush on 2 × 4 wave-tiles (flush_bf24_kernel, EKF_OPT_FLUSH_FORM = 24) and on 2 × 2
     wave-tiles (flush_f32_wave_kernel<.., true>, default) run the same MFMA sequence per element
     (same part products in the same order, bf16 MFMA deterministic): bit-identical state, fast
     groups and groups with augmented rows (general path on the two 2 × 2 halves) alike, fp32 and
@@ -750,9 +742,8 @@ def test_bf16_2x4_flush_equals_2x2(ekf_mod, monkeypatch, prec, N, T, extra_every
     active = N - 12 - 2 * ((3 * T + 1) // extra_every) if extra_every else N - 10
     w = G.make_world(N, active=active)
     st = G.initial_state(w)
-    monkeypatch.setenv("EKF_FLUSH_VARIANT", "24")
-    a = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
-    monkeypatch.delenv("EKF_FLUSH_VARIANT")
+    a = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6,
+                         options={"flush_form": 24})
     b = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
     assert a.flush_kernel_name(T).startswith("flush_bf24_kernel"), a.flush_kernel_name(T)
     assert b.flush_kernel_name(T).endswith(", true>"), b.flush_kernel_name(T)

@@ -5,8 +5,11 @@ returns). Here an instance spans G cooperating workgroups; if one of them never 
 others give up after a bounded spin. The launch must then leave that instance exactly as it was
 before the call — robot strip, mean, pose, savedLineCount and the landmark block, including across
 the deferred flushes of later groups — while every other instance of the same launch proceeds.
-The test hook EKF_TEST_DROP_WG=e makes the last workgroup of instance e never run (a workgroup
-that is not co-resident), EKF_SPIN_LOG2 shortens the spin bound.
+The test hook EKF_OPT_TEST_DROP_WG = e + 1 makes the last workgroup of instance e never run (a
+workgroup that is not co-resident), EKF_OPT_SPIN_LOG2 shortens the spin bound, and
+EKF_OPT_TEST_VERDICT_TIMEOUT = e + 1 makes one non-lead workgroup's verdict poll time out while the
+others complete (the race of two polls against the spin bound). The library reads no environment
+variables: a stray EKF_TEST_DROP_WG in the environment changes nothing.
 """
 import numpy as np
 import pytest
@@ -22,16 +25,12 @@ def rel(a, b):
 
 
 @pytest.mark.parametrize("prec,T,spec", [(1, 4, "1"), (1, 1, "0"), (0, 3, "1"), (2, 4, "1")])
-def test_timeout_rolls_back_the_instance(ekf_mod, oracle_mod, monkeypatch, prec, T, spec):
+def test_timeout_rolls_back_the_instance(ekf_mod, oracle_mod, prec, T, spec, hook="test_drop_wg"):
     N, E = 1024, 3   # G = 6 workgroups per instance
     w = G.make_world(N)
     st = G.initial_state(w)
-    monkeypatch.setenv("EKF_TEST_DROP_WG", "1")
-    monkeypatch.setenv("EKF_SPIN_LOG2", "12")
-    monkeypatch.setenv("EKF_SPECULATE", spec)
-    ens = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T)
-    for k in ("EKF_TEST_DROP_WG", "EKF_SPIN_LOG2", "EKF_SPECULATE"):
-        monkeypatch.delenv(k)
+    ens = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T,
+                           options={hook: 2, "spin_log2": 12, "speculate": int(spec)})
     for e in range(E):
         ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
     before = ens.download_state(1)
@@ -61,12 +60,31 @@ def test_timeout_rolls_back_the_instance(ekf_mod, oracle_mod, monkeypatch, prec,
     ens.close()
 
 
+@pytest.mark.parametrize("prec,T", [(1, 4), (0, 3), (2, 4)])
+def test_verdict_timeout_of_one_workgroup_rolls_back(ekf_mod, oracle_mod, prec, T):
+    """One non-lead workgroup's speculative verdict poll times out while every other workgroup
+    (the lead included) sees a passed verdict: that workgroup must not restart alone on the
+    sequential path and the lead must not commit without its completion word: the
+    instance's calls roll back, the other instances proceed."""
+    test_timeout_rolls_back_the_instance(ekf_mod, oracle_mod, prec, T, "1", hook="test_verdict_timeout")
+
+
+def test_environment_is_not_read(ekf_mod, monkeypatch):
+    """The former environment knobs have no effect: a stray EKF_TEST_DROP_WG (which used to make
+    an instance time out on every scan) leaves every call committing."""
+    monkeypatch.setenv("EKF_TEST_DROP_WG", "0")
+    monkeypatch.setenv("EKF_SPECULATE", "2")
+    monkeypatch.setenv("EKF_SPIN_LOG2", "8")
+    test_no_rollback_without_timeout(ekf_mod)
+
+
 def test_no_rollback_without_timeout(ekf_mod):
     """A normal launch commits: the committed copy alternates, nothing is rolled back."""
     N, E = 1024, 2
     w = G.make_world(N)
     st = G.initial_state(w)
     ens = ekf_mod.Ensemble(N, E, 1, max_lines=8, flush_interval=2)
+    assert ens.get_option("test_drop_wg") == 0 and ens.get_option("speculate") == 1
     for e in range(E):
         ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
     for step in range(1, 4):

@@ -1,4 +1,4 @@
-"""§8f #4: one EKF instance with P row-sharded over ranks (slam_ros_amd/rowshard.py)
+"""§8f #4: one EKF instance with P row-sharded over ranks (tests/rowshard_protocol.py)
 against the single-process CPU restatement (oracle/, fast mode). gloo, world_size 2 and 3: the
 trajectory — matches, augmentation rows that land on either rank, the capacity reset — must be
 bit-identical, association included (the sharded gating picks the first passing landmark over
@@ -40,7 +40,7 @@ def scenario():
 def worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from slam_ros_amd.rowshard import RowShardedRobot
+    from tests.rowshard_protocol import RowShardedRobot
     st, scans = scenario()
     rob = RowShardedRobot(N, dist)
     rob.set_state(st.dense_P(), st.y, st.saved, st.pose)
