@@ -59,6 +59,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: dense fp32 MFMA (v_mfma_f32_32x32x2_f32)
 MFMA_F64_PEAK_TFS = 78.6    # MI355X_MICROARCH.md: dense fp64 MFMA
 MFMA_BF16_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (v_mfma_f32_32x32x16_bf16)
+MFMA_F16_PEAK_TFS = 2500.0   # MI355X_MICROARCH.md: dense fp16 MFMA (v_mfma_f32_32x32x16_f16), as bf16
 L_LINES = 8
 
 
@@ -87,7 +88,7 @@ def parse():
                     help="nccl (= RCCL on ROCm); gloo only to rehearse ranks on one GPU")
     ap.add_argument("--preroll", type=int, default=200,
                     help="untimed clock pre-roll steps before the warm-up (steady GPU clocks)")
-    ap.add_argument("--arith", choices=["exact", "bf16x6"], default="bf16x6",
+    ap.add_argument("--arith", choices=["exact", "bf16x6", "f16x3"], default="bf16x6",
                     help="fp32 flush arithmetic (slam_ekf.h EKF_ARITH_*): exact = fp32 MFMA, the state "
                          "bit-identical for every T; bf16x6 = fp32 operands split exactly into three "
                          "bf16 parts, six bf16 MFMAs per product (f32 storage only)")
@@ -260,11 +261,11 @@ def main():
     profile = None if args.world == "bench" else args.world
     st = G.initial_state(world_map, profile=profile)
 
-    arith = {"exact": ekf.ARITH_EXACT, "bf16x6": ekf.ARITH_BF16X6}[args.arith]
+    arith = {"exact": ekf.ARITH_EXACT, "bf16x6": ekf.ARITH_BF16X6, "f16x3": ekf.ARITH_F16X3}[args.arith]
     if prec == ekf.PREC_F64:
         arith = ekf.ARITH_EXACT   # the split-bf16 flush serves fp32 operands (fp32 and fp16 storage)
     if args.flush_interval <= 0:
-        args.flush_interval = 4 if prec == ekf.PREC_F64 else (12 if arith == ekf.ARITH_BF16X6 else 8)
+        args.flush_interval = 4 if prec == ekf.PREC_F64 else (8 if arith == ekf.ARITH_EXACT else 12)
     ens = ekf.Ensemble(N, E, prec, max_lines=L_LINES, device=local, pipeline=bool(args.pipeline),
                       flush_interval=args.flush_interval, arith=arith,
                       options={"speculate": args.speculate})
@@ -373,10 +374,13 @@ def main():
     alg_bytes = E * n * (n + 1) * bpe   # one read + write of the packed block per flush
     alg_flops = steps_per_launch * E * 2 * L_LINES * n * (n + 1)
     bf_form = bool(dom and (dom["kernel"].endswith(", true>") or dom["kernel"].startswith("flush_bf24_kernel")))
+    f16_form = bool(dom and dom["kernel"].endswith(", true, true>"))
     # the MFMA roof of the instruction the flush executes: the split-bf16 flush runs six bf16
     # products per fp32 product (executed flops = 6 x algorithmic, dense bf16 peak); the exact
     # forms run v_mfma_f32_32x32x2_f32 (fp32 and fp16 storage) or v_mfma_f64_16x16x4_f64
-    if bf_form:
+    if f16_form:
+        mfma_mult, mfma_peak, mfma_dtype = 3, MFMA_F16_PEAK_TFS, "f16 (three split products per fp32 product)"
+    elif bf_form:
         mfma_mult, mfma_peak, mfma_dtype = 6, MFMA_BF16_PEAK_TFS, "bf16 (six split products per fp32 product)"
     elif prec == ekf.PREC_F64:
         mfma_mult, mfma_peak, mfma_dtype = 1, MFMA_F64_PEAK_TFS, "f64"
@@ -415,7 +419,7 @@ def main():
             "parallelism": (f"ensemble x{world} ({'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} "
                             f"broadcast of {B} scans per collective)") if world > 1 else "ensemble x1",
                 "pipeline": bool(args.pipeline), "flush_interval": args.flush_interval,
-            "arith": "bf16x6" if arith == ekf.ARITH_BF16X6 else "exact",
+            "arith": {ekf.ARITH_EXACT: "exact", ekf.ARITH_BF16X6: "bf16x6", ekf.ARITH_F16X3: "f16x3"}[arith],
             "association": {0: "sequential", 1: "speculative", 2: "speculative, every guess wrong"}[args.speculate],
             "world": args.world,
         },

@@ -36,7 +36,7 @@ extern "C" {
  *    that can never use it; EKF_ST_SYNC_TIMEOUT rolls the call back instead of committing it.
  * 3: ekf_set_option / ekf_get_option replace the environment variables the library used to read
  *    (EKF_SPECULATE, EKF_SPIN_LOG2, EKF_TEST_DROP_WG, EKF_MFREP, EKF_SCAN_STAMPS,
- *    EKF_DD_BLOCKS_PER_CU, EKF_FLUSH_VARIANT); ekf_shard_abort. */
+ *    EKF_DD_BLOCKS_PER_CU, EKF_FLUSH_VARIANT); ekf_shard_abort; EKF_ARITH_F16X3. */
 #define SLAM_EKF_ABI_VERSION 3
 #define EKF_MAX_LINES 64 /* lines per scan per instance; main.cpp:99 reserves 20 */
 
@@ -86,8 +86,16 @@ enum { EKF_R_INTENDED = 0, EKF_R_AS_WRITTEN = 1 };
  *   by the same bf16 MFMAs on the planes and keeps the diagonal blocks in fp64. Groups of an even number of steps (2..16) without
  *   augmented rows or a reset take the split-bf16 flush; a group with augmentation or the reset,
  *   and an odd-sized group (a partial group flushed by a drain), take the EXACT forms
- *   (ekf_flush_kernel_name reports the form a group size runs). */
-enum { EKF_ARITH_EXACT = 0, EKF_ARITH_BF16X6 = 1 };
+ *   (ekf_flush_kernel_name reports the form a group size runs).
+ * F16X3: the same requirements, schedule and fallbacks as BF16X6, with a two-part fp16 split
+ *   instead: every operand row is scaled by 2^σ (σ per instance, from the largest landmark variance
+ *   vmax: |2^σ·V| <= 2^12 because each step's downdate V·Vᵀ is bounded by the variances it reduces;
+ *   the association kernel lowers σ when a new landmark raises vmax, always at a step that takes the
+ *   EXACT forms), split into hi + lo fp16 parts (22 significant bits), and each product runs as three
+ *   v_mfma_f32_32x32x16_f16 — (lo, hi), (hi, lo), (hi, hi) — accumulated in fp32, the accumulators
+ *   holding P·2^(2σ) (power-of-two scalings, exact). Half the MFMA work and two thirds of the plane
+ *   bytes of BF16X6; per product within ≈2^-21 relative (BF16X6: 2^-23), held to the same bar. */
+enum { EKF_ARITH_EXACT = 0, EKF_ARITH_BF16X6 = 1, EKF_ARITH_F16X3 = 2 };
 
 typedef struct ekf_config {
     int32_t capacity;      /* N = LINESIZE (Robot.h:13); landmarks per instance */

@@ -107,9 +107,12 @@ struct ekf_ctx {
     void* ops_u;              // operand rows of every ring slot (U), slot_bytes apart
     void* ops_v;              // ... (V)
     long long slot_bytes;
-    void* ops_b;              // EKF_ARITH_BF16X6: bf16 planes of V of every ring slot (else null)
+    void* ops_b;              // split-plane arithmetics: the planes of V of every ring slot (else null)
     long long bslot_bytes;
-    bool bf;                  // the split-bf16 flush applies (arith, fp32, symmetric R, kmax 16)
+    bool bf;                  // a split-plane flush applies (arith, fp32 operands, symmetric R, kmax 16)
+    int pmode;                // its plane arithmetic: 1 EKF_ARITH_BF16X6, 2 EKF_ARITH_F16X3 (0: none)
+    int* psig;                // [E] EKF_ARITH_F16X3 plane exponent σ (device; the association kernel's
+    double* pvmax;            // [E] lead lowers it when a new landmark raises the largest variance)
     std::vector<int> pexp_h;
     // flush scheduling (see the top of this file)
     int T;                    // flush interval
@@ -175,7 +178,7 @@ static void free_all(ekf_ctx* c)
 {
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->cur, c->pose, c->xpre, c->saved, c->D,
                                c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->wt24, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->pexp, c->sink, c->mbox,
-                               c->sync, c->Ust, c->Vst, c->dense,
+                               c->sync, c->Ust, c->Vst, c->dense, c->psig, c->pvmax,
                                c->sh_rob, c->sh_rec, c->sh_hist, c->sh_pkg, c->sh_flags, c->sh_out, c->sh_match};
     ptrs.push_back(c->ops_u);
     ptrs.push_back(c->ops_v);
@@ -256,6 +259,17 @@ static int choose_exponent(const ekf_ctx* c, double vmax)
     return std::max(-24, std::min(ekf::F16_EXP_DEFAULT, x));
 }
 
+// EKF_ARITH_F16X3 plane exponent of instance e from its largest landmark variance (every context
+// keeps it; only F16X3 reads it)
+static int set_plane_scale(ekf_ctx* c, int e, double vmax)
+{
+    const int sg = ekf::plane_sigma(vmax);
+    const double vm = (vmax > 0.0 && std::isfinite(vmax)) ? vmax : 0.0;
+    HIP_TRY(hipMemcpy(c->psig + e, &sg, sizeof(int), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->pvmax + e, &vm, sizeof(double), hipMemcpyHostToDevice));
+    return EKF_OK;
+}
+
 static int set_robot_ctor(ekf_ctx* c, int e, double x, double y, double th)
 {
     // Robot::Robot (Robot.cpp:20-35): P_t0[0][0] = P_t0[1][1] = 0.05, P_t0[2][2] = 0, the rest
@@ -278,6 +292,8 @@ static int set_robot_ctor(ekf_ctx* c, int e, double x, double y, double th)
     HIP_TRY(hipMemcpyAsync(c->xpre + 3 * e, pose, sizeof(pose), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->saved + e, &zero, sizeof(int), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    const int rc = set_plane_scale(c, e, 0.0);   // an empty map
+    if (rc) return rc;
     return set_exponent(c, e, c->cfg.precision == EKF_PREC_F16 ? ekf::F16_EXP_DEFAULT : 0);
 }
 
@@ -295,9 +311,9 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
          cfg->precision != EKF_PREC_F16) ||
         (cfg->r_mode != EKF_R_INTENDED && cfg->r_mode != EKF_R_AS_WRITTEN) ||
         cfg->flush_interval < 0 || cfg->flush_interval > 16 ||
-        (cfg->arith != EKF_ARITH_EXACT && cfg->arith != EKF_ARITH_BF16X6) ||
-        // the split-bf16 flush needs symmetric fp32 operands with kmax = 16 (slam_ekf.h)
-        (cfg->arith == EKF_ARITH_BF16X6 &&
+        (cfg->arith != EKF_ARITH_EXACT && cfg->arith != EKF_ARITH_BF16X6 && cfg->arith != EKF_ARITH_F16X3) ||
+        // the split-plane flushes need symmetric fp32 operands with kmax = 16 (slam_ekf.h)
+        (cfg->arith != EKF_ARITH_EXACT &&
          (cfg->precision == EKF_PREC_F64 || cfg->r_mode != EKF_R_INTENDED || cfg->max_lines > 8)))
         return EKF_EINVAL;
     int ndev = 0;
@@ -349,14 +365,19 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     c->slot_bytes = (long long)(((c->op_inst * c->op_elem * E) + 255) / 256 * 256);
     ALLOC(c->ops_u, (size_t)c->slot_bytes * c->ring.size());
     ALLOC(c->ops_v, (size_t)c->slot_bytes * c->ring.size());
-    // split-bf16 flush: V's three bf16 planes per slot (written by the association kernel)
-    c->bf = cfg->arith == EKF_ARITH_BF16X6;   // (validated above: fp32 / fp16, symmetric R, kmax 16)
+    // split-plane flushes: V's planes per slot (written by the association kernel), three bf16
+    // (BF16X6) or two fp16 (F16X3) per operand element
+    c->bf = cfg->arith != EKF_ARITH_EXACT;   // (validated above: fp32 / fp16, symmetric R, kmax 16)
+    c->pmode = c->bf ? cfg->arith : 0;
     c->ops_b = nullptr;
     c->bslot_bytes = 0;
     if (c->bf) {
-        c->bslot_bytes = (long long)((c->op_inst * 3 * 2 * E + 255) / 256 * 256);
+        const int npl = c->pmode == EKF_ARITH_F16X3 ? 2 : 3;
+        c->bslot_bytes = (long long)((c->op_inst * npl * 2 * E + 255) / 256 * 256);
         ALLOC(c->ops_b, (size_t)c->bslot_bytes * c->ring.size());
     }
+    ALLOC(c->psig, sizeof(int) * E);
+    ALLOC(c->pvmax, sizeof(double) * E);
     for (size_t i = 0; i < c->ring.size(); i++) {
         ekf::Slot& sl = c->ring[i];
         sl.Uop = (char*)c->ops_u + (size_t)c->slot_bytes * i;
@@ -702,7 +723,9 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.live = c->cur;
     p.Dd = c->D;
     p.mfrep = c->mfrep;
-    p.bf = c->bf ? 1 : 0;
+    p.bf = c->pmode;
+    p.psig = c->psig;
+    p.pvmax = c->pvmax;
     p.Etot = c->cfg.instances;
     p.spin_log2 = c->spin_log2;
     p.test_drop = c->test_drop;
@@ -778,7 +801,7 @@ static int enqueue_flush(ekf_ctx* c)
     dp.nslots = (int)c->ring.size();
     dp.slot0 = (int)(c->unflushed0 % (long long)c->ring.size());
     dp.dbg = c->dbg;
-    dp.bf = c->bf ? 1 : 0;
+    dp.bf = c->pmode;
     dp.bbase = c->ops_b;
     dp.bslot_bytes = c->bslot_bytes;
     for (int q = 0; q < nst; q++) dp.steps[q] = slot_of(c, c->unflushed0 + q);
@@ -974,9 +997,10 @@ extern "C" int ekf_upload_state(ekf_ctx* c, int e, const double* P, const double
     if (rc) return rc;
     if (P) {
         double vmax = 0.0;
-        if (c->cfg.precision == EKF_PREC_F16)
-            for (int i = 3; i < d.n; i++) vmax = std::max(vmax, std::fabs(P[(size_t)i * d.n + i]));
+        for (int i = 3; i < d.n; i++) vmax = std::max(vmax, std::fabs(P[(size_t)i * d.n + i]));
         rc = set_exponent(c, e, choose_exponent(c, vmax));
+        if (rc) return rc;
+        rc = set_plane_scale(c, e, vmax);
         if (rc) return rc;
         double* tmp = nullptr;
         HIP_TRY(dense_scratch(c, &tmp));
@@ -1050,13 +1074,14 @@ extern "C" int ekf_init_lowrank(ekf_ctx* c, int e, const double* diag, const dou
     rc = strip_copy(c, e, &cb);
     if (rc) return rc;
     double vmax = 0.0;
-    if (c->cfg.precision == EKF_PREC_F16)
-        for (int i = 3; i < d.n; i++) {
-            double v = diag[i];
-            for (int k = 0; k < rank; k++) v += U[(size_t)i * rank + k] * U[(size_t)i * rank + k];
-            vmax = std::max(vmax, std::fabs(v));
-        }
+    for (int i = 3; i < d.n; i++) {
+        double v = diag[i];
+        for (int k = 0; k < rank; k++) v += U[(size_t)i * rank + k] * U[(size_t)i * rank + k];
+        vmax = std::max(vmax, std::fabs(v));
+    }
     rc = set_exponent(c, e, choose_exponent(c, vmax));
+    if (rc) return rc;
+    rc = set_plane_scale(c, e, vmax);
     if (rc) return rc;
     double *dd = nullptr, *du = nullptr;
     HIP_TRY(hipMalloc((void**)&dd, sizeof(double) * d.n));
@@ -1109,6 +1134,7 @@ extern "C" int ekf_rescale(ekf_ctx* c, int e, int ex)
         double vmax = 0.0;
         for (int i = 3; i < d.n; i++) vmax = std::max(vmax, std::fabs(dg[i]));
         rc = set_exponent(c, e, ex == EKF_EXP_AUTO ? choose_exponent(c, vmax) : ex);
+        if (rc == EKF_OK) rc = set_plane_scale(c, e, vmax);
         if (rc == EKF_OK) {
             err = ekf::launch_pack(d, c->cfg.precision, tmp, X, Rs, c->tile_rc, c->pexp_h[e], c->stream);
             if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
@@ -1660,6 +1686,18 @@ extern "C" const char* ekf_flush_kernel_name(const ekf_ctx* c, int nsteps)
         return "downdate_f64_kernel";
     }
     const bool half = c->cfg.precision == EKF_PREC_F16;
+    if (c->pmode == EKF_ARITH_F16X3 && nsteps >= 2 && nsteps <= 16 && nsteps % 2 == 0) {
+        static const char* f16n[2][9] = {
+            {"", "flush_f32_wave_kernel<float, 2, true, true>", "flush_f32_wave_kernel<float, 4, true, true>",
+             "flush_f32_wave_kernel<float, 6, true, true>", "flush_f32_wave_kernel<float, 8, true, true>",
+             "flush_f32_wave_kernel<float, 10, true, true>", "flush_f32_wave_kernel<float, 12, true, true>",
+             "flush_f32_wave_kernel<float, 14, true, true>", "flush_f32_wave_kernel<float, 16, true, true>"},
+            {"", "flush_f32_wave_kernel<_Float16, 2, true, true>", "flush_f32_wave_kernel<_Float16, 4, true, true>",
+             "flush_f32_wave_kernel<_Float16, 6, true, true>", "flush_f32_wave_kernel<_Float16, 8, true, true>",
+             "flush_f32_wave_kernel<_Float16, 10, true, true>", "flush_f32_wave_kernel<_Float16, 12, true, true>",
+             "flush_f32_wave_kernel<_Float16, 14, true, true>", "flush_f32_wave_kernel<_Float16, 16, true, true>"}};
+        return f16n[half ? 1 : 0][nsteps / 2];
+    }
     if (c->bf && nsteps >= 2 && nsteps <= 16 && nsteps % 2 == 0 && c->dd_variant == 24) {
         static const char* b24[2][9] = {
             {"", "flush_bf24_kernel<float, 2>", "flush_bf24_kernel<float, 4>", "flush_bf24_kernel<float, 6>",

@@ -37,7 +37,8 @@ enum {
     RES_ROLLBACK = 15,// 1: the call timed out and was rolled back (no downdate, rows or reset)
     RES_MATCH = 16,                     // [EKF_MAX_LINES]
     RES_EXTRA = 16 + EKF_MAX_LINES,     // [EKF_MAX_LINES] line indices, in order
-    RES_STRIDE = 16 + 2 * EKF_MAX_LINES,
+    RES_PSIG = 16 + 2 * EKF_MAX_LINES,  // EKF_ARITH_F16X3: the plane exponent σ of this step's planes
+    RES_STRIDE = 16 + 2 * EKF_MAX_LINES + 4,
 };
 
 // Per-step outputs that outlive the step's association kernel (a ring of slots): the
@@ -50,8 +51,9 @@ struct Slot {
     double* patch;      // [E][max_lines][2][M]   rows of landmarks added by this step
     double* patch_diag; // [E][max_lines][4]      their 2x2 diagonal blocks
     int* res;           // [E][RES_STRIDE]
-    void* Bop;          // [E][nb][3][64][8] bf16: V split into hi + mid + lo planes, in the operand
-                        // order of v_mfma_f32_32x32x16_bf16 (EKF_ARITH_BF16X6 only, else nullptr)
+    void* Bop;          // [E][nb][npl][64][8] V split into planes in the operand order of the 32x32x16
+                        // MFMAs: EKF_ARITH_BF16X6 hi + mid + lo bf16 (npl = 3), EKF_ARITH_F16X3 hi +
+                        // lo fp16 of 2^σ·V (npl = 2); nullptr for EKF_ARITH_EXACT
 };
 
 constexpr int PMAX = 32;
@@ -100,8 +102,10 @@ struct ScanParams {
                           // (copy live[e] read, the other written and committed with Rs / y)
     int mfrep;            // split-bf16 context: pending steps replayed on read by bf16 MFMA from
                           // the operand planes, diagonal blocks kept in Dd
-    int bf;               // split-bf16 context: fp16 storage rounded once per flush group, also in
-                          // the on-read replay
+    int bf;               // split-plane context (1 EKF_ARITH_BF16X6, 2 EKF_ARITH_F16X3): fp16 storage
+                          // rounded once per flush group, also in the on-read replay
+    int* psig;            // [Etot] EKF_ARITH_F16X3 plane exponent σ (the lead lowers it when a new
+    double* pvmax;        // [Etot] landmark raises the largest landmark variance vmax)
     double* pose;         // [E][3]
     double* xpre;         // [E][3]
     int* saved;           // [E]
@@ -179,7 +183,8 @@ struct DowndateParams {
     unsigned long long* dbg;  // EKF_SCAN_STAMPS buffer (timing experiments of the flush only)
     const void* bbase;    // EKF_ARITH_BF16X6: bf16 operand planes of ring slot i at bbase + i·bslot_bytes
     long long bslot_bytes;
-    int bf;               // 1: plain groups of 2, 4, 6 or 8 steps run the split-bf16 wave flush
+    int bf;               // plain groups of 2..16 steps (even) run the split-plane wave flush:
+                          // 1 EKF_ARITH_BF16X6, 2 EKF_ARITH_F16X3 (σ of each step in RES_PSIG)
     const int* wt24;      // [nwt24] split-bf16 wave-tiles of 2 × 4 tiles (wr | wc << 16), panel order
     int nwt24;
     Slot steps[PMAX];

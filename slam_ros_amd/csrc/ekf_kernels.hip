@@ -1299,15 +1299,20 @@ __device__ __forceinline__ void staged_pair_block(const PllView<T>& v, int wa, i
 // M-block mb in acc[mb][i]. Not the fp32 chain of the flush (the split-bf16 flush is not one
 // either): held to the same parity bar.
 typedef __bf16 bf16x8r __attribute__((ext_vector_type(8)));
-template <int NB, typename RA, typename RB>
+typedef _Float16 f16x8r __attribute__((ext_vector_type(8)));
+// F16 (EKF_ARITH_F16X3): two fp16 planes (hi, lo of 2^σ·V), three products (lo, hi), (hi, lo),
+// (hi, hi) on v_mfma_f32_16x16x32_f16; acc then holds 2^(2σ)·ΔX (the caller scales it back)
+template <int NB, bool F16, typename RA, typename RB>
 __device__ __forceinline__ void plane_replay(const Slot* pend, int e, size_t inst_bf, int M, unsigned amask,
                                              int lane, RA row_a, RB row_b, f32x4v (&acc)[NB])
 {
+    constexpr int NPL = F16 ? 2 : 3;
+    using PV = typename std::conditional<F16, f16x8r, bf16x8r>::type;
 #pragma unroll
     for (int mb = 0; mb < NB; mb++) acc[mb] = f32x4v{0.f, 0.f, 0.f, 0.f};
     const int kg = lane >> 4, h = kg & 1, r16 = lane & 15;
     typedef unsigned u32x4r __attribute__((ext_vector_type(4)));
-    const bf16x8r zero = __builtin_bit_cast(bf16x8r, u32x4r{0u, 0u, 0u, 0u});
+    const PV zero = __builtin_bit_cast(PV, u32x4r{0u, 0u, 0u, 0u});
     const int rb_ = row_b(r16);
     int ra_[NB];
 #pragma unroll
@@ -1322,25 +1327,46 @@ __device__ __forceinline__ void plane_replay(const Slot* pend, int e, size_t ins
         const unsigned short* pb = qb >= 0 ? reinterpret_cast<const unsigned short*>(pend[qb].Bop) + (size_t)e * inst_bf : pa;
         const unsigned short* pq = (kg >= 2) ? pb : pa;
         const bool none = kg >= 2 && qb < 0;
-        bf16x8r B[3], A[NB][3];
+        PV B[NPL], A[NB][NPL];
 #pragma unroll
-        for (int pl = 0; pl < 3; pl++)
-            B[pl] = (!none && rb_ >= 0 && rb_ < M) ? *reinterpret_cast<const bf16x8r*>(pq + op_index_bf(rb_, h, pl)) : zero;
+        for (int pl = 0; pl < NPL; pl++)
+            B[pl] = (!none && rb_ >= 0 && rb_ < M) ? *reinterpret_cast<const PV*>(pq + op_index_pl(rb_, h, pl, NPL)) : zero;
 #pragma unroll
         for (int mb = 0; mb < NB; mb++)
 #pragma unroll
-            for (int pl = 0; pl < 3; pl++)
+            for (int pl = 0; pl < NPL; pl++)
                 A[mb][pl] = (!none && ra_[mb] >= 0 && ra_[mb] < M)
-                                ? *reinterpret_cast<const bf16x8r*>(pq + op_index_bf(ra_[mb], h, pl)) : zero;
+                                ? *reinterpret_cast<const PV*>(pq + op_index_pl(ra_[mb], h, pl, NPL)) : zero;
+        if constexpr (F16) {
 #pragma unroll
-        for (int pp = 0; pp < 6; pp++) {
-            const int a = (0x102010 >> (4 * (5 - pp))) & 0xf;   // (mid, mid), (hi, lo), (lo, hi),
-            const int b = (0x120100 >> (4 * (5 - pp))) & 0xf;   // (hi, mid), (mid, hi), (hi, hi)
+            for (int pp = 0; pp < 3; pp++) {
+                const int a = pp == 0 ? 1 : 0, b = pp == 1 ? 1 : 0;   // (lo, hi), (hi, lo), (hi, hi)
 #pragma unroll
-            for (int mb = 0; mb < NB; mb++)
-                acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mb][a], B[b], acc[mb], 0, 0, 0);
+                for (int mb = 0; mb < NB; mb++)
+                    acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[mb][a], B[b], acc[mb], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int pp = 0; pp < 6; pp++) {
+                const int a = (0x102010 >> (4 * (5 - pp))) & 0xf;   // (mid, mid), (hi, lo), (lo, hi),
+                const int b = (0x120100 >> (4 * (5 - pp))) & 0xf;   // (hi, mid), (mid, hi), (hi, hi)
+#pragma unroll
+                for (int mb = 0; mb < NB; mb++)
+                    acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mb][a], B[b], acc[mb], 0, 0, 0);
+            }
         }
     }
+}
+
+// EKF_ARITH_F16X3: x = 2^σ·v as hi + lo fp16 (hi = fp16(x) round-to-nearest, lo = fp16(x − hi), the
+// remainder exact in fp32): 22 significant bits; (a, b) packed into one dword per part, a low
+__device__ __forceinline__ void split_pack_f16(float a, float b, int sig, unsigned (&o)[2])
+{
+    const float xa = ldexpf(a, sig), xb = ldexpf(b, sig);
+    const _Float16 ha = (_Float16)xa, hb = (_Float16)xb;
+    const _Float16 la = (_Float16)(xa - (float)ha), lb = (_Float16)(xb - (float)hb);
+    o[0] = (unsigned)__builtin_bit_cast(unsigned short, ha) | ((unsigned)__builtin_bit_cast(unsigned short, hb) << 16);
+    o[1] = (unsigned)__builtin_bit_cast(unsigned short, la) | ((unsigned)__builtin_bit_cast(unsigned short, lb) << 16);
 }
 
 // Speculative association (lines <= SPEC_L, G <= SPEC_GMAX): every line's winner is guessed
@@ -1350,10 +1376,11 @@ __device__ __forceinline__ void plane_replay(const Slot* pend, int e, size_t ins
 // whose exact first passing candidate differs from the guess. Three exchanges per scan instead
 // of one per line; on a flag the scan restarts on the sequential path (identical results).
 
-// ST: phase timers (EKF_SCAN_STAMPS=1). HOT: the launch guarantees symmetric fp32 operands with
-// kmax = 16 (the bench and every EKF_R_SYMMETRIC fp32/fp16 context with max_lines <= 8): the
-// per-line loops then carry no code for the other operand forms
-template <typename T, bool ST, bool HOT>
+// ST: phase timers (EKF_OPT_SCAN_STAMPS). HOT (1, 2): the launch guarantees symmetric fp32 operands
+// with kmax = 16 (the bench and every EKF_R_INTENDED fp32/fp16 context with max_lines <= 8): the
+// per-line loops then carry no code for the other operand forms; HOT = 2 also fixes the plane
+// arithmetic to EKF_ARITH_F16X3, HOT = 1 to EKF_ARITH_BF16X6 or none. HOT = 0: decided at run time
+template <typename T, bool ST, int HOT>
 __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
 {
     const Dims d = p.d;
@@ -1420,6 +1447,14 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // fp32 operand storage (fp32 and fp16 P): the split-bf16 planes, the MFMA replay
     constexpr bool kPlanes = sizeof(typename Stor<T>::C) == 4;
     __shared__ __attribute__((aligned(16))) float sh_vpl[kPlanes ? SCAN_THREADS * 32 : 4];
+    // plane arithmetic (HOT fixes it at compile time): EKF_ARITH_F16X3 planes hold hi + lo fp16 of
+    // 2^σ·V, σ = psig[e] for every step since the last augmentation (the lead changes it only at a
+    // step that adds landmarks, after this launch's planes are written with the old value), so
+    // the MFMA replay of plain pending steps returns 2^(2σ)·ΔX
+    const bool pf16 = kPlanes && (HOT == 2 || (HOT == 0 && p.bf == 2));
+    const int npl = pf16 ? 2 : 3;
+    const int psig = pf16 ? p.psig[e] : 0;
+    const double rsc = pf16 ? ldexp(1.0, -2 * psig) : 1.0;
     // phase timers only in the ST instantiation (EKF_SCAN_STAMPS=1): the product kernel carries
     // no timer code at all (its uniform branches and registers cost ≈2 µs per scan)
     unsigned long long* const pdbg = ST ? p.dbg : nullptr;
@@ -1571,8 +1606,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     using C = typename Stor<T>::C;   // operand (compute) type
     C* Uop = reinterpret_cast<C*>(p.cur.Uop) + (size_t)e * opstride;
     C* Vop = reinterpret_cast<C*>(p.cur.Vop) + (size_t)e * opstride;
-    // EKF_ARITH_BF16X6: V's bf16 planes for the split-bf16 flush (null otherwise)
-    unsigned short* Bop = p.cur.Bop ? reinterpret_cast<unsigned short*>(p.cur.Bop) + (size_t)e * opstride * 3
+    // split-plane arithmetics: V's planes for the split flush (null otherwise)
+    unsigned short* Bop = p.cur.Bop ? reinterpret_cast<unsigned short*>(p.cur.Bop) + (size_t)e * opstride * npl
                                     : nullptr;
     // (staged in LDS, sh_vpl, and written once at the end: per-match 2-byte global stores cost
     // ≈4 µs of the chain, since on CDNA every store counts in vmcnt and each later load wait
@@ -1951,7 +1986,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     return w >= 0 ? 2 * w + (c & 1) : -1;
                 };
                 f32x4v dacc[1];
-                plane_replay<1>(p.pend, e, opstride * 3, M, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow, dacc);
+                if (HOT == 2 || (HOT == 0 && pf16))
+                    plane_replay<1, true>(p.pend, e, opstride * 2, M, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow, dacc);
+                if (HOT == 1 || (HOT == 0 && !pf16))
+                    plane_replay<1, false>(p.pend, e, opstride * 3, M, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow, dacc);
                 float* scr = sh_stg;   // (not staged in this mode) 16 × 16 floats
 #pragma unroll
                 for (int i = 0; i < 4; i++) scr[(4 * (lane_r >> 4) + i) * 16 + (lane_r & 15)] = dacc[0][i];
@@ -1964,7 +2002,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     double* r = sh_wd + pu * SPEC_WD + (pt == pu ? 6 : 14 + 4 * pt);
 #pragma unroll
                     for (int a = 0; a < 4; a++)
-                        r[a] = from_domain<T>(xr[a], pv.ex) - (double)scr[(2 * pu + (a >> 1)) * 16 + 2 * pt + (a & 1)];
+                        r[a] = from_domain<T>(xr[a], pv.ex) - (double)scr[(2 * pu + (a >> 1)) * 16 + 2 * pt + (a & 1)] * rsc;
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_wave_barrier();
@@ -2102,8 +2140,12 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         return w >= 0 ? 2 * w + (c & 1) : -1;
                     };
                     f32x4v dacc[8];
-                    plane_replay<8>(p.pend, e, opstride * 3, M, amask, l,
-                                    [&](int mb, int r) { return rbase + 16 * mb + r; }, wrow, dacc);
+                    if (HOT == 2 || (HOT == 0 && pf16))
+                        plane_replay<8, true>(p.pend, e, opstride * 2, M, amask, l,
+                                              [&](int mb, int r) { return rbase + 16 * mb + r; }, wrow, dacc);
+                    if (HOT == 1 || (HOT == 0 && !pf16))
+                        plane_replay<8, false>(p.pend, e, opstride * 3, M, amask, l,
+                                               [&](int mb, int r) { return rbase + 16 * mb + r; }, wrow, dacc);
                     float* scr = sh_vpl + (tid & ~63) * 32;
 #pragma unroll
                     for (int mb = 0; mb < 8; mb++)
@@ -2125,10 +2167,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                             if (t < L && sh_spec[t] >= 0) {
                                 const int c0 = 2 * t;
                                 sh_blk[t][tid] = make_float4(
-                                    (float)(from_domain<T>(srow[t][0], pv.ex) - (double)d0[c0 >> 2][c0 & 3]),
-                                    (float)(from_domain<T>(srow[t][1], pv.ex) - (double)d0[c0 >> 2][(c0 & 3) + 1]),
-                                    (float)(from_domain<T>(srow[t][2], pv.ex) - (double)d1[c0 >> 2][c0 & 3]),
-                                    (float)(from_domain<T>(srow[t][3], pv.ex) - (double)d1[c0 >> 2][(c0 & 3) + 1]));
+                                    (float)(from_domain<T>(srow[t][0], pv.ex) - (double)d0[c0 >> 2][c0 & 3] * rsc),
+                                    (float)(from_domain<T>(srow[t][1], pv.ex) - (double)d0[c0 >> 2][(c0 & 3) + 1] * rsc),
+                                    (float)(from_domain<T>(srow[t][2], pv.ex) - (double)d1[c0 >> 2][c0 & 3] * rsc),
+                                    (float)(from_domain<T>(srow[t][3], pv.ex) - (double)d1[c0 >> 2][(c0 & 3) + 1] * rsc));
                             }
                     }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -2457,6 +2499,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     const int reset = (s + nadd > N - p.reset_margin) ? 1 : 0;
 
     // ---------------- augmentation (Robot.cpp:776-866) ----------------
+    double vnew = 0.0;   // the lead: the largest variance of the new landmarks (EKF_ARITH_F16X3's σ)
     if (!reset) {
         for (int q = 0; q < nadd; q++) {
             const ekf_line ln = sh_lines[sh_extra[q]];
@@ -2506,6 +2549,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         if (j == sq) Dj[a * 2 + b] = gsum + h;   // the new landmark's kept diagonal block
                         if (!lead) continue;
                         pdiag[q * 4 + a * 2 + b] = gsum + h;
+                        if (a == b) vnew = fmax(vnew, gsum + h);
                         // fp16 storage: the new landmark's variances bound its whole row and
                         // column (|P_ij| <= sqrt(P_ii P_jj)), and downdates only shrink them
                         if (Stor<T>::half && fabs(ldexp(gsum + h, pv.ex)) > F16_RANGE_WARN)
@@ -2583,18 +2627,34 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     }
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
-                        unsigned w[3][4];
+                        if (HOT == 2 || (HOT == 0 && pf16)) {   // EKF_ARITH_F16X3: hi, lo of 2^σ·V
+                            unsigned w[2][4];
 #pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            unsigned o[3];
-                            split_pack(v[4 * q + h], v[4 * q + 2 + h], o);
+                            for (int q = 0; q < 4; q++) {
+                                unsigned o[2];
+                                split_pack_f16(v[4 * q + h], v[4 * q + 2 + h], psig, o);
+                                w[0][q] = o[0];
+                                w[1][q] = o[1];
+                            }
 #pragma unroll
-                            for (int pl = 0; pl < 3; pl++) w[pl][q] = o[pl];
+                            for (int pl = 0; pl < 2; pl++)
+                                *reinterpret_cast<u32x4v*>(Bop + op_index_pl(2 * j + pp, h, pl, 2)) =
+                                    u32x4v{w[pl][0], w[pl][1], w[pl][2], w[pl][3]};
                         }
+                        if (HOT == 1 || (HOT == 0 && !pf16)) {   // EKF_ARITH_BF16X6: hi, mid, lo
+                            unsigned w[3][4];
 #pragma unroll
-                        for (int pl = 0; pl < 3; pl++)
-                            *reinterpret_cast<u32x4v*>(Bop + op_index_bf(2 * j + pp, h, pl)) =
-                                u32x4v{w[pl][0], w[pl][1], w[pl][2], w[pl][3]};
+                            for (int q = 0; q < 4; q++) {
+                                unsigned o[3];
+                                split_pack(v[4 * q + h], v[4 * q + 2 + h], o);
+#pragma unroll
+                                for (int pl = 0; pl < 3; pl++) w[pl][q] = o[pl];
+                            }
+#pragma unroll
+                            for (int pl = 0; pl < 3; pl++)
+                                *reinterpret_cast<u32x4v*>(Bop + op_index_bf(2 * j + pp, h, pl)) =
+                                    u32x4v{w[pl][0], w[pl][1], w[pl][2], w[pl][3]};
+                        }
                     }
                 }
             }
@@ -2638,8 +2698,21 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             res[RES_NADD] = reset ? 0 : nadd;
             res[RES_KSTEPS] = (sizeof(C) == 4) ? m : (m + 1) / 2;
             res[RES_ROLLBACK] = 0;
+            res[RES_PSIG] = psig;
             p.saved[e] = reset ? 0 : s + nadd;
             p.live[e] = 1 - cb;
+            if (pf16) {
+                // the plane exponent of the later steps: |V_ik| <= sqrt(P_ii) <= sqrt(vmax) while no
+                // landmark is added, so σ changes only here, at a step whose group and pending
+                // replays take the exact forms (it adds rows, or resets the map)
+                if (reset) {
+                    p.pvmax[e] = 0.0;
+                    p.psig[e] = PLANE_SIGMA_EMPTY;
+                } else if (vnew > p.pvmax[e]) {
+                    p.pvmax[e] = vnew;
+                    p.psig[e] = plane_sigma(vnew);
+                }
+            }
         } else {
             res[RES_STATUS] = 0;
             res[RES_M] = 0;
@@ -3665,7 +3738,7 @@ __device__ __forceinline__ void wt_general(const DowndateParams& p, int e, const
 #ifndef EKF_BF_WAVES
 #define EKF_BF_WAVES 1   // split-bf16 flush: waves per SIMD (2: ≤ 256 registers, ring depth 2; measured equal)
 #endif
-template <typename TS, int NS, bool BF = false>
+template <typename TS, int NS, bool BF = false, bool F16 = false>
 __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_wave_kernel(DowndateParams p)
 {
     static_assert(NS >= 2 && NS % 2 == 0 && NS <= PMAX, "even step count");
@@ -3767,9 +3840,11 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
 
     if constexpr (BF) {
         if (fast) {
-            typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+            // planes: BF16X6 hi, mid, lo bf16 (six products); F16X3 hi, lo fp16 of 2^σ·V (three)
+            constexpr int NPL = F16 ? 2 : 3;
+            typedef typename std::conditional<F16, f16x8r, bf16x8r>::type bf16x8;
             constexpr int RD = EKF_BF_WAVES > 1 ? 2 : (NS % 4 == 0 ? 4 : (NS % 3 == 0 ? 3 : 2));   // operand ring depth
-            const size_t pstride = (size_t)d.nb * 3 * 64;   // bf16x8 per instance
+            const size_t pstride = (size_t)d.nb * NPL * 64;   // 16-byte operands per instance
             // step q's planes: slot (slot0 + q) mod nslots
             auto pl_base = [&](int q) __attribute__((always_inline)) {
                 int sl = p.slot0 + q;
@@ -3781,23 +3856,23 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
             using Raw = typename std::conditional<HALF, f16x4, f32x4>::type;
             Raw pref[WT_N][4];
             f32x16 acc[WT_N];
-            bf16x8 R[RD][WT_R + WT_C][3];
+            bf16x8 R[RD][WT_R + WT_C][NPL];
             // step q of wave-tile t into ring set r: A row blocks, then B row blocks, three planes
             auto load_ops = [&](int r, const Item& t, int q) __attribute__((always_inline)) {
                 const bf16x8* b = pl_base(q) + t.e * pstride + lane;
 #ifdef EKF_XP_BF_HALF_OPS   // timing experiment (results invalid): A planes only, reused as B
 #pragma unroll
                 for (int i = 0; i < WT_R; i++) {
-                    const bf16x8* rb = b + (size_t)op_row(t, 0, i) * 3 * 64;
+                    const bf16x8* rb = b + (size_t)op_row(t, 0, i) * NPL * 64;
 #pragma unroll
-                    for (int pl = 0; pl < 3; pl++) R[r][i][pl] = R[r][WT_R + i][pl] = rb[pl * 64];
+                    for (int pl = 0; pl < NPL; pl++) R[r][i][pl] = R[r][WT_R + i][pl] = rb[pl * 64];
                 }
 #else
 #pragma unroll
                 for (int i = 0; i < WT_R + WT_C; i++) {
-                    const bf16x8* rb = b + (size_t)(i < WT_R ? op_row(t, 0, i) : op_row(t, 1, i - WT_R)) * 3 * 64;
+                    const bf16x8* rb = b + (size_t)(i < WT_R ? op_row(t, 0, i) : op_row(t, 1, i - WT_R)) * NPL * 64;
 #pragma unroll
-                    for (int pl = 0; pl < 3; pl++) R[r][i][pl] = rb[pl * 64];
+                    for (int pl = 0; pl < NPL; pl++) R[r][i][pl] = rb[pl * 64];
                 }
 #endif
             };
@@ -3811,10 +3886,14 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
             };
             // the accumulators hold −P: fp32 storage −X; fp16 storage −2^−x·X (X = fp16(2^x·P), the
             // instance's exponent; power-of-two scalings, exact), so that both operands are the
-            // unscaled V planes; the store scales back and rounds to fp16 once per group
+            // unscaled V planes; the store scales back and rounds to fp16 once per group. F16X3: the
+            // planes carry 2^σ·V (σ of the group's steps, all equal in a plain group), so the
+            // accumulators hold −2^(2σ)·P
             auto in_scale = [&](const Item& t) __attribute__((always_inline)) {
-                if constexpr (HALF) return -ldexpf(1.0f, -sload(p.pexp + t.e));
-                else return -1.0f;
+                int ex = 0;
+                if constexpr (HALF) ex -= sload(p.pexp + t.e);
+                if constexpr (F16) ex += 2 * sload(p.steps[0].res + (size_t)t.e * RES_STRIDE + RES_PSIG);
+                return -ldexpf(1.0f, ex);
             };
             Item cur, nxt, nxt2;
             first_item(cur);
@@ -3865,23 +3944,43 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
                     else load_ops(ql % RD, ldi, ql - NS);
 #endif
                     const int r = q % RD;
-                    // part products smallest first: (mid, mid), (hi, lo), (lo, hi), (hi, mid),
-                    // (mid, hi), (hi, hi)
+                    if constexpr (F16) {
+                        // (lo, hi), (hi, lo), (hi, hi): 12 MFMAs beside the 8 plane loads
 #pragma unroll
-                    for (int pp = 0; pp < 6; pp++) {
-                        const int pa = (0x102010 >> (4 * (5 - pp))) & 0xf;
-                        const int pb = (0x120100 >> (4 * (5 - pp))) & 0xf;
+                        for (int pp = 0; pp < 3; pp++) {
+                            const int pa = pp == 0 ? 1 : 0, pb = pp == 1 ? 1 : 0;
 #pragma unroll
-                        for (int rr = 0; rr < WT_R; rr++)
+                            for (int rr = 0; rr < WT_R; rr++)
 #pragma unroll
-                            for (int c = 0; c < WT_C; c++)
-                                acc[rr * WT_C + c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                                    R[r][rr][pa], R[r][WT_R + c][pb], acc[rr * WT_C + c], 0, 0, 0);
-                    }
+                                for (int c = 0; c < WT_C; c++)
+                                    acc[rr * WT_C + c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+                                        R[r][rr][pa], R[r][WT_R + c][pb], acc[rr * WT_C + c], 0, 0, 0);
+                        }
 #pragma unroll
-                    for (int i = 0; i < 12; i++) {
-                        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
-                        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // VMEM read
+                        for (int i = 0; i < 8; i++) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // VMEM read
+                        }
+                        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                    } else {
+                        // part products smallest first: (mid, mid), (hi, lo), (lo, hi), (hi, mid),
+                        // (mid, hi), (hi, hi)
+#pragma unroll
+                        for (int pp = 0; pp < 6; pp++) {
+                            const int pa = (0x102010 >> (4 * (5 - pp))) & 0xf;
+                            const int pb = (0x120100 >> (4 * (5 - pp))) & 0xf;
+#pragma unroll
+                            for (int rr = 0; rr < WT_R; rr++)
+#pragma unroll
+                                for (int c = 0; c < WT_C; c++)
+                                    acc[rr * WT_C + c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                        R[r][rr][pa], R[r][WT_R + c][pb], acc[rr * WT_C + c], 0, 0, 0);
+                        }
+#pragma unroll
+                        for (int i = 0; i < 12; i++) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
+                            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // VMEM read
+                        }
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -4751,9 +4850,9 @@ int scan_blocks_per_cu(int precision)
 {
     int nb = 0;
     hipError_t err =
-        (precision == EKF_PREC_F64) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<double, false, false>, SCAN_BLOCK, 0)
-        : (precision == EKF_PREC_F16) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<_Float16, false, false>, SCAN_BLOCK, 0)
-        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<float, false, false>, SCAN_BLOCK, 0);
+        (precision == EKF_PREC_F64) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<double, false, 0>, SCAN_BLOCK, 0)
+        : (precision == EKF_PREC_F16) ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<_Float16, false, 0>, SCAN_BLOCK, 0)
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, scan_kernel<float, false, 0>, SCAN_BLOCK, 0);
     return err == hipSuccess ? nb : 0;
 }
 
@@ -4761,9 +4860,9 @@ size_t scan_lds_bytes(int precision)
 {
     hipFuncAttributes a;
     hipError_t err =
-        (precision == EKF_PREC_F64) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<double, false, false>))
-        : (precision == EKF_PREC_F16) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<_Float16, false, false>))
-        : hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<float, false, false>));
+        (precision == EKF_PREC_F64) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<double, false, 0>))
+        : (precision == EKF_PREC_F16) ? hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<_Float16, false, 0>))
+        : hipFuncGetAttributes(&a, reinterpret_cast<const void*>(scan_kernel<float, false, 0>));
     return err == hipSuccess ? a.sharedSizeBytes : 0;
 }
 
@@ -4780,17 +4879,20 @@ hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st)
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 {
     const dim3 grid(p.G * p.E), block(SCAN_BLOCK);
-    if (p.dbg) {   // phase timers (EKF_SCAN_STAMPS=1): the instrumented instantiation
-        if (precision == EKF_PREC_F64) hipLaunchKernelGGL((scan_kernel<double, true, false>), grid, block, 0, st, p);
-        else if (precision == EKF_PREC_F16) hipLaunchKernelGGL((scan_kernel<_Float16, true, false>), grid, block, 0, st, p);
-        else hipLaunchKernelGGL((scan_kernel<float, true, false>), grid, block, 0, st, p);
+    if (p.dbg) {   // phase timers (EKF_OPT_SCAN_STAMPS): the instrumented instantiation
+        if (precision == EKF_PREC_F64) hipLaunchKernelGGL((scan_kernel<double, true, 0>), grid, block, 0, st, p);
+        else if (precision == EKF_PREC_F16) hipLaunchKernelGGL((scan_kernel<_Float16, true, 0>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((scan_kernel<float, true, 0>), grid, block, 0, st, p);
+    } else if (precision != EKF_PREC_F64 && p.r_mode != 1 && p.d.kmax == 16 && p.bf == 2) {
+        if (precision == EKF_PREC_F16) hipLaunchKernelGGL((scan_kernel<_Float16, false, 2>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((scan_kernel<float, false, 2>), grid, block, 0, st, p);
     } else if (precision != EKF_PREC_F64 && p.r_mode != 1 && p.d.kmax == 16) {
-        if (precision == EKF_PREC_F16) hipLaunchKernelGGL((scan_kernel<_Float16, false, true>), grid, block, 0, st, p);
-        else hipLaunchKernelGGL((scan_kernel<float, false, true>), grid, block, 0, st, p);
+        if (precision == EKF_PREC_F16) hipLaunchKernelGGL((scan_kernel<_Float16, false, 1>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((scan_kernel<float, false, 1>), grid, block, 0, st, p);
     } else {
-        if (precision == EKF_PREC_F64) hipLaunchKernelGGL((scan_kernel<double, false, false>), grid, block, 0, st, p);
-        else if (precision == EKF_PREC_F16) hipLaunchKernelGGL((scan_kernel<_Float16, false, false>), grid, block, 0, st, p);
-        else hipLaunchKernelGGL((scan_kernel<float, false, false>), grid, block, 0, st, p);
+        if (precision == EKF_PREC_F64) hipLaunchKernelGGL((scan_kernel<double, false, 0>), grid, block, 0, st, p);
+        else if (precision == EKF_PREC_F16) hipLaunchKernelGGL((scan_kernel<_Float16, false, 0>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((scan_kernel<float, false, 0>), grid, block, 0, st, p);
     }
     return hipGetLastError();
 }
@@ -4820,7 +4922,7 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     const bool wave_ok = wave_shape && (p.nsteps >= 6 || p.variant == 8);
     const bool bf_shape = p.nsteps >= 2 && p.nsteps <= 16 && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
                           p.nwt > 0 && p.wt != nullptr;
-    if (p.bf && bf_shape && p.variant == 24 && p.nwt24 > 0 && p.wt24 != nullptr) {
+    if (p.bf == 1 && bf_shape && p.variant == 24 && p.nwt24 > 0 && p.wt24 != nullptr) {
         // EKF_ARITH_BF16X6, EKF_FLUSH_VARIANT=24: the 2 × 4 split-bf16 wave flush (measured 7 %
         // slower than the 2 × 2 form below at T = 12; kept as an option, bit-identical)
         const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
@@ -4844,7 +4946,29 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
 #undef EKF_BF24_CASE
         return hipGetLastError();
     }
-    if (p.bf && bf_shape) {   // EKF_ARITH_BF16X6: split-bf16 wave flush, groups of 2-16 steps (even)
+    if (p.bf == 2 && bf_shape) {   // EKF_ARITH_F16X3: split-fp16 wave flush, groups of 2-16 steps (even)
+        const unsigned wgrid = (unsigned)(8 * EKF_BF_WAVES * ((p.ncu + 7) / 8));
+#define EKF_F16_CASE(NSV)                                                                               \
+    case NSV:                                                                                           \
+        if (half) hipExtLaunchKernelGGL((flush_f32_wave_kernel<_Float16, NSV, true, true>), dim3(wgrid),  \
+                                        dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p);                      \
+        else hipExtLaunchKernelGGL((flush_f32_wave_kernel<float, NSV, true, true>), dim3(wgrid),          \
+                                   dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p);                           \
+        break;
+        switch (p.nsteps) {
+            EKF_F16_CASE(2)
+            EKF_F16_CASE(4)
+            EKF_F16_CASE(6)
+            EKF_F16_CASE(8)
+            EKF_F16_CASE(10)
+            EKF_F16_CASE(12)
+            EKF_F16_CASE(14)
+            EKF_F16_CASE(16)
+        }
+#undef EKF_F16_CASE
+        return hipGetLastError();
+    }
+    if (p.bf == 1 && bf_shape) {   // EKF_ARITH_BF16X6: split-bf16 wave flush, groups of 2-16 steps (even)
         const unsigned wgrid = (unsigned)(8 * EKF_BF_WAVES * ((p.ncu + 7) / 8));   // EKF_BF_WAVES workgroups per CU
 #define EKF_BF_CASE(NSV)                                                                                \
     case NSV:                                                                                           \

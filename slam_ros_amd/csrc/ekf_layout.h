@@ -137,6 +137,35 @@ EKF_HD int64_t op_index_bf(int row, int k, int pl)
     return (((int64_t)rb * 3 + pl) * 64 + lane) * 8 + s;
 }
 
+// The same operand order for npl planes per 32-row block: 3 (EKF_ARITH_BF16X6: hi, mid, lo bf16)
+// or 2 (EKF_ARITH_F16X3: hi, lo fp16 of the row-scaled value)
+EKF_HD int64_t op_index_pl(int row, int k, int pl, int npl)
+{
+    const int rb = row >> 5;
+    const int lane = (row & 31) + 32 * (k & 1);
+    const int s = k >> 1;
+    return (((int64_t)rb * npl + pl) * 64 + lane) * 8 + s;
+}
+
+// EKF_ARITH_F16X3 plane exponent σ of an instance whose largest landmark variance is vmax: the
+// planes hold fp16 parts of 2^σ·V, and every operand value of a plain step obeys |V_ik| ≤
+// sqrt(P_ii) (V·Vᵀ is the step's downdate, P − V·Vᵀ ⪰ 0, and variances only shrink between
+// augmentations), so |2^σ·V| ≤ 2^12: two binades below fp16's largest finite value, and values
+// down to 2^-17 of the largest keep their full 22-bit hi + lo split. An empty map (vmax = 0) keeps
+// PLANE_SIGMA_EMPTY until its first landmark.
+constexpr int PLANE_SIGMA_EMPTY = 0;
+EKF_HD int plane_sigma(double vmax)
+{
+    if (!(vmax > 0.0) || vmax > 1e300) return PLANE_SIGMA_EMPTY;
+    // the largest s with vmax·4^s <= 2^24, i.e. sqrt(vmax)·2^s <= 2^12 (exact power-of-four steps)
+    int s = 12;
+    const double lim = 16777216.0;   // 2^24
+    double x = vmax * 16777216.0;    // vmax·4^12
+    while (x > lim && s > -60) { x *= 0.25; s--; }
+    while (x * 4.0 <= lim && s < 60) { x *= 4.0; s++; }
+    return s;
+}
+
 EKF_HD int64_t op_index_f64(int row, int k, int kmax)
 {
     const int rb = row >> 5;

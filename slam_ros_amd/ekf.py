@@ -21,7 +21,7 @@ from . import build as _build
 EKF_MAX_LINES = 64
 PREC_F64, PREC_F32, PREC_F16 = 0, 1, 2
 R_INTENDED, R_AS_WRITTEN = 0, 1
-ARITH_EXACT, ARITH_BF16X6 = 0, 1   # fp32 flush arithmetic (slam_ekf.h EKF_ARITH_*)
+ARITH_EXACT, ARITH_BF16X6, ARITH_F16X3 = 0, 1, 2   # fp32 flush arithmetic (slam_ekf.h EKF_ARITH_*)
 ST_SINGULAR_S, ST_CAPACITY, ST_NONSYM, ST_SYNC_TIMEOUT, ST_RANGE = 1, 2, 4, 8, 16
 EXP_AUTO = -1000
 # per-context options (slam_ekf.h EKF_OPT_*, ekf_set_option)

@@ -566,10 +566,11 @@ def test_wave_flush_equals_drained(ekf_mod, monkeypatch, prec, N, T, lines, extr
         assert sa == sb
 
 
+@pytest.mark.parametrize("arith", [1, 2])
 @pytest.mark.parametrize("N,T,lines,extra_every", [(80, 8, 6, 3), (80, 2, 8, 0), (64, 6, 6, 4),
                                                   (1024, 8, 8, 0), (1024, 4, 6, 5), (96, 3, 8, 0),
                                                   (1024, 12, 8, 0), (256, 16, 6, 7), (80, 16, 7, 0)])
-def test_bf16x6_flush_close_to_exact(ekf_mod, oracle_mod, N, T, lines, extra_every):
+def test_bf16x6_flush_close_to_exact(ekf_mod, oracle_mod, N, T, lines, extra_every, arith):
     """EKF_ARITH_BF16X6 (split-bf16 wave flush for plain groups of 2, 4, 6 or 8 steps; groups
     with augmentation rows or the reset, odd group sizes and the partial last group fall back to
     the fp32 forms): same associations as the exact arithmetic drained after every scan, and the
@@ -584,7 +585,7 @@ def test_bf16x6_flush_close_to_exact(ekf_mod, oracle_mod, N, T, lines, extra_eve
     active = N - 12 - 2 * ((3 * T + 1) // extra_every) if extra_every else N - 10
     w = G.make_world(N, active=active)
     st = G.initial_state(w)
-    a = ekf_mod.Ensemble(N, E, 1, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
+    a = ekf_mod.Ensemble(N, E, 1, max_lines=8, flush_interval=T, arith=arith)
     b = ekf_mod.Ensemble(N, E, 1, max_lines=8)
     if T % 2 == 0:
         assert is_bf_form(a.flush_kernel_name(T)), a.flush_kernel_name(T)
@@ -626,14 +627,15 @@ def test_bf16x6_flush_close_to_exact(ekf_mod, oracle_mod, N, T, lines, extra_eve
             assert meas[0]["P_bf_vs_fp64"] <= meas[0]["P_exact_vs_fp64"] + k * 1e-6, meas[0]
             assert meas[0]["y_bf_vs_fp64"] <= meas[0]["y_exact_vs_fp64"] + k * 1e-8, meas[0]
     from tests.test_bench_config import record
-    record(f"bf16x6_vs_exact_N{N}_T{T}_L{lines}_x{extra_every}", meas)
+    record(f"{'bf16x6' if arith == 1 else 'f16x3'}_vs_exact_N{N}_T{T}_L{lines}_x{extra_every}", meas)
     # kmax > 16 (max_lines 16) can never take the split-bf16 flush: rejected, no silent fallback
     with pytest.raises(ekf_mod.EkfError):
         ekf_mod.Ensemble(N, 1, 1, max_lines=16, flush_interval=8, arith=ekf_mod.ARITH_BF16X6)
 
 
+@pytest.mark.parametrize("arith", [1, 2])
 @pytest.mark.parametrize("N,T,extra_every", [(256, 8, 0), (256, 12, 5), (80, 16, 0), (1024, 6, 4)])
-def test_bf16x6_fp16_storage(ekf_mod, oracle_mod, N, T, extra_every):
+def test_bf16x6_fp16_storage(ekf_mod, oracle_mod, N, T, extra_every, arith):
     """fp16 storage with EKF_ARITH_BF16X6 (split-bf16 flush on the fp16 tiles, rounded once per
     group — the general path of groups with augmented rows and the on-read replay too; MFMA replay
     of plain pending steps, the VALU replay after augmented rows) against the
@@ -643,7 +645,7 @@ def test_bf16x6_fp16_storage(ekf_mod, oracle_mod, N, T, extra_every):
     active = N - 12 - 2 * ((3 * T + 1) // extra_every) if extra_every else N - 10
     w = G.make_world(N, active=active)
     st = G.initial_state(w)
-    a = ekf_mod.Ensemble(N, E, 2, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
+    a = ekf_mod.Ensemble(N, E, 2, max_lines=8, flush_interval=T, arith=arith)
     assert a.flush_kernel_name(T if T % 2 == 0 else T - 1).startswith("flush_f32_wave_kernel<_Float16")
     for e in range(E):
         a.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
