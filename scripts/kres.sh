@@ -19,6 +19,6 @@ for line in sys.stdin:
         out.append(dict(cur))
 for d in out:
     if pat.search(d.get('name', '')):
-        print(d.get('name'), 'vgpr', d.get('vgpr_count'), 'agpr', d.get('agpr_count'), 'sgpr_spill', d.get('sgpr_spill_count'), 'vgpr_spill', d.get('vgpr_spill_count'), 'scratch', d.get('private_segment_fixed_size'))
+        print(d.get('name'), 'lds', d.get('group_segment_fixed_size'), 'vgpr', d.get('vgpr_count'), 'agpr', d.get('agpr_count'), 'sgpr_spill', d.get('sgpr_spill_count'), 'vgpr_spill', d.get('vgpr_spill_count'), 'scratch', d.get('private_segment_fixed_size'))
 " "$PAT"
 rm -rf $T

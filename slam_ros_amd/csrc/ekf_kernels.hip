@@ -1052,11 +1052,12 @@ __device__ __forceinline__ bool guess_pass(const Guess& gs, double za, double zr
 }
 
 constexpr int SPEC_L = HIST_LDS;                    // lines
-#ifndef EKF_SPEC_K
-#define EKF_SPEC_K 4
-#endif
-constexpr int SPEC_K = EKF_SPEC_K;                  // guessed candidates per line per workgroup
-constexpr int LW_CNT = 8 * SPEC_K, LW_MORE = 8 * SPEC_K + 3;   // list word: count, more bits
+// guessed candidates per line per workgroup: with SPEC_K = SPEC_L every line's guess can be
+// resolved (line t needs its first t + 1 candidates at most: only t earlier lines can take one)
+constexpr int SPEC_K = 8;
+// list words per (workgroup, line): A = local indices 0..3 (8 bits each), the count (bits 32..35)
+// and a more bit (36); B = local indices 4..7, written and read only when the count exceeds 4
+constexpr int LW_CNT = 32, LW_MORE = 36;
 constexpr int SPEC_PB = 2;                          // guessed columns per pass over the pending steps
 #ifndef EKF_STAGED_DEPTH
 #define EKF_STAGED_DEPTH 1
@@ -1429,6 +1430,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // speculative association
     __shared__ unsigned long long sh_wl[SPEC_L][SCAN_THREADS / 64];
     __shared__ unsigned long long sh_lists[SPEC_GMAX * SPEC_L];
+    __shared__ unsigned long long sh_listsb[SPEC_GMAX * SPEC_L];   // the B words (count > 4)
     __shared__ int sh_glist[SPEC_L][SPEC_K + 1];
     __shared__ int sh_spec[SPEC_L];
     __shared__ int sh_flag;
@@ -1782,14 +1784,15 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 gp = ((gp >> 1) | (gp << (L - 1))) & ((1u << L) - 1u);
         }
         // per wave and line the guessed candidates (ballot), then the workgroup's first SPEC_K
-        // in landmark order: word = 8-bit local indices | count << 32 | more << 35
+        // in landmark order: word A = 8-bit local indices 0..3 | count << 32 | more << 36, word B =
+        // local indices 4..7
         for (int t = 0; t < L; t++) {
             const unsigned long long mk = __ballot((gp >> t) & 1u);
             if ((tid & 63) == 0 && tid < SCAN_THREADS) sh_wl[t][tid >> 6] = mk;
         }
         __syncthreads();
         if (tid < L) {
-            unsigned long long word = 0;
+            unsigned long long word = 0, wordb = 0;
             int cnt = 0, more = 0;
             for (int w = 0; w < SCAN_THREADS / 64 && !more; w++) {
                 unsigned long long mk = sh_wl[tid][w];
@@ -1797,24 +1800,37 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     if (cnt == SPEC_K) { more = 1; break; }
                     const int b = __builtin_ctzll(mk);
                     mk &= mk - 1;
-                    word |= (unsigned long long)(w * 64 + b) << (8 * cnt);
+                    if (cnt < 4) word |= (unsigned long long)(w * 64 + b) << (8 * cnt);
+                    else wordb |= (unsigned long long)(w * 64 + b) << (8 * (cnt - 4));
                     cnt++;
                 }
             }
             word |= ((unsigned long long)cnt << LW_CNT) | ((unsigned long long)more << LW_MORE);
             sh_lists[g * SPEC_L + tid] = word;
+            sh_listsb[g * SPEC_L + tid] = wordb;
         }
         __syncthreads();
         EKF_STAMP(5);
         // ---- (b) exchange 1 (parity 0): every workgroup's lists ----
         if (G > 1) {
-            // one self-tagged word per (workgroup, line), polled directly by its readers
+            // self-tagged words per (workgroup, line), polled directly by their readers: A always,
+            // B (at SPEC_L words further) only when A's count says it is there
             const int lb = p.mbw - MB_LIST_BACK;
             double* slot = mbox + (size_t)g * p.mbw + lb;
-            if (tid < SPEC_L) mb_store_tagged(slot + tid, p.epoch, tid < L ? sh_lists[g * SPEC_L + tid] : 0ull);
+            if (tid < SPEC_L) {
+                const unsigned long long wa = tid < L ? sh_lists[g * SPEC_L + tid] : 0ull;
+                if (((wa >> LW_CNT) & 15) > 4) mb_store_tagged(slot + SPEC_L + tid, p.epoch, sh_listsb[g * SPEC_L + tid]);
+                mb_store_tagged(slot + tid, p.epoch, wa);
+            }
             for (int k = tid; k < G * L; k += SCAN_BLOCK) {
                 const int gq = k / L, t = k - gq * L;
-                if (gq != g) sh_lists[gq * SPEC_L + t] = mb_wait_tagged(mbox + (size_t)gq * p.mbw + lb + t, p.epoch, tstatus, p.spin_log2);
+                if (gq != g) {
+                    const double* src = mbox + (size_t)gq * p.mbw + lb;
+                    const unsigned long long wa = mb_wait_tagged(src + t, p.epoch, tstatus, p.spin_log2);
+                    sh_lists[gq * SPEC_L + t] = wa;
+                    if (((wa >> LW_CNT) & 15) > 4)
+                        sh_listsb[gq * SPEC_L + t] = mb_wait_tagged(src + SPEC_L + t, p.epoch, tstatus, p.spin_log2);
+                }
             }
             __syncthreads();
         }
@@ -1828,7 +1844,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         for (int k = tid; k < G * SPEC_L; k += SCAN_BLOCK) {
             const int gq = k / SPEC_L, t = k - gq * SPEC_L;
             const unsigned long long w = sh_lists[gq * SPEC_L + t];
-            if (t < L && ((w >> LW_CNT) & 7)) atomicMin(&sh_first[t], gq * SCAN_THREADS + (int)(w & 255));
+            if (t < L && ((w >> LW_CNT) & 15)) atomicMin(&sh_first[t], gq * SCAN_THREADS + (int)(w & 255));
         }
         __syncthreads();
         {
@@ -1852,11 +1868,13 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         if (sh_flag == 2) {
             if (tid < L) {
                 int cnt = 0, more = 0;
-                for (int gq = 0; gq < G; gq++) {
+                for (int gq = 0; gq < G && cnt < SPEC_K; gq++) {
                     const unsigned long long w = sh_lists[gq * SPEC_L + tid];
-                    const int c = (int)((w >> LW_CNT) & 7);
+                    const unsigned long long wb = sh_listsb[gq * SPEC_L + tid];
+                    const int c = (int)((w >> LW_CNT) & 15);
                     for (int k = 0; k < c; k++) {
-                        if (cnt < SPEC_K) sh_glist[tid][cnt++] = gq * SCAN_THREADS + (int)((w >> (8 * k)) & 255);
+                        const int loc = (int)(((k < 4 ? w : wb) >> (8 * (k & 3))) & 255);
+                        if (cnt < SPEC_K) sh_glist[tid][cnt++] = gq * SCAN_THREADS + loc;
                         else more = 1;
                     }
                     if ((w >> LW_MORE) & 1) more = 1;
