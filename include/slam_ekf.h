@@ -36,7 +36,9 @@ extern "C" {
  *    that can never use it; EKF_ST_SYNC_TIMEOUT rolls the call back instead of committing it.
  * 3: ekf_set_option / ekf_get_option replace the environment variables the library used to read
  *    (EKF_SPECULATE, EKF_SPIN_LOG2, EKF_TEST_DROP_WG, EKF_MFREP, EKF_SCAN_STAMPS,
- *    EKF_DD_BLOCKS_PER_CU, EKF_FLUSH_VARIANT); ekf_shard_abort; EKF_ARITH_F16X3. */
+ *    EKF_DD_BLOCKS_PER_CU, EKF_FLUSH_VARIANT); EKF_ARITH_F16X3; the row shard replaced by a
+ *    partitioned instance (ekf_shard_create ... ekf_shard_end: tiles partitioned, O(n) state
+ *    replicated). */
 #define SLAM_EKF_ABI_VERSION 3
 #define EKF_MAX_LINES 64 /* lines per scan per instance; main.cpp:99 reserves 20 */
 
@@ -238,45 +240,45 @@ int ekf_get_ellipse(ekf_ctx* ctx, int e, float axii[2], float* angle);
  * eigenvector; that branch of GSL is not restated here, axii and angle are left untouched. */
 int ekf_ellipse_of_block(const double P22[4], float axii[2], float* angle);
 
-/* One instance row-sharded across ranks: each rank's context holds
- * instance 0 (instances = 1, EKF_ARITH_EXACT, fp32 or fp64, no pipeline) and owns the landmarks
- * [first, end); the reference's sequential localize (Robot.cpp:298-641) runs as phases, the caller
- * doing the per-line exchanges between them (no reference member maps to these; they replace the
- * single call Robot::localize, Robot.h:34, for a map sharded over processes):
- *   ekf_shard_begin(enc, lines)              predict; the owned landmarks' scan state
- *   for each line i:
- *     ekf_shard_gate(i, &j)                  first passing owned unmatched landmark (INT_MAX: none)
- *     j* = MIN over ranks                     (the reference takes the first in index order)
- *     ekf_shard_package(i, j*, pkg)          on j*'s owner: S, S^-1, v, H, K/U robot rows, V history
- *     broadcast pkg from the owner
- *     ekf_shard_apply(i, j* or -1, pkg)      gain rows of the owned landmarks, robot update
- *   ekf_shard_end()                          commit; augmentation (Robot.cpp:776-866): each rank
- *                                            writes its columns of the new landmarks' rows, the
- *                                            owner of a new landmark its strip columns and mean;
- *                                            the capacity reset (Robot.cpp:893-904)
- *   ekf_shard_operands(U, V, 0) / all-gather the owned rows / ekf_shard_operands(U, V, 1)
- *   ekf_shard_patch(rows, 0) / all-gather the owned columns / ekf_shard_patch(rows, 1)
- *   ekf_shard_commit()                       the step joins the deferred flush, which runs on the
- *                                            wave-tiles holding an owned row block only
- * With the same inputs the owned rows of P, the owned mean entries, the robot block and the pose
- * are bit-identical to a single context's (exact arithmetic). */
-int ekf_shard_init(ekf_ctx* ctx, int first, int end);
-int ekf_shard_begin(ekf_ctx* ctx, const double enc[3], const ekf_line* lines, int nlines);
-int ekf_shard_gate(ekf_ctx* ctx, int line, int* first_pass);
-int ekf_shard_package_words(const ekf_ctx* ctx);   /* doubles in a package */
-int ekf_shard_package(ekf_ctx* ctx, int line, int jstar, double* pkg);
-int ekf_shard_apply(ekf_ctx* ctx, int line, int jstar, const double* pkg);
-int ekf_shard_end(ekf_ctx* ctx);
-size_t ekf_shard_operand_bytes(const ekf_ctx* ctx);   /* bytes of each of U and V */
-int ekf_shard_operands(ekf_ctx* ctx, void* U, void* V, int upload);
-size_t ekf_shard_patch_bytes(const ekf_ctx* ctx);   /* bytes of the new-landmark rows [max_lines][2][2N] */
-int ekf_shard_patch(ekf_ctx* ctx, double* rows, int upload);
-int ekf_shard_commit(ekf_ctx* ctx);
-int ekf_shard_status(ekf_ctx* ctx, int* status);   /* status bits of the scan (GSL_EDOM, NSYM) */
-/* Abandons the open scan (between ekf_shard_begin and ekf_shard_end: nothing of the committed state
- * has been written yet), e.g. after a failed exchange; a phase that fails abandons it too. A
- * sharded context rejects the whole-instance entry points (ekf_localize, ekf_localize_device,
- * ekf_predict, ekf_update) with EKF_EINVAL. */
+/* One instance with its landmark block partitioned over ranks, for maps
+ * whose packed P should not (or cannot) live on one GPU. No reference member maps to these: they
+ * replace the single call Robot::localize (Robot.h:34, Robot.cpp:126-904) for an instance spread over
+ * processes. ekf_shard_create makes rank `rank` of `world` a context of one instance (instances =
+ * 1, EKF_ARITH_EXACT, fp32 with flush_interval <= 8 or fp64 with <= 4, no pipeline, max_lines <= 8)
+ * that stores only its share of the packed landmark block: the tiles of tile rows [row_begin,
+ * row_end) (ekf_shard_tiles), a contiguous slice balanced by tile count, about 1/world of it
+ * (ekf_landmark_block_bytes). Everything of size O(n) (robot strip, mean, the landmarks' scan
+ * state and diagonal blocks, the downdate operands) is replicated and evolves identically on every
+ * rank. ekf_upload_state / ekf_init_lowrank store the rank's tiles; ekf_download_state returns the
+ * full robot rows and mean and the rank's tiles, zero elsewhere (the ranks' landmark blocks sum to
+ * the instance's).
+ * Per scan (Robot.cpp:126-904, the sequential association), every call asynchronous on the context
+ * stream except ekf_shard_end; buf is the caller's device buffer of ekf_shard_buffer_words doubles
+ * ([N][4] 2x2 blocks), which the caller sums over the ranks where marked (each rank fills the
+ * blocks its tiles hold, zeros elsewhere: the sum is exact):
+ *   ekf_shard_begin(enc, lines, L, buf)     predict (Robot.cpp:130-286); the rank's diagonal blocks
+ *   SUM buf over ranks
+ *   for each line i < L, in order:
+ *     ekf_shard_line(i, buf)                gate of every landmark (Robot.cpp:313-498: the first
+ *                                           passing unmatched one, found by every rank alike), the
+ *                                           winner's package, the rank's blocks of its column
+ *     SUM buf over ranks
+ *     ekf_shard_apply(i, buf)               gain rows of every landmark, robot update (Robot.cpp:522-602)
+ *   ekf_shard_end(out)                      augmentation (Robot.cpp:776-866), the capacity reset
+ *                                           (Robot.cpp:893-904), commit; the step joins the flush,
+ *                                           which rewrites the rank's tiles only; out[0] as
+ *                                           ekf_read_results (synchronous)
+ * With the same inputs the state is bit-identical to a single context's (exact arithmetic). A
+ * partitioned context rejects ekf_localize, ekf_localize_device, ekf_predict and ekf_update. */
+int ekf_shard_create(const ekf_config* cfg, int rank, int world, ekf_ctx** out);
+int ekf_shard_tiles(const ekf_ctx* ctx, int* row_begin, int* row_end);
+size_t ekf_shard_buffer_words(const ekf_ctx* ctx);
+int ekf_shard_begin(ekf_ctx* ctx, const double enc[3], const ekf_line* lines, int nlines, double* buf);
+int ekf_shard_line(ekf_ctx* ctx, int line, double* buf);
+int ekf_shard_apply(ekf_ctx* ctx, int line, const double* buf);
+int ekf_shard_end(ekf_ctx* ctx, ekf_result* out);
+/* Abandons the open scan (before ekf_shard_end nothing of the committed state has been written),
+ * e.g. after a failed exchange; a phase that fails abandons it too. */
 int ekf_shard_abort(ekf_ctx* ctx);
 
 /* Introspection for the benchmark's roofline accounting. */

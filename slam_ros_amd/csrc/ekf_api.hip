@@ -43,24 +43,26 @@ struct ekf_ctx {
     hipStream_t dstream;      // D
     size_t elem;              // bytes per stored landmark-block element
     size_t op_elem;           // bytes per downdate operand element (fp32 for fp16 storage)
-    size_t pll_inst;          // elements per instance
+    size_t pll_inst;          // elements per instance (the whole packed block)
+    long long t0 = 0, t1 = 0; // tiles stored per instance [t0, t1): all, unless partitioned (ekf_shard_create)
+    size_t xinst;             // stored landmark-block elements per instance ((t1 − t0)·TILE_ELEMS)
     size_t op_inst;           // operand elements per instance
     void* X[2];
     double* Rs;               // [2][E][3][n] robot strip, two copies (the association kernel reads
     double* y;                // [2][E][n]    copy cur[e] and writes the other; the lead commits it)
     int* cur;                 // [E] committed copy per instance (device; read back when needed)
     double* dense = nullptr;   // n × n fp64 scratch of upload / download / rescale (allocated on first use, kept)
-    // row shard (ekf_shard_*): owned landmarks [sh_a, sh_b) of instance 0, the running scan's state
-    int sh_a = -1, sh_b = -1;
+    // partitioned instance (ekf_shard_create): rank sh_rank of sh_world stores tile rows [sh_r0, sh_r1);
+    // the running scan's replicated state
+    int sh_rank = -1, sh_world = 0, sh_r0 = 0, sh_r1 = 0;
     double* sh_rob = nullptr;
     double* sh_rec = nullptr;
     double* sh_hist = nullptr;
     double* sh_pkg = nullptr;
     int* sh_flags = nullptr;
-    int* sh_out = nullptr;
-    int* sh_match = nullptr;
-    int sh_line = -1, sh_m = 0, sh_L = 0, sh_s = 0, sh_nextra = 0, sh_open = 0;
-    std::vector<int> sh_match_h;
+    int* sh_ctl = nullptr;
+    int sh_L = 0, sh_line = 0, sh_open = 0;   // sh_open: 1 during a scan; sh_line: the next line expected
+    ekf::Slot sh_null;        // a step that applies nothing (pads an odd partial group to the wave flush)
     double* pose;
     double* xpre;
     int* saved;
@@ -179,7 +181,8 @@ static void free_all(ekf_ctx* c)
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->cur, c->pose, c->xpre, c->saved, c->D,
                                c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->wt24, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->pexp, c->sink, c->mbox,
                                c->sync, c->Ust, c->Vst, c->dense, c->psig, c->pvmax,
-                               c->sh_rob, c->sh_rec, c->sh_hist, c->sh_pkg, c->sh_flags, c->sh_out, c->sh_match};
+                               c->sh_rob, c->sh_rec, c->sh_hist, c->sh_pkg, c->sh_flags, c->sh_ctl,
+                               c->sh_null.res};
     ptrs.push_back(c->ops_u);
     ptrs.push_back(c->ops_v);
     ptrs.push_back(c->ops_b);
@@ -221,6 +224,17 @@ static int drain(ekf_ctx* c)
 }
 
 static inline int cur_buf(const ekf_ctx* c) { return c->last_out; }
+
+// instance e's stored tiles in buffer buf; and the kernels' view of instance 0, in which tile t sits
+// at t·TILE_ELEMS (a partitioned instance stores the tiles [t0, t1) only: the view is shifted)
+static inline char* xinst_ptr(const ekf_ctx* c, int buf, int e)
+{
+    return (char*)c->X[buf] + (size_t)e * c->xinst * c->elem;
+}
+static inline void* xview(const ekf_ctx* c, int buf)
+{
+    return (char*)c->X[buf] - (ptrdiff_t)c->t0 * ekf::TILE_ELEMS * (ptrdiff_t)c->elem;
+}
 
 // Committed copy of instance e's robot strip and mean (the association kernel flips it when it
 // commits a launch): read back after the stream has drained up to here.
@@ -275,8 +289,7 @@ static int set_robot_ctor(ekf_ctx* c, int e, double x, double y, double th)
     // Robot::Robot (Robot.cpp:20-35): P_t0[0][0] = P_t0[1][1] = 0.05, P_t0[2][2] = 0, the rest
     // (and y, savedLineCount) zero.
     const Dims& d = c->d;
-    HIP_TRY(hipMemsetAsync((char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem, 0,
-                           c->pll_inst * c->elem, c->stream));
+    HIP_TRY(hipMemsetAsync(xinst_ptr(c, cur_buf(c), e), 0, c->xinst * c->elem, c->stream));
     const int zero = 0;
     const double v = 0.05;
     HIP_TRY(hipMemcpyAsync(c->cur + e, &zero, sizeof(int), hipMemcpyHostToDevice, c->stream));
@@ -297,7 +310,46 @@ static int set_robot_ctor(ekf_ctx* c, int e, double x, double y, double th)
     return set_exponent(c, e, c->cfg.precision == EKF_PREC_F16 ? ekf::F16_EXP_DEFAULT : 0);
 }
 
+// One packed-tile-row partition of the landmark block over `world` ranks: boundaries on even tile
+// rows (whole wave-tile rows of the flush) balancing the tiles per rank; rank's rows [r0, r1)
+static void tile_partition(int nb, int world, int rank, int& r0, int& r1)
+{
+    const long long total = (long long)nb * (nb + 1) / 2;
+    auto boundary = [&](int k) {
+        if (k <= 0) return 0;
+        if (k >= world) return nb;
+        // the even tile row whose prefix of tiles is closest to k/world of them
+        const long long want = total * k / world;
+        int bi = 0;
+        while (bi + 2 < nb && ekf::tile_index(bi + 2, bi + 2, nb) <= want) bi += 2;
+        if (bi + 2 < nb && ekf::tile_index(bi + 2, bi + 2, nb) - want < want - ekf::tile_index(bi, bi, nb)) bi += 2;
+        return bi;
+    };
+    r0 = boundary(rank);
+    r1 = boundary(rank + 1);
+}
+
+static int create_ctx(const ekf_config* cfg, int sh_rank, int sh_world, ekf_ctx** out);
+
 extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
+{
+    return create_ctx(cfg, -1, 0, out);
+}
+
+extern "C" int ekf_shard_create(const ekf_config* cfg, int rank, int world, ekf_ctx** out)
+{
+    if (!cfg || !out) return EKF_EINVAL;
+    *out = nullptr;
+    // one instance, the exact arithmetic, fp32 or fp64 storage, the sequential schedule, groups the
+    // wave flushes take (fp32 <= 8 steps, fp64 <= 4)
+    if (world < 1 || rank < 0 || rank >= world || cfg->instances != 1 || cfg->pipeline ||
+        cfg->arith != EKF_ARITH_EXACT || (cfg->precision != EKF_PREC_F32 && cfg->precision != EKF_PREC_F64) ||
+        cfg->flush_interval > (cfg->precision == EKF_PREC_F64 ? ekf::F64_WAVE_MAXS : 8) || cfg->max_lines > 8)
+        return EKF_EINVAL;
+    return create_ctx(cfg, rank, world, out);
+}
+
+static int create_ctx(const ekf_config* cfg, int sh_rank, int sh_world, ekf_ctx** out)
 {
     if (!cfg || !out) return EKF_EINVAL;
     *out = nullptr;
@@ -334,6 +386,20 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     c->elem = (cfg->precision == EKF_PREC_F64) ? 8 : (cfg->precision == EKF_PREC_F32) ? 4 : 2;
     c->op_elem = (cfg->precision == EKF_PREC_F64) ? 8 : 4;   // operands in the compute type
     c->pll_inst = (size_t)d.ntiles * ekf::TILE_ELEMS;
+    c->t0 = 0;
+    c->t1 = d.ntiles;
+    if (sh_world > 0) {
+        tile_partition(d.nb, sh_world, sh_rank, c->sh_r0, c->sh_r1);
+        if (c->sh_r0 >= c->sh_r1) {   // more ranks than wave-tile rows
+            delete c;
+            return EKF_ERANGE;
+        }
+        c->sh_rank = sh_rank;
+        c->sh_world = sh_world;
+        c->t0 = ekf::tile_index(c->sh_r0, c->sh_r0, d.nb);
+        c->t1 = c->sh_r1 < d.nb ? ekf::tile_index(c->sh_r1, c->sh_r1, d.nb) : d.ntiles;
+    }
+    c->xinst = (size_t)(c->t1 - c->t0) * ekf::TILE_ELEMS;
     c->op_inst = (size_t)d.nb * 64 * (d.kmax / 2);
     c->G = (d.N + ekf::SCAN_THREADS - 1) / ekf::SCAN_THREADS;
     // pipeline: the association kernels of an instance spread over G > 1 cooperating workgroups
@@ -346,8 +412,8 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         if (hipMalloc((void**)&(ptr), (bytes)) != hipSuccess) goto fail;        \
         if (hipMemset((void*)(ptr), 0, (bytes)) != hipSuccess) goto fail;       \
     } while (0)
-    ALLOC(c->X[0], c->pll_inst * c->elem * E);
-    if (c->cfg.pipeline) ALLOC(c->X[1], c->pll_inst * c->elem * E);
+    ALLOC(c->X[0], c->xinst * c->elem * E);
+    if (c->cfg.pipeline) ALLOC(c->X[1], c->xinst * c->elem * E);
     else c->X[1] = nullptr;
     ALLOC(c->Rs, sizeof(double) * 3 * d.n * E * 2);
     ALLOC(c->y, sizeof(double) * d.n * E * 2);
@@ -410,6 +476,24 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
     c->mfrep = c->bf ? 1 : 0;
     c->dbg = nullptr;
     ALLOC(c->mbox, sizeof(double) * 2 * c->G * c->mbw * E);
+    if (c->sh_world > 0) {
+        // the partitioned instance's scan state (replicated on every rank) and a step that applies
+        // nothing (rolled back: every flush form skips it), which pads an odd partial group
+        ALLOC(c->sh_rob, sizeof(double) * 12);
+        ALLOC(c->sh_rec, sizeof(double) * d.N * ekf::SH_REC);
+        ALLOC(c->sh_hist, sizeof(double) * d.N * d.max_lines * 8);
+        ALLOC(c->sh_pkg, sizeof(double) * (ekf::MB_WORDS_FIXED + 4 * d.max_lines));
+        ALLOC(c->sh_flags, sizeof(int) * d.N);
+        ALLOC(c->sh_ctl, sizeof(int) * ekf::SC_WORDS);
+        ALLOC(c->sh_null.res, sizeof(int) * ekf::RES_STRIDE);
+        const int one = 1;
+        if (hipMemcpy(c->sh_null.res + ekf::RES_ROLLBACK, &one, sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+            goto fail;
+        c->sh_null.Uop = c->ring[0].Uop;
+        c->sh_null.Vop = c->ring[0].Vop;
+        c->sh_null.patch = c->ring[0].patch;
+        c->sh_null.patch_diag = c->ring[0].patch_diag;
+    }
     c->sync_stride = ((ekf::SYNC_WG0 + c->G + 15) / 16) * 16;
     ALLOC(c->sync, sizeof(int) * c->sync_stride * E);
 #undef ALLOC
@@ -488,6 +572,14 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
                     v.rc = wr | (wc << 16);
                     wt.push_back(v);
                 }
+        if (c->sh_world > 0) {   // a partitioned instance flushes its tile rows only
+            std::vector<ekf::WtEntry> keep;
+            for (const auto& v : wt) {
+                const int r = (v.rc & 0xffff) * ekf::WT_R;
+                if (r >= c->sh_r0 && r < c->sh_r1) keep.push_back(v);
+            }
+            wt.swap(keep);
+        }
         c->nwt = (int)wt.size();
         if (hipMalloc((void**)&c->wt, sizeof(ekf::WtEntry) * wt.size()) != hipSuccess) goto fail;
         if (hipMemcpy(c->wt, wt.data(), sizeof(ekf::WtEntry) * wt.size(), hipMemcpyHostToDevice) !=
@@ -514,6 +606,12 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
                     v.rc = wr | (wc << 16);
                     w64.push_back(v);
                 }
+        if (c->sh_world > 0) {
+            std::vector<ekf::WtEntry> keep;
+            for (const auto& v : w64)
+                if (v.rows[0] >= c->sh_r0 && v.rows[0] < c->sh_r1) keep.push_back(v);
+            w64.swap(keep);
+        }
         c->nwt64 = (int)w64.size();
         if (hipMalloc((void**)&c->wt64, sizeof(ekf::WtEntry) * w64.size()) != hipSuccess) goto fail;
         if (hipMemcpy(c->wt64, w64.data(), sizeof(ekf::WtEntry) * w64.size(), hipMemcpyHostToDevice) !=
@@ -538,7 +636,9 @@ extern "C" int ekf_create(const ekf_config* cfg, ekf_ctx** out)
         c->dd_per_cu = 8;   // downdate workgroups per CU (4 waves each; EKF_OPT_FLUSH_BLOCKS_PER_CU)
         c->dd_grid = prop.multiProcessorCount * c->dd_per_cu;
         c->ncu = prop.multiProcessorCount;
-        c->dd_variant = 0;   // automatic flush form (EKF_OPT_FLUSH_FORM)
+        // automatic flush form (EKF_OPT_FLUSH_FORM); a partitioned instance: the wave form for every
+        // group (its wave tables hold the rank's tile rows only; the other forms walk every tile)
+        c->dd_variant = c->sh_world > 0 ? 8 : 0;
         // all G workgroups of an instance must be co-resident (they exchange per line). A plain
         // launch gets the same residency as a cooperative one for the same grid
         // (cdna_hip_programming.md §1; the cooperative form only adds a launch-time check of the
@@ -805,10 +905,16 @@ static int enqueue_flush(ekf_ctx* c)
     dp.bbase = c->ops_b;
     dp.bslot_bytes = c->bslot_bytes;
     for (int q = 0; q < nst; q++) dp.steps[q] = slot_of(c, c->unflushed0 + q);
+    if (c->sh_world > 0 && c->cfg.precision == EKF_PREC_F32 && (nst & 1)) {
+        // a partitioned instance flushes with the wave form only (even groups): pad with a step
+        // that applies nothing
+        dp.steps[nst] = c->sh_null;
+        dp.nsteps = nst + 1;
+    }
     const int in = c->last_out;
     const int out = c->cfg.pipeline ? 1 - in : in;
-    dp.Pin = c->X[in];
-    dp.Pout = c->X[out];
+    dp.Pin = xview(c, in);
+    dp.Pout = xview(c, out);
     EvPair* pr = prof_begin(c, 1, fs, false);
     if (pr) c->ev_nsteps.push_back(nst);
     HIP_TRY(ekf::launch_downdate(dp, c->cfg.precision, c->dd_grid, fs, pr ? pr->a : nullptr,
@@ -837,7 +943,7 @@ static int enqueue(ekf_ctx* c, int phase, const double* enc, const ekf_line* lin
 {
     // a row-sharded context keeps only its own rows current: the whole-instance scan would read
     // stale ones (slam_ekf.h ekf_shard_abort)
-    if (c->sh_a >= 0) return EKF_EINVAL;
+    if (c->sh_world > 0) return EKF_EINVAL;
     ekf::ScanParams sp = scan_params(c, phase, enc, lines, nlines);
     if (!(phase & ekf::PHASE_UPDATE)) {
         EvPair* pr = prof_begin(c, 0, c->stream);
@@ -849,7 +955,7 @@ static int enqueue(ekf_ctx* c, int phase, const double* enc, const ekf_line* lin
     if (c->ev_base) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_base, 0));
     const int np = (int)(c->nsteps - c->pend0);
     if (np > ekf::PMAX) return EKF_EINVAL;   // unreachable: T <= 16
-    sp.Pread = c->X[c->base];
+    sp.Pread = xview(c, c->base);
     sp.npend = np;
     for (int q = 0; q < np; q++) sp.pend[q] = slot_of(c, c->pend0 + q);
     sp.cur = slot_of(c, c->nsteps);
@@ -934,7 +1040,7 @@ extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
 extern "C" int ekf_localize(ekf_ctx* c, const double* enc, const ekf_line* lines,
                             const int32_t* nlines, ekf_result* out)
 {
-    if (!c || !enc || !lines || !nlines || c->sh_a >= 0) return EKF_EINVAL;
+    if (!c || !enc || !lines || !nlines || c->sh_world > 0) return EKF_EINVAL;
     int rc = stage_inputs(c, enc, lines, nlines);
     if (rc) return rc;
     rc = enqueue(c, ekf::PHASE_BOTH, c->d_enc, c->d_lines, c->d_nlines);
@@ -951,7 +1057,7 @@ extern "C" int ekf_localize_device(ekf_ctx* c, const double* d_enc, const ekf_li
 
 extern "C" int ekf_predict(ekf_ctx* c, const double* enc)
 {
-    if (!c || !enc || c->sh_a >= 0) return EKF_EINVAL;
+    if (!c || !enc || c->sh_world > 0) return EKF_EINVAL;
     int rc = stage_inputs(c, enc, nullptr, nullptr);
     if (rc) return rc;
     return enqueue(c, ekf::PHASE_PREDICT, c->d_enc, c->d_lines, c->d_nlines);
@@ -960,7 +1066,7 @@ extern "C" int ekf_predict(ekf_ctx* c, const double* enc)
 extern "C" int ekf_update(ekf_ctx* c, const ekf_line* lines, const int32_t* nlines,
                           ekf_result* out)
 {
-    if (!c || !lines || !nlines || c->sh_a >= 0) return EKF_EINVAL;
+    if (!c || !lines || !nlines || c->sh_world > 0) return EKF_EINVAL;
     int rc = stage_inputs(c, nullptr, lines, nlines);
     if (rc) return rc;
     rc = enqueue(c, ekf::PHASE_UPDATE, c->d_enc, c->d_lines, c->d_nlines);
@@ -1007,9 +1113,8 @@ extern "C" int ekf_upload_state(ekf_ctx* c, int e, const double* P, const double
         hipError_t err = hipMemcpyAsync(tmp, P, sizeof(double) * d.n * d.n, hipMemcpyHostToDevice,
                                         c->stream);
         if (err == hipSuccess)
-            err = ekf::launch_pack(d, c->cfg.precision, tmp,
-                                   (char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem,
-                                   strip_of(c, cb, e), c->tile_rc, c->pexp_h[e], c->stream);
+            err = ekf::launch_pack(d, c->cfg.precision, tmp, xinst_ptr(c, cur_buf(c), e),
+                                   strip_of(c, cb, e), c->tile_rc, c->pexp_h[e], c->stream, c->t0, c->t1);
         if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
         HIP_TRY(err);
     }
@@ -1041,9 +1146,8 @@ extern "C" int ekf_download_state(ekf_ctx* c, int e, double* P, double* y, int* 
     if (P) {
         double* tmp = nullptr;
         HIP_TRY(dense_scratch(c, &tmp));
-        hipError_t err = ekf::launch_unpack(d, c->cfg.precision, tmp,
-                                            (const char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem,
-                                            strip_of(c, cb, e), c->pexp_h[e], c->stream);
+        hipError_t err = ekf::launch_unpack(d, c->cfg.precision, tmp, xinst_ptr(c, cur_buf(c), e),
+                                            strip_of(c, cb, e), c->pexp_h[e], c->stream, c->t0, c->t1);
         if (err == hipSuccess)
             err = hipMemcpyAsync(P, tmp, sizeof(double) * d.n * d.n, hipMemcpyDeviceToHost,
                                  c->stream);
@@ -1091,9 +1195,8 @@ extern "C" int ekf_init_lowrank(ekf_ctx* c, int e, const double* diag, const dou
     if (err == hipSuccess && rank > 0)
         err = hipMemcpyAsync(du, U, sizeof(double) * d.n * rank, hipMemcpyHostToDevice, c->stream);
     if (err == hipSuccess)
-        err = ekf::launch_lowrank(d, c->cfg.precision, dd, du, rank,
-                                  (char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem,
-                                  strip_of(c, cb, e), c->tile_rc, c->pexp_h[e], c->stream);
+        err = ekf::launch_lowrank(d, c->cfg.precision, dd, du, rank, xinst_ptr(c, cur_buf(c), e),
+                                  strip_of(c, cb, e), c->tile_rc, c->pexp_h[e], c->stream, c->t0, c->t1);
     if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
     (void)hipFree(dd);
     if (du) (void)hipFree(du);
@@ -1120,7 +1223,7 @@ extern "C" int ekf_rescale(ekf_ctx* c, int e, int ex)
     int cb = 0;
     rc = strip_copy(c, e, &cb);
     if (rc) return rc;
-    void* X = (char*)c->X[cur_buf(c)] + (size_t)e * c->pll_inst * c->elem;
+    void* X = xinst_ptr(c, cur_buf(c), e);
     double* Rs = strip_of(c, cb, e);
     double* tmp = nullptr;
     HIP_TRY(dense_scratch(c, &tmp));
@@ -1339,39 +1442,35 @@ extern "C" int ekf_get_ellipse(ekf_ctx* c, int e, float axii[2], float* angle)
 
 extern "C" size_t ekf_landmark_block_bytes(const ekf_ctx* c)
 {
-    return c ? c->pll_inst * c->elem : 0;
+    return c ? c->xinst * c->elem : 0;
 }
 
 extern "C" int ekf_state_dim(const ekf_ctx* c) { return c ? c->d.n : 0; }
 
 // ---------------------------------------------------------------------------------------
-// One instance row-sharded across ranks: this context keeps the
-// landmarks [first, end) of instance 0. The scan runs as host-driven phases of the scan kernel's
-// sequential association (ekf::shard_kernel); between them the caller exchanges, per line, the
-// first passing landmark (MIN over ranks) and the winner's package, and at the end of the scan
-// the operand rows (all-gather). The flush runs the product kernels on the wave-tiles that touch
-// the owned rows only.
+// One instance with its landmark block partitioned over ranks: this
+// context (ekf_shard_create) stores the packed tiles of its tile rows only; the scan runs as
+// phases of ekf::shard_kernel over every landmark (replicated state), and the caller sums the
+// [N][4] exchange buffer over the ranks between phases: the diagonal blocks after begin, the
+// winner's column after each line. Everything is stream-ordered on the context stream: no host
+// round trip until ekf_shard_end.
 
-static ekf::ShardParams shard_params(ekf_ctx* c, int phase)
+static ekf::ShardParams shard_params(ekf_ctx* c, int phase, double* buf)
 {
     ekf::ShardParams p;
     memset(&p, 0, sizeof(p));
     p.d = c->d;
-    p.a = c->sh_a;
-    p.b = c->sh_b;
     p.phase = phase;
     p.line = c->sh_line;
-    p.jstar = -1;
-    p.m = c->sh_m;
     p.L = c->sh_L;
-    p.s = c->sh_s;
-    p.nextra = c->sh_nextra;
     p.r_mode = c->cfg.r_mode;
     p.gate = c->cfg.mahalanobis;
     p.enc_noise = c->cfg.encoder_noise;
     const int np = (int)(c->nsteps - c->pend0);
     p.npend = np;
-    p.Pread = c->X[c->base];
+    p.Pread = xview(c, c->base);
+    p.t0 = c->t0;
+    p.t1 = c->t1;
     for (int q = 0; q < np; q++) p.pend[q] = slot_of(c, c->pend0 + q);
     p.cur = slot_of(c, c->nsteps);
     p.Rs = strip_of(c, 0, 0);
@@ -1383,18 +1482,16 @@ static ekf::ShardParams shard_params(ekf_ctx* c, int phase)
     p.hist = c->sh_hist;
     p.flags = c->sh_flags;
     p.pkg = c->sh_pkg;
-    p.out = c->sh_out;
+    p.ctl = c->sh_ctl;
+    p.col = buf;
     p.enc = c->d_enc;
     p.lines = c->d_lines;
     p.pexp = c->pexp;
-    p.match = c->sh_match;
     p.reset_margin = c->cfg.reset_margin;
     return p;
 }
 
-static int shard_words(const ekf_ctx* c) { return ekf::MB_WORDS_FIXED + 4 * c->d.max_lines; }
-
-// a HIP failure inside a shard phase abandons the open scan (slam_ekf.h ekf_shard_abort)
+// a HIP failure inside a scan abandons it (slam_ekf.h ekf_shard_abort)
 #define SH_TRY(expr)                                                                        \
     do {                                                                                    \
         hipError_t _e = (expr);                                                             \
@@ -1405,221 +1502,74 @@ static int shard_words(const ekf_ctx* c) { return ekf::MB_WORDS_FIXED + 4 * c->d
         }                                                                                   \
     } while (0)
 
-extern "C" int ekf_shard_init(ekf_ctx* c, int first, int end)
+extern "C" int ekf_shard_tiles(const ekf_ctx* c, int* row_begin, int* row_end)
 {
-    if (!c) return EKF_EINVAL;
-    if (c->cfg.instances != 1 || c->cfg.pipeline || c->bf || c->cfg.arith != EKF_ARITH_EXACT ||
-        c->cfg.precision == EKF_PREC_F16 || c->sh_a >= 0)
-        return EKF_EINVAL;
-    if (first < 0 || end > c->d.N || first >= end) return EKF_ERANGE;
-    int rc = drain(c);
-    if (rc) return rc;
-    int cb = 0;
-    rc = strip_copy(c, 0, &cb);
-    if (rc) return rc;
-    if (cb != 0) {   // the shard phases keep the committed strip and mean in copy 0
-        HIP_TRY(hipMemcpyAsync(strip_of(c, 0, 0), strip_of(c, 1, 0), sizeof(double) * 3 * c->d.n,
-                               hipMemcpyDeviceToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(mean_of(c, 0, 0), mean_of(c, 1, 0), sizeof(double) * c->d.n,
-                               hipMemcpyDeviceToDevice, c->stream));
-        HIP_TRY(hipMemsetAsync(c->cur, 0, sizeof(int), c->stream));
-    }
-    const size_t N = (size_t)c->d.N;
-    {
-        // every scratch buffer or none: a failure frees what was allocated, so a retry neither
-        // leaks nor finds half-initialised pointers
-        void** bufs[7] = {(void**)&c->sh_rob, (void**)&c->sh_rec, (void**)&c->sh_hist, (void**)&c->sh_pkg,
-                          (void**)&c->sh_flags, (void**)&c->sh_out, (void**)&c->sh_match};
-        const size_t bytes[7] = {sizeof(double) * 12, sizeof(double) * N * ekf::SH_REC,
-                                 sizeof(double) * N * c->d.max_lines * 8, sizeof(double) * shard_words(c),
-                                 sizeof(int) * N, sizeof(int) * 2, sizeof(int) * 2 * c->d.max_lines};
-        for (int k = 0; k < 7; k++) {
-            if (*bufs[k] == nullptr && hipMalloc(bufs[k], bytes[k]) != hipSuccess) {
-                for (int q = 0; q < 7; q++) {
-                    if (*bufs[q]) (void)hipFree(*bufs[q]);
-                    *bufs[q] = nullptr;
-                }
-                return EKF_ENOMEM;
-            }
-        }
-    }
-    c->sh_match_h.assign(2 * c->d.max_lines, -1);
-    // the flush's wave-tiles restricted to those holding a tile of an owned row block (a tile of
-    // two ranks' rows is kept by both, identically); groups of 2 and 4 steps take the wave form too
-    const int rb0 = (2 * first) / ekf::TILE, rb1 = (2 * end - 1) / ekf::TILE;
-    auto owned = [&](int blk) { return blk >= rb0 && blk <= rb1; };
-    auto restrict_table = [&](ekf::WtEntry* dev, int& cnt, int nr, int nc) -> int {
-        if (!dev || cnt <= 0) return EKF_OK;
-        std::vector<ekf::WtEntry> all(cnt), keep;
-        HIP_TRY(hipMemcpy(all.data(), dev, sizeof(ekf::WtEntry) * cnt, hipMemcpyDeviceToHost));
-        for (const auto& w : all) {
-            bool k = false;
-            for (int r = 0; r < nr; r++)
-                for (int q = 0; q < nc; q++) {
-                    if (!((w.valid >> (r * nc + q)) & 1)) continue;
-                    const int bi = (w.rows[0] >> (16 * r)) & 0xffff, bj = (w.rows[1] >> (16 * q)) & 0xffff;
-                    k |= owned(bi) || owned(bj);
-                }
-            if (k) keep.push_back(w);
-        }
-        if (!keep.empty())
-            HIP_TRY(hipMemcpy(dev, keep.data(), sizeof(ekf::WtEntry) * keep.size(), hipMemcpyHostToDevice));
-        cnt = (int)keep.size();
-        return EKF_OK;
-    };
-    rc = restrict_table(c->wt, c->nwt, ekf::WT_R, ekf::WT_C);
-    if (rc) return rc;
-    rc = restrict_table(c->wt64, c->nwt64, 1, ekf::WT64_C);
-    if (rc) return rc;
-    c->dd_variant = 8;
-    c->sh_a = first;
-    c->sh_b = end;
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (!c || c->sh_world <= 0 || !row_begin || !row_end) return EKF_EINVAL;
+    *row_begin = c->sh_r0;
+    *row_end = c->sh_r1;
     return EKF_OK;
 }
 
-extern "C" int ekf_shard_begin(ekf_ctx* c, const double enc[3], const ekf_line* lines, int nlines)
+extern "C" size_t ekf_shard_buffer_words(const ekf_ctx* c) { return (c && c->sh_world > 0) ? 4 * (size_t)c->d.N : 0; }
+
+extern "C" int ekf_shard_begin(ekf_ctx* c, const double enc[3], const ekf_line* lines, int nlines, double* buf)
 {
-    if (!c || c->sh_a < 0 || !enc || (nlines > 0 && !lines)) return EKF_EINVAL;
+    if (!c || c->sh_world <= 0 || !enc || !buf || (nlines > 0 && !lines) || c->sh_open) return EKF_EINVAL;
     if (nlines < 0 || nlines > c->d.max_lines) return EKF_ERANGE;
-    if (c->sh_open) return EKF_EINVAL;
     std::vector<ekf_line> pad(c->d.max_lines);
     memset(pad.data(), 0, sizeof(ekf_line) * pad.size());
     for (int i = 0; i < nlines; i++) pad[i] = lines[i];
     int rc = stage_inputs(c, enc, pad.data(), &nlines);
     if (rc) return rc;
-    int s = 0;
-    HIP_TRY(hipMemcpyAsync(&s, c->saved, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    c->sh_line = -1;
-    c->sh_m = 0;
+    c->sh_line = 0;
     c->sh_L = nlines;
-    c->sh_s = s;
-    c->sh_nextra = 0;
-    c->sh_match_h.assign(2 * c->d.max_lines, -1);
-    HIP_TRY(hipMemsetAsync(c->sh_out, 0, sizeof(int) * 2, c->stream));
-    HIP_TRY(ekf::launch_shard(shard_params(c, ekf::SH_BEGIN), c->cfg.precision, c->stream));
     c->sh_open = 1;
+    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_BEGIN, buf), c->cfg.precision, c->stream));
     return EKF_OK;
 }
 
-extern "C" int ekf_shard_gate(ekf_ctx* c, int line, int* first_pass)
+extern "C" int ekf_shard_line(ekf_ctx* c, int line, double* buf)
 {
-    if (!c || !c->sh_open || !first_pass) return EKF_EINVAL;
+    if (!c || c->sh_open != 1 || !buf || line != c->sh_line) return EKF_EINVAL;
     if (line < 0 || line >= c->sh_L) return EKF_ERANGE;
-    c->sh_line = line;
-    const int init[2] = {0x7fffffff, 0};
-    SH_TRY(hipMemcpyAsync(c->sh_out, init, sizeof(int), hipMemcpyHostToDevice, c->stream));
-    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_GATE), c->cfg.precision, c->stream));
-    SH_TRY(hipMemcpyAsync(first_pass, c->sh_out, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    SH_TRY(hipStreamSynchronize(c->stream));
+    if (line == 0)   // the summed diagonal blocks of begin's exchange
+        SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_DIAG, buf), c->cfg.precision, c->stream));
+    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_GATE, buf), c->cfg.precision, c->stream));
+    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_COLUMN, buf), c->cfg.precision, c->stream));
     return EKF_OK;
 }
 
-extern "C" int ekf_shard_package_words(const ekf_ctx* c) { return c ? shard_words(c) : 0; }
-
-extern "C" int ekf_shard_package(ekf_ctx* c, int line, int jstar, double* pkg)
+extern "C" int ekf_shard_apply(ekf_ctx* c, int line, const double* buf)
 {
-    if (!c || !c->sh_open || !pkg || line != c->sh_line) return EKF_EINVAL;
-    if (jstar < c->sh_a || jstar >= c->sh_b) return EKF_ERANGE;
-    ekf::ShardParams p = shard_params(c, ekf::SH_PACKAGE);
-    p.jstar = jstar;
-    SH_TRY(hipMemsetAsync(c->sh_pkg, 0, sizeof(double) * shard_words(c), c->stream));
-    SH_TRY(ekf::launch_shard(p, c->cfg.precision, c->stream));
-    SH_TRY(hipMemcpyAsync(pkg, c->sh_pkg, sizeof(double) * shard_words(c), hipMemcpyDeviceToHost, c->stream));
-    SH_TRY(hipStreamSynchronize(c->stream));
+    if (!c || c->sh_open != 1 || !buf || line != c->sh_line) return EKF_EINVAL;
+    double* b = const_cast<double*>(buf);   // (read only by these phases)
+    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_APPLY, b), c->cfg.precision, c->stream));
+    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_ROBOT, b), c->cfg.precision, c->stream));
+    c->sh_line++;
     return EKF_OK;
 }
 
-extern "C" int ekf_shard_apply(ekf_ctx* c, int line, int jstar, const double* pkg)
+extern "C" int ekf_shard_end(ekf_ctx* c, ekf_result* out)
 {
-    if (!c || !c->sh_open || line != c->sh_line || (jstar >= 0 && !pkg)) return EKF_EINVAL;
-    if (jstar >= c->d.N) return EKF_ERANGE;
-    ekf::ShardParams p = shard_params(c, ekf::SH_APPLY);
-    p.jstar = jstar;
-    if (jstar >= 0)
-        SH_TRY(hipMemcpyAsync(c->sh_pkg, pkg, sizeof(double) * shard_words(c), hipMemcpyHostToDevice, c->stream));
-    SH_TRY(ekf::launch_shard(p, c->cfg.precision, c->stream));
-    if (jstar >= 0) {
-        // the robot block after the match (Robot.cpp:560-602), the same on every rank
-        SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_ROBOT), c->cfg.precision, c->stream));
-        c->sh_match_h[line] = jstar;
-        c->sh_m++;
-    } else {
-        c->sh_match_h[c->d.max_lines + c->sh_nextra] = line;
-        c->sh_nextra++;
-    }
-    SH_TRY(hipStreamSynchronize(c->stream));
-    return EKF_OK;
-}
-
-extern "C" size_t ekf_shard_operand_bytes(const ekf_ctx* c) { return c ? c->op_inst * c->op_elem : 0; }
-
-extern "C" int ekf_shard_operands(ekf_ctx* c, void* U, void* V, int upload)
-{
-    if (!c || !c->sh_open || !U || !V) return EKF_EINVAL;
-    const ekf::Slot& cur = slot_of(c, c->nsteps);
-    const size_t bytes = c->op_inst * c->op_elem;
-    const hipMemcpyKind k = upload ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
-    SH_TRY(hipMemcpyAsync(upload ? cur.Uop : U, upload ? U : cur.Uop, bytes, k, c->stream));
-    SH_TRY(hipMemcpyAsync(upload ? cur.Vop : V, upload ? V : cur.Vop, bytes, k, c->stream));
-    SH_TRY(hipStreamSynchronize(c->stream));
-    return EKF_OK;
-}
-
-// Closes the scan: the owned strip columns and mean, the robot block, pose and the step's record,
-// then (ekf_shard_commit, after the operand all-gather) the step joins the flush schedule.
-extern "C" int ekf_shard_end(ekf_ctx* c)
-{
-    if (!c || !c->sh_open) return EKF_EINVAL;
-    SH_TRY(hipMemcpyAsync(c->sh_match, c->sh_match_h.data(), sizeof(int) * 2 * c->d.max_lines,
-                           hipMemcpyHostToDevice, c->stream));
-    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_END), c->cfg.precision, c->stream));
-    SH_TRY(hipStreamSynchronize(c->stream));
-    return EKF_OK;
-}
-
-extern "C" size_t ekf_shard_patch_bytes(const ekf_ctx* c)
-{
-    return c ? sizeof(double) * c->d.max_lines * 2 * c->d.M : 0;
-}
-
-// The step's new-landmark rows (patch buffer, [max_lines][2][M]): each rank writes the columns of
-// its landmarks; the caller all-gathers them like the operand rows (upload = 1 sets them)
-extern "C" int ekf_shard_patch(ekf_ctx* c, double* rows, int upload)
-{
-    if (!c || !c->sh_open || !rows) return EKF_EINVAL;
-    const ekf::Slot& cur = slot_of(c, c->nsteps);
-    const size_t bytes = ekf_shard_patch_bytes(c);
-    SH_TRY(hipMemcpyAsync(upload ? (void*)cur.patch : (void*)rows, upload ? (const void*)rows : (const void*)cur.patch,
-                           bytes, upload ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, c->stream));
-    SH_TRY(hipStreamSynchronize(c->stream));
-    return EKF_OK;
-}
-
-extern "C" int ekf_shard_commit(ekf_ctx* c)
-{
-    if (!c || !c->sh_open) return EKF_EINVAL;
+    if (!c || c->sh_open != 1 || c->sh_line != c->sh_L) return EKF_EINVAL;
+    // (with no line, begin's exchange is not consumed: the end needs no diagonal block)
+    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_END, nullptr), c->cfg.precision, c->stream));
     c->sh_open = 0;
+    // the step joins the deferred flush of the rank's tiles
     c->nsteps++;
-    if (c->nsteps - c->unflushed0 >= c->T) return enqueue_flush(c);
-    return EKF_OK;
+    if (c->nsteps - c->unflushed0 >= c->T) {
+        const int rc = enqueue_flush(c);
+        if (rc) return rc;
+    }
+    return ekf_read_results(c, out);
 }
 
 extern "C" int ekf_shard_abort(ekf_ctx* c)
 {
     // before ekf_shard_end nothing of the committed state is written (the phases use the scan's
-    // scratch and the current ring slot, which only ekf_shard_commit adds to the schedule)
-    if (!c || c->sh_a < 0) return EKF_EINVAL;
+    // scratch and the current ring slot, which only ekf_shard_end adds to the schedule)
+    if (!c || c->sh_world <= 0) return EKF_EINVAL;
     c->sh_open = 0;
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return EKF_OK;
-}
-
-extern "C" int ekf_shard_status(ekf_ctx* c, int* status)
-{
-    if (!c || !status) return EKF_EINVAL;
-    HIP_TRY(hipMemcpyAsync(status, c->sh_out + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return EKF_OK;
 }

@@ -120,21 +120,27 @@ struct ScanParams {
     unsigned long long* dbg;  // optional [E][16] phase timers (s_memrealtime ticks, 100 MHz)
 };
 
-// One instance row-sharded across ranks: the sequential association
-// of the scan kernel (Robot.cpp:298-641) as host-driven phases over the rank's landmarks [a, b),
-// the per-line exchanges (MIN of the first passing landmark, the winner's package) done by the
-// caller between launches. Per-landmark running state lives in `rec` between the phases.
-enum { SH_BEGIN = 0, SH_GATE = 1, SH_PACKAGE = 2, SH_APPLY = 3, SH_END = 4, SH_ROBOT = 5 };
+// One instance whose landmark block is partitioned over ranks: rank r
+// stores the packed tiles of tile rows [r0, r1) only (a contiguous slice of the packed array,
+// balanced by tile count); everything of size O(n) — robot strip, mean, the landmarks' scan state,
+// their diagonal blocks, the operand rows — is replicated and evolves identically on every rank.
+// A scan runs the sequential association (Robot.cpp:298-641) as phases over ALL landmarks; the only
+// exchanges are sums of [N][4] buffers in which every rank fills the 2×2 blocks its tiles hold:
+// the diagonal blocks once per scan, the winner's column once per matched line.
+enum { SH_BEGIN = 0, SH_DIAG = 1, SH_GATE = 2, SH_COLUMN = 3, SH_APPLY = 4, SH_ROBOT = 5, SH_END = 6 };
 constexpr int SH_REC = 20;   // doubles per landmark: rr0..2 (6), yb (2), Dj (4), ma0, s0j, c0j, s0f, c0f, spare
+// device control words of the running scan (no host round trip between phases)
+enum { SC_WIN = 0, SC_STATUS = 1, SC_M = 2, SC_NEXTRA = 3, SC_S = 4, SC_MATCH = 8,
+       SC_EXTRA = 8 + EKF_MAX_LINES, SC_WORDS = 8 + 2 * EKF_MAX_LINES };
 struct ShardParams {
     Dims d;
-    int a, b;             // owned landmarks
     int phase;
-    int line, jstar, m, L, s, nextra;
+    int line, L;
     int r_mode;
     double gate, enc_noise;
     int npend;
-    const void* Pread;    // [ntiles][1024] (instance 0)
+    const void* Pread;    // tile t (t0 <= t < t1) of instance 0 at Pread + t·TILE_ELEMS (the slice, shifted)
+    long long t0, t1;     // the rank's tiles (global packed indices)
     Slot cur;
     Slot pend[PMAX];
     double* Rs;           // [3][n] robot strip (the committed copy)
@@ -146,11 +152,11 @@ struct ShardParams {
     double* hist;         // [N][max_lines][8] U rows and V rows of each match of the scan
     int* flags;           // [N] bit 0 matched, bit 1 singular at this line
     double* pkg;          // [MB words + 4·max_lines] the line's gain package
-    int* out;             // [2] first passing landmark (atomic min), status bits (atomic or)
+    int* ctl;             // [SC_WORDS]
+    double* col;          // [N][4] the exchange buffer (caller's device memory)
     const double* enc;    // [3]
     const ekf_line* lines;// [max_lines]
     const int* pexp;
-    const int* match;     // [2][max_lines] the lines' winners, then the unmatched lines in order (SH_END)
     int reset_margin;
 };
 hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st);
@@ -198,11 +204,13 @@ size_t scan_lds_bytes(int precision);   // static LDS of the association kernel
 hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st,
                            hipEvent_t ev_a = nullptr, hipEvent_t ev_b = nullptr);
 // ex: fp16 storage exponent of the instance (ignored for f32 / f64)
+// [t0, t1): the tiles stored (t1 < 0: all); Pll points at tile t0
 hipError_t launch_pack(const Dims& d, int precision, const double* Pfull, void* Pll, double* Rs,
-                       const int2* tile_rc, int ex, hipStream_t st);
+                       const int2* tile_rc, int ex, hipStream_t st, int64_t t0 = 0, int64_t t1 = -1);
 hipError_t launch_unpack(const Dims& d, int precision, double* Pfull, const void* Pll,
-                         const double* Rs, int ex, hipStream_t st);
+                         const double* Rs, int ex, hipStream_t st, int64_t t0 = 0, int64_t t1 = -1);
 hipError_t launch_lowrank(const Dims& d, int precision, const double* diag, const double* U,
-                          int rank, void* Pll, double* Rs, const int2* tile_rc, int ex, hipStream_t st);
+                          int rank, void* Pll, double* Rs, const int2* tile_rc, int ex, hipStream_t st,
+                          int64_t t0 = 0, int64_t t1 = -1);
 
 }  // namespace ekf

@@ -2754,11 +2754,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
 }
 
 // ---------------------------------------------------------------------------------------
-// One instance row-sharded across ranks (ShardParams): the scan kernel's
-// sequential association path phase by phase over the rank's landmarks [a, b), one thread per
+// One instance with its landmark block partitioned over ranks (ShardParams): the
+// scan kernel's sequential association path phase by phase over every landmark, one thread per
 // landmark, every expression the scan kernel's (the same inline functions in this contract(on)
 // region), so that a sharded run is bit-identical to a single-context one. Between phases the
-// caller exchanges the first passing landmark (MIN over ranks) and the winner's package.
+// caller sums the [N][4] exchange buffer over the ranks (each fills the blocks its tiles hold).
 // Predict (Robot.cpp:130-286) as the scan kernel's init_state: F3, x_pre and the 3×3 block
 __device__ __forceinline__ void shard_predict(const double pose[3], const double enc[3], double enc_noise,
                                               double F3[9], double R33[9], double xp[3])
@@ -2806,9 +2806,9 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
     using C = typename Stor<T>::C;
     const Dims d = p.d;
     const int n = d.n;
-    const int gid = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    const int j = p.a + gid;
-    const bool own = j < p.b;
+    const int j = (int)(blockIdx.x * blockDim.x + threadIdx.x);   // every rank runs every landmark
+    const bool own = j < d.N;
+    int* ctl = p.ctl;
     __shared__ int4 sh_ctl[PMAX];
     if ((int)threadIdx.x < p.npend) {
         const int* r = p.pend[threadIdx.x].res;
@@ -2828,6 +2828,12 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
     pv.pend = p.pend;
     pv.ctl = sh_ctl;
     pv.rnd = 1;
+    // block (j, w) of the landmark block is this rank's if the tile that stores it is
+    auto local_blk = [&](int ja, int wb) {
+        const int ba = (2 * ja) >> 5, bb = (2 * wb) >> 5;
+        const long long t = tile_index(ba < bb ? ba : bb, ba < bb ? bb : ba, d.nb);
+        return t >= p.t0 && t < p.t1;
+    };
     const bool sym = p.r_mode != 1 && sizeof(C) == 4;
     const int b0 = 3 + 2 * j;
     double* rc = p.rec + (size_t)j * SH_REC;
@@ -2838,27 +2844,45 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
         xp[0] = p.rob[9]; xp[1] = p.rob[10]; xp[2] = p.rob[11];
     }
     if (p.phase == SH_ROBOT) {
-        // the robot block and x_pre after the line's match (Robot.cpp:560-602), one thread
-        if (gid == 0) {
-            robot_update(R33, xp, p.pkg);
+        // after line `line` (one thread): the robot block and x_pre after its match (Robot.cpp:560-602),
+        // the match list, and the winner word reset for the next line's gate
+        if (j == 0) {
+            const int jstar = ctl[SC_WIN];
+            if (jstar != 0x7fffffff) {
+                robot_update(R33, xp, p.pkg);
 #pragma unroll
-            for (int a = 0; a < 9; a++) p.rob[a] = R33[a];
-            p.rob[9] = xp[0]; p.rob[10] = xp[1]; p.rob[11] = xp[2];
+                for (int a = 0; a < 9; a++) p.rob[a] = R33[a];
+                p.rob[9] = xp[0]; p.rob[10] = xp[1]; p.rob[11] = xp[2];
+                ctl[SC_MATCH + p.line] = jstar;
+                ctl[SC_M] += 1;
+            } else {
+                ctl[SC_MATCH + p.line] = -1;
+                ctl[SC_EXTRA + ctl[SC_NEXTRA]] = p.line;
+                ctl[SC_NEXTRA] += 1;
+            }
+            ctl[SC_WIN] = 0x7fffffff;
         }
         return;
     }
 
     if (p.phase == SH_BEGIN) {
-        // the committed robot block and pose, predicted (every thread the same), the owned strip
-        // columns predicted (Robot.cpp:242), the diagonal block with the pending steps applied
+        // the committed robot block and pose, predicted (every thread the same), every landmark's
+        // strip columns predicted (Robot.cpp:242) and scan-start angle; the rank's diagonal blocks
+        // with the pending steps applied into the exchange buffer (zero where another rank's)
+        const int s = p.saved[0];
 #pragma unroll
         for (int a = 0; a < 9; a++) R33[a] = p.Rs[(a / 3) * n + (a % 3)];
         double F3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
         shard_predict(p.pose, p.enc, p.enc_noise, F3, R33, xp);
-        if (gid == 0) {
+        if (j == 0) {
 #pragma unroll
             for (int a = 0; a < 9; a++) p.rob[a] = R33[a];
             p.rob[9] = xp[0]; p.rob[10] = xp[1]; p.rob[11] = xp[2];
+            ctl[SC_WIN] = 0x7fffffff;
+            ctl[SC_STATUS] = 0;
+            ctl[SC_M] = 0;
+            ctl[SC_NEXTRA] = 0;
+            ctl[SC_S] = s;
         }
         if (!own) return;
         double2 rr0 = *reinterpret_cast<const double2*>(p.Rs + b0);
@@ -2867,19 +2891,26 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
         const double2 yb = *reinterpret_cast<const double2*>(p.y + b0);
         predict_cols(F3, rr0, rr1, rr2);
         double Dj[4] = {0, 0, 0, 0};
-        if (j < p.s) pll_block(pv, 2 * j, 2 * j, Dj);
+        if (j < s && local_blk(j, j)) pll_block(pv, 2 * j, 2 * j, Dj);
         double s0j, c0j;
         sincos(yb.x, &s0j, &c0j);
         float s0f, c0f;
         __sincosf((float)yb.x, &s0f, &c0f);
-        const double v[SH_REC] = {rr0.x, rr0.y, rr1.x, rr1.y, rr2.x, rr2.y, yb.x, yb.y, Dj[0], Dj[1], Dj[2], Dj[3],
+        const double v[SH_REC] = {rr0.x, rr0.y, rr1.x, rr1.y, rr2.x, rr2.y, yb.x, yb.y, 0, 0, 0, 0,
                                   yb.x, s0j, c0j, (double)s0f, (double)c0f, 0, 0, 0};
 #pragma unroll
         for (int k = 0; k < SH_REC; k++) rc[k] = v[k];
+        *reinterpret_cast<double4*>(p.col + 4 * (size_t)j) = make_double4(Dj[0], Dj[1], Dj[2], Dj[3]);
         p.flags[j] = 0;
         return;
     }
     if (!own) return;
+    if (p.phase == SH_DIAG) {   // the summed diagonal blocks (every rank contributed its own)
+        const double4 dj = *reinterpret_cast<const double4*>(p.col + 4 * (size_t)j);
+        rc[8] = dj.x; rc[9] = dj.y; rc[10] = dj.z; rc[11] = dj.w;
+        return;
+    }
+    const int s = ctl[SC_S];
     double2 rr0 = make_double2(rc[0], rc[1]), rr1 = make_double2(rc[2], rc[3]), rr2 = make_double2(rc[4], rc[5]);
     double2 yb = make_double2(rc[6], rc[7]);
     double Dj[4] = {rc[8], rc[9], rc[10], rc[11]};
@@ -2890,18 +2921,12 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
     double Rm[4];
     line_R(ln, p.line, p.r_mode, Rm);
 
-    if (p.phase == SH_GATE || p.phase == SH_PACKAGE) {
-        // gating of the owned candidate (Robot.cpp:313-498) exactly as the sequential path
-        if (p.phase == SH_PACKAGE && j != p.jstar) return;
-        if (!(j < p.s) || (fl & 1)) {
-            if (p.phase == SH_GATE) p.flags[j] = fl & 1;
-            return;
-        }
+    // the gate of one landmark exactly as the sequential path (Robot.cpp:313-498)
+    auto gate_of = [&](Cand& c, bool& pass, bool& sing) {
         Block5 b5;
         fill_block5(b5, R33, rr0, rr1, rr2, Dj);
         double sn, cs;
-        Cand c;
-        bool pass = false, sing = false;
+        pass = sing = false;
         if (!quick_reject(b5, yb.x, yb.y, ma0, s0f, c0f, xp, ln.alpha, ln.r, Rm, p.gate) &&
             (sincos_near(yb.x, ma0, s0j, c0j, sn, cs),
              !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate))) {
@@ -2909,33 +2934,59 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
             sing = c.singular;
             pass = c.pass;
         }
-        if (p.phase == SH_GATE) {
-            p.flags[j] = (fl & 1) | (sing ? 2 : 0);
-            if (pass) atomicMin(p.out, j);
+    };
+
+    if (p.phase == SH_GATE) {
+        // the first passing unmatched landmark of the line: every rank finds the same one
+        if (!(j < s) || (fl & 1)) {
+            p.flags[j] = fl & 1;
             return;
         }
-        // the winner's package and its V rows of the earlier matches (Robot.cpp:560-568)
-        build_package(c, R33, rr0, rr1, rr2, p.pkg);
-        for (int q = 0; q < p.m; q++) {
-            const double* h = p.hist + ((size_t)j * d.max_lines + q) * 8 + 4;
-            p.pkg[MB_VH + 4 * q + 0] = h[0];
-            p.pkg[MB_VH + 4 * q + 1] = h[1];
-            p.pkg[MB_VH + 4 * q + 2] = h[2];
-            p.pkg[MB_VH + 4 * q + 3] = h[3];
+        Cand c;
+        bool pass, sing;
+        gate_of(c, pass, sing);
+        p.flags[j] = (fl & 1) | (sing ? 2 : 0);
+        if (pass) atomicMin(ctl + SC_WIN, j);
+        return;
+    }
+
+    if (p.phase == SH_COLUMN) {
+        // the winner's gain package (its thread) and the rank's blocks of its column, with the
+        // pending steps applied, into the exchange buffer (zero where another rank's)
+        const int jstar = ctl[SC_WIN];
+        double blk[4] = {0, 0, 0, 0};
+        if (jstar != 0x7fffffff) {
+            if (local_blk(j, jstar)) pll_block(pv, 2 * j, 2 * jstar, blk);
+            if (j == jstar) {
+                Cand c;
+                bool pass, sing;
+                gate_of(c, pass, sing);
+                build_package(c, R33, rr0, rr1, rr2, p.pkg);
+                const int m = ctl[SC_M];
+                for (int q = 0; q < m; q++) {   // the winner's V rows of the earlier matches (Robot.cpp:560-568)
+                    const double* h = p.hist + ((size_t)j * d.max_lines + q) * 8 + 4;
+                    p.pkg[MB_VH + 4 * q + 0] = h[0];
+                    p.pkg[MB_VH + 4 * q + 1] = h[1];
+                    p.pkg[MB_VH + 4 * q + 2] = h[2];
+                    p.pkg[MB_VH + 4 * q + 3] = h[3];
+                }
+            }
         }
+        *reinterpret_cast<double4*>(p.col + 4 * (size_t)j) = make_double4(blk[0], blk[1], blk[2], blk[3]);
         return;
     }
 
     if (p.phase == SH_APPLY) {
+        const int jstar = ctl[SC_WIN];
         // GSL_EDOM counts only for the candidates the reference evaluates (up to the winner)
-        int st = (fl & 2) && j <= (p.jstar < 0 ? 0x7fffffff : p.jstar) ? (int)EKF_ST_SINGULAR : 0;
+        int st = (fl & 2) && j <= jstar ? (int)EKF_ST_SINGULAR : 0;
         if (p.r_mode == 1 && (p.line == 1 || p.line == 2)) st |= EKF_ST_NSYM;
-        if (st) atomicOr(p.out + 1, st);
-        if (p.jstar < 0) return;
-        double blk[4];
-        pll_block(pv, 2 * j, 2 * p.jstar, blk);
+        if (st) atomicOr(ctl + SC_STATUS, st);
+        if (jstar == 0x7fffffff) return;
+        const double4 cb = *reinterpret_cast<const double4*>(p.col + 4 * (size_t)j);   // summed over ranks
+        double blk[4] = {cb.x, cb.y, cb.z, cb.w};
         const double* pk = p.pkg;
-        const int m = p.m;
+        const int m = ctl[SC_M];
         double kk[4], uu[4];
         gain_rows<0>(pk, m,
                      [&](int q) {
@@ -2977,7 +3028,7 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
                 Vop[op_index_f64(lr, 2 * m + 1, d.kmax)] = (C)kk[2 * pp + 1];
             }
         }
-        if (j == p.jstar) fl |= 1;
+        if (j == jstar) fl |= 1;
         p.flags[j] = fl & 1;
         const double v[12] = {rr0.x, rr0.y, rr1.x, rr1.y, rr2.x, rr2.y, yb.x, yb.y, Dj[0], Dj[1], Dj[2], Dj[3]};
 #pragma unroll
@@ -2985,21 +3036,22 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
         return;
     }
 
-    // SH_END: augmentation (Robot.cpp:776-866) as the scan kernel's commit: the new landmarks'
-    // rows (this rank's columns of them to the step's patch buffer, all-gathered by the caller),
-    // the new landmark's strip columns and mean on its owner, the 2×2 diagonal blocks on every
-    // rank; the capacity reset (Robot.cpp:893-904)
+    // SH_END: augmentation (Robot.cpp:776-866) as the scan kernel's commit: the new landmarks' rows
+    // to the step's patch buffer (every rank all of them: its flush takes the columns of its tiles),
+    // the new landmarks' strip columns and mean, the 2×2 diagonal blocks; the capacity reset
+    // (Robot.cpp:893-904)
+    const int m = ctl[SC_M], nextra = ctl[SC_NEXTRA];
     double pose[3] = {xp[0], xp[1], xp[2]};
-    if (p.L == 0 || p.m == 0) pose[2] = normalize_radian(xp[2]);
+    if (p.L == 0 || m == 0) pose[2] = normalize_radian(xp[2]);
     const int N = d.N, M = d.M;
-    const int nadd = min(p.nextra, N - p.s);
-    const int reset = (p.s + nadd > N - p.reset_margin) ? 1 : 0;
+    const int nadd = min(nextra, N - s);
+    const int reset = (s + nadd > N - p.reset_margin) ? 1 : 0;
     double* patch = p.cur.patch;
     double* pdiag = p.cur.patch_diag;
     if (!reset) {
         for (int q = 0; q < nadd; q++) {
-            const ekf_line lq = p.lines[p.match[d.max_lines + q]];
-            const int sq = p.s + q;
+            const ekf_line lq = p.lines[ctl[SC_EXTRA + q]];
+            const int sq = s + q;
             double alfa = lq.alpha;
             const double r = lq.r + (pose[0] * cos(alfa) + pose[1] * sin(alfa));
             alfa += pose[2];
@@ -3019,7 +3071,7 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
                 rr2 = make_double2(R33[8], ca * R33[2] + sa * R33[5]);
                 yb = make_double2(normalize_radian(alfa), r);
             }
-            if (gid == 0) {
+            if (j == 0) {
                 const double Gx[6] = {0, 0, 1, ca, sa, 0};
                 const double Gl[4] = {1.0, 0, xp[1] * ca - xp[0] * sa, 1};
                 double GP[6], GlR[4];
@@ -3043,14 +3095,14 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
         }
     }
     if (reset) rr0 = rr1 = rr2 = yb = make_double2(0.0, 0.0);
-    // the owned strip columns and mean, the operand padding past the matches
+    // the strip columns and mean, the operand padding past the matches
     *reinterpret_cast<double2*>(p.Rs + b0) = rr0;
     *reinterpret_cast<double2*>(p.Rs + n + b0) = rr1;
     *reinterpret_cast<double2*>(p.Rs + 2 * n + b0) = rr2;
     *reinterpret_cast<double2*>(p.y + b0) = yb;
     C* Uop = reinterpret_cast<C*>(p.cur.Uop);
     C* Vop = reinterpret_cast<C*>(p.cur.Vop);
-    for (int k = 2 * p.m; k < d.kmax; k++)
+    for (int k = 2 * m; k < d.kmax; k++)
 #pragma unroll
         for (int pp = 0; pp < 2; pp++) {
             if constexpr (sizeof(C) == 4) {
@@ -3061,26 +3113,26 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
                 Vop[op_index_f64(2 * j + pp, k, d.kmax)] = (C)0.0;
             }
         }
-    if (gid == 0) {
+    if (j == 0) {
         // commit (Robot.cpp:702-716)
         for (int a = 0; a < 9; a++) p.Rs[(a / 3) * n + (a % 3)] = R33[a];
         p.y[0] = xp[0]; p.y[1] = xp[1]; p.y[2] = xp[2];
         p.pose[0] = pose[0]; p.pose[1] = pose[1]; p.pose[2] = pose[2];
         int* res = p.cur.res;
         res[RES_NLINES] = p.L;
-        res[RES_SAVED_IN] = p.s;
+        res[RES_SAVED_IN] = s;
         res[RES_DBG] = 16;
-        res[RES_STATUS] = (p.nextra > nadd) ? EKF_ST_CAP : 0;
-        res[RES_M] = p.m;
-        res[RES_NEXTRA] = p.nextra;
-        res[RES_SAVED] = reset ? 0 : p.s + nadd;
+        res[RES_STATUS] = ((nextra > nadd) ? EKF_ST_CAP : 0) | ctl[SC_STATUS];
+        res[RES_M] = m;
+        res[RES_NEXTRA] = nextra;
+        res[RES_SAVED] = reset ? 0 : s + nadd;
         res[RES_RESET] = reset;
         res[RES_NADD] = reset ? 0 : nadd;
-        res[RES_KSTEPS] = (sizeof(C) == 4) ? p.m : (p.m + 1) / 2;
+        res[RES_KSTEPS] = (sizeof(C) == 4) ? m : (m + 1) / 2;
         res[RES_ROLLBACK] = 0;
-        for (int i = 0; i < p.L; i++) res[RES_MATCH + i] = p.match[i];
-        for (int q = 0; q < p.nextra; q++) res[RES_EXTRA + q] = p.match[d.max_lines + q];
-        p.saved[0] = reset ? 0 : p.s + nadd;
+        for (int i = 0; i < p.L; i++) res[RES_MATCH + i] = ctl[SC_MATCH + i];
+        for (int q = 0; q < nextra; q++) res[RES_EXTRA + q] = ctl[SC_EXTRA + q];
+        p.saved[0] = reset ? 0 : s + nadd;
     }
 }
 
@@ -4788,16 +4840,19 @@ __device__ __forceinline__ void tile_rc_of(int rem, int& r, int& c)
     }
 }
 
+// pack / unpack / lowrank cover the tiles [t0, t1) (a partitioned instance stores a slice; Pll points
+// at the slice's first tile, t0)
 template <typename T>
 __global__ void pack_kernel(Dims d, const double* __restrict__ Pfull, T* __restrict__ Pll,
-                            double* __restrict__ Rs, const int2* __restrict__ tile_rc, int ex)
+                            double* __restrict__ Rs, const int2* __restrict__ tile_rc, int ex,
+                            int64_t t0, int64_t t1)
 {
-    const int64_t total = d.ntiles * TILE_ELEMS;
+    const int64_t total = (t1 - t0) * TILE_ELEMS;
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
          g += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t t = g / TILE_ELEMS;
+        const int64_t t = t0 + g / TILE_ELEMS;
         int r, c;
-        tile_rc_of<T>((int)(g - t * TILE_ELEMS), r, c);
+        tile_rc_of<T>((int)(g % TILE_ELEMS), r, c);
         const int2 rc = tile_rc[t];
         const int i = rc.x * TILE + r, j = rc.y * TILE + c;
         double v = 0.0;
@@ -4813,7 +4868,7 @@ __global__ void pack_kernel(Dims d, const double* __restrict__ Pfull, T* __restr
 
 template <typename T>
 __global__ void unpack_kernel(Dims d, double* __restrict__ Pfull, const T* __restrict__ Pll,
-                              const double* __restrict__ Rs, int ex)
+                              const double* __restrict__ Rs, int ex, int64_t t0, int64_t t1)
 {
     const int64_t total = (int64_t)d.n * d.n;
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
@@ -4822,7 +4877,14 @@ __global__ void unpack_kernel(Dims d, double* __restrict__ Pfull, const T* __res
         double v;
         if (a < 3) v = Rs[(size_t)a * d.n + b];
         else if (b < 3) v = Rs[(size_t)b * d.n + a];
-        else v = from_domain<T>(from_store<T>(Pll[ll_offset<typename Stor<T>::L>(a - 3, b - 3, d.nb)]), ex);
+        else {
+            // the tiles of another rank read as 0
+            const int ba = (a - 3) >> 5, bb = (b - 3) >> 5;
+            const int64_t t = tile_index(ba < bb ? ba : bb, ba < bb ? bb : ba, d.nb);
+            v = (t >= t0 && t < t1)
+                    ? from_domain<T>(from_store<T>(Pll[ll_offset<typename Stor<T>::L>(a - 3, b - 3, d.nb) - t0 * TILE_ELEMS]), ex)
+                    : 0.0;
+        }
         Pfull[g] = v;
     }
 }
@@ -4830,14 +4892,15 @@ __global__ void unpack_kernel(Dims d, double* __restrict__ Pfull, const T* __res
 template <typename T>
 __global__ void lowrank_kernel(Dims d, const double* __restrict__ diag,
                                const double* __restrict__ U, int rank, T* __restrict__ Pll,
-                               double* __restrict__ Rs, const int2* __restrict__ tile_rc, int ex)
+                               double* __restrict__ Rs, const int2* __restrict__ tile_rc, int ex,
+                               int64_t t0, int64_t t1)
 {
-    const int64_t total = d.ntiles * TILE_ELEMS;
+    const int64_t total = (t1 - t0) * TILE_ELEMS;
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
          g += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t t = g / TILE_ELEMS;
+        const int64_t t = t0 + g / TILE_ELEMS;
         int r, c;
-        tile_rc_of<T>((int)(g - t * TILE_ELEMS), r, c);
+        tile_rc_of<T>((int)(g % TILE_ELEMS), r, c);
         const int2 rc = tile_rc[t];
         const int i = rc.x * TILE + r, j = rc.y * TILE + c;
         double v = 0.0;
@@ -4886,8 +4949,7 @@ size_t scan_lds_bytes(int precision)
 
 hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st)
 {
-    const int cnt = p.b - p.a;
-    const unsigned grid = (unsigned)((cnt + 255) / 256 > 0 ? (cnt + 255) / 256 : 1);
+    const unsigned grid = (unsigned)((p.d.N + 255) / 256);   // every landmark
     if (precision == EKF_PREC_F64) hipLaunchKernelGGL(shard_kernel<double>, dim3(grid), dim3(256), 0, st, p);
     else if (precision == EKF_PREC_F32) hipLaunchKernelGGL(shard_kernel<float>, dim3(grid), dim3(256), 0, st, p);
     else return hipErrorInvalidValue;
@@ -5051,50 +5113,54 @@ static int grid_for(int64_t work, int block)
 }
 
 hipError_t launch_pack(const Dims& d, int precision, const double* Pfull, void* Pll, double* Rs,
-                       const int2* tile_rc, int ex, hipStream_t st)
+                       const int2* tile_rc, int ex, hipStream_t st, int64_t t0, int64_t t1)
 {
-    const int grid = grid_for(d.ntiles * TILE_ELEMS, 256);
+    if (t1 < 0) t1 = d.ntiles;
+    const int grid = grid_for((t1 - t0) * TILE_ELEMS, 256);
     if (precision == EKF_PREC_F64)
         hipLaunchKernelGGL(pack_kernel<double>, dim3(grid), dim3(256), 0, st, d, Pfull,
-                           (double*)Pll, Rs, tile_rc, ex);
+                           (double*)Pll, Rs, tile_rc, ex, t0, t1);
     else if (precision == EKF_PREC_F16)
         hipLaunchKernelGGL(pack_kernel<_Float16>, dim3(grid), dim3(256), 0, st, d, Pfull,
-                           (_Float16*)Pll, Rs, tile_rc, ex);
+                           (_Float16*)Pll, Rs, tile_rc, ex, t0, t1);
     else
         hipLaunchKernelGGL(pack_kernel<float>, dim3(grid), dim3(256), 0, st, d, Pfull,
-                           (float*)Pll, Rs, tile_rc, ex);
+                           (float*)Pll, Rs, tile_rc, ex, t0, t1);
     return hipGetLastError();
 }
 
 hipError_t launch_unpack(const Dims& d, int precision, double* Pfull, const void* Pll,
-                         const double* Rs, int ex, hipStream_t st)
+                         const double* Rs, int ex, hipStream_t st, int64_t t0, int64_t t1)
 {
+    if (t1 < 0) t1 = d.ntiles;
     const int grid = grid_for((int64_t)d.n * d.n, 256);
     if (precision == EKF_PREC_F64)
         hipLaunchKernelGGL(unpack_kernel<double>, dim3(grid), dim3(256), 0, st, d, Pfull,
-                           (const double*)Pll, Rs, ex);
+                           (const double*)Pll, Rs, ex, t0, t1);
     else if (precision == EKF_PREC_F16)
         hipLaunchKernelGGL(unpack_kernel<_Float16>, dim3(grid), dim3(256), 0, st, d, Pfull,
-                           (const _Float16*)Pll, Rs, ex);
+                           (const _Float16*)Pll, Rs, ex, t0, t1);
     else
         hipLaunchKernelGGL(unpack_kernel<float>, dim3(grid), dim3(256), 0, st, d, Pfull,
-                           (const float*)Pll, Rs, ex);
+                           (const float*)Pll, Rs, ex, t0, t1);
     return hipGetLastError();
 }
 
 hipError_t launch_lowrank(const Dims& d, int precision, const double* diag, const double* U,
-                          int rank, void* Pll, double* Rs, const int2* tile_rc, int ex, hipStream_t st)
+                          int rank, void* Pll, double* Rs, const int2* tile_rc, int ex, hipStream_t st,
+                          int64_t t0, int64_t t1)
 {
-    const int grid = grid_for(d.ntiles * TILE_ELEMS, 256);
+    if (t1 < 0) t1 = d.ntiles;
+    const int grid = grid_for((t1 - t0) * TILE_ELEMS, 256);
     if (precision == EKF_PREC_F64)
         hipLaunchKernelGGL(lowrank_kernel<double>, dim3(grid), dim3(256), 0, st, d, diag, U,
-                           rank, (double*)Pll, Rs, tile_rc, ex);
+                           rank, (double*)Pll, Rs, tile_rc, ex, t0, t1);
     else if (precision == EKF_PREC_F16)
         hipLaunchKernelGGL(lowrank_kernel<_Float16>, dim3(grid), dim3(256), 0, st, d, diag, U,
-                           rank, (_Float16*)Pll, Rs, tile_rc, ex);
+                           rank, (_Float16*)Pll, Rs, tile_rc, ex, t0, t1);
     else
         hipLaunchKernelGGL(lowrank_kernel<float>, dim3(grid), dim3(256), 0, st, d, diag, U,
-                           rank, (float*)Pll, Rs, tile_rc, ex);
+                           rank, (float*)Pll, Rs, tile_rc, ex, t0, t1);
     return hipGetLastError();
 }
 

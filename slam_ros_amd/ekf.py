@@ -43,10 +43,8 @@ EXPORTED = [
     "ekf_landmark_block_bytes",
     "ekf_state_dim", "ekf_profile_enable", "ekf_profile_read", "ekf_profile_flushes",
     "ekf_flush_kernel_name", "ekf_debug_scan_stamps", "ekf_debug_result_words",
-    "ekf_shard_init", "ekf_shard_begin", "ekf_shard_gate", "ekf_shard_package_words", "ekf_shard_package",
-    "ekf_shard_apply", "ekf_shard_end", "ekf_shard_operand_bytes", "ekf_shard_operands", "ekf_shard_patch_bytes",
-    "ekf_shard_patch", "ekf_shard_commit",
-    "ekf_shard_status", "ekf_shard_abort",
+    "ekf_shard_create", "ekf_shard_tiles", "ekf_shard_buffer_words", "ekf_shard_begin", "ekf_shard_line",
+    "ekf_shard_apply", "ekf_shard_end", "ekf_shard_abort",
 ]
 
 
@@ -131,19 +129,13 @@ def load_library(path: str = ""):
         "ekf_flush_kernel_name": (ctypes.c_char_p, [vp, ctypes.c_int]),
         "ekf_debug_scan_stamps": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_ulonglong)]),
         "ekf_debug_result_words": (ctypes.c_int, [vp, ctypes.c_int, ip]),
-        "ekf_shard_init": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int]),
-        "ekf_shard_begin": (ctypes.c_int, [vp, dp, vp, ctypes.c_int]),
-        "ekf_shard_gate": (ctypes.c_int, [vp, ctypes.c_int, ip]),
-        "ekf_shard_package_words": (ctypes.c_int, [vp]),
-        "ekf_shard_package": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, dp]),
-        "ekf_shard_apply": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, dp]),
-        "ekf_shard_end": (ctypes.c_int, [vp]),
-        "ekf_shard_operand_bytes": (sz, [vp]),
-        "ekf_shard_operands": (ctypes.c_int, [vp, vp, vp, ctypes.c_int]),
-        "ekf_shard_patch_bytes": (sz, [vp]),
-        "ekf_shard_patch": (ctypes.c_int, [vp, dp, ctypes.c_int]),
-        "ekf_shard_commit": (ctypes.c_int, [vp]),
-        "ekf_shard_status": (ctypes.c_int, [vp, ip]),
+        "ekf_shard_create": (ctypes.c_int, [ctypes.POINTER(EkfConfig), ctypes.c_int, ctypes.c_int, cp]),
+        "ekf_shard_tiles": (ctypes.c_int, [vp, ip, ip]),
+        "ekf_shard_buffer_words": (sz, [vp]),
+        "ekf_shard_begin": (ctypes.c_int, [vp, dp, vp, ctypes.c_int, vp]),
+        "ekf_shard_line": (ctypes.c_int, [vp, ctypes.c_int, vp]),
+        "ekf_shard_apply": (ctypes.c_int, [vp, ctypes.c_int, vp]),
+        "ekf_shard_end": (ctypes.c_int, [vp, vp]),
         "ekf_shard_abort": (ctypes.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
@@ -194,7 +186,9 @@ class Ensemble:
                  max_lines: int = 20, device: int = -1, r_mode: int = R_INTENDED,
                  reset_margin: int = 10, mahalanobis: float = 0.4, encoder_noise: float = 0.024,
                  pipeline: bool = False, flush_interval: int = 1, arith: int = ARITH_EXACT,
-                 options: dict | None = None):
+                 options: dict | None = None, shard: tuple[int, int] | None = None):
+        """shard = (rank, world): a partitioned instance (slam_ekf.h ekf_shard_create; instances = 1)
+        storing its share of the landmark block only; rowshard_gpu.ShardedInstance drives it."""
         self._lib = load_library()
         cfg = EkfConfig()
         self._lib.ekf_config_init(ctypes.byref(cfg))
@@ -205,7 +199,11 @@ class Ensemble:
         cfg.flush_interval = int(flush_interval)
         cfg.arith = int(arith)
         h = ctypes.c_void_p()
-        _check(self._lib.ekf_create(ctypes.byref(cfg), ctypes.byref(h)), "ekf_create")
+        if shard is None:
+            _check(self._lib.ekf_create(ctypes.byref(cfg), ctypes.byref(h)), "ekf_create")
+        else:
+            _check(self._lib.ekf_shard_create(ctypes.byref(cfg), int(shard[0]), int(shard[1]), ctypes.byref(h)),
+                   "ekf_shard_create")
         self._h = h
         self.capacity, self.instances, self.precision = capacity, instances, precision
         self.max_lines = max_lines

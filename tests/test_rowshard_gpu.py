@@ -1,11 +1,10 @@
-"""One instance row-sharded across two ranks on the product kernels:
-two gloo ranks on the one GPU of the test box, each a context owning half of the landmarks
-(ekf_shard_*), against a single context of the same library on the same scans. Exact arithmetic:
-the owned rows of P (all columns), the robot block and strip columns of the owned landmarks, the
-owned entries of the mean, the pose and every association are bit-identical (the phases run the
-scan kernel's sequential-path expressions; the flush is the product wave kernel on the wave-tiles
-that hold an owned row block, with the all-gathered operand rows), augmentation and the capacity
-reset included."""
+"""One instance with its landmark block partitioned over two ranks on the product kernels
+(DESIGN.md §7): two gloo ranks on the one GPU of the test box, each a partitioned
+context (ekf_shard_create) storing its share of the packed tiles, against a single context of the
+same library on the same scans. Exact arithmetic: every association, the robot rows, the mean, the
+pose and savedLineCount on every rank, and the landmark block — the sum of the ranks' tiles — are
+bit-identical, augmentation and the capacity reset included; each rank stores at most 0.55 of the
+single context's landmark-block bytes. The per-scan wall time of the two-rank run is recorded."""
 import os
 import socket
 import subprocess
@@ -50,6 +49,7 @@ def test_two_rank_shard_equals_single_context(ekf_mod, tmp_path, prec, N, T, sca
         resets += r[0]["reset"]
         added += r[0]["new_landmarks"]
     P, y, saved, pose = one.download_state(0)
+    block_bytes = one.landmark_block_bytes()
     one.close()
     if extra_every:
         assert added > 0 or resets > 0
@@ -61,17 +61,23 @@ def test_two_rank_shard_equals_single_context(ekf_mod, tmp_path, prec, N, T, sca
            "--extra-every", str(extra_every)]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-3000:]
-    covered = 0
+    Psum = np.zeros_like(P)
+    rows = []
     for r in range(2):
         d = np.load(tmp_path / f"rank{r}.npz")
-        idx = d["rows"]
-        covered += len(idx)
         assert [list(m) for m in d["matches"]] == ref_matches, r
-        np.testing.assert_array_equal(d["P_rows"], P[idx])            # owned rows, every column
-        np.testing.assert_array_equal(d["P_robot"][:, :3], P[:3, :3])
-        np.testing.assert_array_equal(d["P_robot"][:, idx], P[:3, idx])
-        np.testing.assert_array_equal(d["y"][idx], y[idx])
-        np.testing.assert_array_equal(d["y"][:3], y[:3])
+        np.testing.assert_array_equal(d["P"][:3, :], P[:3, :])      # robot rows: replicated
+        np.testing.assert_array_equal(d["y"], y)
         np.testing.assert_array_equal(d["pose"], pose)
         assert int(d["saved"]) == saved
-    assert covered == 2 * N
+        Psum[3:, 3:] += d["P"][3:, 3:]                                 # the rank's tiles, zero elsewhere
+        rows.append(tuple(d["tile_rows"]))
+        # ≈1/2 of the packed block per rank; partition boundaries fall on even tile rows, coarse for
+        # a small block (N = 256: 16 tile rows)
+        assert int(d["block_bytes"]) <= (0.55 if N >= 1000 else 0.65) * block_bytes, (r, int(d["block_bytes"]), block_bytes)
+        times = d["times"]
+    np.testing.assert_array_equal(Psum[3:, 3:], P[3:, 3:])
+    assert rows[0][0] == 0 and rows[0][1] == rows[1][0] and rows[1][1] == (2 * N + 31) // 32
+    from tests.test_bench_config import record
+    record(f"rowshard_N{N}_T{T}_p{prec}", {"scan_ms_median": float(np.median(times)) * 1e3,
+                                            "tile_rows": rows, "block_bytes_single": block_bytes})
