@@ -3836,15 +3836,18 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
     const int lofs = lane * kh;
 
     // the pipelined loop needs every step of every instance this wave visits to be a plain
-    // downdate (no reset, no new rows)
-    bool fast = true;
+    // downdate (no reset, no new rows); the split-plane form also takes steps that add rows (it
+    // writes them into the wave-tiles they touch, between the steps' MFMAs)
+    bool fast = true, fast_rows = true;
     {
         const int e_lo = g0 / nwt, e_hi = (g_end - 1) / nwt;
         for (int e = e_lo; e <= e_hi; e++)
 #pragma unroll
             for (int q = 0; q < NS; q++) {
                 const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
-                fast = fast && !sload(r + RES_RESET) && sload(r + RES_NADD) == 0 && !sload(r + RES_ROLLBACK);
+                const bool ok = !sload(r + RES_RESET) && !sload(r + RES_ROLLBACK);
+                fast_rows = fast_rows && ok;
+                fast = fast && ok && sload(r + RES_NADD) == 0;
             }
     }
 
@@ -3887,10 +3890,10 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
     // every slot is stored, the invalid ones (outside the packed triangle) to the sink tile: no
     // branch around a store (a conditional store splits the wait-count tracking, and the join
     // then waits for every outstanding load, the next wave-tile's prefetch included)
-    auto store_tiles = [&](const Item& t, const f32x16 (&acc)[WT_N]) __attribute__((always_inline)) {
+    auto store_tiles = [&](const Item& t, const f32x16 (&acc)[WT_N], bool skip = false) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < WT_N; i++) {
-            TS* tl = ((t.w.valid >> i) & 1) ? Pout + tile_ptr(t, i) : sink;
+            TS* tl = ((t.w.valid >> i) & 1) && !skip ? Pout + tile_ptr(t, i) : sink;
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) tile_st(tl, lane, qq, acc[i]);
         }
@@ -3909,7 +3912,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
     };
 
     if constexpr (BF) {
-        if (fast) {
+        if (fast_rows) {
             // planes: BF16X6 hi, mid, lo bf16 (six products); F16X3 hi, lo fp16 of 2^σ·V (three)
             constexpr int NPL = F16 ? 2 : 3;
             typedef typename std::conditional<F16, f16x8r, bf16x8r>::type bf16x8;
@@ -3957,15 +3960,47 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
             // the accumulators hold −P: fp32 storage −X; fp16 storage −2^−x·X (X = fp16(2^x·P), the
             // instance's exponent; power-of-two scalings, exact), so that both operands are the
             // unscaled V planes; the store scales back and rounds to fp16 once per group. F16X3: the
-            // planes carry 2^σ·V (σ of the group's steps, all equal in a plain group), so the
-            // accumulators hold −2^(2σ)·P
+            // planes of step q carry 2^σ_q·V, so during step q the accumulators hold −2^(2σ_q)·P (σ
+            // changes only at a step that adds rows: the accumulators are rescaled after it)
+            // per instance of the wave-tiles (uniform, few registers): the landmarks the group's steps
+            // add [u_lo, u_hi), σ of the first and last step, the steps after which σ changes
+            auto rec_of = [&](int e, int q, int w) __attribute__((always_inline)) {
+                return sload(p.steps[q].res + (size_t)e * RES_STRIDE + w);
+            };
+            int st_e = -1, u_lo = 0, u_hi = 0, sg0 = 0, sgl = 0;
+            unsigned smask = 0;
+            auto load_steps = [&](int e) __attribute__((always_inline)) {
+                u_lo = 0x7fffffff;
+                u_hi = 0;
+                smask = 0;
+                int prev = 0;
+#pragma unroll
+                for (int q = 0; q < NS; q++) {
+                    const int na = rec_of(e, q, RES_NADD), s0 = rec_of(e, q, RES_SAVED_IN);
+                    if (na > 0) {
+                        u_lo = min(u_lo, s0);
+                        u_hi = max(u_hi, s0 + na);
+                    }
+                    const int sg = F16 ? rec_of(e, q, RES_PSIG) : 0;
+                    if (q == 0) sg0 = sg;
+                    else if (sg != prev) smask |= 1u << (q - 1);
+                    prev = sg;
+                }
+                sgl = prev;
+                st_e = e;
+            };
             auto in_scale = [&](const Item& t) __attribute__((always_inline)) {
-                int ex = 0;
+                int ex = 2 * sg0;
                 if constexpr (HALF) ex -= sload(p.pexp + t.e);
-                if constexpr (F16) ex += 2 * sload(p.steps[0].res + (size_t)t.e * RES_STRIDE + RES_PSIG);
                 return -ldexpf(1.0f, ex);
             };
+            auto skip_of = [&](const Item& t) __attribute__((always_inline)) {
+                if (t.e != st_e) load_steps(t.e);
+                const int ra = (t.w.rc & 0xffff) * WT_R * 16, ca = (t.w.rc >> 16) * WT_C * 16;   // landmarks
+                return smask != 0 || (u_lo < ra + WT_R * 16 && u_hi > ra) || (u_lo < ca + WT_C * 16 && u_hi > ca);
+            };
             Item cur, nxt, nxt2;
+            bool any_skip = false;
             first_item(cur);
             next_item(cur, nxt);
             load_tiles(cur);
@@ -3988,6 +4023,11 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
                 const bool more = g + K < g_end;
                 next_item(nxt, nxt2);
                 const Item ldi = more ? nxt : cur;   // the last wave-tile re-reads its own rows
+                // a wave-tile holding a landmark some step of the group added, or of an instance whose
+                // σ changes inside the group, is computed here but stored to the sink: the second pass
+                // (below) runs it through the general loop
+                const bool skip = skip_of(cur);
+                any_skip |= skip;
                 const float isc = in_scale(cur);
 #pragma unroll
                 for (int i = 0; i < WT_N; i++)
@@ -4057,7 +4097,8 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
 #ifdef EKF_XP_FLUSH_STAMPS
                 const unsigned long long xt2 = __builtin_amdgcn_s_memtime();
 #endif
-                const float osc = 1.0f / isc;   // (−1, or −2^x: exact)
+                // back from the last step's domain (−1, −2^x, −2^(x − 2σ): exact)
+                const float osc = F16 ? 1.0f / (isc * ldexpf(1.0f, 2 * (sgl - sg0))) : 1.0f / isc;
 #pragma unroll
                 for (int i = 0; i < WT_N; i++)
 #pragma unroll
@@ -4065,7 +4106,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
 #ifdef EKF_XP_BF_NO_TILES
                 if (acc[0][0] == 1234.5f && acc[3][15] == -1234.5f)   // (never true: keeps the MFMAs live)
 #endif
-                store_tiles(cur, acc);
+                store_tiles(cur, acc, skip);
 #ifdef EKF_XP_FLUSH_STAMPS
                 __builtin_amdgcn_sched_barrier(0);
                 const unsigned long long xt3 = __builtin_amdgcn_s_memtime();
@@ -4084,6 +4125,21 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
                 atomicAdd(p.dbg + 29, __builtin_amdgcn_s_memrealtime() - xr0);
             }
 #endif
+            // second pass: the skipped wave-tiles through the general loop (their input tiles are
+            // as read: the first pass stored them to the sink). Exact arithmetic on the fp32 operand
+            // rows there, the split arithmetic elsewhere: both within the fp32 bar (slam_ekf.h)
+            if (any_skip) {
+                Item t;
+                first_item(t);
+                for (int gg = g0; gg < g_end; gg += K) {
+                    if (gg != g0) {
+                        Item nn;
+                        next_item(t, nn);
+                        t = nn;
+                    }
+                    if (skip_of(t)) wt_general<TS, NS>(p, t.e, t.w, lane);
+                }
+            }
             return;
         }
     } else if (fast) {
