@@ -38,11 +38,11 @@ def counters(path):
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
 
 
-def main(tag):
+def main(tag, out=None):
     import bench
     from slam_ros_amd import ekf
     src = os.path.join(ROOT, "gpurun_out", tag)
-    out = os.path.join(ROOT, "profiles", tag)
+    out = out or os.path.join(ROOT, "profiles", tag)
     os.makedirs(out, exist_ok=True)
     shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(out, "kernel_stats.csv"))
     shutil.copy(os.path.join(src, "bench.json"), os.path.join(out, "bench.json"))
@@ -81,7 +81,8 @@ def main(tag):
           "traffic_over_alg": hbm / b["roofline"]["alg_bytes_per_launch"],
           "sq": {k: v for k, v in c.items() if k.startswith("SQ_") or k.startswith("GRBM")},
           "l2": {k: v for k, v in c.items() if k.startswith("TCC_HIT") or k.startswith("TCC_MISS")},
-          "lib_sha": bench.lib_sha(ekf.LIB_PATH), "source": f"profiles/{tag}/counters_avg_per_dispatch.json"}
+          "lib_sha": bench.lib_sha(ekf.LIB_PATH), "source": f"profiles/{tag}/counters_avg_per_dispatch.json",
+          "arith": cfg.get("arith")}
     json.dump(tj, open(os.path.join(out, "traffic.json"), "w"), indent=1)
     print(json.dumps({k: tj[k] for k in ("kernel", "hbm_bytes_per_launch", "traffic_over_alg")}))
     sq = tj["sq"]
@@ -91,4 +92,4 @@ def main(tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)

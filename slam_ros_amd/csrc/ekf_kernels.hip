@@ -3808,8 +3808,11 @@ __device__ __forceinline__ void wt_general(const DowndateParams& p, int e, const
 #ifndef EKF_BF_WAVES
 #define EKF_BF_WAVES 1   // split-bf16 flush: waves per SIMD (2: ≤ 256 registers, ring depth 2; measured equal)
 #endif
+#ifndef EKF_F16_WAVES
+#define EKF_F16_WAVES 1  // split-fp16 flush: waves per SIMD (2: ≤ 256 registers, ring depth 2)
+#endif
 template <typename TS, int NS, bool BF = false, bool F16 = false>
-__global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_wave_kernel(DowndateParams p)
+__global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVES) : 1) void flush_f32_wave_kernel(DowndateParams p)
 {
     static_assert(NS >= 2 && NS % 2 == 0 && NS <= PMAX, "even step count");
     static_assert(BF || NS <= 8, "fp32 wave flush: at most 8 steps (operands of every step in registers)");
@@ -3916,7 +3919,8 @@ __global__ __launch_bounds__(DD_THREADS, BF ? EKF_BF_WAVES : 1) void flush_f32_w
             // planes: BF16X6 hi, mid, lo bf16 (six products); F16X3 hi, lo fp16 of 2^σ·V (three)
             constexpr int NPL = F16 ? 2 : 3;
             typedef typename std::conditional<F16, f16x8r, bf16x8r>::type bf16x8;
-            constexpr int RD = EKF_BF_WAVES > 1 ? 2 : (NS % 4 == 0 ? 4 : (NS % 3 == 0 ? 3 : 2));   // operand ring depth
+            constexpr int WAVES = F16 ? EKF_F16_WAVES : EKF_BF_WAVES;
+            constexpr int RD = WAVES > 1 ? 2 : (NS % 4 == 0 ? 4 : (NS % 3 == 0 ? 3 : 2));   // operand ring depth
             const size_t pstride = (size_t)d.nb * NPL * 64;   // 16-byte operands per instance
             // step q's planes: slot (slot0 + q) mod nslots
             auto pl_base = [&](int q) __attribute__((always_inline)) {
@@ -5083,7 +5087,7 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
         return hipGetLastError();
     }
     if (p.bf == 2 && bf_shape) {   // EKF_ARITH_F16X3: split-fp16 wave flush, groups of 2-16 steps (even)
-        const unsigned wgrid = (unsigned)(8 * EKF_BF_WAVES * ((p.ncu + 7) / 8));
+        const unsigned wgrid = (unsigned)(8 * EKF_F16_WAVES * ((p.ncu + 7) / 8));
 #define EKF_F16_CASE(NSV)                                                                               \
     case NSV:                                                                                           \
         if (half) hipExtLaunchKernelGGL((flush_f32_wave_kernel<_Float16, NSV, true, true>), dim3(wgrid),  \
