@@ -3,8 +3,8 @@ and how often the speculative path falls back, at the bench configuration (N = 4
 split-bf16 flush, T = 12):
 
   spec1   the default: speculative association, bench world (SURVEY §8d parameters tuned, scan_gen)
-  spec0   EKF_SPECULATE=0: the sequential chain (one cross-workgroup exchange per line) every scan
-  spec2   EKF_SPECULATE=2: every guess deliberately wrong — the full speculative path, its verdict
+  spec0   speculate option 0: the sequential chain (one cross-workgroup exchange per line) every scan
+  spec2   speculate option 2: every guess deliberately wrong — the full speculative path, its verdict
           fails, then the sequential restart (the worst case a wrong guess can cost)
   survey  SURVEY §8d literally (scan_gen profile "survey"), speculative
   surveyR the same with §8d's gate-margin rejection: a scan is redrawn while some candidate that

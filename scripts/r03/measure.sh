@@ -1,5 +1,5 @@
 # Bench lines of record for DESIGN §5 (one box): fp16 / fp64 / N=1024 / N=256, the association's
-# bad cases (EKF_SPECULATE=0 and 2) and SURVEY §8d's world, then scripts/assoc_cases.py.
+# bad cases (speculate option 0 and 2) and SURVEY §8d's world, then scripts/assoc_cases.py.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${TAG:-r03_measure}
