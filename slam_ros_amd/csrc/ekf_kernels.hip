@@ -927,21 +927,31 @@ __device__ __forceinline__ void gain_rows(const double* pk, int t, UQ uq_of, VQ 
                                           double2& rr0, double2& rr1, double2& rr2, double2& yb,
                                           double Dj[4], double kk[4], double uu[4])
 {
-    auto correct = [&](int q) {   // earlier matches of this scan, in order
-        const double4 uq = uq_of(q);
-        const double4 vh = vq_of(q);
-        blk[0] -= uq.x * vh.x + uq.y * vh.y;
-        blk[1] -= uq.x * vh.z + uq.y * vh.w;
-        blk[2] -= uq.z * vh.x + uq.w * vh.y;
-        blk[3] -= uq.z * vh.z + uq.w * vh.w;
+    // earlier matches of this scan, in order: four independent fused chains (one per entry), the
+    // rows of match q + 1 loaded before match q's products (LDS latency off the chain). t is the
+    // scan's match count, the same on every lane: a scalar loop
+    auto correct = [&](const double4& uq, const double4& vh) __attribute__((always_inline)) {
+        blk[0] = fma(-uq.x, vh.x, blk[0]);
+        blk[1] = fma(-uq.x, vh.z, blk[1]);
+        blk[2] = fma(-uq.z, vh.x, blk[2]);
+        blk[3] = fma(-uq.z, vh.z, blk[3]);
+        blk[0] = fma(-uq.y, vh.y, blk[0]);
+        blk[1] = fma(-uq.y, vh.w, blk[1]);
+        blk[2] = fma(-uq.w, vh.y, blk[2]);
+        blk[3] = fma(-uq.w, vh.w, blk[3]);
     };
-    if constexpr (MAXQ > 0) {
-#pragma unroll
-        for (int q = 0; q < MAXQ; q++)
-            if (q < t) correct(q);
-    } else {
-        for (int q = 0; q < t; q++) correct(q);
+    // Matches in pairs (both pairs' rows loaded together: one LDS round trip per two matches),
+    // then the odd one; the products in q order either way
+    const int tu = __builtin_amdgcn_readfirstlane(MAXQ > 0 ? min(t, MAXQ) : t);
+    int q = 0;
+#pragma unroll 1
+    for (; q + 1 < tu; q += 2) {
+        const double4 ua = uq_of(q), va = vq_of(q);
+        const double4 ub = uq_of(q + 1), vb = vq_of(q + 1);
+        correct(ua, va);
+        correct(ub, vb);
     }
+    if (q < tu) correct(uq_of(q), vq_of(q));
     const double S0 = pk[MB_S], S1 = pk[MB_S + 1], S2 = pk[MB_S + 2], S3 = pk[MB_S + 3];
     const double Si0 = pk[MB_SI], Si1 = pk[MB_SI + 1], Si2 = pk[MB_SI + 2], Si3 = pk[MB_SI + 3];
     const double v0 = pk[MB_V], v1 = pk[MB_V + 1];
@@ -2239,7 +2249,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     const ekf_line ln = sh_lines[i];
                     double Rm[4];
                     line_R(ln, i, r_mode, Rm);
-                    const int w = sh_spec[i];
+                    const int w = __builtin_amdgcn_readfirstlane(sh_spec[i]);   // uniform: scalar branches, m scalar
                     int deep = 0;   // diagnostics: 1 past the quick filter, 2 past the fp32 one, 3 past the fp64 one
                     // the gate of line i on the state before it (the guessed winner itself, j == w, is
                     // evaluated exactly by the replay wave, which flags a failed gate (sh_flag) and its
@@ -2271,7 +2281,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                                 pll_block(pv, 2 * j, 2 * w, blk);   // fp64 operands: read in the loop
                             }
                             double kk[4], uu[4];
-                            gain_rows<SPEC_L>(pk, m, uq_owned, [&](int q) { return sh_wh[i][q][1]; }, blk, rr0, rr1,
+                            gain_rows<SPEC_L>(pk, m, [&](int q) { return sh_uhist[q][tid]; },   // m < SPEC_L = HIST_LDS
+                                              [&](int q) { return sh_wh[i][q][1]; }, blk, rr0, rr1,
                                               rr2, yb, Dj, kk, uu);
                             const float F[3] = {(float)pk[PK_F], (float)pk[PK_F + 1], (float)pk[PK_F + 2]};
                             store_rows(m, kk, uu, false, F);
