@@ -47,7 +47,7 @@ def main(tag, out=None):
     shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(out, "kernel_stats.csv"))
     shutil.copy(os.path.join(src, "bench.json"), os.path.join(out, "bench.json"))
     ctr = {}
-    for sub in ("fetch", "write", "sq", "l2"):
+    for sub in ("fetch", "write", "sq", "l2", "insts"):
         for k, v in counters(os.path.join(src, sub, "run_counter_collection.csv")).items():
             ctr.setdefault(k, {}).update(v)
     json.dump(ctr, open(os.path.join(out, "counters_avg_per_dispatch.json"), "w"), indent=1)
@@ -85,6 +85,23 @@ def main(tag, out=None):
           "arith": cfg.get("arith")}
     json.dump(tj, open(os.path.join(out, "traffic.json"), "w"), indent=1)
     print(json.dumps({k: tj[k] for k in ("kernel", "hbm_bytes_per_launch", "traffic_over_alg")}))
+    # instructions per wave of the association kernel (SQ_INSTS_* / SQ_WAVES per dispatch) and per
+    # line (÷ the scan's L lines): the chain's instruction count
+    scan = [k for k in ctr if "scan_kernel" in k and "SQ_WAVES" in ctr[k]]
+    if scan:
+        L = cfg.get("lines_per_scan", 8)
+        ins = {}
+        for k in scan:
+            c2 = ctr[k]
+            w = max(c2["SQ_WAVES"], 1.0)
+            per = {n[len("SQ_INSTS_"):].lower(): c2[n] / w for n in c2 if n.startswith("SQ_INSTS_")}
+            per["total"] = sum(per.get(x, 0) for x in ("valu", "salu", "lds", "smem", "vmem", "branch"))
+            per["total_per_line"] = per["total"] / L
+            ins[k] = {"waves_per_dispatch": c2["SQ_WAVES"], "per_wave": per}
+        json.dump(ins, open(os.path.join(out, "scan_instructions.json"), "w"), indent=1)
+        for k, v in ins.items():
+            print("scan instructions per wave", k[:60], round(v["per_wave"]["total"]), "per line",
+                  round(v["per_wave"]["total_per_line"]))
     sq = tj["sq"]
     if sq.get("SQ_WAVE_CYCLES"):
         print("SQ_WAIT_ANY/WAVE", sq.get("SQ_WAIT_ANY", 0) / sq["SQ_WAVE_CYCLES"],
