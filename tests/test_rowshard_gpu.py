@@ -31,6 +31,18 @@ def free_port():
 def test_two_rank_shard_equals_single_context(ekf_mod, tmp_path, prec, N, T, scans, active, extra_every):
     """(active, extra_every): every extra_every-th scan carries two unmatched lines — augmented
     landmarks landing on either rank, and (active = N − 10) the capacity reset."""
+    run_sharded(ekf_mod, tmp_path, prec, N, T, scans, active, extra_every, world=2, backend="gloo")
+
+
+@pytest.mark.parametrize("prec,N,T,scans,active,extra_every", [(1, 1024, 4, 9, 1000, 3), (0, 512, 4, 6, 0, 0)])
+def test_rccl_device_sum_world1(ekf_mod, tmp_path, prec, N, T, scans, active, extra_every):
+    """The nccl (RCCL) backend's path: the exchange buffer all-reduced in place on the device, on
+    the context's stream, with no host staging. One GPU holds one RCCL rank, so this runs a world of
+    one (the partition is the whole block); the two-rank protocol itself is covered over gloo."""
+    run_sharded(ekf_mod, tmp_path, prec, N, T, scans, active, extra_every, world=1, backend="nccl")
+
+
+def run_sharded(ekf_mod, tmp_path, prec, N, T, scans, active, extra_every, world, backend):
     w = G.make_world(N, active=active or N - 10)
     st = G.initial_state(w)
     one = ekf_mod.Ensemble(N, 1, prec, max_lines=8, flush_interval=T)
@@ -54,16 +66,16 @@ def test_two_rank_shard_equals_single_context(ekf_mod, tmp_path, prec, N, T, sca
     if extra_every:
         assert added > 0 or resets > 0
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "tests", "rowshard_gpu_worker.py"), "--out", str(tmp_path), "--N", str(N),
            "--T", str(T), "--scans", str(scans), "--precision", str(prec), "--active", str(active),
-           "--extra-every", str(extra_every)]
+           "--extra-every", str(extra_every), "--backend", backend]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-3000:]
     Psum = np.zeros_like(P)
     rows = []
-    for r in range(2):
+    for r in range(world):
         d = np.load(tmp_path / f"rank{r}.npz")
         assert [list(m) for m in d["matches"]] == ref_matches, r
         np.testing.assert_array_equal(d["P"][:3, :], P[:3, :])      # robot rows: replicated
@@ -74,10 +86,12 @@ def test_two_rank_shard_equals_single_context(ekf_mod, tmp_path, prec, N, T, sca
         rows.append(tuple(d["tile_rows"]))
         # ≈1/2 of the packed block per rank; partition boundaries fall on even tile rows, coarse for
         # a small block (N = 256: 16 tile rows)
-        assert int(d["block_bytes"]) <= (0.55 if N >= 1000 else 0.65) * block_bytes, (r, int(d["block_bytes"]), block_bytes)
+        if world == 2:
+            assert int(d["block_bytes"]) <= (0.55 if N >= 1000 else 0.65) * block_bytes, (r, int(d["block_bytes"]), block_bytes)
         times = d["times"]
     np.testing.assert_array_equal(Psum[3:, 3:], P[3:, 3:])
-    assert rows[0][0] == 0 and rows[0][1] == rows[1][0] and rows[1][1] == (2 * N + 31) // 32
+    assert rows[0][0] == 0 and rows[-1][1] == (2 * N + 31) // 32
+    assert all(rows[r][1] == rows[r + 1][0] for r in range(world - 1))
     from tests.test_bench_config import record
-    record(f"rowshard_N{N}_T{T}_p{prec}", {"scan_ms_median": float(np.median(times)) * 1e3,
+    record(f"rowshard_{backend}{world}_N{N}_T{T}_p{prec}", {"scan_ms_median": float(np.median(times)) * 1e3,
                                             "tile_rows": rows, "block_bytes_single": block_bytes})
