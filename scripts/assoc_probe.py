@@ -1,6 +1,6 @@
 """Association-kernel phase timers (EKF_OPT_SCAN_STAMPS = 1; thread 0 of workgroup 0 of each instance,
 s_memrealtime, 100 MHz), µs per launch averaged over instances, at the bench's shapes
-(f32, E = 8, L = m = 8; the bench's split-bf16 arithmetic, PROBE_ARITH=exact for the exact one).
+(f32, E = 8, L = m = 8; split-bf16 arithmetic, PROBE_ARITH=exact / f16x3 for the others).
 usage: python scripts/assoc_probe.py [N:T ...]"""
 import json
 import os
@@ -20,7 +20,7 @@ for c in cfgs:
     N, T = (int(x) for x in c.split(":"))
     w = G.make_world(N)
     st = G.initial_state(w)
-    arith = ekf.ARITH_EXACT if os.environ.get("PROBE_ARITH") == "exact" else ekf.ARITH_BF16X6
+    arith = {"exact": ekf.ARITH_EXACT, "f16x3": ekf.ARITH_F16X3}.get(os.environ.get("PROBE_ARITH"), ekf.ARITH_BF16X6)
     ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8, flush_interval=T, arith=arith,
                        options={"scan_stamps": 1})
     for e in range(E):
