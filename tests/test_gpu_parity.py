@@ -738,9 +738,10 @@ def test_singular_status_counts_only_evaluated_candidates(ekf_mod, oracle_mod, m
 def test_bf16_2x4_flush_equals_2x2(ekf_mod, monkeypatch, prec, N, T, extra_every):
     """The split-bf16 flush on 2 × 4 wave-tiles (flush_bf24_kernel, EKF_OPT_FLUSH_FORM = 24) and on 2 × 2
     wave-tiles (flush_f32_wave_kernel<.., true>, default) run the same MFMA sequence per element
-    (same part products in the same order, bf16 MFMA deterministic): bit-identical state, fast
-    groups and groups with augmented rows (general path on the two 2 × 2 halves) alike, fp32 and
-    fp16 storage, block sizes that are not multiples of the wave-tile."""
+    (same part products in the same order, bf16 MFMA deterministic): bit-identical state for plain
+    groups, fp32 and fp16 storage, block sizes that are not multiples of the wave-tile. Groups with
+    augmented rows: the 2 × 4 form runs every wave-tile on the general loop, the 2 × 2 form only
+    those the new rows touch, so the two agree to the storage bar there."""
     E = 3
     active = N - 12 - 2 * ((3 * T + 1) // extra_every) if extra_every else N - 10
     w = G.make_world(N, active=active)
@@ -766,4 +767,9 @@ def test_bf16_2x4_flush_equals_2x2(ekf_mod, monkeypatch, prec, N, T, extra_every
     for e in range(E):
         Pa, ya, sa, pa = a.download_state(e)
         Pb, yb, sb, pb = b.download_state(e)
-        assert np.array_equal(Pa, Pb) and np.array_equal(ya, yb) and sa == sb, e
+        assert sa == sb, e
+        if extra_every:
+            assert rel(Pa, Pb) <= (1e-6 if prec == 1 else 1e-3), (e, rel(Pa, Pb))
+            assert rel(ya, yb) <= 1e-10, (e, rel(ya, yb))
+        else:
+            assert np.array_equal(Pa, Pb) and np.array_equal(ya, yb), e

@@ -94,4 +94,5 @@ def run_sharded(ekf_mod, tmp_path, prec, N, T, scans, active, extra_every, world
     assert all(rows[r][1] == rows[r + 1][0] for r in range(world - 1))
     from tests.test_bench_config import record
     record(f"rowshard_{backend}{world}_N{N}_T{T}_p{prec}", {"scan_ms_median": float(np.median(times)) * 1e3,
-                                            "tile_rows": rows, "block_bytes_single": block_bytes})
+                                            "tile_rows": [[int(a), int(b)] for a, b in rows],
+                                            "block_bytes_single": int(block_bytes)})
