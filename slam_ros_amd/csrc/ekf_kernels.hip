@@ -1078,7 +1078,10 @@ constexpr int SPEC_WD = 14 + 4 * (SPEC_L - 1);      // winner record: rr, Dj, y,
 // speculative package: the words of build_package, then the robot 3×3 block and x_pre after the
 // line's update (robot_update), computed once by the replay wave for every landmark wave
 constexpr int PK_R33 = MB_VH, PK_XP = MB_VH + 9, PK_F = MB_VH + 12;   // + the symmetric factor (sym_factor)
-constexpr int PKW = MB_VH + 15;                     // package words (speculative lines; V rows in sh_wh)
+// 1.0 if the guessed winner passed its exact gate; 0.0: it failed, the line is unmatched unless
+// another landmark passes (which the landmark waves flag), and the other words are not written
+constexpr int PK_OK = MB_VH + 15;
+constexpr int PKW = MB_VH + 16;                     // package words (speculative lines; V rows in sh_wh)
 
 // Blocks (j, cols[t]) for t < SPEC_L and (j, j) (last; only if `diag`) of the landmark block
 // with the pending steps applied, fp32 operands, every pending step with ks <= 8: the guessed
@@ -1770,7 +1773,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
 
     bool matched = false;
     int m = 0, nextra = 0, status = 0, tstatus = 0;
-    int dpath = 0;   // diagnostic: 1 fast guess, 2 collision-resolved guess, 4 unresolved, 8 verdict failed
+    int dpath = 0;   // diagnostic: 1 fast guess, 2 collision-resolved guess, 4 unresolved, 8 verdict failed,
+                     // 32 a guessed winner failed its exact gate and its line stayed unmatched (16: sequential)
     int par0 = 0;   // mailbox parity of line 0 on the sequential path
     bool sequential = true;
 
@@ -2076,7 +2080,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     wma0 = r[10];
                     sincos(wma0, &ws0, &wc0);   // sincos_near's scan-start values (as the owner's)
                 }
-                int ml = 0, bad = 0;
+                int ml = 0;
                 const bool lst = pdbg && g == 0 && u == 0;
                 unsigned long long tl = lst ? __builtin_amdgcn_s_memrealtime() : 0ull;
                 // lane u evaluates line u: its line in registers, and the lines with a winner as a
@@ -2087,19 +2091,26 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 for (int t = 0; t < L; t++) {
                     if (!((wmask >> t) & 1ull)) continue;
                     double* pk = sh_pk[t];
+                    int okl = 1;
+                    Cand c;
                     if (u == t) {
                         const ekf_line ln = lnu;
                         double Rm[4];
                         line_R(ln, t, r_mode, Rm);
                         Block5 b5;
                         fill_block5(b5, R33l, w0, w1, w2, wD);
-                        Cand c;
                         double sn, cs;
                         sincos_near(wy.x, wma0, ws0, wc0, sn, cs);
                         eval_candidate(b5, wy.x, wy.y, sn, cs, xpl, ln.alpha, ln.r, Rm, p.gate, c);
-                        bad |= c.pass ? 0 : 1;
                         // GSL_EDOM of the winner (the reference evaluated it: Robot.cpp:454)
                         if (c.singular) atomicOr(&sh_rwst, (int)EKF_ST_SINGULAR);
+                        okl = c.pass ? 1 : 0;
+                        pk[PK_OK] = okl ? 1.0 : 0.0;
+                    }
+                    // the guessed winner failed its exact gate: no update from this line (the
+                    // landmark waves check that no other landmark passes it)
+                    const int ok = __builtin_amdgcn_readlane(okl, t);
+                    if (ok && u == t) {
                         // the package in registers, the robot block after the line from it (for
                         // every lane and every landmark wave), then all of it to LDS
                         double pkl[PKW];
@@ -2124,6 +2135,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     __builtin_amdgcn_wave_barrier();
                     if (u == 0) __hip_atomic_store(&sh_ready, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if (!ok) continue;   // (ml counts matches: unchanged)
                     if (u != t) {   // (lane t has them)
 #pragma unroll
                         for (int a = 0; a < 9; a++) R33l[a] = pk[PK_R33 + a];
@@ -2142,9 +2154,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     ml++;
                     if (lst) { const unsigned long long t2 = __builtin_amdgcn_s_memrealtime(); sh_stamp[4] += t2 - tl; tl = t2; }
                 }
-                bad = __any(bad) ? 1 : 0;
                 if (u == 0) {
-                    sh_flag = bad;
+                    sh_flag = 0;   // (a failed guessed winner is settled per line by the landmark waves)
                     if (pdbg && g == 0) {
                         const unsigned long long te = __builtin_amdgcn_s_memrealtime();
                         sh_stamp[13] += te - t_l0;
@@ -2252,8 +2263,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     const int w = __builtin_amdgcn_readfirstlane(sh_spec[i]);   // uniform: scalar branches, m scalar
                     int deep = 0;   // diagnostics: 1 past the quick filter, 2 past the fp32 one, 3 past the fp64 one
                     // the gate of line i on the state before it (the guessed winner itself, j == w, is
-                    // evaluated exactly by the replay wave, which flags a failed gate (sh_flag) and its
-                    // GSL_EDOM (sh_rwst)). Its first filter runs in one block with the line's gain rows,
+                    // evaluated exactly by the replay wave, which reports the result in the package
+                    // (PK_OK) and its GSL_EDOM in sh_rwst; a failed winner leaves the line unmatched
+                    // unless another landmark passes, which flags a violation). Its first filter runs in one block with the line's gain rows,
                     // which do not depend on it: two independent chains for the scheduler to interleave
                     const bool cand = own && j < s && !matched && j != w;
                     Block5 b5;
@@ -2262,6 +2274,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     const double xpg[3] = {xp[0], xp[1], xp[2]};
                     bool deeper = false;
                     const double* pk = nullptr;
+                    bool wok = true;   // the guessed winner passed its exact gate (PK_OK)
                     if (w >= 0) {
                         int polls = 0;
                         while (__hip_atomic_load(&sh_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= i) {
@@ -2270,9 +2283,12 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         }
                         sub(17);
                         pk = sh_pk[i];
-                        if (r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
+                        wok = __builtin_amdgcn_readfirstlane(pk[PK_OK] != 0.0 ? 1 : 0) != 0;
+                        if (r_mode == 1 && (i == 1 || i == 2) && wok) status |= EKF_ST_NSYM;
                         if (own) {
                             deeper = cand && !quick_reject(b5, ybx, yby, ma0, s0f, c0f, xpg, ln.alpha, ln.r, Rm, p.gate);
+                        }
+                        if (own && wok) {
                             double blk[4];
                             if constexpr (sizeof(typename Stor<T>::C) == 4) {
                                 const float4 bk = sh_blk[i][tid];
@@ -2303,11 +2319,12 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                             eval_candidate(b5, ybx, yby, sn, cs, xpg, ln.alpha, ln.r, Rm, p.gate, c);
                             // GSL_EDOM counts only for candidates the reference evaluates: the
                             // unmatched ones up to the winner (Robot.cpp:313-498 stops there)
-                            if (c.singular && (w < 0 || j <= w)) status |= EKF_ST_SINGULAR;
+                            if (c.singular && (w < 0 || !wok || j <= w)) status |= EKF_ST_SINGULAR;
                             pass = c.pass;
                         }
-                        // the guess must be the first passing unmatched landmark
-                        if (pass && (w < 0 || j < w)) viol = 1;
+                        // the guess must be the first passing unmatched landmark; a guessed
+                        // winner that failed leaves the line unmatched only if none passes
+                        if (pass && (w < 0 || !wok || j < w)) viol = 1;
                     }
                     if (pdbg && g == 0) {   // waves of workgroup 0 whose lanes went deeper
                         const bool d1 = __any(deep >= 1), d2 = __any(deep >= 2), d3 = __any(deep >= 3);
@@ -2319,8 +2336,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         }
                     }
                     sub(16);
-                    if (w < 0) {
+                    if (w < 0 || !wok) {
                         // no match: the line goes to extraLines (Robot.cpp:308-310, 492-496)
+                        if (w >= 0) dpath |= 32;   // diagnostics: a guessed winner failed, line unmatched
                         if (lead) {
                             res[RES_MATCH + i] = -1;
                             res[RES_EXTRA + nextra] = i;
