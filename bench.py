@@ -12,11 +12,12 @@ pre-roll (--preroll steps of the same workload, default 200 ≈ 30 ms, reported 
 `clock_preroll_steps`) lets the GPU reach the clocks it holds under this load: a step is ≈0.12 ms,
 so a few warm-up steps alone measure the clock ramp (≈12 % lower with 8 warm-up steps).
 
-Schedule (defaults): the landmark block is flushed once per T = 12 scans (flush_interval), in
-place, between association kernels (--pipeline 1 overlaps them instead), by the split-bf16 flush
-(--arith bf16x6, slam_ekf.h EKF_ARITH_BF16X6: fp32 operands split exactly into three bf16
-parts, six bf16 MFMAs per product, fp32 accumulation; held to the fp32 parity bar,
-tests/test_bench_config.py). With --arith exact (fp32 MFMA, T = 8) every schedule is
+Schedule (defaults): the landmark block is flushed once per T = 16 scans (flush_interval), in
+place, between association kernels (--pipeline 1 overlaps them instead), by the split-fp16 flush
+(--arith f16x3, slam_ekf.h EKF_ARITH_F16X3: fp32 operands scaled by 2^σ and split into hi + lo
+fp16 parts, three fp16 MFMAs per product, fp32 accumulation; held to the fp32 parity bar,
+tests/test_bench_config.py; --arith bf16x6 is the exact three-part bf16 split, six products).
+With --arith exact (fp32 MFMA, T = 8) every schedule is
 bit-identical to a per-scan in-place update (tests/test_gpu_parity.py::
 test_deferred_flush_equals_drained). The timed region ends with ekf_sync, which flushes the
 partial group: every step's downdate is in P. HIP events in the timed region bracket the flush
@@ -79,8 +80,8 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=0,
                     help="1: overlap the association kernels with the previous group's flush")
     ap.add_argument("--flush-interval", type=int, default=0,
-                    help="T: rewrite the landmark block once per T scans (0: 12 for f32 with the "
-                         "split-bf16 flush, 8 for f32 exact and f16, 4 for f64)")
+                    help="T: rewrite the landmark block once per T scans (0: 16 with a split "
+                         "arithmetic, 8 exact, 4 for f64)")
     ap.add_argument("--bcast-every", type=int, default=0,
                     help="scans per broadcast (default: the flush interval); broadcasts run one "
                          "group ahead of the scans that use them")
@@ -88,10 +89,11 @@ def parse():
                     help="nccl (= RCCL on ROCm); gloo only to rehearse ranks on one GPU")
     ap.add_argument("--preroll", type=int, default=200,
                     help="untimed clock pre-roll steps before the warm-up (steady GPU clocks)")
-    ap.add_argument("--arith", choices=["exact", "bf16x6", "f16x3"], default="bf16x6",
+    ap.add_argument("--arith", choices=["exact", "bf16x6", "f16x3"], default="f16x3",
                     help="fp32 flush arithmetic (slam_ekf.h EKF_ARITH_*): exact = fp32 MFMA, the state "
                          "bit-identical for every T; bf16x6 = fp32 operands split exactly into three "
-                         "bf16 parts, six bf16 MFMAs per product (f32 storage only)")
+                         "bf16 parts, six bf16 MFMAs per product; f16x3 = hi + lo fp16 of 2^σ·V, "
+                         "three fp16 MFMAs per product")
     ap.add_argument("--dump-state", default="",
                     help="directory: after all steps each rank writes its instances' final state "
                          "(state_<global instance>.npz: P, y, saved, pose) for multi-rank checks")
@@ -265,7 +267,7 @@ def main():
     if prec == ekf.PREC_F64:
         arith = ekf.ARITH_EXACT   # the split-bf16 flush serves fp32 operands (fp32 and fp16 storage)
     if args.flush_interval <= 0:
-        args.flush_interval = 4 if prec == ekf.PREC_F64 else (8 if arith == ekf.ARITH_EXACT else 12)
+        args.flush_interval = 4 if prec == ekf.PREC_F64 else (8 if arith == ekf.ARITH_EXACT else 16)
     ens = ekf.Ensemble(N, E, prec, max_lines=L_LINES, device=local, pipeline=bool(args.pipeline),
                       flush_interval=args.flush_interval, arith=arith,
                       options={"speculate": args.speculate})

@@ -1463,12 +1463,15 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     constexpr bool kPlanes = sizeof(typename Stor<T>::C) == 4;
     __shared__ __attribute__((aligned(16))) float sh_vpl[kPlanes ? SCAN_THREADS * 32 : 4];
     // plane arithmetic (HOT fixes it at compile time): EKF_ARITH_F16X3 planes hold hi + lo fp16 of
-    // 2^σ·V, σ = psig[e] for every step since the last augmentation (the lead changes it only at a
-    // step that adds landmarks, after this launch's planes are written with the old value), so
-    // the MFMA replay of plain pending steps returns 2^(2σ)·ΔX
+    // 2^σ·V. σ follows the largest landmark variance vmax (pvmax[e]) but changes only at the first
+    // scan of a flush group (every workgroup of the instance computes it from pvmax), so that a
+    // group's steps share one σ and the flush takes its pipelined path; mid-group only a reset
+    // (σ empty) or a new landmark 64× above the variance σ was set for (then at the step that adds
+    // it: that group and every pending replay over it take the exact forms). The MFMA replay of
+    // plain pending steps returns 2^(2σ)·ΔX.
     const bool pf16 = kPlanes && (HOT == 2 || (HOT == 0 && p.bf == 2));
     const int npl = pf16 ? 2 : 3;
-    const int psig = pf16 ? p.psig[e] : 0;
+    const int psig = !pf16 ? 0 : p.npend == 0 ? plane_sigma(p.pvmax[e]) : p.psig[e];
     const double rsc = pf16 ? ldexp(1.0, -2 * psig) : 1.0;
     // phase timers only in the ST instantiation (EKF_SCAN_STAMPS=1): the product kernel carries
     // no timer code at all (its uniform branches and registers cost ≈2 µs per scan)
@@ -2749,15 +2752,18 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             p.saved[e] = reset ? 0 : s + nadd;
             p.live[e] = 1 - cb;
             if (pf16) {
-                // the plane exponent of the later steps: |V_ik| <= sqrt(P_ii) <= sqrt(vmax) while no
-                // landmark is added, so σ changes only here, at a step whose group and pending
-                // replays take the exact forms (it adds rows, or resets the map)
+                // the plane exponent of the later steps: |V_ik| <= sqrt(P_ii) <= sqrt(vmax), and
+                // |2^σ·V| <= 2^12 at σ = plane_sigma(vmax). A larger vmax waits for the next group
+                // (the first scan of a group recomputes σ) while |2^σ·V| stays <= 2^15 (fp16's
+                // range is 2^16): σ at most 3 above plane_sigma(vmax)
                 if (reset) {
                     p.pvmax[e] = 0.0;
                     p.psig[e] = PLANE_SIGMA_EMPTY;
-                } else if (vnew > p.pvmax[e]) {
-                    p.pvmax[e] = vnew;
-                    p.psig[e] = plane_sigma(vnew);
+                } else {
+                    const double vm = fmax(p.pvmax[e], vnew);
+                    const int target = plane_sigma(vm);
+                    p.pvmax[e] = vm;
+                    p.psig[e] = target < psig - 3 ? target : psig;
                 }
             }
         } else {
@@ -3877,9 +3883,9 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
 #pragma unroll
             for (int q = 0; q < NS; q++) {
                 const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
-                const bool ok = !sload(r + RES_RESET) && !sload(r + RES_ROLLBACK);
-                fast_rows = fast_rows && ok;
-                fast = fast && ok && sload(r + RES_NADD) == 0;
+                const bool rb = sload(r + RES_ROLLBACK), rs = sload(r + RES_RESET);
+                fast_rows = fast_rows && !rb;
+                fast = fast && !rb && !rs && sload(r + RES_NADD) == 0;
             }
     }
 
@@ -4000,15 +4006,28 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
             auto rec_of = [&](int e, int q, int w) __attribute__((always_inline)) {
                 return sload(p.steps[q].res + (size_t)e * RES_STRIDE + w);
             };
+            // A step that resets the map (Robot.cpp:893-904) zeroes the block: only the landmarks
+            // added after the instance's last reset of the group are nonzero at its end, so the
+            // union is taken over those steps and every other wave-tile of the instance is stored
+            // as zero (rz); σ changes before that reset do not matter.
             int st_e = -1, u_lo = 0, u_hi = 0, sg0 = 0, sgl = 0;
             unsigned smask = 0;
+            bool rz = false;
             auto load_steps = [&](int e) __attribute__((always_inline)) {
                 u_lo = 0x7fffffff;
                 u_hi = 0;
                 smask = 0;
+                rz = false;
                 int prev = 0;
 #pragma unroll
                 for (int q = 0; q < NS; q++) {
+                    if (rec_of(e, q, RES_RESET)) {   // (its own new rows are wiped with the map)
+                        u_lo = 0x7fffffff;
+                        u_hi = 0;
+                        smask = 0;
+                        rz = true;
+                        continue;
+                    }
                     const int na = rec_of(e, q, RES_NADD), s0 = rec_of(e, q, RES_SAVED_IN);
                     if (na > 0) {
                         u_lo = min(u_lo, s0);
@@ -4027,10 +4046,18 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                 if constexpr (HALF) ex -= sload(p.pexp + t.e);
                 return -ldexpf(1.0f, ex);
             };
-            auto skip_of = [&](const Item& t) __attribute__((always_inline)) {
+            auto touched = [&](const Item& t) __attribute__((always_inline)) {
                 if (t.e != st_e) load_steps(t.e);
                 const int ra = (t.w.rc & 0xffff) * WT_R * 16, ca = (t.w.rc >> 16) * WT_C * 16;   // landmarks
-                return smask != 0 || (u_lo < ra + WT_R * 16 && u_hi > ra) || (u_lo < ca + WT_C * 16 && u_hi > ca);
+                return (u_lo < ra + WT_R * 16 && u_hi > ra) || (u_lo < ca + WT_C * 16 && u_hi > ca);
+            };
+            auto skip_of = [&](const Item& t) __attribute__((always_inline)) {
+                const bool tc = touched(t);
+                return tc || (!rz && smask != 0);
+            };
+            auto zero_of = [&](const Item& t) __attribute__((always_inline)) {
+                const bool tc = touched(t);
+                return rz && !tc;
             };
             Item cur, nxt, nxt2;
             bool any_skip = false;
@@ -4060,6 +4087,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                 // σ changes inside the group, is computed here but stored to the sink: the second pass
                 // (below) runs it through the general loop
                 const bool skip = skip_of(cur);
+                const bool zero = zero_of(cur);   // (reset instance, untouched: stored as zero)
                 any_skip |= skip;
                 const float isc = in_scale(cur);
 #pragma unroll
@@ -4135,7 +4163,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
 #pragma unroll
                 for (int i = 0; i < WT_N; i++)
 #pragma unroll
-                    for (int k = 0; k < 16; k++) acc[i][k] = acc[i][k] * osc;
+                    for (int k = 0; k < 16; k++) acc[i][k] = zero ? 0.0f : acc[i][k] * osc;
 #ifdef EKF_XP_BF_NO_TILES
                 if (acc[0][0] == 1234.5f && acc[3][15] == -1234.5f)   // (never true: keeps the MFMAs live)
 #endif

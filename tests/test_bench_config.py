@@ -161,14 +161,16 @@ def test_bench_config_fp32_t12_bf16x6(ekf_mod, oracle_mod, n_cap):
     record(f"f32_T12_N{n_cap}_E8_bf16x6", out)
 
 
-@pytest.mark.parametrize("n_cap,prec", [(256, 1), (1024, 1), (4096, 1), (4096, 2)])
-def test_bench_config_t12_f16x3(ekf_mod, oracle_mod, n_cap, prec):
+@pytest.mark.parametrize("n_cap,prec,T", [(256, 1, 16), (1024, 1, 16), (4096, 1, 16), (4096, 1, 12), (4096, 2, 16),
+                                          (1024, 1, 12)])
+def test_bench_config_f16x3(ekf_mod, oracle_mod, n_cap, prec, T):
     """EKF_ARITH_F16X3 (operands split into hi + lo fp16 of 2^σ·V, three fp16 MFMA products, the
-    MFMA replay on the same planes) at T = 12, E = 8 over 20 scans with no intermediate drains:
-    the fp32 bar (1e-6 on P, 1e-8 on y; fp16 storage its re-stated 1e-3) against the restatement,
-    association identical."""
-    out = run_config(ekf_mod, oracle_mod, prec, 12, 20, arith=ekf_mod.ARITH_F16X3, N=n_cap)
-    record(f"{'f32' if prec == 1 else 'f16'}_T12_N{n_cap}_E8_f16x3", out)
+    MFMA replay on the same planes) at the bench's T = 16 (and 12), E = 8 over 20 scans with no
+    intermediate drains (a group of T, then the rest flushed by ekf_sync): the fp32 bar (1e-6 on P,
+    1e-8 on y; fp16 storage its re-stated 1e-3) per group against the re-synced restatement, the
+    trajectory to k times it, association identical."""
+    out = run_config(ekf_mod, oracle_mod, prec, T, 20, arith=ekf_mod.ARITH_F16X3, N=n_cap)
+    record(f"{'f32' if prec == 1 else 'f16'}_T{T}_N{n_cap}_E8_f16x3", out)
 
 
 def test_bench_config_fp32_t16_bf16x6(ekf_mod, oracle_mod):
