@@ -117,7 +117,8 @@ typedef struct ekf_config {
     int32_t flush_interval;/* T >= 1: the landmark block is rewritten once per T scans by one
                               rank-2·Σm MFMA pass; scans in between read it with the pending
                               downdates applied on read. Bit-identical state for every T (the
-                              MFMA chain is an ordered FMA chain); T = 1: once per scan. <= 16 */
+                              MFMA chain is an ordered FMA chain); T = 1: once per scan. <= 16
+                              (<= 24 with EKF_ARITH_F16X3) */
     int32_t arith;         /* EKF_ARITH_* (fp32 flush arithmetic); formerly reserved, 0 = EXACT */
     double mahalanobis;    /* MAHALANOBIS gate, Robot.h:15 (0.4) */
     double encoder_noise;  /* ENCODERNOISE, Robot.h:17 (0.024) */

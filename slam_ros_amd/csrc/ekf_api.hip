@@ -362,7 +362,8 @@ static int create_ctx(const ekf_config* cfg, int sh_rank, int sh_world, ekf_ctx*
         (cfg->precision != EKF_PREC_F64 && cfg->precision != EKF_PREC_F32 &&
          cfg->precision != EKF_PREC_F16) ||
         (cfg->r_mode != EKF_R_INTENDED && cfg->r_mode != EKF_R_AS_WRITTEN) ||
-        cfg->flush_interval < 0 || cfg->flush_interval > 16 ||
+        cfg->flush_interval < 0 ||
+        cfg->flush_interval > (cfg->arith == EKF_ARITH_F16X3 ? ekf::F16X3_MAXS : 16) ||
         (cfg->arith != EKF_ARITH_EXACT && cfg->arith != EKF_ARITH_BF16X6 && cfg->arith != EKF_ARITH_F16X3) ||
         // the split-plane flushes need symmetric fp32 operands with kmax = 16 (slam_ekf.h)
         (cfg->arith != EKF_ARITH_EXACT &&
@@ -1636,17 +1637,19 @@ extern "C" const char* ekf_flush_kernel_name(const ekf_ctx* c, int nsteps)
         return "downdate_f64_kernel";
     }
     const bool half = c->cfg.precision == EKF_PREC_F16;
-    if (c->pmode == EKF_ARITH_F16X3 && nsteps >= 2 && nsteps <= 16 && nsteps % 2 == 0) {
-        static const char* f16n[2][9] = {
-            {"", "flush_f32_wave_kernel<float, 2, true, true>", "flush_f32_wave_kernel<float, 4, true, true>",
-             "flush_f32_wave_kernel<float, 6, true, true>", "flush_f32_wave_kernel<float, 8, true, true>",
-             "flush_f32_wave_kernel<float, 10, true, true>", "flush_f32_wave_kernel<float, 12, true, true>",
-             "flush_f32_wave_kernel<float, 14, true, true>", "flush_f32_wave_kernel<float, 16, true, true>"},
-            {"", "flush_f32_wave_kernel<_Float16, 2, true, true>", "flush_f32_wave_kernel<_Float16, 4, true, true>",
-             "flush_f32_wave_kernel<_Float16, 6, true, true>", "flush_f32_wave_kernel<_Float16, 8, true, true>",
-             "flush_f32_wave_kernel<_Float16, 10, true, true>", "flush_f32_wave_kernel<_Float16, 12, true, true>",
-             "flush_f32_wave_kernel<_Float16, 14, true, true>", "flush_f32_wave_kernel<_Float16, 16, true, true>"}};
-        return f16n[half ? 1 : 0][nsteps / 2];
+    if (c->pmode == EKF_ARITH_F16X3 && nsteps >= 2 && nsteps <= ekf::F16X3_MAXS && nsteps % 2 == 0) {
+        struct Names {
+            char n[2][ekf::F16X3_MAXS / 2 + 1][64];
+            Names()
+            {
+                for (int h = 0; h < 2; h++)
+                    for (int k = 0; k <= ekf::F16X3_MAXS / 2; k++)
+                        snprintf(n[h][k], sizeof n[h][k], "flush_f32_wave_kernel<%s, %d, true, true>",
+                                 h ? "_Float16" : "float", 2 * k);
+            }
+        };
+        static const Names f16n;   // (initialised once, thread-safe)
+        return f16n.n[half ? 1 : 0][nsteps / 2];
     }
     if (c->bf && nsteps >= 2 && nsteps <= 16 && nsteps % 2 == 0 && c->dd_variant == 24) {
         static const char* b24[2][9] = {

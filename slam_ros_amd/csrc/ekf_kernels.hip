@@ -1673,15 +1673,18 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // come from Dd (the last committed step's, exact); fp32 storage
     bool mf = false;
     unsigned amask = 0;   // pending steps with a downdate (ks > 0)
-    if (spec_ok && sym && sizeof(typename Stor<T>::C) == 4 && p.npend <= SPEC_QMAX && d.kmax / 2 >= 8) {
+    // (the MFMA replay reads the planes, not the LDS stage: any number of pending steps)
+    if (spec_ok && sym && sizeof(typename Stor<T>::C) == 4 && d.kmax / 2 >= 8) {
         __syncthreads();   // sh_ctl
-        staged = true;
-        for (int q = 0; q < p.npend; q++) staged &= sh_ctl[q].y <= 8;
-        mf = staged && p.mfrep && kPlanes;
+        bool st = true;
+        for (int q = 0; q < p.npend; q++) st &= sh_ctl[q].y <= 8;
+        bool m = st && p.mfrep && kPlanes;
         for (int q = 0; q < p.npend; q++) {
-            mf &= !sh_ctl[q].x && sh_ctl[q].z == 0;
+            m &= !sh_ctl[q].x && sh_ctl[q].z == 0;
             if (sh_ctl[q].y > 0) amask |= 1u << q;
         }
+        staged = st && (p.npend <= SPEC_QMAX || m);
+        mf = m && staged;
     }
     double Dj[4] = {0, 0, 0, 0};   // owned diagonal block
     if (own && j < s) {
@@ -5117,7 +5120,7 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     const bool wave_shape = p.nsteps >= 2 && p.nsteps <= 8 && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
                             p.nwt > 0 && p.wt != nullptr;
     const bool wave_ok = wave_shape && (p.nsteps >= 6 || p.variant == 8);
-    const bool bf_shape = p.nsteps >= 2 && p.nsteps <= 16 && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
+    const bool bf_shape = p.nsteps >= 2 && p.nsteps <= (p.bf == 2 ? F16X3_MAXS : 16) && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
                           p.nwt > 0 && p.wt != nullptr;
     if (p.bf == 1 && bf_shape && p.variant == 24 && p.nwt24 > 0 && p.wt24 != nullptr) {
         // EKF_ARITH_BF16X6, EKF_FLUSH_VARIANT=24: the 2 × 4 split-bf16 wave flush (measured 7 %
@@ -5143,7 +5146,7 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
 #undef EKF_BF24_CASE
         return hipGetLastError();
     }
-    if (p.bf == 2 && bf_shape) {   // EKF_ARITH_F16X3: split-fp16 wave flush, groups of 2-16 steps (even)
+    if (p.bf == 2 && bf_shape) {   // EKF_ARITH_F16X3: split-fp16 wave flush, groups of 2-24 steps (even)
         const unsigned wgrid = (unsigned)(8 * EKF_F16_WAVES * ((p.ncu + 7) / 8));
 #define EKF_F16_CASE(NSV)                                                                               \
     case NSV:                                                                                           \
@@ -5161,6 +5164,10 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
             EKF_F16_CASE(12)
             EKF_F16_CASE(14)
             EKF_F16_CASE(16)
+            EKF_F16_CASE(18)
+            EKF_F16_CASE(20)
+            EKF_F16_CASE(22)
+            EKF_F16_CASE(24)
         }
 #undef EKF_F16_CASE
         return hipGetLastError();

@@ -162,10 +162,10 @@ def test_bench_config_fp32_t12_bf16x6(ekf_mod, oracle_mod, n_cap):
 
 
 @pytest.mark.parametrize("n_cap,prec,T", [(256, 1, 16), (1024, 1, 16), (4096, 1, 16), (4096, 1, 12), (4096, 2, 16),
-                                          (1024, 1, 12)])
+                                          (1024, 1, 12), (4096, 1, 20), (4096, 1, 24), (1024, 1, 24)])
 def test_bench_config_f16x3(ekf_mod, oracle_mod, n_cap, prec, T):
     """EKF_ARITH_F16X3 (operands split into hi + lo fp16 of 2^σ·V, three fp16 MFMA products, the
-    MFMA replay on the same planes) at the bench's T = 16 (and 12), E = 8 over 20 scans with no
+    MFMA replay on the same planes) at T = 12 to 24, E = 8 over 20 scans with no
     intermediate drains (a group of T, then the rest flushed by ekf_sync): the fp32 bar (1e-6 on P,
     1e-8 on y; fp16 storage its re-stated 1e-3) per group against the re-synced restatement, the
     trajectory to k times it, association identical."""
