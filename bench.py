@@ -12,7 +12,7 @@ pre-roll (--preroll steps of the same workload, default 200 ≈ 30 ms, reported 
 `clock_preroll_steps`) lets the GPU reach the clocks it holds under this load: a step is ≈0.12 ms,
 so a few warm-up steps alone measure the clock ramp (≈12 % lower with 8 warm-up steps).
 
-Schedule (defaults): the landmark block is flushed once per T = 16 scans (flush_interval), in
+Schedule (defaults): the landmark block is flushed once per T = 20 scans (flush_interval), in
 place, between association kernels (--pipeline 1 overlaps them instead), by the split-fp16 flush
 (--arith f16x3, slam_ekf.h EKF_ARITH_F16X3: fp32 operands scaled by 2^σ and split into hi + lo
 fp16 parts, three fp16 MFMAs per product, fp32 accumulation; held to the fp32 parity bar,
@@ -80,8 +80,8 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=0,
                     help="1: overlap the association kernels with the previous group's flush")
     ap.add_argument("--flush-interval", type=int, default=0,
-                    help="T: rewrite the landmark block once per T scans (0: 16 with a split "
-                         "arithmetic, 8 exact, 4 for f64)")
+                    help="T: rewrite the landmark block once per T scans (0: 20 with f16x3, 12 "
+                         "with bf16x6, 8 exact, 4 for f64)")
     ap.add_argument("--bcast-every", type=int, default=0,
                     help="scans per broadcast (default: the flush interval); broadcasts run one "
                          "group ahead of the scans that use them")
@@ -267,7 +267,7 @@ def main():
     if prec == ekf.PREC_F64:
         arith = ekf.ARITH_EXACT   # the split-bf16 flush serves fp32 operands (fp32 and fp16 storage)
     if args.flush_interval <= 0:
-        args.flush_interval = 4 if prec == ekf.PREC_F64 else (8 if arith == ekf.ARITH_EXACT else 16)
+        args.flush_interval = 4 if prec == ekf.PREC_F64 else (8 if arith == ekf.ARITH_EXACT else (20 if arith == ekf.ARITH_F16X3 else 12))
     ens = ekf.Ensemble(N, E, prec, max_lines=L_LINES, device=local, pipeline=bool(args.pipeline),
                       flush_interval=args.flush_interval, arith=arith,
                       options={"speculate": args.speculate})
