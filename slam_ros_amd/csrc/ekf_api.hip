@@ -1639,17 +1639,19 @@ extern "C" const char* ekf_flush_kernel_name(const ekf_ctx* c, int nsteps)
     const bool half = c->cfg.precision == EKF_PREC_F16;
     if (c->pmode == EKF_ARITH_F16X3 && nsteps >= 2 && nsteps <= ekf::F16X3_MAXS && nsteps % 2 == 0) {
         struct Names {
-            char n[2][ekf::F16X3_MAXS / 2 + 1][64];
+            char n[2][2][ekf::F16X3_MAXS / 2 + 1][64];
             Names()
             {
-                for (int h = 0; h < 2; h++)
-                    for (int k = 0; k <= ekf::F16X3_MAXS / 2; k++)
-                        snprintf(n[h][k], sizeof n[h][k], "flush_f32_wave_kernel<%s, %d, true, true>",
-                                 h ? "_Float16" : "float", 2 * k);
+                for (int f = 0; f < 2; f++)
+                    for (int h = 0; h < 2; h++)
+                        for (int k = 0; k <= ekf::F16X3_MAXS / 2; k++)
+                            snprintf(n[f][h][k], sizeof n[f][h][k],
+                                     f ? "flush_bf24_kernel<%s, %d, true>" : "flush_f32_wave_kernel<%s, %d, true, true>",
+                                     h ? "_Float16" : "float", 2 * k);
             }
         };
         static const Names f16n;   // (initialised once, thread-safe)
-        return f16n.n[half ? 1 : 0][nsteps / 2];
+        return f16n.n[c->dd_variant == 24 ? 1 : 0][half ? 1 : 0][nsteps / 2];
     }
     if (c->bf && nsteps >= 2 && nsteps <= 16 && nsteps % 2 == 0 && c->dd_variant == 24) {
         static const char* b24[2][9] = {

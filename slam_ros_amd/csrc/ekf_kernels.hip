@@ -4427,14 +4427,19 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
 // ahead, operand ring one step ahead across wave-tile boundaries, −P in the accumulators (fp16:
 // scaled out of the storage exponent), invalid slots stored to the sink. Groups in which some
 // instance of the wave resets or adds rows run wt_general on the two 2 × 2 halves.
+// F16 (EKF_ARITH_F16X3, EKF_OPT_FLUSH_FORM = 24): two fp16 planes of 2^σ·V, three products; the
+// 2 × 2 form then streams 8 KB of planes per wave and step for 12 MFMAs, which at the four waves'
+// MFMA rate is more than a CU's 64 B per clock: 2 × 4 streams 12 KB for 24. Groups whose σ
+// changes run the general halves too.
 constexpr int W4_R = 2, W4_C = 4, W4_N = W4_R * W4_C;
-template <typename TS, int NS>
+template <typename TS, int NS, bool F16 = false>
 __global__ __launch_bounds__(DD_THREADS, 1) void flush_bf24_kernel(DowndateParams p)
 {
     static_assert(NS >= 2 && NS % 2 == 0 && NS <= PMAX, "even step count");
     constexpr bool HALF = sizeof(TS) == 2;
-    constexpr int RD = 2;   // operand ring depth (divides NS)
-    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    constexpr int NPL = F16 ? 2 : 3;
+    constexpr int RD = (F16 && NS % 4 == 0) ? 4 : 2;   // operand ring depth (divides NS)
+    typedef typename std::conditional<F16, f16x8r, bf16x8r>::type bf16x8;
     using Raw = typename std::conditional<HALF, f16x4, f32x4>::type;
     const Dims d = p.d;
     const int nwt = p.nwt24;
@@ -4461,6 +4466,7 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_bf24_kernel(DowndateParam
             for (int q = 0; q < NS; q++) {
                 const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
                 fast = fast && !sload(r + RES_RESET) && sload(r + RES_NADD) == 0 && !sload(r + RES_ROLLBACK);
+                if (F16) fast = fast && sload(r + RES_PSIG) == sload(p.steps[0].res + (size_t)e * RES_STRIDE + RES_PSIG);
             }
     }
     struct Item {
@@ -4518,7 +4524,7 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_bf24_kernel(DowndateParam
         return;
     }
 
-    const size_t pstride = (size_t)nb * 3 * 64;   // bf16x8 per instance
+    const size_t pstride = (size_t)nb * NPL * 64;   // 16-byte operands per instance
     auto pl_base = [&](int q) __attribute__((always_inline)) {
         int sl = p.slot0 + q;
         if (sl >= p.nslots) sl -= p.nslots;
@@ -4526,14 +4532,14 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_bf24_kernel(DowndateParam
     };
     Raw pref[W4_N][4];
     f32x16 acc[W4_N];
-    bf16x8 R[RD][W4_R + W4_C][3];
+    bf16x8 R[RD][W4_R + W4_C][NPL];
     auto load_ops = [&](int r, const Item& t, int q) __attribute__((always_inline)) {
         const bf16x8* b = pl_base(q) + t.e * pstride + lane;
 #pragma unroll
         for (int i = 0; i < W4_R + W4_C; i++) {
-            const bf16x8* rb = b + (size_t)(i < W4_R ? op_rowA(t, i) : op_rowB(t, i - W4_R)) * 3 * 64;
+            const bf16x8* rb = b + (size_t)(i < W4_R ? op_rowA(t, i) : op_rowB(t, i - W4_R)) * NPL * 64;
 #pragma unroll
-            for (int pl = 0; pl < 3; pl++) R[r][i][pl] = rb[pl * 64];
+            for (int pl = 0; pl < NPL; pl++) R[r][i][pl] = rb[pl * 64];
         }
     };
     auto load_tiles = [&](const Item& t) __attribute__((always_inline)) {
@@ -4545,9 +4551,12 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_bf24_kernel(DowndateParam
             for (int qq = 0; qq < 4; qq++) pref[i][qq] = __builtin_nontemporal_load(tl + lane + qq * 64);
         }
     };
+    // −P in the accumulators, scaled: fp16 storage out of its exponent x, F16 by 2^(2σ) (the
+    // group's one σ): −2^(2σ − x)
     auto in_scale = [&](const Item& t) __attribute__((always_inline)) {
-        if constexpr (HALF) return -ldexpf(1.0f, -sload(p.pexp + t.e));
-        else return -1.0f;
+        int ex = F16 ? 2 * sload(p.steps[0].res + (size_t)t.e * RES_STRIDE + RES_PSIG) : 0;
+        if constexpr (HALF) ex -= sload(p.pexp + t.e);
+        return -ldexpf(1.0f, ex);
     };
     Item cur, nxt, nxt2;
     load_item(g0 / nwt, g0 - (g0 / nwt) * nwt, cur);
@@ -4575,26 +4584,45 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_bf24_kernel(DowndateParam
             if (ql < NS) load_ops(ql % RD, cur, ql);
             else load_ops(ql % RD, ldi, ql - NS);
             const int r = q % RD;
-            // part products smallest first: (mid, mid), (hi, lo), (lo, hi), (hi, mid), (mid, hi), (hi, hi)
+            if constexpr (F16) {
+                // (lo, hi), (hi, lo), (hi, hi): 24 MFMAs beside the 12 plane loads
 #pragma unroll
-            for (int pp = 0; pp < 6; pp++) {
-                const int pa = (0x102010 >> (4 * (5 - pp))) & 0xf;
-                const int pb = (0x120100 >> (4 * (5 - pp))) & 0xf;
+                for (int pp = 0; pp < 3; pp++) {
+                    const int pa = pp == 0 ? 1 : 0, pb = pp == 1 ? 1 : 0;
 #pragma unroll
-                for (int rr = 0; rr < W4_R; rr++)
+                    for (int rr = 0; rr < W4_R; rr++)
 #pragma unroll
-                    for (int c = 0; c < W4_C; c++)
-                        acc[rr * W4_C + c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                            R[r][rr][pa], R[r][W4_R + c][pb], acc[rr * W4_C + c], 0, 0, 0);
-            }
+                        for (int c = 0; c < W4_C; c++)
+                            acc[rr * W4_C + c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+                                R[r][rr][pa], R[r][W4_R + c][pb], acc[rr * W4_C + c], 0, 0, 0);
+                }
 #pragma unroll
-            for (int i = 0; i < 6; i++) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);   // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);   // VMEM read
+                for (int i = 0; i < 12; i++) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // VMEM read
+                }
+            } else {
+                // part products smallest first: (mid, mid), (hi, lo), (lo, hi), (hi, mid), (mid, hi), (hi, hi)
+#pragma unroll
+                for (int pp = 0; pp < 6; pp++) {
+                    const int pa = (0x102010 >> (4 * (5 - pp))) & 0xf;
+                    const int pb = (0x120100 >> (4 * (5 - pp))) & 0xf;
+#pragma unroll
+                    for (int rr = 0; rr < W4_R; rr++)
+#pragma unroll
+                        for (int c = 0; c < W4_C; c++)
+                            acc[rr * W4_C + c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                R[r][rr][pa], R[r][W4_R + c][pb], acc[rr * W4_C + c], 0, 0, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < 6; i++) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);   // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);   // VMEM read
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        const float osc = 1.0f / isc;   // (−1, or −2^x: exact)
+        const float osc = 1.0f / isc;   // (a power of two: exact)
 #pragma unroll
         for (int i = 0; i < W4_N; i++) {
             bool v;
@@ -5144,6 +5172,33 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
             EKF_BF24_CASE(16)
         }
 #undef EKF_BF24_CASE
+        return hipGetLastError();
+    }
+    if (p.bf == 2 && bf_shape && p.variant == 24 && p.nwt24 > 0 && p.wt24 != nullptr) {
+        // EKF_ARITH_F16X3, EKF_OPT_FLUSH_FORM = 24: the 2 × 4 split-fp16 flush
+        const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));
+#define EKF_F24_CASE(NSV)                                                                               \
+    case NSV:                                                                                           \
+        if (half) hipExtLaunchKernelGGL((flush_bf24_kernel<_Float16, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, st, \
+                                        ev_a, ev_b, 0, p);                                               \
+        else hipExtLaunchKernelGGL((flush_bf24_kernel<float, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, \
+                                   ev_b, 0, p);                                                          \
+        break;
+        switch (p.nsteps) {
+            EKF_F24_CASE(2)
+            EKF_F24_CASE(4)
+            EKF_F24_CASE(6)
+            EKF_F24_CASE(8)
+            EKF_F24_CASE(10)
+            EKF_F24_CASE(12)
+            EKF_F24_CASE(14)
+            EKF_F24_CASE(16)
+            EKF_F24_CASE(18)
+            EKF_F24_CASE(20)
+            EKF_F24_CASE(22)
+            EKF_F24_CASE(24)
+        }
+#undef EKF_F24_CASE
         return hipGetLastError();
     }
     if (p.bf == 2 && bf_shape) {   // EKF_ARITH_F16X3: split-fp16 wave flush, groups of 2-24 steps (even)

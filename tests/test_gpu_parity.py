@@ -734,10 +734,12 @@ def test_singular_status_counts_only_evaluated_candidates(ekf_mod, oracle_mod, m
         ens.close()
 
 
-@pytest.mark.parametrize("prec,N,T,extra_every", [(1, 1024, 12, 0), (1, 200, 8, 3), (2, 512, 10, 0), (1, 100, 16, 0)])
-def test_bf16_2x4_flush_equals_2x2(ekf_mod, monkeypatch, prec, N, T, extra_every):
-    """The split-bf16 flush on 2 × 4 wave-tiles (flush_bf24_kernel, EKF_OPT_FLUSH_FORM = 24) and on 2 × 2
-    wave-tiles (flush_f32_wave_kernel<.., true>, default) run the same MFMA sequence per element
+@pytest.mark.parametrize("arith", [1, 2])
+@pytest.mark.parametrize("prec,N,T,extra_every", [(1, 1024, 12, 0), (1, 200, 8, 3), (2, 512, 10, 0), (1, 100, 16, 0),
+                                                  (1, 1024, 20, 0)])
+def test_bf16_2x4_flush_equals_2x2(ekf_mod, monkeypatch, prec, N, T, extra_every, arith):
+    """The split-bf16 / split-fp16 flush on 2 × 4 wave-tiles (flush_bf24_kernel, EKF_OPT_FLUSH_FORM = 24)
+    and on 2 × 2 wave-tiles (flush_f32_wave_kernel<.., true>, default) run the same MFMA sequence per element
     (same part products in the same order, bf16 MFMA deterministic): bit-identical state for plain
     groups, fp32 and fp16 storage, block sizes that are not multiples of the wave-tile. Groups with
     augmented rows: the 2 × 4 form runs every wave-tile on the general loop, the 2 × 2 form only
@@ -746,11 +748,13 @@ def test_bf16_2x4_flush_equals_2x2(ekf_mod, monkeypatch, prec, N, T, extra_every
     active = N - 12 - 2 * ((3 * T + 1) // extra_every) if extra_every else N - 10
     w = G.make_world(N, active=active)
     st = G.initial_state(w)
-    a = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6,
-                         options={"flush_form": 24})
-    b = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=ekf_mod.ARITH_BF16X6)
+    if arith == 1 and T > 16:
+        pytest.skip("EKF_ARITH_BF16X6: flush_interval <= 16")
+    a = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=arith, options={"flush_form": 24})
+    b = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=arith)
     assert a.flush_kernel_name(T).startswith("flush_bf24_kernel"), a.flush_kernel_name(T)
     assert b.flush_kernel_name(T).endswith(", true>"), b.flush_kernel_name(T)
+    assert a.flush_kernel_name(T).endswith(", true>") == (arith == 2), a.flush_kernel_name(T)
     for ens in (a, b):
         for e in range(E):
             ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
