@@ -100,6 +100,8 @@ def parse():
     ap.add_argument("--speculate", type=int, choices=[0, 1, 2], default=1,
                     help="association path (EKF_OPT_SPECULATE): 1 speculative (default), 0 the "
                          "sequential chain every scan, 2 every guess wrong (fallback cost)")
+    ap.add_argument("--flush-form", type=int, default=0,
+                    help="EKF_OPT_FLUSH_FORM (A/B runs): 0 default, 24 the 2 x 4 split flush")
     ap.add_argument("--world", choices=["bench", "survey"], default="bench",
                     help="scan_gen parameter profile: bench (default) or SURVEY.md §8d literally")
     ap.add_argument("--parity-scans", type=int, default=-1,
@@ -270,7 +272,7 @@ def main():
         args.flush_interval = 4 if prec == ekf.PREC_F64 else (8 if arith == ekf.ARITH_EXACT else (20 if arith == ekf.ARITH_F16X3 else 12))
     ens = ekf.Ensemble(N, E, prec, max_lines=L_LINES, device=local, pipeline=bool(args.pipeline),
                       flush_interval=args.flush_interval, arith=arith,
-                      options={"speculate": args.speculate})
+                      options={"speculate": args.speculate, "flush_form": args.flush_form})
     # one real stream for everything (torch's default stream has handle 0, which the C-ABI reads
     # as "the context's own stream"): the payload copies, the RCCL waits (work.wait() orders the
     # current stream) and the EKF kernels are then ordered on the same queue
