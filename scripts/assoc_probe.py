@@ -18,8 +18,9 @@ E = 8
 cfgs = sys.argv[1:] or ["4096:8", "4096:1", "1024:8"]
 for c in cfgs:
     N, T = (int(x) for x in c.split(":"))
+    world = os.environ.get("PROBE_WORLD") or None   # "survey": SURVEY §8d's literal world
     w = G.make_world(N)
-    st = G.initial_state(w)
+    st = G.initial_state(w, profile=world)
     arith = {"exact": ekf.ARITH_EXACT, "f16x3": ekf.ARITH_F16X3}.get(os.environ.get("PROBE_ARITH"), ekf.ARITH_BF16X6)
     ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8, flush_interval=T, arith=arith,
                        options={"scan_stamps": 1})
@@ -27,9 +28,9 @@ for c in cfgs:
         ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
     base = ens.scan_stamps()
     for s in range(1, 25):
-        enc, lines, nl = G.make_scan(w, s, instances=E)
+        enc, lines, nl = G.make_scan(w, s, instances=E, profile=world)
         r = ens.localize(enc, lines, nl)
-        if not os.environ.get("PROBE_NOASSERT"):
+        if not os.environ.get("PROBE_NOASSERT") and not world:
             assert all(x["matches"] == 8 for x in r)
     stp = [a - b for a, b in zip(ens.scan_stamps(), base)]
     n = stp[9] or 1
@@ -42,5 +43,7 @@ for c in cfgs:
     out["past_quick_filter"] = stp[20]           # ... with a lane past the quick certified filter
     out["past_f32_filter"] = stp[21]             # ... past the fp32 certified filter
     out["past_f64_filter"] = stp[23]             # ... and past the fp64 one (exact evaluation)
-    print(json.dumps({"N": N, "T": T, "E": E, "arith": "exact" if arith == ekf.ARITH_EXACT else "bf16x6", "launches_x_instances": stp[9], "us": out}), flush=True)
+    an = {ekf.ARITH_EXACT: "exact", ekf.ARITH_BF16X6: "bf16x6", ekf.ARITH_F16X3: "f16x3"}[arith]
+    print(json.dumps({"N": N, "T": T, "E": E, "arith": an, "world": world or "bench", "launches_x_instances": stp[9],
+                      "us": out}), flush=True)
     ens.close()
