@@ -955,7 +955,7 @@ static int enqueue(ekf_ctx* c, int phase, const double* enc, const ekf_line* lin
     // X[base] and the ring slot this step reuses are released by the event guarding base
     if (c->ev_base) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_base, 0));
     const int np = (int)(c->nsteps - c->pend0);
-    if (np > ekf::PMAX) return EKF_EINVAL;   // unreachable: T <= 16
+    if (np > ekf::PMAX) return EKF_EINVAL;   // unreachable: T <= 24
     sp.Pread = xview(c, c->base);
     sp.npend = np;
     for (int q = 0; q < np; q++) sp.pend[q] = slot_of(c, c->pend0 + q);
