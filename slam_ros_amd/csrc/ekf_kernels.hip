@@ -3847,8 +3847,22 @@ __device__ __forceinline__ void wt_general(const DowndateParams& p, int e, const
 #define EKF_BF_WAVES 1   // split-bf16 flush: waves per SIMD (2: ≤ 256 registers, ring depth 2; measured equal)
 #endif
 #ifndef EKF_F16_WAVES
-#define EKF_F16_WAVES 1  // split-fp16 flush: waves per SIMD (2: ≤ 256 registers, ring depth 2)
+#define EKF_F16_WAVES 1  // split-fp16 flush: waves per SIMD (2: ≤ 256 registers, ring depth 2; measured equal)
 #endif
+#ifndef EKF_F16_TILES_LATE
+#define EKF_F16_TILES_LATE 1   // split-fp16 flush: deep operand ring, next tiles issued late (below)
+#endif
+#ifndef EKF_F16_RDMAX
+#define EKF_F16_RDMAX 8
+#endif
+// the largest divisor of ns not above rmax (at least 2)
+constexpr int ring_depth(int ns, int rmax)
+{
+    int r = 2;
+    for (int k = 2; k <= rmax; k++)
+        if (ns % k == 0) r = k;
+    return r;
+}
 template <typename TS, int NS, bool BF = false, bool F16 = false>
 __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVES) : 1) void flush_f32_wave_kernel(DowndateParams p)
 {
@@ -3958,7 +3972,17 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
             constexpr int NPL = F16 ? 2 : 3;
             typedef typename std::conditional<F16, f16x8r, bf16x8r>::type bf16x8;
             constexpr int WAVES = F16 ? EKF_F16_WAVES : EKF_BF_WAVES;
-            constexpr int RD = WAVES > 1 ? 2 : (NS % 4 == 0 ? 4 : (NS % 3 == 0 ? 3 : 2));   // operand ring depth
+            // operand ring depth (divides NS: a ring slot keeps its step index across wave-tiles).
+            // F16 with late tiles: the deepest ring of at most EKF_F16_RDMAX step-sets, and the next
+            // wave-tile's tiles issued RD − 1 steps before its start (below)
+            constexpr int RD = WAVES > 1 ? 2
+                               : (F16 && EKF_F16_TILES_LATE) ? ring_depth(NS, EKF_F16_RDMAX)
+                               : (NS % 4 == 0 ? 4 : (NS % 3 == 0 ? 3 : 2));
+            constexpr bool LATE = F16 && EKF_F16_TILES_LATE && WAVES == 1 && RD >= 3;
+            // vmcnt retires in issue order, so every operand wait after the tile loads also waits for
+            // them: issued at step TQ, the first such wait comes RD − 1 steps later, and so does
+            // the next wave-tile's first use of them
+            constexpr int TQ = NS - RD + 1;
             const size_t pstride = (size_t)d.nb * NPL * 64;   // 16-byte operands per instance
             // step q's planes: slot (slot0 + q) mod nslots
             auto pl_base = [&](int q) __attribute__((always_inline)) {
@@ -4100,7 +4124,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
 #pragma unroll
                         for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = (float)pref[i][qq][j] * isc;
 #ifndef EKF_XP_BF_NO_TILES   // timing experiment (results invalid): no tile stream after the first
-                if (more) load_tiles(nxt);
+                if (!LATE && more) load_tiles(nxt);
 #endif
 #ifdef EKF_XP_TILE_WAIT   // timing experiment: wait for the next wave-tile's tiles right away
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -4111,6 +4135,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
 #endif
 #pragma unroll
                 for (int q = 0; q < NS; q++) {
+                    if (LATE && q == TQ && more) load_tiles(nxt);
                     // ring set of step q + RD − 1 (this wave-tile's, else the next one's)
                     const int ql = q + RD - 1;
 #ifndef EKF_XP_BF_NO_OPS
