@@ -921,7 +921,11 @@ __device__ __forceinline__ void build_package(const Cand& c, const double R33[9]
 // of the scan applied (Robot.cpp:560-568, in order), W = P·Hᵀ, K = W·S⁻¹, U = K·S, y += K·v
 // (Robot.cpp:522-589), and the eager downdate of its robot-strip columns and diagonal block.
 // `uq_of(q)` / `vq_of(q)` return the landmark's U rows and jstar's V rows of the scan's match q.
-// MAXQ > 0: at most MAXQ earlier matches, the loop unrolled (its loads issued together).
+// MAXQ > 0 (the speculative path): all MAXQ rows of uq_of / vq_of are read and applied, those past
+// the t-th being +0 (the caller zeroes them), straight-line code; MAXQ == 0: the first t, in pairs.
+#ifndef EKF_GAIN_FIXQ
+#define EKF_GAIN_FIXQ 1
+#endif
 template <int MAXQ, typename UQ, typename VQ>
 __device__ __forceinline__ void gain_rows(const double* pk, int t, UQ uq_of, VQ vq_of, double blk[4],
                                           double2& rr0, double2& rr1, double2& rr2, double2& yb,
@@ -940,18 +944,25 @@ __device__ __forceinline__ void gain_rows(const double* pk, int t, UQ uq_of, VQ 
         blk[2] = fma(-uq.w, vh.y, blk[2]);
         blk[3] = fma(-uq.w, vh.w, blk[3]);
     };
-    // Matches in pairs (both pairs' rows loaded together: one LDS round trip per two matches),
-    // then the odd one; the products in q order either way
-    const int tu = __builtin_amdgcn_readfirstlane(MAXQ > 0 ? min(t, MAXQ) : t);
-    int q = 0;
+    if constexpr (MAXQ > 0 && EKF_GAIN_FIXQ) {
+        // all MAXQ rows, branch-free (the caller's rows past the t-th are +0: exact no-ops), so
+        // that the loads issue together and the chains interleave with the caller's other work
+#pragma unroll
+        for (int q = 0; q < MAXQ; q++) correct(uq_of(q), vq_of(q));
+    } else {
+        // matches in pairs (both pairs' rows loaded together: one LDS round trip per two
+        // matches), then the odd one; the products in q order either way
+        const int tu = __builtin_amdgcn_readfirstlane(MAXQ > 0 ? min(t, MAXQ) : t);
+        int q = 0;
 #pragma unroll 1
-    for (; q + 1 < tu; q += 2) {
-        const double4 ua = uq_of(q), va = vq_of(q);
-        const double4 ub = uq_of(q + 1), vb = vq_of(q + 1);
-        correct(ua, va);
-        correct(ub, vb);
+        for (; q + 1 < tu; q += 2) {
+            const double4 ua = uq_of(q), va = vq_of(q);
+            const double4 ub = uq_of(q + 1), vb = vq_of(q + 1);
+            correct(ua, va);
+            correct(ub, vb);
+        }
+        if (q < tu) correct(uq_of(q), vq_of(q));
     }
-    if (q < tu) correct(uq_of(q), vq_of(q));
     const double S0 = pk[MB_S], S1 = pk[MB_S + 1], S2 = pk[MB_S + 2], S3 = pk[MB_S + 3];
     const double Si0 = pk[MB_SI], Si1 = pk[MB_SI + 1], Si2 = pk[MB_SI + 2], Si3 = pk[MB_SI + 3];
     const double v0 = pk[MB_V], v1 = pk[MB_V + 1];
@@ -1454,6 +1465,12 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     if (tid < SPEC_L) sh_first[tid] = 0x7fffffff;
     __shared__ double sh_wd[SPEC_L * SPEC_WD];
     __shared__ double4 sh_wh[SPEC_L][SPEC_L][2];
+    // the earlier-match rows start as +0: the speculative gain rows run all SPEC_L corrections
+    // unconditionally, and a zero row leaves a chain as it is (x + (−0·0) == x)
+    for (int k = tid; k < SPEC_L * SPEC_L * 2; k += SCAN_BLOCK) (&sh_wh[0][0][0])[k] = make_double4(0.0, 0.0, 0.0, 0.0);
+    if (tid < SCAN_THREADS)
+#pragma unroll
+        for (int q = 0; q < HIST_LDS; q++) sh_uhist[q][tid] = make_double4(0.0, 0.0, 0.0, 0.0);
     __shared__ double sh_pk[SPEC_L][PKW];
     __shared__ float sh_stg[SPEC_L * SPEC_QMAX * 2 * 4 * 8];   // staged pending-step rows
     __shared__ unsigned long long sh_stamp[EKF_NSTAMP];
@@ -2292,9 +2309,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         wok = __builtin_amdgcn_readfirstlane(pk[PK_OK] != 0.0 ? 1 : 0) != 0;
                         if (r_mode == 1 && (i == 1 || i == 2) && wok) status |= EKF_ST_NSYM;
                         if (own) {
+                            // the quick filter and the gain rows in one block (independent chains);
+                            // the gain rows take effect only if the guessed winner passed (wok,
+                            // uniform; otherwise the package words are not written)
                             deeper = cand && !quick_reject(b5, ybx, yby, ma0, s0f, c0f, xpg, ln.alpha, ln.r, Rm, p.gate);
-                        }
-                        if (own && wok) {
                             double blk[4];
                             if constexpr (sizeof(typename Stor<T>::C) == 4) {
                                 const float4 bk = sh_blk[i][tid];
@@ -2303,11 +2321,16 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                                 pll_block(pv, 2 * j, 2 * w, blk);   // fp64 operands: read in the loop
                             }
                             double kk[4], uu[4];
+                            double2 g0 = rr0, g1 = rr1, g2 = rr2, gy = yb;
+                            double gD[4] = {Dj[0], Dj[1], Dj[2], Dj[3]};
                             gain_rows<SPEC_L>(pk, m, [&](int q) { return sh_uhist[q][tid]; },   // m < SPEC_L = HIST_LDS
-                                              [&](int q) { return sh_wh[i][q][1]; }, blk, rr0, rr1,
-                                              rr2, yb, Dj, kk, uu);
-                            const float F[3] = {(float)pk[PK_F], (float)pk[PK_F + 1], (float)pk[PK_F + 2]};
-                            store_rows(m, kk, uu, false, F);
+                                              [&](int q) { return sh_wh[i][q][1]; }, blk, g0, g1, g2, gy, gD, kk, uu);
+                            if (wok) {
+                                rr0 = g0; rr1 = g1; rr2 = g2; yb = gy;
+                                Dj[0] = gD[0]; Dj[1] = gD[1]; Dj[2] = gD[2]; Dj[3] = gD[3];
+                                const float F[3] = {(float)pk[PK_F], (float)pk[PK_F + 1], (float)pk[PK_F + 2]};
+                                store_rows(m, kk, uu, false, F);
+                            }
                         }
                         sub(18);
                     } else {
