@@ -921,11 +921,8 @@ __device__ __forceinline__ void build_package(const Cand& c, const double R33[9]
 // of the scan applied (Robot.cpp:560-568, in order), W = P·Hᵀ, K = W·S⁻¹, U = K·S, y += K·v
 // (Robot.cpp:522-589), and the eager downdate of its robot-strip columns and diagonal block.
 // `uq_of(q)` / `vq_of(q)` return the landmark's U rows and jstar's V rows of the scan's match q.
-// MAXQ > 0 (the speculative path): all MAXQ rows of uq_of / vq_of are read and applied, those past
-// the t-th being +0 (the caller zeroes them), straight-line code; MAXQ == 0: the first t, in pairs.
-#ifndef EKF_GAIN_FIXQ
-#define EKF_GAIN_FIXQ 1
-#endif
+// MAXQ > 0: at most MAXQ earlier matches (the speculative path). (Applying all MAXQ rows
+// branch-free on zeroed rows measured slower: DESIGN.md §10.)
 template <int MAXQ, typename UQ, typename VQ>
 __device__ __forceinline__ void gain_rows(const double* pk, int t, UQ uq_of, VQ vq_of, double blk[4],
                                           double2& rr0, double2& rr1, double2& rr2, double2& yb,
@@ -944,25 +941,18 @@ __device__ __forceinline__ void gain_rows(const double* pk, int t, UQ uq_of, VQ 
         blk[2] = fma(-uq.w, vh.y, blk[2]);
         blk[3] = fma(-uq.w, vh.w, blk[3]);
     };
-    if constexpr (MAXQ > 0 && EKF_GAIN_FIXQ) {
-        // all MAXQ rows, branch-free (the caller's rows past the t-th are +0: exact no-ops), so
-        // that the loads issue together and the chains interleave with the caller's other work
-#pragma unroll
-        for (int q = 0; q < MAXQ; q++) correct(uq_of(q), vq_of(q));
-    } else {
-        // matches in pairs (both pairs' rows loaded together: one LDS round trip per two
-        // matches), then the odd one; the products in q order either way
-        const int tu = __builtin_amdgcn_readfirstlane(MAXQ > 0 ? min(t, MAXQ) : t);
-        int q = 0;
+    // matches in pairs (both pairs' rows loaded together: one LDS round trip per two matches),
+    // then the odd one; the products in q order either way
+    const int tu = __builtin_amdgcn_readfirstlane(MAXQ > 0 ? min(t, MAXQ) : t);
+    int q = 0;
 #pragma unroll 1
-        for (; q + 1 < tu; q += 2) {
-            const double4 ua = uq_of(q), va = vq_of(q);
-            const double4 ub = uq_of(q + 1), vb = vq_of(q + 1);
-            correct(ua, va);
-            correct(ub, vb);
-        }
-        if (q < tu) correct(uq_of(q), vq_of(q));
+    for (; q + 1 < tu; q += 2) {
+        const double4 ua = uq_of(q), va = vq_of(q);
+        const double4 ub = uq_of(q + 1), vb = vq_of(q + 1);
+        correct(ua, va);
+        correct(ub, vb);
     }
+    if (q < tu) correct(uq_of(q), vq_of(q));
     const double S0 = pk[MB_S], S1 = pk[MB_S + 1], S2 = pk[MB_S + 2], S3 = pk[MB_S + 3];
     const double Si0 = pk[MB_SI], Si1 = pk[MB_SI + 1], Si2 = pk[MB_SI + 2], Si3 = pk[MB_SI + 3];
     const double v0 = pk[MB_V], v1 = pk[MB_V + 1];
@@ -1465,12 +1455,6 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     if (tid < SPEC_L) sh_first[tid] = 0x7fffffff;
     __shared__ double sh_wd[SPEC_L * SPEC_WD];
     __shared__ double4 sh_wh[SPEC_L][SPEC_L][2];
-    // the earlier-match rows start as +0: the speculative gain rows run all SPEC_L corrections
-    // unconditionally, and a zero row leaves a chain as it is (x + (−0·0) == x)
-    for (int k = tid; k < SPEC_L * SPEC_L * 2; k += SCAN_BLOCK) (&sh_wh[0][0][0])[k] = make_double4(0.0, 0.0, 0.0, 0.0);
-    if (tid < SCAN_THREADS)
-#pragma unroll
-        for (int q = 0; q < HIST_LDS; q++) sh_uhist[q][tid] = make_double4(0.0, 0.0, 0.0, 0.0);
     __shared__ double sh_pk[SPEC_L][PKW];
     __shared__ float sh_stg[SPEC_L * SPEC_QMAX * 2 * 4 * 8];   // staged pending-step rows
     __shared__ unsigned long long sh_stamp[EKF_NSTAMP];
