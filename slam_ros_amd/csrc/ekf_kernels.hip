@@ -1447,6 +1447,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     __shared__ unsigned long long sh_listsb[SPEC_GMAX * SPEC_L];   // the B words (count > 4)
     __shared__ int sh_glist[SPEC_L][SPEC_K + 1];
     __shared__ int sh_spec[SPEC_L];
+    __shared__ int sh_addq[SPEC_L];   // per guessed winner: the latest pending step that added it, or -1
+    __shared__ int sh_psg[PMAX];      // pending steps' plane exponents (EKF_ARITH_F16X3)
     __shared__ int sh_flag;
     __shared__ int sh_ready;
     __shared__ int sh_rwst;   // status bits of the replay wave (the winners' GSL_EDOM)
@@ -1560,9 +1562,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // the scan's other inputs, issued with the state loads (one memory round trip): the pending
     // steps' control words, the line count, savedLineCount and the line words
     int4 ctl_pre = make_int4(0, 0, 0, 0);
+    int psg_pre = 0;
     if ((p.phase & PHASE_UPDATE) && tid < p.npend) {
         const int* r = p.pend[tid].res + (size_t)e * RES_STRIDE;
         ctl_pre = make_int4(r[RES_RESET], r[RES_KSTEPS], r[RES_NADD], r[RES_SAVED_IN]);
+        psg_pre = r[RES_PSIG];
     }
     const int L_pre = p.nlines[e];
     const int s_pre = (p.phase & PHASE_UPDATE) ? p.saved[e] : 0;
@@ -1648,7 +1652,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     pv.pend = p.pend;
     pv.ctl = sh_ctl;
     pv.rnd = !p.bf;
-    if (tid < p.npend) sh_ctl[tid] = ctl_pre;
+    if (tid < p.npend) {
+        sh_ctl[tid] = ctl_pre;
+        sh_psg[tid] = psg_pre;
+    }
 
     int L = L_pre;
     L = L < 0 ? 0 : (L > d.max_lines ? d.max_lines : L);
@@ -1673,15 +1680,20 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // steps are applied by bf16 MFMA on the operand planes (plane_replay) and the diagonal blocks
     // come from Dd (the last committed step's, exact); fp32 storage
     bool mf = false;
+    bool aug_pend = false;   // some pending step adds landmarks (uniform)
     unsigned amask = 0;   // pending steps with a downdate (ks > 0)
     // (the MFMA replay reads the planes, not the LDS stage: any number of pending steps)
     if (spec_ok && sym && sizeof(typename Stor<T>::C) == 4 && d.kmax / 2 >= 8) {
         __syncthreads();   // sh_ctl
         bool st = true;
         for (int q = 0; q < p.npend; q++) st &= sh_ctl[q].y <= 8;
+        // pending steps that add landmarks stay on the MFMA replay: a block touching a landmark
+        // added at step q* starts from q*'s patch (its V rows are zero before), below; a reset or
+        // a plane exponent other than this scan's takes the exact forms
         bool m = st && p.mfrep && kPlanes;
         for (int q = 0; q < p.npend; q++) {
-            m &= !sh_ctl[q].x && sh_ctl[q].z == 0;
+            m &= !sh_ctl[q].x && (!pf16 || sh_psg[q] == psig);
+            aug_pend |= sh_ctl[q].z > 0;
             if (sh_ctl[q].y > 0) amask |= 1u << q;
         }
         staged = st && (p.npend <= SPEC_QMAX || m);
@@ -1948,6 +1960,14 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 const int w = t < L ? sh_spec[t] : -1;
                 cols[t] = w >= 0 ? w : j;
             }
+            if (tid < SPEC_L) {   // (read after the records' barrier)
+                const int w = tid < L ? sh_spec[tid] : -1;
+                int qa = -1;
+                if (mf && aug_pend && w >= 0)
+                    for (int q = 0; q < p.npend; q++)
+                        if (w >= sh_ctl[q].w && w < sh_ctl[q].w + sh_ctl[q].z) qa = q;
+                sh_addq[tid] = qa;
+            }
             C srow[SPEC_L + 1][4];
             if (staged && own) staged_blocks_load<T>(pv, j, cols, srow);
             int pu = 0, pt = 0;   // replay-wave lane → mutual block (pu, pt), pt <= pu
@@ -2037,7 +2057,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 if (lane_r < L * (L + 1) / 2 && sh_spec[pu] >= 0 && sh_spec[pt] >= 0) {
                     const bool swap = ((2 * sh_spec[pu]) >> 5) > ((2 * sh_spec[pt]) >> 5);
-                    const C xr[4] = {pacc[0], swap ? pacc[2] : pacc[1], swap ? pacc[1] : pacc[2], pacc[3]};
+                    C xr[4] = {pacc[0], swap ? pacc[2] : pacc[1], swap ? pacc[1] : pacc[2], pacc[3]};
+                    const int qs = max(sh_addq[pu], sh_addq[pt]);   // (as for the landmark waves' blocks)
+                    if (qs >= 0) patch_block<T>(pv, p.pend[qs], sh_ctl[qs], 2 * sh_spec[pu], 2 * sh_spec[pt], false, xr);
                     double* r = sh_wd + pu * SPEC_WD + (pt == pu ? 6 : 14 + 4 * pt);
 #pragma unroll
                     for (int a = 0; a < 4; a++)
@@ -2208,15 +2230,26 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                             d0[k] = *reinterpret_cast<const f32x4v*>(r0 + 4 * k);
                             d1[k] = *reinterpret_cast<const f32x4v*>(r0 + 16 + 4 * k);
                         }
+                        // a block touching a landmark added during the pending steps starts from
+                        // the patch of the step that added the later of its two landmarks (the
+                        // higher index: landmarks are appended); the replay's ΔX holds only the
+                        // steps after it (their V rows are zero before)
+                        int qj = -1;
+                        if (aug_pend)
+                            for (int q = 0; q < p.npend; q++)
+                                if (j >= sh_ctl[q].w && j < sh_ctl[q].w + sh_ctl[q].z) qj = q;
 #pragma unroll
                         for (int t = 0; t < SPEC_L; t++)
                             if (t < L && sh_spec[t] >= 0) {
+                                C b[4] = {srow[t][0], srow[t][1], srow[t][2], srow[t][3]};
+                                const int qs = max(qj, sh_addq[t]);
+                                if (qs >= 0) patch_block<T>(pv, p.pend[qs], sh_ctl[qs], 2 * j, 2 * sh_spec[t], false, b);
                                 const int c0 = 2 * t;
                                 sh_blk[t][tid] = make_float4(
-                                    (float)(from_domain<T>(srow[t][0], pv.ex) - (double)d0[c0 >> 2][c0 & 3] * rsc),
-                                    (float)(from_domain<T>(srow[t][1], pv.ex) - (double)d0[c0 >> 2][(c0 & 3) + 1] * rsc),
-                                    (float)(from_domain<T>(srow[t][2], pv.ex) - (double)d1[c0 >> 2][c0 & 3] * rsc),
-                                    (float)(from_domain<T>(srow[t][3], pv.ex) - (double)d1[c0 >> 2][(c0 & 3) + 1] * rsc));
+                                    (float)(from_domain<T>(b[0], pv.ex) - (double)d0[c0 >> 2][c0 & 3] * rsc),
+                                    (float)(from_domain<T>(b[1], pv.ex) - (double)d0[c0 >> 2][(c0 & 3) + 1] * rsc),
+                                    (float)(from_domain<T>(b[2], pv.ex) - (double)d1[c0 >> 2][c0 & 3] * rsc),
+                                    (float)(from_domain<T>(b[3], pv.ex) - (double)d1[c0 >> 2][(c0 & 3) + 1] * rsc));
                             }
                     }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
