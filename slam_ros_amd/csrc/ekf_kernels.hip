@@ -2594,14 +2594,27 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // ---------------- augmentation (Robot.cpp:776-866) ----------------
     double vnew = 0.0;   // the lead: the largest variance of the new landmarks (EKF_ARITH_F16X3's σ)
     if (!reset) {
+        // the new landmarks' world-frame line and its sin/cos (Robot.cpp:787-803), lane q of every
+        // wave for new landmark q (nadd <= max_lines <= 64), then read from that lane: one set of
+        // fp64 trigonometry per wave instead of one per new landmark
+        double a_r = 0.0, a_al = 0.0, a_sa = 0.0, a_ca = 1.0;
+        {
+            const int ql = threadIdx.x & 63;
+            if (ql < nadd) {
+                const ekf_line lq = sh_lines[sh_extra[ql]];
+                double alfa = lq.alpha;
+                a_r = lq.r + (pose[0] * cos(alfa) + pose[1] * sin(alfa));
+                alfa += pose[2];
+                sincos(alfa, &a_sa, &a_ca);
+                a_al = alfa;
+            }
+        }
         for (int q = 0; q < nadd; q++) {
             const ekf_line ln = sh_lines[sh_extra[q]];
             const int sq = s + q;
-            double alfa = ln.alpha;
-            const double r = ln.r + (pose[0] * cos(alfa) + pose[1] * sin(alfa));
-            alfa += pose[2];
-            double sa, ca;
-            sincos(alfa, &sa, &ca);
+            const double r = __shfl(a_r, q, 64);
+            const double alfa = __shfl(a_al, q, 64);
+            const double sa = __shfl(a_sa, q, 64), ca = __shfl(a_ca, q, 64);
             if (own && j < sq) {
                 // landmark columns of P[l0:l0+2, 0:l0] = Gx·P[0:3, 0:l0] (Robot.cpp:852-862)
                 double* prow = patch + (size_t)(q * 2) * M;
