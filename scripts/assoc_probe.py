@@ -22,7 +22,10 @@ for c in cfgs:
     w = G.make_world(N)
     st = G.initial_state(w, profile=world)
     arith = {"exact": ekf.ARITH_EXACT, "f16x3": ekf.ARITH_F16X3}.get(os.environ.get("PROBE_ARITH"), ekf.ARITH_BF16X6)
-    ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8, flush_interval=T, arith=arith,
+    prec = {"f64": ekf.PREC_F64, "f16": ekf.PREC_F16}.get(os.environ.get("PROBE_PREC"), ekf.PREC_F32)
+    if prec == ekf.PREC_F64:
+        arith = ekf.ARITH_EXACT
+    ens = ekf.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=arith,
                        options={"scan_stamps": 1})
     for e in range(E):
         ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
@@ -44,6 +47,7 @@ for c in cfgs:
     out["past_f32_filter"] = stp[21]             # ... past the fp32 certified filter
     out["past_f64_filter"] = stp[23]             # ... and past the fp64 one (exact evaluation)
     an = {ekf.ARITH_EXACT: "exact", ekf.ARITH_BF16X6: "bf16x6", ekf.ARITH_F16X3: "f16x3"}[arith]
-    print(json.dumps({"N": N, "T": T, "E": E, "arith": an, "world": world or "bench", "launches_x_instances": stp[9],
+    print(json.dumps({"N": N, "T": T, "E": E, "arith": an, "precision": os.environ.get("PROBE_PREC", "f32"),
+                      "world": world or "bench", "launches_x_instances": stp[9],
                       "us": out}), flush=True)
     ens.close()
