@@ -1441,6 +1441,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     __shared__ double4 sh_vhist[HIST_V][SCAN_THREADS];
     static_assert(sizeof(float4) * SPEC_L == sizeof(double4) * HIST_V, "block buffer aliases sh_vhist");
     float4 (*sh_blk)[SCAN_THREADS] = reinterpret_cast<float4 (*)[SCAN_THREADS]>(&sh_vhist[0][0]);
+    // fp64 operands: the owned blocks of the guessed columns in fp64 (48 KB; a placeholder otherwise)
+    constexpr bool kB64 = sizeof(typename Stor<T>::C) == 8;
+    __shared__ double4 sh_blk64[kB64 ? SPEC_L : 1][kB64 ? SCAN_THREADS : 1];
     // speculative association
     __shared__ unsigned long long sh_wl[SPEC_L][SCAN_THREADS / 64];
     __shared__ unsigned long long sh_lists[SPEC_GMAX * SPEC_L];
@@ -2283,6 +2286,24 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                                 if (t0 + b < L && sh_spec[t0 + b] >= 0)
                                     sh_blk[t0 + b][tid] = make_float4((float)bk[b][0], (float)bk[b][1], (float)bk[b][2], (float)bk[b][3]);
                         }
+                    } else {
+                        // fp64 operands: the same blocks in fp64, ahead of the line loop (they used
+                        // to be read, pending steps replayed, inside it: a memory round trip per
+                        // line on the landmark waves' chain)
+                        for (int t0 = 0; t0 < L; t0 += SPEC_PB) {
+                            int cols[SPEC_PB];
+                            double bk[SPEC_PB][4];
+#pragma unroll
+                            for (int b = 0; b < SPEC_PB; b++) {
+                                const int w = (t0 + b < L) ? sh_spec[t0 + b] : -1;
+                                cols[b] = 2 * (w >= 0 ? w : j);
+                            }
+                            pll_blocks<T, SPEC_PB>(pv, 2 * j, cols, bk);
+#pragma unroll
+                            for (int b = 0; b < SPEC_PB; b++)
+                                if (t0 + b < L && sh_spec[t0 + b] >= 0)
+                                    sh_blk64[t0 + b][tid] = make_double4(bk[b][0], bk[b][1], bk[b][2], bk[b][3]);
+                        }
                     }
                 }
                 EKF_STAMP(11);
@@ -2335,7 +2356,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                                 const float4 bk = sh_blk[i][tid];
                                 blk[0] = bk.x; blk[1] = bk.y; blk[2] = bk.z; blk[3] = bk.w;
                             } else {
-                                pll_block(pv, 2 * j, 2 * w, blk);   // fp64 operands: read in the loop
+                                const double4 bk = sh_blk64[i][tid];
+                                blk[0] = bk.x; blk[1] = bk.y; blk[2] = bk.z; blk[3] = bk.w;
                             }
                             double kk[4], uu[4];
                             double2 g0 = rr0, g1 = rr1, g2 = rr2, gy = yb;
