@@ -245,7 +245,7 @@ int ekf_ellipse_of_block(const double P22[4], float axii[2], float* angle);
  * whose packed P should not (or cannot) live on one GPU. No reference member maps to these: they
  * replace the single call Robot::localize (Robot.h:34, Robot.cpp:126-904) for an instance spread over
  * processes. ekf_shard_create makes rank `rank` of `world` a context of one instance (instances =
- * 1, EKF_ARITH_EXACT, fp32 with flush_interval <= 8 or fp64 with <= 4, no pipeline, max_lines <= 8)
+ * 1, EKF_ARITH_EXACT, fp32 or fp64 with flush_interval <= 8, no pipeline, max_lines <= 8)
  * that stores only its share of the packed landmark block: the tiles of tile rows [row_begin,
  * row_end) (ekf_shard_tiles), a contiguous slice balanced by tile count, about 1/world of it
  * (ekf_landmark_block_bytes). Everything of size O(n) (robot strip, mean, the landmarks' scan

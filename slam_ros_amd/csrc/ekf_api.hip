@@ -341,7 +341,7 @@ extern "C" int ekf_shard_create(const ekf_config* cfg, int rank, int world, ekf_
     if (!cfg || !out) return EKF_EINVAL;
     *out = nullptr;
     // one instance, the exact arithmetic, fp32 or fp64 storage, the sequential schedule, groups the
-    // wave flushes take (fp32 <= 8 steps, fp64 <= 4)
+    // wave flushes take (fp32 <= 8 steps, fp64 <= 8)
     if (world < 1 || rank < 0 || rank >= world || cfg->instances != 1 || cfg->pipeline ||
         cfg->arith != EKF_ARITH_EXACT || (cfg->precision != EKF_PREC_F32 && cfg->precision != EKF_PREC_F64) ||
         cfg->flush_interval > (cfg->precision == EKF_PREC_F64 ? ekf::F64_WAVE_MAXS : 8) || cfg->max_lines > 8)
@@ -1631,9 +1631,11 @@ extern "C" const char* ekf_flush_kernel_name(const ekf_ctx* c, int nsteps)
 {
     if (!c || nsteps < 1) return "";
     if (c->cfg.precision == EKF_PREC_F64) {
-        static const char* f64w[5] = {"", "flush_f64_wave_kernel<1>", "flush_f64_wave_kernel<2>",
-                                      "flush_f64_wave_kernel<3>", "flush_f64_wave_kernel<4>"};
-        if (nsteps <= 4 && c->d.kmax == 16 && c->dd_variant != 2) return f64w[nsteps];
+        static const char* f64w[ekf::F64_WAVE_MAXS + 1] = {
+            "", "flush_f64_wave_kernel<1>", "flush_f64_wave_kernel<2>", "flush_f64_wave_kernel<3>",
+            "flush_f64_wave_kernel<4>", "flush_f64_wave_kernel<5>", "flush_f64_wave_kernel<6>",
+            "flush_f64_wave_kernel<7>", "flush_f64_wave_kernel<8>"};
+        if (nsteps <= ekf::F64_WAVE_MAXS && c->d.kmax == 16 && c->dd_variant != 2) return f64w[nsteps];
         return "downdate_f64_kernel";
     }
     const bool half = c->cfg.precision == EKF_PREC_F16;

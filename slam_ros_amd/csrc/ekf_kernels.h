@@ -59,7 +59,8 @@ struct Slot {
 constexpr int PMAX = 32;
 constexpr int WT_R = 2, WT_C = 2, WT_N = WT_R * WT_C;   // f32 wave flush: tiles per wave-tile
 constexpr int WT64_C = 2;                                 // f64 wave flush: 1 × 2 tiles per wave-tile
-constexpr int F64_WAVE_MAXS = 4;                          // f64 wave flush: steps per launch
+constexpr int F64_WAVE_MAXS = 8;                          // f64 wave flush: steps per launch
+constexpr int F64_RING = 4;                                // f64 wave flush: operand ring depth
 constexpr int F16X3_MAXS = 24;                            // split-fp16 contexts: flush_interval <= 24
 
 // one wave-tile of the wave flush (host-built table, read with scalar loads): the linear indices

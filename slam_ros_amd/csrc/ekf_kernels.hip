@@ -4740,7 +4740,7 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_bf24_kernel(DowndateParam
     }
 }
 
-// f64 flush, barrier-free per-wave form for groups of NS <= F64_WAVE_MAXS steps (kmax <= 16):
+// f64 flush, barrier-free per-wave form for groups of NS <= F64_WAVE_MAXS steps (kmax == 16):
 // the f32 wave kernel's scheme at fp64. One wave per SIMD walks wave-tiles of 1 × 2 tiles (eight
 // 16×16 v_mfma_f64_16x16x4_f64 accumulators, 64 registers); while wave-tile k runs its NS × 32
 // MFMAs, the tiles of wave-tile k+1 (issued first) and, step by step, its operand rows stream
@@ -4880,15 +4880,18 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f64_wave_kernel(DowndateP
     };
 
     if (fast) {
+        // operand ring of RD steps: step q + RD's rows load into step q's registers after its
+        // MFMAs (the next wave-tile's once q + RD >= NS; RD = NS up to four steps)
+        constexpr int RD = NS < F64_RING ? NS : F64_RING;
         f64x2 pref[WT64_C][8];
-        f64x2 opa[NS][4], opb[NS][WT64_C][4];
+        f64x2 opa[RD][4], opb[RD][WT64_C][4];
         f64x4 acc[WT64_C][4];
         Item cur, nxt, nxt2;
         first_item(cur);
         next_item(cur, nxt);
         load_tiles(cur, pref);
 #pragma unroll
-        for (int q = 0; q < NS; q++) load_ops(cur, q, opa[q], opb[q]);
+        for (int q = 0; q < RD; q++) load_ops(cur, q, opa[q], opb[q]);
         int g = g0;
         while (true) {
             const bool more = g + K < g_end;
@@ -4899,9 +4902,10 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f64_wave_kernel(DowndateP
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int q = 0; q < NS; q++) {
-                mfma_step(opa[q], opb[q], acc);
+                mfma_step(opa[q % RD], opb[q % RD], acc);
                 __builtin_amdgcn_sched_barrier(0);
-                load_ops(ldi, q, opa[q], opb[q]);   // step q's rows of the next wave-tile
+                if (q + RD < NS) load_ops(cur, q + RD, opa[q % RD], opb[q % RD]);
+                else load_ops(ldi, q + RD - NS, opa[q % RD], opb[q % RD]);   // the next wave-tile's
             }
             store_tiles(cur, acc);
             if (!more) break;
@@ -5235,7 +5239,11 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
             case 1: hipExtLaunchKernelGGL((flush_f64_wave_kernel<1>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p); break;
             case 2: hipExtLaunchKernelGGL((flush_f64_wave_kernel<2>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p); break;
             case 3: hipExtLaunchKernelGGL((flush_f64_wave_kernel<3>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p); break;
-            default: hipExtLaunchKernelGGL((flush_f64_wave_kernel<4>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p); break;
+            case 4: hipExtLaunchKernelGGL((flush_f64_wave_kernel<4>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p); break;
+            case 5: hipExtLaunchKernelGGL((flush_f64_wave_kernel<5>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p); break;
+            case 6: hipExtLaunchKernelGGL((flush_f64_wave_kernel<6>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p); break;
+            case 7: hipExtLaunchKernelGGL((flush_f64_wave_kernel<7>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p); break;
+            default: hipExtLaunchKernelGGL((flush_f64_wave_kernel<8>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p); break;
             }
             return hipGetLastError();
         }
