@@ -273,6 +273,91 @@ __device__ __forceinline__ void patch_block(const PllView<T>& v, const Slot& sq,
     }
 }
 
+// One pending step's downdate on B blocks (i0, j0[b]) in their stored orientations (pll_blocks):
+// the owned rows i0, i0+1 of U and V are loaded once per k-chunk (their lanes' addresses are
+// spread over many cache lines) and each column landmark's rows once (U_col for a transposed
+// block, V_col otherwise; the guessed columns are the same for the whole wave). Per element the
+// FMA chain of pll_blocks' per-block form, operand for operand.
+template <typename T, int B>
+__device__ __forceinline__ void pll_shared_step(const PllView<T>& v, const Slot& sq, int ks, int i0,
+                                                const int (&j0)[B], const bool (&swap)[B],
+                                                typename Stor<T>::C (&acc)[B][4])
+{
+    using C = typename Stor<T>::C;
+    if constexpr (sizeof(C) == 4) {
+        const int kh = v.kmax / 2;
+        const float* U = reinterpret_cast<const float*>(sq.Uop) + v.e * v.opstride;
+        const float* V = reinterpret_cast<const float*>(sq.Vop) + v.e * v.opstride;
+        auto row = [&](int r) { return ((size_t)(r >> 5) * 64 + (r & 31)) * kh; };
+        const float* uo = U + row(i0);
+        const float* vo = V + row(i0);
+        const float* xc[B];
+#pragma unroll
+        for (int b = 0; b < B; b++) xc[b] = (swap[b] ? U : V) + row(j0[b]);
+        for (int s0 = 0; s0 < ks; s0 += 4) {
+            // [row, row + 1] × [k half 0, k half 1] of the owned U and V rows
+            const f32x4v ue0 = *reinterpret_cast<const f32x4v*>(uo + s0);
+            const f32x4v ue1 = *reinterpret_cast<const f32x4v*>(uo + kh + s0);
+            const f32x4v uo0 = *reinterpret_cast<const f32x4v*>(uo + 32 * kh + s0);
+            const f32x4v uo1 = *reinterpret_cast<const f32x4v*>(uo + 33 * kh + s0);
+            const f32x4v ve0 = *reinterpret_cast<const f32x4v*>(vo + s0);
+            const f32x4v ve1 = *reinterpret_cast<const f32x4v*>(vo + kh + s0);
+            const f32x4v vo0 = *reinterpret_cast<const f32x4v*>(vo + 32 * kh + s0);
+            const f32x4v vo1 = *reinterpret_cast<const f32x4v*>(vo + 33 * kh + s0);
+#pragma unroll
+            for (int b = 0; b < B; b++) {
+                const f32x4v ce0 = *reinterpret_cast<const f32x4v*>(xc[b] + s0);
+                const f32x4v ce1 = *reinterpret_cast<const f32x4v*>(xc[b] + kh + s0);
+                const f32x4v co0 = *reinterpret_cast<const f32x4v*>(xc[b] + 32 * kh + s0);
+                const f32x4v co1 = *reinterpret_cast<const f32x4v*>(xc[b] + 33 * kh + s0);
+                const bool sw = swap[b];
+                const f32x4v ae0 = sw ? ce0 : ue0, ae1 = sw ? ce1 : ue1, ao0 = sw ? co0 : uo0, ao1 = sw ? co1 : uo1;
+                const f32x4v be0 = sw ? ve0 : ce0, be1 = sw ? ve1 : ce1, bo0 = sw ? vo0 : co0, bo1 = sw ? vo1 : co1;
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+                    if (s0 + s >= ks) break;
+                    acc[b][0] = fmaf(ao0[s], bo0[s], fmaf(ae0[s], be0[s], acc[b][0]));
+                    acc[b][1] = fmaf(ao0[s], bo1[s], fmaf(ae0[s], be1[s], acc[b][1]));
+                    acc[b][2] = fmaf(ao1[s], bo0[s], fmaf(ae1[s], be0[s], acc[b][2]));
+                    acc[b][3] = fmaf(ao1[s], bo1[s], fmaf(ae1[s], be1[s], acc[b][3]));
+                }
+            }
+        }
+    } else {
+        const int kq = v.kmax / 4;
+        const double* U = reinterpret_cast<const double*>(sq.Uop) + v.e * v.opstride;
+        const double* V = reinterpret_cast<const double*>(sq.Vop) + v.e * v.opstride;
+        auto row = [&](int r) { return ((size_t)(r >> 5) * 64 + (r & 15)) * (2 * kq) + ((r >> 4) & 1) * kq; };
+        const double* uo = U + row(i0);
+        const double* vo = V + row(i0);
+        const double* xc[B];
+#pragma unroll
+        for (int b = 0; b < B; b++) xc[b] = (swap[b] ? U : V) + row(j0[b]);
+        for (int s = 0; s < ks; s++)
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                const size_t o = (size_t)16 * kk * 2 * kq + s;
+                const double u0 = uo[o], u1 = uo[o + 2 * kq];
+                const double w0 = vo[o], w1 = vo[o + 2 * kq];
+#pragma unroll
+                for (int b = 0; b < B; b++) {
+                    const double c0 = xc[b][o], c1 = xc[b][o + 2 * kq];
+                    const bool sw = swap[b];
+                    const double x0 = sw ? c0 : u0, x1 = sw ? c1 : u1;
+                    const double y0 = sw ? w0 : c0, y1 = sw ? w1 : c1;
+                    acc[b][0] = fma(x0, y0, (double)acc[b][0]);
+                    acc[b][1] = fma(x0, y1, (double)acc[b][1]);
+                    acc[b][2] = fma(x1, y0, (double)acc[b][2]);
+                    acc[b][3] = fma(x1, y1, (double)acc[b][3]);
+                }
+            }
+    }
+#pragma unroll
+    for (int b = 0; b < B; b++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) acc[b][k] = vround<T>(v, acc[b][k]);
+}
+
 // 2x2 blocks (i0, i0+1) × (j0[b], j0[b]+1), b < B, of the landmark block (i0, j0[b] even) as
 // they will be once the pending steps are flushed: per step (in order) a reset, or the rank-2m
 // downdate as the k-ordered FMA chain the MFMA executes, then the step's augmented rows rounded
@@ -300,7 +385,12 @@ __device__ __forceinline__ void pll_blocks(const PllView<T>& v, int i0, const in
             continue;
         }
         const int ks = cw.y;
-        if (ks > 0) {
+        if (ks > 0 && B > 1) {
+            // several blocks: the owned rows' U and V loaded once per k-chunk, each column's
+            // one operand per block (a block stored in owned-first orientation runs U_own·V_col,
+            // a transposed one U_col·V_own): the same operands as the per-block form below
+            pll_shared_step<T, B>(v, sq, ks, i0, j0, swap, acc);
+        } else if (ks > 0) {
             if constexpr (sizeof(C) == 4) {
                 // v_mfma_f32_32x32x2_f32 = ordered fmaf chain (k0 lanes 0-31, then k1)
                 const int kh = v.kmax / 2;
@@ -1070,6 +1160,10 @@ constexpr int SPEC_K = 8;
 // and a more bit (36); B = local indices 4..7, written and read only when the count exceeds 4
 constexpr int LW_CNT = 32, LW_MORE = 36;
 constexpr int SPEC_PB = 2;                          // guessed columns per pass over the pending steps
+#ifndef EKF_SPEC_PB64
+#define EKF_SPEC_PB64 4
+#endif
+constexpr int SPEC_PB64 = EKF_SPEC_PB64;            // ... fp64 operands (pll_shared_step: owned rows once per pass)
 #ifndef EKF_STAGED_DEPTH
 #define EKF_STAGED_DEPTH 1
 #endif
@@ -1683,6 +1777,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // steps are applied by bf16 MFMA on the operand planes (plane_replay) and the diagonal blocks
     // come from Dd (the last committed step's, exact); fp32 storage
     bool mf = false;
+    int rpath = 0;   // diagnostic (RES_DBG): 64 the pending replay took an exact form, 128 a pending
+                     // reset, 256 a pending plane exponent other than this scan's
     bool aug_pend = false;   // some pending step adds landmarks (uniform)
     unsigned amask = 0;   // pending steps with a downdate (ks > 0)
     // (the MFMA replay reads the planes, not the LDS stage: any number of pending steps)
@@ -1696,12 +1792,14 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         bool m = st && p.mfrep && kPlanes;
         for (int q = 0; q < p.npend; q++) {
             m &= !sh_ctl[q].x && (!pf16 || sh_psg[q] == psig);
+            rpath |= (sh_ctl[q].x ? 128 : 0) | (pf16 && sh_psg[q] != psig ? 256 : 0);
             aug_pend |= sh_ctl[q].z > 0;
             if (sh_ctl[q].y > 0) amask |= 1u << q;
         }
         staged = st && (p.npend <= SPEC_QMAX || m);
         mf = m && staged;
     }
+    if (p.npend > 0 && !mf) rpath |= 64;
     double Dj[4] = {0, 0, 0, 0};   // owned diagonal block
     if (own && j < s) {
         if (mf && p.npend > 0) {
@@ -1796,7 +1894,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     bool matched = false;
     int m = 0, nextra = 0, status = 0, tstatus = 0;
     int dpath = 0;   // diagnostic: 1 fast guess, 2 collision-resolved guess, 4 unresolved, 8 verdict failed,
-                     // 32 a guessed winner failed its exact gate and its line stayed unmatched (16: sequential)
+                     // 32 a guessed winner failed its exact gate and its line stayed unmatched (16: sequential;
+                     // 64-256: rpath)
     int par0 = 0;   // mailbox parity of line 0 on the sequential path
     bool sequential = true;
 
@@ -2290,17 +2389,17 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         // fp64 operands: the same blocks in fp64, ahead of the line loop (they used
                         // to be read, pending steps replayed, inside it: a memory round trip per
                         // line on the landmark waves' chain)
-                        for (int t0 = 0; t0 < L; t0 += SPEC_PB) {
-                            int cols[SPEC_PB];
-                            double bk[SPEC_PB][4];
+                        for (int t0 = 0; t0 < L; t0 += SPEC_PB64) {
+                            int cols[SPEC_PB64];
+                            double bk[SPEC_PB64][4];
 #pragma unroll
-                            for (int b = 0; b < SPEC_PB; b++) {
+                            for (int b = 0; b < SPEC_PB64; b++) {
                                 const int w = (t0 + b < L) ? sh_spec[t0 + b] : -1;
                                 cols[b] = 2 * (w >= 0 ? w : j);
                             }
-                            pll_blocks<T, SPEC_PB>(pv, 2 * j, cols, bk);
+                            pll_blocks<T, SPEC_PB64>(pv, 2 * j, cols, bk);
 #pragma unroll
-                            for (int b = 0; b < SPEC_PB; b++)
+                            for (int b = 0; b < SPEC_PB64; b++)
                                 if (t0 + b < L && sh_spec[t0 + b] >= 0)
                                     sh_blk64[t0 + b][tid] = make_double4(bk[b][0], bk[b][1], bk[b][2], bk[b][3]);
                         }
@@ -2808,7 +2907,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         const bool commit = !(wgst & EKF_ST_TIMEOUT_BIT);
         res[RES_NLINES] = L;
         res[RES_SAVED_IN] = s;
-        res[RES_DBG] = dpath | (sequential ? 16 : 0);
+        res[RES_DBG] = dpath | rpath | (sequential ? 16 : 0);
         for (int t = 0; t < 5; t++) res[RES_DBG + 1 + t] = t < SPEC_L ? sh_spec[t] : -2;
         if (commit) {
             yw[0] = xp[0];
