@@ -173,8 +173,8 @@ enum {
     EKF_OPT_FLUSH_FORM = 3,
     /* workgroups per CU of the grid-strided flush forms, 1..16 (8) */
     EKF_OPT_FLUSH_BLOCKS_PER_CU = 4,
-    /* split-bf16 contexts: pending steps applied on read by MFMA on the operand planes (1,
-     * default) or by the exact staged replay (0) */
+    /* pending steps applied on read by MFMA (1, default): split arithmetics on the operand planes,
+     * fp64 storage by the flush's own f64 MFMA (bit-identical); 0: the per-element replay forms */
     EKF_OPT_MFMA_REPLAY = 5,
     /* 1: the association kernel's instrumented instantiation with phase timers
      * (ekf_debug_scan_stamps); 0 (default) the product kernel */

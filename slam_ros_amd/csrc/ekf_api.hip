@@ -824,6 +824,7 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.live = c->cur;
     p.Dd = c->D;
     p.mfrep = c->mfrep;
+    p.mfrep64 = (c->cfg.precision == EKF_PREC_F64 && c->mfrep_opt) ? 1 : 0;
     p.bf = c->pmode;
     p.psig = c->psig;
     p.pvmax = c->pvmax;

@@ -102,6 +102,8 @@ struct ScanParams {
     int test_verdict;     // test hook: e + 1 = workgroup 1 of instance e sees its verdict poll time out
     double* Dd;           // [2][Etot][N][4] diagonal landmark blocks after the last committed step
                           // (copy live[e] read, the other written and committed with Rs / y)
+    int mfrep64;          // fp64 context: pending steps replayed on read by f64 MFMA (the flush's own
+                          // instruction: bit-identical chains; EKF_OPT_MFMA_REPLAY)
     int mfrep;            // split-bf16 context: pending steps replayed on read by bf16 MFMA from
                           // the operand planes, diagonal blocks kept in Dd
     int bf;               // split-plane context (1 EKF_ARITH_BF16X6, 2 EKF_ARITH_F16X3): fp16 storage

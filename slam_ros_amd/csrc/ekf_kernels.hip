@@ -1555,7 +1555,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     __shared__ double sh_wd[SPEC_L * SPEC_WD];
     __shared__ double4 sh_wh[SPEC_L][SPEC_L][2];
     __shared__ double sh_pk[SPEC_L][PKW];
-    __shared__ float sh_stg[SPEC_L * SPEC_QMAX * 2 * 4 * 8];   // staged pending-step rows
+    __shared__ __attribute__((aligned(16))) float sh_stg[SPEC_L * SPEC_QMAX * 2 * 4 * 8];   // staged pending-step rows
     __shared__ unsigned long long sh_stamp[EKF_NSTAMP];
     // EKF_ARITH_BF16X6 (fp32 storage): the owned rows' V values of this scan's matches (k-major
     // per row), split into bf16 planes and stored once at the end
@@ -1799,12 +1799,22 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         staged = st && (p.npend <= SPEC_QMAX || m);
         mf = m && staged;
     }
-    if (p.npend > 0 && !mf) rpath |= 64;
+    // fp64 storage, plain pending steps (no reset, no augmented rows): the owned rows' blocks of
+    // the guessed columns and the owned diagonal blocks by v_mfma_f64_16x16x4f64 over the pending
+    // steps' operand rows, the flush's own instruction on its own operands (below, phase (e))
+    bool m64 = false;
+    if constexpr (sizeof(typename Stor<T>::C) == 8)
+        if (spec_ok && p.mfrep64 && d.kmax == 16 && p.npend > 0) {
+            bool m = true;
+            for (int q = 0; q < p.npend; q++) m &= !sh_ctl[q].x && sh_ctl[q].z == 0;
+            m64 = m;
+        }
+    if (p.npend > 0 && !mf && !m64) rpath |= 64;
     double Dj[4] = {0, 0, 0, 0};   // owned diagonal block
     if (own && j < s) {
         if (mf && p.npend > 0) {
             Dj[0] = djb.x; Dj[1] = djb.y; Dj[2] = djb.z; Dj[3] = djb.w;
-        } else if (staged) {
+        } else if (staged || m64) {
             // the guess only needs it approximately: the last flushed value (exact one below)
 #pragma unroll
             for (int a = 0; a < 4; a++) Dj[a] = from_domain<T>(dj0[a], pv.ex);
@@ -1898,6 +1908,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                      // 64-256: rpath)
     int par0 = 0;   // mailbox parity of line 0 on the sequential path
     bool sequential = true;
+    // a restart after a failed verdict: the owned blocks of the guessed columns as the speculative
+    // pass computed them (scan start, pending steps applied) serve the lines whose winner was guessed
+    bool blk_cached = false;
+    float4 (*const sh_cblk)[SCAN_THREADS] = reinterpret_cast<float4 (*)[SCAN_THREADS]>(sh_stg);
 
     if (spec_ok) {
         // ---- (a) guesses: per line, does the owned landmark pass under the predicted state ----
@@ -2071,7 +2085,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 sh_addq[tid] = qa;
             }
             C srow[SPEC_L + 1][4];
-            if (staged && own) staged_blocks_load<T>(pv, j, cols, srow);
+            if ((staged || m64) && own) staged_blocks_load<T>(pv, j, cols, srow);
             int pu = 0, pt = 0;   // replay-wave lane → mutual block (pu, pt), pt <= pu
             C pacc[4] = {0, 0, 0, 0};
             const int lane_r = tid - SCAN_THREADS;
@@ -2358,6 +2372,110 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                   }
+                } else if (m64) {
+                  if constexpr (sizeof(C) == 8) {
+                    // fp64: the wave's 128 owned rows (8 M-blocks of 16) against the 16 winner rows
+                    // and against themselves (their diagonal blocks), one v_mfma_f64_16x16x4f64 per
+                    // M-block and k-chunk on the flush's operand rows in the flush's k order: per
+                    // element the flush's own chain, bit for bit. A block stored transposed (the
+                    // winner's tile row first) evolves as U_col·V_own: each k-chunk runs both
+                    // products with the other one's winner column zeroed (it adds ±0). The chains
+                    // start from the stored blocks (srow), handed from the owner threads to the MFMA
+                    // lanes and back through LDS: sh_blk64 (winners) and sh_uhist[0] (diagonal
+                    // blocks).
+                    typedef double d64x2 __attribute__((ext_vector_type(2)));
+                    typedef double d64x4 __attribute__((ext_vector_type(4)));
+                    constexpr int KH = 8;   // doubles per lane and row block (kmax = 16)
+                    const int l = tid & 63;
+                    const int wb = tid & ~63;                          // the wave's first thread
+                    const int rb0 = (2 * (g * SCAN_THREADS + wb)) >> 5;   // its first tile row (4 of them)
+                    double4* dg = sh_uhist[0];   // (this wave's part: free until its first match)
+                    if (own) {
+#pragma unroll
+                        for (int t = 0; t < SPEC_L; t++) sh_blk64[t][tid] = make_double4(srow[t][0], srow[t][1], srow[t][2], srow[t][3]);
+                        dg[tid] = make_double4(srow[SPEC_L][0], srow[SPEC_L][1], srow[SPEC_L][2], srow[SPEC_L][3]);
+                    } else {
+#pragma unroll
+                        for (int t = 0; t < SPEC_L; t++) sh_blk64[t][tid] = make_double4(0, 0, 0, 0);
+                        dg[tid] = make_double4(0, 0, 0, 0);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    // this lane's winner column c = l % 16: row wr of winner t = c / 2 (B operands
+                    // hold column l % 16 at k-offset l / 16, A operands row l % 16)
+                    const int c = l & 15, t = c >> 1;
+                    const int wsp = t < L ? sh_spec[t] : -1;
+                    const int wr = wsp >= 0 ? 2 * wsp + (c & 1) : 0;
+                    const size_t coff = (size_t)(wr >> 5) * 64 * KH + ((wr & 15) + 16 * (l >> 4)) * KH + ((wr >> 4) & 1) * 4;
+                    auto comp = [](double4& v, int k) -> double& { return reinterpret_cast<double*>(&v)[k]; };
+#pragma unroll 1
+                    for (int r4 = 0; r4 < 4; r4++) {
+                        const int rb = rb0 + r4;
+                        // (the last workgroup's waves may reach past the landmark block: no rows,
+                        // no operand rows there)
+                        if (rb >= d.nb) break;
+                        const bool sw = wsp >= 0 && rb > (wr >> 5);   // stored transposed
+                        const bool nsw = wsp >= 0 && !sw;
+                        d64x4 acc[2], dac[2];
+#pragma unroll
+                        for (int h = 0; h < 2; h++)
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                const int rl = 32 * r4 + 16 * h + 4 * i + (l >> 4);   // row in the wave (tile_off_f64)
+                                const int ow = wb + (rl >> 1);
+                                acc[h][i] = comp(sh_blk64[t][ow], (rl & 1) * 2 + (c & 1));
+                                const int cl = 32 * r4 + 16 * h + c;
+                                dac[h][i] = (rl >> 1) == (cl >> 1) ? comp(dg[ow], (rl & 1) * 2 + (cl & 1)) : 0.0;
+                            }
+                        for (int q = 0; q < p.npend; q++) {
+                            if (sh_ctl[q].y <= 0) continue;   // no match, or rolled back: nothing
+                            const double* Uq = reinterpret_cast<const double*>(p.pend[q].Uop) + e * opstride;
+                            const double* Vq = reinterpret_cast<const double*>(p.pend[q].Vop) + e * opstride;
+                            const d64x2* uo = reinterpret_cast<const d64x2*>(Uq + (size_t)rb * 64 * KH + l * KH);
+                            const d64x2* vo = reinterpret_cast<const d64x2*>(Vq + (size_t)rb * 64 * KH + l * KH);
+                            d64x2 ua[4], va[4], cu[2], cv[2];
+#pragma unroll
+                            for (int k = 0; k < 4; k++) { ua[k] = uo[k]; va[k] = vo[k]; }
+#pragma unroll
+                            for (int k = 0; k < 2; k++) {
+                                cu[k] = reinterpret_cast<const d64x2*>(Uq + coff)[k];
+                                cv[k] = reinterpret_cast<const d64x2*>(Vq + coff)[k];
+                            }
+#pragma unroll
+                            for (int s4 = 0; s4 < 4; s4++) {
+                                const double bv = nsw ? cv[s4 >> 1][s4 & 1] : 0.0;
+                                const double bu = sw ? cu[s4 >> 1][s4 & 1] : 0.0;
+#pragma unroll
+                                for (int h = 0; h < 2; h++) {
+                                    const double au = ua[2 * h + (s4 >> 1)][s4 & 1];
+                                    const double av = va[2 * h + (s4 >> 1)][s4 & 1];
+                                    acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(au, bv, acc[h], 0, 0, 0);
+                                    acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bu, acc[h], 0, 0, 0);
+                                    dac[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(au, av, dac[h], 0, 0, 0);
+                                }
+                            }
+                        }
+                        __builtin_amdgcn_wave_barrier();   // (every lane read its starting values)
+#pragma unroll
+                        for (int h = 0; h < 2; h++)
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                const int rl = 32 * r4 + 16 * h + 4 * i + (l >> 4);
+                                const int ow = wb + (rl >> 1);
+                                comp(sh_blk64[t][ow], (rl & 1) * 2 + (c & 1)) = acc[h][i];
+                                const int cl = 32 * r4 + 16 * h + c;
+                                if ((rl >> 1) == (cl >> 1)) comp(dg[ow], (rl & 1) * 2 + (cl & 1)) = dac[h][i];
+                            }
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    if (own && j < s) {
+                        const double4 dd = dg[tid];
+                        Dj[0] = dd.x; Dj[1] = dd.y; Dj[2] = dd.z; Dj[3] = dd.w;
+                    }
+                  }
                 } else if (own) {
                     if (staged) {
                         double blk[SPEC_L + 1][4];
@@ -2572,6 +2690,14 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 init_state();
                 Dj[0] = Dj[1] = Dj[2] = Dj[3] = 0.0;
                 if (own && j < s) pll_block(pv, 2 * j, 2 * j, Dj);
+                // fp32 operands: out of sh_blk, which aliases the V history the restart writes, into
+                // the stage (free once the speculative pass is over); fp64: sh_blk64 as it is
+                if constexpr (!kB64)
+                    if (own)
+#pragma unroll
+                        for (int t = 0; t < SPEC_L; t++)
+                            if (t < L && sh_spec[t] >= 0) sh_cblk[t][tid] = sh_blk[t][tid];
+                blk_cached = true;
                 matched = false;
                 m = nextra = status = 0;
                 ops_early = 0;   // (the sequential path rewrites every operand row)
@@ -2581,7 +2707,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             par0 = 1;   // the lists' parity-0 words may still be read
             // unresolved guesses: straight to the sequential path, which needs the exact owned
             // diagonal block (the staged path only loaded the last flushed one, for the guess)
-            if (staged && own && j < s) pll_block(pv, 2 * j, 2 * j, Dj);
+            if ((staged || m64) && own && j < s) pll_block(pv, 2 * j, 2 * j, Dj);
         }
     }
 
@@ -2671,18 +2797,36 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         // loads before waiting on either (another workgroup's winner: every workgroup reloads, its
         // own staged candidate included)
         double blk[4] = {0.0, 0.0, 0.0, 0.0};
+        int tsc = -1;   // the winner's guess index, when its blocks are cached (blk_cached)
+        if (blk_cached)
+#pragma unroll
+            for (int t = 0; t < SPEC_L; t++)
+                if (t < L && sh_spec[t] == jstar) tsc = t;
+        auto owned_block = [&]() {
+            if (tsc >= 0) {
+                if constexpr (kB64) {
+                    const double4 b = sh_blk64[tsc][tid];
+                    blk[0] = b.x; blk[1] = b.y; blk[2] = b.z; blk[3] = b.w;
+                } else {
+                    const float4 b = sh_cblk[tsc][tid];
+                    blk[0] = b.x; blk[1] = b.y; blk[2] = b.z; blk[3] = b.w;
+                }
+            } else {
+                pll_block(pv, 2 * j, 2 * jstar, blk);
+            }
+        };
         if (G > 1) {
             // (every thread passed the poll barrier after its mailbox stores read sh_pkg)
             const double* ps = mbox + ((size_t)par * G + gstar) * p.mbw;
             double pk0 = 0.0, pk1 = 0.0;
             if (tid < npk) pk0 = mb_load(ps + tid);
             if (tid + SCAN_BLOCK < npk) pk1 = mb_load(ps + tid + SCAN_BLOCK);
-            if (own) pll_block(pv, 2 * j, 2 * jstar, blk);
+            if (own) owned_block();
             if (tid < npk) sh_pkg[tid] = pk0;
             if (tid + SCAN_BLOCK < npk) sh_pkg[tid + SCAN_BLOCK] = pk1;
             __syncthreads();
         } else if (own) {
-            pll_block(pv, 2 * j, 2 * jstar, blk);
+            owned_block();
         }
         if (r_mode == 1 && (i == 1 || i == 2)) status |= EKF_ST_NSYM;
         if (own) {

@@ -707,6 +707,38 @@ def test_f64_wave_flush_equals_tile_kernel(ekf_mod, monkeypatch, N, T, lines, ex
         assert sa == sb
 
 
+@pytest.mark.parametrize("N,T,lines", [(2000, 4, 8), (4096, 4, 8), (100, 8, 8), (300, 6, 5)])
+def test_f64_mfma_replay_equals_per_element_replay(ekf_mod, N, T, lines):
+    """fp64 storage, speculative association with pending steps: the owned blocks of the guessed
+    columns and the diagonal blocks replayed by v_mfma_f64_16x16x4f64 (EKF_OPT_MFMA_REPLAY = 1,
+    default) give the same matches, P and y bit for bit as the per-element FMA replay (0). N = 100
+    and 300 leave lanes without a landmark in the last wave; N = 4096 is the bench's shape."""
+    E = 3
+    w = G.make_world(N)
+    st = G.initial_state(w)
+    a = ekf_mod.Ensemble(N, E, 0, max_lines=8, flush_interval=T)
+    b = ekf_mod.Ensemble(N, E, 0, max_lines=8, flush_interval=T, options={"mfma_replay": 0})
+    for ens in (a, b):
+        for e in range(E):
+            ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+    for step in range(1, 2 * T + 3):
+        enc, ln, nl = G.make_scan(w, step, instances=E, lines=lines)
+        ra = a.localize(enc, ln, nl)
+        rb = b.localize(enc, ln, nl)
+        for e in range(E):
+            assert ra[e]["match"] == rb[e]["match"], (step, e)
+            assert ra[e]["status"] == rb[e]["status"] == 0
+    for e in range(E):
+        Pa, ya, sa, pa = a.download_state(e)
+        Pb, yb, sb, pb = b.download_state(e)
+        bad = np.argwhere(Pa != Pb)
+        assert bad.size == 0, (e, bad[:12].tolist(), rel(Pa, Pb))
+        np.testing.assert_array_equal(ya, yb)
+        np.testing.assert_array_equal(pa, pb)
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("prec", [0, 1])
 @pytest.mark.parametrize("spec", ["1", "0"])
 def test_singular_status_counts_only_evaluated_candidates(ekf_mod, oracle_mod, monkeypatch, prec, spec):
