@@ -9,5 +9,5 @@ if [ "${PART:-all}" != lines ]; then
   cp gpurun_out/bench_config_parity.json gpurun_out/r04_final_check/ 2>/dev/null
 fi
 if [ "${PART:-all}" != check ]; then
-  LINES="r04_final_n4096|--steps 20 --warmup 5;r04_final_n1024|--steps 20 --warmup 5 --capacity 1024;r04_final_n256|--steps 20 --warmup 5 --capacity 256;r04_final_f16|--steps 20 --warmup 5 --precision f16;r04_final_f64|--steps 20 --warmup 5 --precision f64" bash scripts/r04/lines.sh
+  LINES="r04_final_n4096|--steps 20 --warmup 5;r04_final_n1024|--steps 20 --warmup 5 --capacity 1024;r04_final_n256|--steps 20 --warmup 5 --capacity 256;r04_final_f16|--steps 20 --warmup 5 --precision f16;r04_final_f64|--steps 20 --warmup 5 --precision f64;r04_final_survey|--steps 20 --warmup 5 --world survey" bash scripts/r04/lines.sh
 fi

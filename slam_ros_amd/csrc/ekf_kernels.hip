@@ -1160,6 +1160,12 @@ constexpr int SPEC_K = 8;
 // and a more bit (36); B = local indices 4..7, written and read only when the count exceeds 4
 constexpr int LW_CNT = 32, LW_MORE = 36;
 constexpr int SPEC_PB = 2;                          // guessed columns per pass over the pending steps
+#ifndef EKF_F16_TILES_ALWAYS
+#define EKF_F16_TILES_ALWAYS 0
+#endif
+#ifndef EKF_F64_TILES_ALWAYS
+#define EKF_F64_TILES_ALWAYS 0
+#endif
 #ifndef EKF_SPEC_PB64
 #define EKF_SPEC_PB64 4
 #endif
@@ -4442,7 +4448,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
 #pragma unroll
                         for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = (float)pref[i][qq][j] * isc;
 #ifndef EKF_XP_BF_NO_TILES   // timing experiment (results invalid): no tile stream after the first
-                if (!LATE && more) load_tiles(nxt);
+                if (!LATE && (EKF_F16_TILES_ALWAYS || more)) load_tiles(EKF_F16_TILES_ALWAYS ? ldi : nxt);
 #endif
 #ifdef EKF_XP_TILE_WAIT   // timing experiment: wait for the next wave-tile's tiles right away
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -4453,7 +4459,8 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
 #endif
 #pragma unroll
                 for (int q = 0; q < NS; q++) {
-                    if (LATE && q == TQ && more) load_tiles(nxt);
+                    // (EKF_F16_TILES_ALWAYS: unconditional, the last wave-tile re-reads its own)
+                    if (LATE && q == TQ && (EKF_F16_TILES_ALWAYS || more)) load_tiles(EKF_F16_TILES_ALWAYS ? ldi : nxt);
                     // ring set of step q + RD − 1 (this wave-tile's, else the next one's)
                     const int ql = q + RD - 1;
 #ifndef EKF_XP_BF_NO_OPS
@@ -5141,7 +5148,13 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f64_wave_kernel(DowndateP
             next_item(nxt, nxt2);
             const Item ldi = more ? nxt : cur;   // the last wave-tile re-reads its own (no branch)
             to_acc(pref, acc);
+#if EKF_F64_TILES_ALWAYS
+            // unconditional (the last wave-tile re-reads its own tiles): a conditional prefetch
+            // makes the wait-count merge at the loop head drain every outstanding access
+            load_tiles(ldi, pref);
+#else
             if (more) load_tiles(nxt, pref);
+#endif
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int q = 0; q < NS; q++) {
