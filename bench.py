@@ -81,7 +81,7 @@ def parse():
                     help="1: overlap the association kernels with the previous group's flush")
     ap.add_argument("--flush-interval", type=int, default=0,
                     help="T: rewrite the landmark block once per T scans (0: 20 with f16x3, 12 "
-                         "with bf16x6 or in the survey world, 8 exact, 4 for f64)")
+                         "with bf16x6 or in the survey world, 8 exact and for f64)")
     ap.add_argument("--bcast-every", type=int, default=0,
                     help="scans per broadcast (default: the flush interval); broadcasts run one "
                          "group ahead of the scans that use them")
@@ -269,7 +269,7 @@ def main():
     if prec == ekf.PREC_F64:
         arith = ekf.ARITH_EXACT   # the split-bf16 flush serves fp32 operands (fp32 and fp16 storage)
     if args.flush_interval <= 0:
-        args.flush_interval = 4 if prec == ekf.PREC_F64 else (8 if arith == ekf.ARITH_EXACT else (20 if arith == ekf.ARITH_F16X3 else 12))
+        args.flush_interval = 8 if prec == ekf.PREC_F64 else (8 if arith == ekf.ARITH_EXACT else (20 if arith == ekf.ARITH_F16X3 else 12))
         if args.world == "survey" and arith != ekf.ARITH_EXACT and prec != ekf.PREC_F64:
             # SURVEY §8d's wide covariances carry the split arithmetic's per-group P error into the
             # state through large innovations: at T = 20 y reached 4.5e-8 within one group (bar
