@@ -121,19 +121,24 @@ def lib_sha(path):
 
 
 def find_traffic(explicit, sha, cfg):
-    """Counter-measured HBM bytes per launch for this build and configuration, or (None, why)."""
+    """Counter-measured HBM bytes per launch for this build and configuration, or (None, why).
+    Every profiles/*/traffic.json is considered (newest first): the first one of this configuration
+    measured on this very library build wins; files without a "world" key were measured in the
+    bench world."""
     paths = [explicit] if explicit else sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json")),
                                                 key=os.path.getmtime, reverse=True)
+    why = "no counter file for this configuration"
     for pth in paths:
         try:
             tj = json.load(open(pth))
         except (OSError, ValueError):
             continue
-        if all(tj.get(k) == v for k, v in cfg.items()):
-            if tj.get("lib_sha") != sha:
-                return None, f"{os.path.relpath(pth, ROOT)}: measured on another build ({tj.get('lib_sha')})"
-            return tj, os.path.relpath(pth, ROOT)
-    return None, "no counter file for this configuration"
+        if all(tj.get(k, "bench" if k == "world" else None) == v for k, v in cfg.items()):
+            if tj.get("lib_sha") == sha:
+                return tj, os.path.relpath(pth, ROOT)
+            if why.startswith("no counter"):
+                why = f"{os.path.relpath(pth, ROOT)}: measured on another build ({tj.get('lib_sha')})"
+    return None, why
 
 
 def reference_path_baseline(N):
@@ -404,7 +409,7 @@ def main():
     sha = lib_sha(ekf.LIB_PATH)
     tj, traffic_src = find_traffic(args.traffic_json, sha, {
         "capacity": N, "instances": E, "precision": args.precision, "flush_interval": args.flush_interval,
-        "pipeline": bool(args.pipeline), "kernel": dom["kernel"] if dom else None})
+        "pipeline": bool(args.pipeline), "kernel": dom["kernel"] if dom else None, "world": args.world})
     traffic = tj.get("hbm_bytes_per_launch") if tj else None
 
     out = {

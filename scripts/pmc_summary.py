@@ -82,7 +82,7 @@ def main(tag, out=None):
           "sq": {k: v for k, v in c.items() if k.startswith("SQ_") or k.startswith("GRBM")},
           "l2": {k: v for k, v in c.items() if k.startswith("TCC_HIT") or k.startswith("TCC_MISS")},
           "lib_sha": bench.lib_sha(ekf.LIB_PATH), "source": f"profiles/{tag}/counters_avg_per_dispatch.json",
-          "arith": cfg.get("arith")}
+          "arith": cfg.get("arith"), "world": cfg.get("world", "bench")}
     json.dump(tj, open(os.path.join(out, "traffic.json"), "w"), indent=1)
     print(json.dumps({k: tj[k] for k in ("kernel", "hbm_bytes_per_launch", "traffic_over_alg")}))
     # instructions per wave of the association kernel (SQ_INSTS_* / SQ_WAVES per dispatch) and per
