@@ -185,6 +185,10 @@ enum {
     /* test hook: e + 1 = on the speculative path, association workgroup 1 of instance e treats
      * its verdict poll as timed out while every other workgroup completes; 0 off (default) */
     EKF_OPT_TEST_VERDICT_TIMEOUT = 8,
+    /* 1 (default): the split-arithmetic flush skips the wave-tiles whose columns lie past every
+     * landmark with a nonzero operand row or new row in the group (unchanged by it: a partly
+     * filled map streams only its active part); 0: every wave-tile */
+    EKF_OPT_ACTIVE_FLUSH = 9,
 };
 int ekf_set_option(ekf_ctx* ctx, int option, int value);
 int ekf_get_option(const ekf_ctx* ctx, int option, int* value);

@@ -97,6 +97,7 @@ struct ekf_ctx {
     int test_drop;            // test hook (EKF_OPT_TEST_DROP_WG = e + 1): instance e's last workgroup never runs
     int test_verdict;         // test hook (EKF_OPT_TEST_VERDICT_TIMEOUT = e + 1)
     int mfrep_opt;            // EKF_OPT_MFMA_REPLAY
+    int active_flush;         // EKF_OPT_ACTIVE_FLUSH
     int mfrep;                // split-bf16 contexts: MFMA replay of pending steps (bf && mfrep_opt)
     int scan_batch;           // instances per association launch (co-residency bound)
     unsigned scan_epoch;      // association launches so far (mailbox tags)
@@ -474,6 +475,7 @@ static int create_ctx(const ekf_config* cfg, int sh_rank, int sh_world, ekf_ctx*
     c->test_drop = 0;
     c->test_verdict = 0;
     c->mfrep_opt = 1;
+    c->active_flush = 1;
     c->mfrep = c->bf ? 1 : 0;
     c->dbg = nullptr;
     ALLOC(c->mbox, sizeof(double) * 2 * c->G * c->mbw * E);
@@ -712,6 +714,7 @@ extern "C" int ekf_set_option(ekf_ctx* c, int opt, int v)
     case EKF_OPT_FLUSH_FORM: if (v != 0 && v != 2 && v != 8 && v != 24) return EKF_ERANGE; break;
     case EKF_OPT_FLUSH_BLOCKS_PER_CU: if (v < 1 || v > 16) return EKF_ERANGE; break;
     case EKF_OPT_MFMA_REPLAY:
+    case EKF_OPT_ACTIVE_FLUSH:
     case EKF_OPT_SCAN_STAMPS: if (v < 0 || v > 1) return EKF_ERANGE; break;
     case EKF_OPT_TEST_DROP_WG:
     case EKF_OPT_TEST_VERDICT_TIMEOUT: if (v < 0 || v > E) return EKF_ERANGE; break;
@@ -746,6 +749,7 @@ extern "C" int ekf_set_option(ekf_ctx* c, int opt, int v)
         break;
     case EKF_OPT_TEST_DROP_WG: c->test_drop = v; break;
     case EKF_OPT_TEST_VERDICT_TIMEOUT: c->test_verdict = v; break;
+    case EKF_OPT_ACTIVE_FLUSH: c->active_flush = v; break;
     }
     return EKF_OK;
 }
@@ -762,6 +766,7 @@ extern "C" int ekf_get_option(const ekf_ctx* c, int opt, int* v)
     case EKF_OPT_SCAN_STAMPS: *v = c->dbg ? 1 : 0; break;
     case EKF_OPT_TEST_DROP_WG: *v = c->test_drop; break;
     case EKF_OPT_TEST_VERDICT_TIMEOUT: *v = c->test_verdict; break;
+    case EKF_OPT_ACTIVE_FLUSH: *v = c->active_flush; break;
     default: return EKF_EINVAL;
     }
     return EKF_OK;
@@ -904,6 +909,8 @@ static int enqueue_flush(ekf_ctx* c)
     dp.slot0 = (int)(c->unflushed0 % (long long)c->ring.size());
     dp.dbg = c->dbg;
     dp.bf = c->pmode;
+    // the association kernel's RES_ZMAX bound (partitioned contexts write other records)
+    dp.zskip = (c->active_flush && c->sh_world == 0) ? 1 : 0;
     dp.bbase = c->ops_b;
     dp.bslot_bytes = c->bslot_bytes;
     for (int q = 0; q < nst; q++) dp.steps[q] = slot_of(c, c->unflushed0 + q);

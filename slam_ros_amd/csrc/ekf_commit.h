@@ -13,12 +13,16 @@ namespace ekf {
 // from before the call (the launch wrote only the inactive copy of the robot strip and mean).
 EKF_HD unsigned done_word(unsigned epoch, int status) { return ((epoch & 0xffffffu) << 8) | ((unsigned)status & 0xffu); }
 
+// bit 7 of a completion word (not a status bit): the workgroup wrote a nonzero operand row this
+// step (its landmarks bound the downdate's nonzero columns: RES_ZMAX)
+constexpr unsigned DONE_NZ = 128u;
+
 // The lead's decision from the G completion words as last seen (words[0] is its own): the OR of
 // the status bits, with EKF_ST_SYNC_TIMEOUT added for every word not (yet) of this epoch. The
 // launch commits iff the result has no timeout bit.
 EKF_HD int commit_fold(int st, unsigned word, unsigned epoch)
 {
-    return st | (((word >> 8) != (epoch & 0xffffffu)) ? (int)EKF_ST_SYNC_TIMEOUT : (int)(word & 0xffu));
+    return st | (((word >> 8) != (epoch & 0xffffffu)) ? (int)EKF_ST_SYNC_TIMEOUT : (int)(word & 0x7fu));
 }
 
 EKF_HD int commit_status(const unsigned* words, int G, unsigned epoch)

@@ -38,6 +38,8 @@ enum {
     RES_MATCH = 16,                     // [EKF_MAX_LINES]
     RES_EXTRA = 16 + EKF_MAX_LINES,     // [EKF_MAX_LINES] line indices, in order
     RES_PSIG = 16 + 2 * EKF_MAX_LINES,  // EKF_ARITH_F16X3: the plane exponent σ of this step's planes
+    RES_ZMAX = 17 + 2 * EKF_MAX_LINES,  // landmarks at or past this index have zero operand rows and no
+                                        // new rows this step (workgroup granularity)
     RES_STRIDE = 16 + 2 * EKF_MAX_LINES + 4,
 };
 
@@ -195,6 +197,7 @@ struct DowndateParams {
     long long bslot_bytes;
     int bf;               // plain groups of 2..16 steps (even) run the split-plane wave flush:
                           // 1 EKF_ARITH_BF16X6, 2 EKF_ARITH_F16X3 (σ of each step in RES_PSIG)
+    int zskip;            // split-plane wave flush: skip wave-tiles past every step's RES_ZMAX
     const int* wt24;      // [nwt24] split-bf16 wave-tiles of 2 × 4 tiles (wr | wc << 16), panel order
     int nwt24;
     Slot steps[PMAX];

@@ -890,9 +890,11 @@ __device__ __forceinline__ void publish_done(int* sync, int g, unsigned epoch, i
 // Run by every thread of workgroup 0 (the words are polled in parallel, thread k word k); the
 // folded status of all G words (= commit_status) is returned to every thread.
 __device__ __forceinline__ int lead_collect(int* sync, int G, unsigned epoch, int own_status, int spin,
-                                            int tid, int* sh_red)
+                                            int tid, int* sh_red, int& zg)
 {
+    // zg: 1 + the highest workgroup whose word carries DONE_NZ (0: none)
     int st = tid == 0 ? commit_fold(0, done_word(epoch, own_status), epoch) : 0;
+    int z = (tid == 0 && (own_status & (int)DONE_NZ)) ? 1 : 0;
     const bool late0 = (own_status & EKF_ST_TIMEOUT_BIT) != 0;
     for (int k = 1 + tid; k < G; k += SCAN_BLOCK) {
         const unsigned* w = reinterpret_cast<const unsigned*>(&sync[SYNC_WG0 + k]);
@@ -905,15 +907,24 @@ __device__ __forceinline__ int lead_collect(int* sync, int G, unsigned epoch, in
             v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         st = commit_fold(st, v, epoch);
+        if ((v >> 8) == (epoch & 0xffffffu) && (v & DONE_NZ)) z = max(z, k + 1);
     }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) st |= __shfl_xor(st, off, 64);
+    for (int off = 32; off > 0; off >>= 1) {
+        st |= __shfl_xor(st, off, 64);
+        z = max(z, __shfl_xor(z, off, 64));
+    }
     __syncthreads();
-    if ((tid & 63) == 0) sh_red[tid >> 6] = st;
+    if ((tid & 63) == 0) sh_red[tid >> 6] = st | (z << 8);
     __syncthreads();
     st = 0;
+    z = 0;
 #pragma unroll
-    for (int w = 0; w < SCAN_BLOCK / 64; w++) st |= sh_red[w];
+    for (int w = 0; w < SCAN_BLOCK / 64; w++) {
+        st |= sh_red[w] & 0xff;
+        z = max(z, sh_red[w] >> 8);
+    }
+    zg = z;
     return st;
 }
 
@@ -1710,7 +1721,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         }
         if (tid == 0 && g != 0) publish_done(sync, g, p.epoch, 0);
         if (g == 0) {
-            const int st = lead_collect(sync, G, p.epoch, 0, p.spin_log2, tid, sh_red);
+            int zg_unused = 0;
+            const int st = lead_collect(sync, G, p.epoch, 0, p.spin_log2, tid, sh_red, zg_unused);
             if (lead) sync[SYNC_WG0] = (int)done_word(p.epoch, st);
             if (lead && !(st & EKF_ST_TIMEOUT_BIT)) {
                 for (int a = 0; a < 9; a++) Rsw[(a / 3) * n + (a % 3)] = R33[a];
@@ -1832,7 +1844,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
 
     // writes a match's owned rows: U/V history and the MFMA downdate operands
     // F: the line's symmetric operand factor (sym_factor; unused otherwise)
+    bool nzr = false;   // this thread wrote a nonzero operand row (DONE_NZ, RES_ZMAX)
     auto store_rows = [&](int t, const double kk[4], const double uu[4], bool vhist, const float F[3]) {
+        nzr = nzr || kk[0] != 0.0 || kk[1] != 0.0 || kk[2] != 0.0 || kk[3] != 0.0 || uu[0] != 0.0 ||
+              uu[1] != 0.0 || uu[2] != 0.0 || uu[3] != 0.0;
         if (t < HIST_LDS)
             sh_uhist[t][tid] = make_double4(uu[0], uu[1], uu[2], uu[3]);
         else
@@ -3035,6 +3050,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     }
                 }
             }
+        if (__ballot(nzr) != 0ull) st |= (int)DONE_NZ;
         if ((tid & 63) == 0 && tid < SCAN_THREADS) sh_red[tid >> 6] = st;
         __syncthreads();
 #pragma unroll
@@ -3050,7 +3066,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // finishes with the timeout bit (above); only its completion word tells the lead.
     EKF_STAMP(25);
     if (tid == 0 && g != 0) publish_done(sync, g, p.epoch, wgst);
-    if (g == 0 && (sequential || G > 1)) wgst = lead_collect(sync, G, p.epoch, wgst, p.spin_log2, tid, sh_red);
+    int zg = (wgst & (int)DONE_NZ) ? 1 : 0;
+    if (g == 0 && (sequential || G > 1)) wgst = lead_collect(sync, G, p.epoch, wgst, p.spin_log2, tid, sh_red, zg);
+    wgst &= ~(int)DONE_NZ;
     EKF_STAMP(26);
     if (lead) {
         sync[SYNC_WG0] = (int)done_word(p.epoch, wgst);
@@ -3076,6 +3094,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             res[RES_KSTEPS] = (sizeof(C) == 4) ? m : (m + 1) / 2;
             res[RES_ROLLBACK] = 0;
             res[RES_PSIG] = psig;
+            // nonzero operand rows only below zg workgroups' landmarks; new rows below s + nadd
+            res[RES_ZMAX] = max(min(zg * SCAN_THREADS, N), reset ? 0 : s + nadd);
             p.saved[e] = reset ? 0 : s + nadd;
             p.live[e] = 1 - cb;
             if (pf16) {
@@ -3102,6 +3122,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             res[RES_NADD] = 0;
             res[RES_KSTEPS] = 0;
             res[RES_ROLLBACK] = 1;
+            res[RES_ZMAX] = 0;
             for (int i = 0; i < L; i++) res[RES_MATCH + i] = -1;
         }
     }
@@ -4232,7 +4253,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
 
     // a wave-tile: instance, table entry (scalar registers)
     struct Item {
-        int e, li;
+        int e, li, g;   // instance, table entry, flat index (g0 + k·K)
         WtEntry w;
     };
     typedef int i32x8 __attribute__((ext_vector_type(8)));
@@ -4252,6 +4273,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
         const int li = g0 - t.e * nwt;
         load_entry(li, t.w);
         t.li = li;
+        t.g = g0;
     };
     auto next_item = [&](const Item& c, Item& t) __attribute__((always_inline)) {
         int li = c.li + K, e = c.e;
@@ -4262,6 +4284,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
         t.e = e;
         load_entry(e < p.E ? li : 0, t.w);
         t.li = li;
+        t.g = c.g + K;
     };
     auto tile_ptr = [&](const Item& t, int i) __attribute__((always_inline)) {
         return (size_t)t.e * inst_elems + (size_t)t.w.tile[i] * TILE_ELEMS;
@@ -4361,7 +4384,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
             // added after the instance's last reset of the group are nonzero at its end, so the
             // union is taken over those steps and every other wave-tile of the instance is stored
             // as zero (rz); σ changes before that reset do not matter.
-            int st_e = -1, u_lo = 0, u_hi = 0, sg0 = 0, sgl = 0;
+            int st_e = -1, u_lo = 0, u_hi = 0, sg0 = 0, sgl = 0, zl = 0;
             unsigned smask = 0;
             bool rz = false;
             auto load_steps = [&](int e) __attribute__((always_inline)) {
@@ -4369,9 +4392,11 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                 u_hi = 0;
                 smask = 0;
                 rz = false;
+                zl = 0;   // landmarks past every step's RES_ZMAX: zero V rows, no new rows
                 int prev = 0;
 #pragma unroll
                 for (int q = 0; q < NS; q++) {
+                    zl = max(zl, rec_of(e, q, RES_ZMAX));
                     if (rec_of(e, q, RES_RESET)) {   // (its own new rows are wiped with the map)
                         u_lo = 0x7fffffff;
                         u_hi = 0;
@@ -4410,10 +4435,30 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                 const bool tc = touched(t);
                 return rz && !tc;
             };
+            // a wave-tile whose columns all lie past zl is unchanged by the group (its V-side rows
+            // are zero in every step, and no step writes new rows there): not loaded, not stored
+            // (a reset zeroes the block: no skipping then)
+            auto dead = [&](const Item& t) __attribute__((always_inline)) {
+                if (!p.zskip || t.e >= p.E) return false;
+                if (t.e != st_e) load_steps(t.e);
+                return !rz && (t.w.rc >> 16) * WT_C * 16 >= zl;
+            };
+            auto next_live = [&](const Item& c, Item& t) __attribute__((always_inline)) {
+                next_item(c, t);
+                while (t.g < g_end && dead(t)) {
+                    const Item u = t;
+                    next_item(u, t);
+                }
+            };
             Item cur, nxt, nxt2;
             bool any_skip = false;
             first_item(cur);
-            next_item(cur, nxt);
+            while (cur.g < g_end && dead(cur)) {
+                const Item u = cur;
+                next_item(u, cur);
+            }
+            if (cur.g >= g_end) return;   // (no live wave-tile: nothing to store, no second pass)
+            next_live(cur, nxt);
             load_tiles(cur);
 #ifdef EKF_XP_BF_NO_OPS   // timing experiment (results invalid): operands loaded once, never in the loop
 #pragma unroll
@@ -4422,7 +4467,6 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
 #pragma unroll
             for (int q = 0; q < RD - 1; q++) load_ops(q, cur, q);
 #endif
-            int g = g0;
 #ifdef EKF_XP_FLUSH_STAMPS   // timing experiment: shader cycles per wave-tile section, in-kernel clock
             unsigned long long xs_b = 0, xs_m = 0, xs_s = 0, xs_n = 0;
             const unsigned long long xc0 = __builtin_amdgcn_s_memtime(), xr0 = __builtin_amdgcn_s_memrealtime();
@@ -4431,8 +4475,8 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
 #ifdef EKF_XP_FLUSH_STAMPS
                 const unsigned long long xt0 = __builtin_amdgcn_s_memtime();
 #endif
-                const bool more = g + K < g_end;
-                next_item(nxt, nxt2);
+                const bool more = nxt.g < g_end;
+                next_live(nxt, nxt2);
                 const Item ldi = more ? nxt : cur;   // the last wave-tile re-reads its own rows
                 // a wave-tile holding a landmark some step of the group added, or of an instance whose
                 // σ changes inside the group, is computed here but stored to the sink: the second pass
@@ -4527,7 +4571,6 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                 xs_b += xt1 - xt0; xs_m += xt2 - xt1; xs_s += xt3 - xt2; xs_n += 1;
 #endif
                 if (!more) break;
-                g += K;
                 cur = nxt;
                 nxt = nxt2;
             }
@@ -4551,7 +4594,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                         next_item(t, nn);
                         t = nn;
                     }
-                    if (skip_of(t)) wt_general<TS, NS>(p, t.e, t.w, lane);
+                    if (!dead(t) && skip_of(t)) wt_general<TS, NS>(p, t.e, t.w, lane);
                 }
             }
             return;

@@ -83,7 +83,7 @@ def test_library_reads_no_environment(ekf_mod):
     src = open(HEADER).read()
     for name in ("EKF_OPT_SPECULATE", "EKF_OPT_SPIN_LOG2", "EKF_OPT_FLUSH_FORM", "EKF_OPT_FLUSH_BLOCKS_PER_CU",
                  "EKF_OPT_MFMA_REPLAY", "EKF_OPT_SCAN_STAMPS", "EKF_OPT_TEST_DROP_WG",
-                 "EKF_OPT_TEST_VERDICT_TIMEOUT"):
+                 "EKF_OPT_TEST_VERDICT_TIMEOUT", "EKF_OPT_ACTIVE_FLUSH"):
         assert name in src
         assert getattr(ekf_mod, name[4:]) == int(re.search(name + r" = (\d+)", src).group(1))
 

@@ -707,6 +707,49 @@ def test_f64_wave_flush_equals_tile_kernel(ekf_mod, monkeypatch, N, T, lines, ex
         assert sa == sb
 
 
+@pytest.mark.parametrize("arith", [1, 2])
+@pytest.mark.parametrize("N,active,T,extra_every", [(1024, 300, 12, 3), (4096, 1500, 20, 4), (512, 100, 8, 0),
+                                                     (1024, 1014, 12, 0)])
+def test_active_flush_equals_full_flush(ekf_mod, arith, N, active, T, extra_every):
+    """A partly filled map: the split flush that skips the wave-tiles past every step's nonzero
+    operand rows and new rows (EKF_OPT_ACTIVE_FLUSH = 1, default) leaves P, y and the matches
+    equal to the flush over every wave-tile (0), with new landmarks appended inside the groups
+    and groups of several lengths."""
+    if arith == 1 and T > 16:
+        pytest.skip("EKF_ARITH_BF16X6 takes flush_interval <= 16")
+    E = 3
+    w = G.make_world(N, active=active)
+    st = G.initial_state(w)
+    a = ekf_mod.Ensemble(N, E, 1, max_lines=8, flush_interval=T, arith=arith)
+    b = ekf_mod.Ensemble(N, E, 1, max_lines=8, flush_interval=T, arith=arith, options={"active_flush": 0})
+    assert a.get_option("active_flush") == 1 and b.get_option("active_flush") == 0
+    for ens in (a, b):
+        for e in range(E):
+            ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+    rng = np.random.default_rng(11)
+    for step in range(1, 2 * T + 3):
+        enc, ln, nl = G.make_scan(w, step, instances=E, lines=6 if extra_every else 8)
+        if extra_every:
+            ex = G.random_lines(rng, 2)[None].repeat(E, axis=0)
+            if step % extra_every == 0:
+                ln = np.concatenate([ln, ex], axis=1)
+                nl = np.full(E, ln.shape[1], dtype=np.int32)
+        ra = a.localize(enc, ln, nl)
+        rb = b.localize(enc, ln, nl)
+        for e in range(E):
+            assert ra[e]["match"] == rb[e]["match"], (step, e)
+            assert ra[e]["status"] == rb[e]["status"] == 0
+    for e in range(E):
+        Pa, ya, sa, pa = a.download_state(e)
+        Pb, yb, sb, pb = b.download_state(e)
+        bad = np.argwhere(Pa != Pb)
+        assert bad.size == 0, (e, bad[:12].tolist(), rel(Pa, Pb))
+        np.testing.assert_array_equal(ya, yb)
+        assert sa == sb
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("N,T,lines", [(2000, 4, 8), (4096, 4, 8), (100, 8, 8), (300, 6, 5)])
 def test_f64_mfma_replay_equals_per_element_replay(ekf_mod, N, T, lines):
     """fp64 storage, speculative association with pending steps: the owned blocks of the guessed
