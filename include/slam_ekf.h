@@ -62,10 +62,19 @@ enum {
                                 exchange within the spin bound: the call is rolled back (the
                                 instance keeps its state from before the call, as if the scan had
                                 not been received; the result record reports no matches) */
-    EKF_ST_RANGE = 16,     /* EKF_PREC_F16 only: a landmark this call added has a variance above a
+    EKF_ST_RANGE = 16,     /* EKF_PREC_F16: a landmark this call added has a variance above a
                               quarter of the fp16 range at the instance's storage exponent
                               (2^exp·P stored; values are still finite). ekf_rescale re-chooses
-                              the exponent; ignoring it lets later landmarks saturate to ±inf. */
+                              the exponent; ignoring it lets later landmarks saturate to ±inf.
+                              EKF_PREC_F32: a new landmark variance above 2^120, within 2^8 of
+                              fp32's range (a diverged filter: the fp64 storage holds it) */
+    EKF_ST_PRECISION = 32, /* EKF_PREC_F32: the call's update shrank some landmark's variance (the
+                              trace of its 2x2 block) by more than 2^4, or left it non-positive:
+                              more than 4 of fp32's 24 significant bits cancel, so the stored
+                              block is no longer guaranteed to resolve the fp64 reference to the
+                              1e-6 bar (informational: the state commits; EKF_PREC_F64 holds any
+                              filter). In SURVEY §8d's world the reference's own motion model runs
+                              away and this is how a diverging instance shows */
 };
 
 /* storage precision of the landmark-landmark covariance block (robot rows, mean: always fp64).
@@ -173,8 +182,11 @@ enum {
     EKF_OPT_FLUSH_FORM = 3,
     /* workgroups per CU of the grid-strided flush forms, 1..16 (8) */
     EKF_OPT_FLUSH_BLOCKS_PER_CU = 4,
-    /* pending steps applied on read by MFMA (1, default): split arithmetics on the operand planes,
-     * fp64 storage by the flush's own f64 MFMA (bit-identical); 0: the per-element replay forms */
+    /* pending steps applied on read by MFMA. 1 (default): split arithmetics by fp32 MFMA on the
+     * fp32 operand rows (exact products: within a flush group the association reads the block at
+     * the EXACT arithmetic's precision; the split products enter P only at the flush), fp64
+     * storage by the flush's own f64 MFMA (bit-identical); 2: split arithmetics by their own split
+     * products on the operand planes (round 4); 0: the per-element replay forms */
     EKF_OPT_MFMA_REPLAY = 5,
     /* 1: the association kernel's instrumented instantiation with phase timers
      * (ekf_debug_scan_stamps); 0 (default) the product kernel */
@@ -217,6 +229,9 @@ int ekf_read_results(ekf_ctx* ctx, ekf_result* out);
  * n×n P_t0 (Robot.h:62) in fp64; y is Robot::y (Robot.h:26); pose = xPos/yPos/thetaPos. */
 int ekf_upload_state(ekf_ctx* ctx, int e, const double* P_full, const double* y, int saved,
                      const double pose[3]);
+/* Any pointer may be NULL. With P_full the call drains first (the pending downdates are flushed);
+ * without it, it only waits for the context's stream: the mean, pose and savedLineCount are
+ * committed by every scan, and the flush schedule is left as it is. */
 int ekf_download_state(ekf_ctx* ctx, int e, double* P_full, double* y, int* saved,
                        double pose[3]);
 /* Device-side initialisation P = diag(d) + U·Uᵀ (U: n×rank row-major, host pointers). */

@@ -1,0 +1,105 @@
+"""Where does the state-vector error of the split arithmetics come from in SURVEY §8d's world?
+
+Runs the survey world (N = 4096, E = 8, L = 8) on the GPU for `pre` untimed scans, then `scans`
+scans with instances 0 and 7 checked against the restatement (oracle/, fast mode) re-synced to the
+GPU state at every flush-group end. Per group and instance: ‖ΔP‖_F/‖P‖_F, ‖Δy‖/‖y‖, the absolute
+pose and landmark parts of Δy, ‖y‖, the map size and whether the group held a reset.
+
+usage: python scripts/r05/survey_parity.py ARITH:T[:opt=v...][,ARITH:T...] [pre] [scans]
+(ARITH in exact, bf16x6, f16x3). One JSON line per configuration.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from slam_ros_amd import ekf, scan_gen as G  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+N, E, L = int(os.environ.get("SP_N", "4096")), 8, 8
+PER_SCAN = os.environ.get("SP_PER_SCAN", "0") == "1"   # y and pose re-synced every scan
+CHECK = (0, 7)
+ARITH = {"exact": ekf.ARITH_EXACT, "bf16x6": ekf.ARITH_BF16X6, "f16x3": ekf.ARITH_F16X3}
+
+
+def rel(a, b):
+    nb = np.linalg.norm(b)
+    return float(np.linalg.norm(a - b) / (nb if nb > 0 else 1.0))
+
+
+def run(arith, T, pre, scans, options=None):
+    w = G.make_world(N)
+    st = G.initial_state(w, profile="survey")
+    ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=L, flush_interval=T, arith=ARITH[arith],
+                       options=options or {})
+    for e in range(E):
+        ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+    for s in range(1, pre + 1):
+        enc, lines, nl = G.make_scan(w, s, instances=E, profile="survey")
+        ens.localize(enc, lines, nl)
+    ens.sync()
+    refs = {}
+    for e in CHECK:
+        refs[e] = O.OracleRobot(N, mode=O.FAST, omp=True)
+        refs[e].set_state(*ens.download_state(e))
+    groups, cur, seq = [], {e: {"resets": 0, "added": 0, "matches": 0} for e in CHECK}, 0
+    t0 = time.time()
+    for k in range(scans):
+        s = pre + 1 + k
+        enc, lines, nl = G.make_scan(w, s, instances=E, profile="survey")
+        res = ens.localize(enc, lines, nl)
+        for e in range(E):
+            seq += 1 if int(ens.result_words(e)[9]) & 16 else 0
+        for e in CHECK:
+            m = refs[e].localize(lines[e], enc[e])
+            if res[e]["match"] != m:
+                cur[e]["assoc_diff"] = cur[e].get("assoc_diff", 0) + 1
+                if not PER_SCAN:
+                    raise AssertionError((arith, T, s, e, res[e]["match"], m))
+            cur[e]["resets"] += res[e]["reset"]
+            cur[e]["added"] += res[e]["new_landmarks"]
+            cur[e]["matches"] += res[e]["matches"]
+            cur[e]["status"] = cur[e].get("status", 0) | res[e]["status"]
+            if PER_SCAN:
+                # the state vector and pose are committed every scan: compare them per scan from
+                # identical inputs (re-synced every scan; P only at the group ends)
+                _, yg, sg, pg = ens.download_state(e, with_P=False)
+                cur[e]["y_scan"] = max(cur[e].get("y_scan", 0.0), rel(yg, refs[e].y))
+                refs[e].set_state(None, yg, sg, pg)
+        if (k + 1) % T == 0 or k + 1 == scans:
+            g = {"end": k + 1}
+            for e in CHECK:
+                P, y, saved, pose = ens.download_state(e)
+                yr = refs[e].y
+                dy = y - yr
+                g[str(e)] = dict(cur[e], p_rel=rel(P, refs[e].P_t0), y_rel=rel(y, yr),
+                                 y_norm=float(np.linalg.norm(yr)), dy_pose=float(np.abs(dy[:3]).max()),
+                                 dy_lm=float(np.linalg.norm(dy[3:])), dy_lm_max=float(np.abs(dy[3:]).max()),
+                                 saved=int(saved), trP=float(np.trace(refs[e].P_t0)),
+                                 P_robot_max=float(np.abs(refs[e].P_t0[:3, :3]).max()), P_max=float(np.abs(P).max()))
+                refs[e].set_state(P, y, saved, pose)
+                del P
+                cur[e] = {"resets": 0, "added": 0, "matches": 0}
+            groups.append(g)
+            print(f"  {arith} T={T} group end {k + 1}: " + " ".join(
+                f"e{e} p {g[str(e)]['p_rel']:.2e} y {g[str(e)]['y_rel']:.2e} yscan {g[str(e)].get('y_scan', 0):.2e} "
+                f"st {g[str(e)].get('status', 0)} ad {g[str(e)].get('assoc_diff', 0)}" for e in CHECK), file=sys.stderr, flush=True)
+    ens.close()
+    worst_y = max(g[str(e)].get("y_scan", g[str(e)]["y_rel"]) for g in groups for e in CHECK)
+    worst_p = max(g[str(e)]["p_rel"] for g in groups for e in CHECK)
+    return {"arith": arith, "T": T, "pre": pre, "scans": scans, "options": options or {},
+            "worst_p": worst_p, "worst_y": worst_y, "sequential_frac": seq / (E * scans),
+            "groups": groups, "secs": time.time() - t0}
+
+
+if __name__ == "__main__":
+    cfgs = [c.split(":") for c in sys.argv[1].split(",")]
+    pre = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    scans = int(sys.argv[3]) if len(sys.argv) > 3 else 48
+    for c in cfgs:   # ARITH:T[:option=value...]
+        opts = {k: int(v) for k, v in (o.split("=") for o in c[2:])}
+        print(json.dumps(run(c[0], int(c[1]), pre, scans, opts)), flush=True)

@@ -33,12 +33,39 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(p) > t for p in deps)
 
 
+# MFMA accumulators in VGPRs (not AGPRs): the fp16 flush rounds every accumulator after each
+# step on the VALU, which cannot read AGPRs, so the AGPR form paid a read + write copy per
+# element per step (fp16 flush 0.84 -> 0.72 ms at N=4096, T=8; fp32 unchanged or faster)
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-mllvm", "-amdgpu-mfma-vgpr-form"]
+# ekf_kernels.hip is compiled as three units (EKF_TU: 1 association kernels, 2 flush kernels, 3 the
+# rest), in parallel with ekf_api.hip: each unit instantiates only the kernels its launchers use
+UNITS = [("ekf_kernels.hip", 1), ("ekf_kernels.hip", 2), ("ekf_kernels.hip", 3), ("ekf_api.hip", 0)]
+
+
+def _compile_link(out: str, defines: list[str], verbose: bool = False) -> None:
+    objdir = out + ".objs"
+    os.makedirs(objdir, exist_ok=True)
+    procs, objs = [], []
+    for src, tu in UNITS:
+        obj = os.path.join(objdir, f"{os.path.splitext(src)[0]}_{tu}.o")
+        cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, *[f"-D{d}" for d in defines],
+               *([f"-DEKF_TU={tu}"] if tu else []), "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    if any(p.wait() != 0 for p in procs):
+        raise subprocess.CalledProcessError(1, "hipcc (libslam_ekf units)")
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    shutil.rmtree(objdir, ignore_errors=True)
+
+
 def build_variant(out: str, defines: list[str]) -> str:
     """An A/B build of the same sources with extra -D flags (scripts only; SLAM_EKF_LIB)."""
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-mllvm", "-amdgpu-mfma-vgpr-form", *[f"-D{d}" for d in defines],
-           "-o", out] + [os.path.join(CSRC, s) for s in SOURCES]
-    subprocess.run(cmd, check=True)
+    _compile_link(out, defines)
     return out
 
 
@@ -50,15 +77,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB_PATH
     os.makedirs(LIB_DIR, exist_ok=True)
     tmp = LIB_PATH + ".tmp"
-    # MFMA accumulators in VGPRs (not AGPRs): the fp16 flush rounds every accumulator after each
-    # step on the VALU, which cannot read AGPRs, so the AGPR form paid a read + write copy per
-    # element per step (fp16 flush 0.84 -> 0.72 ms at N=4096, T=8; fp32 unchanged or faster)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-mllvm", "-amdgpu-mfma-vgpr-form",
-           "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    _compile_link(tmp, [], verbose)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
 

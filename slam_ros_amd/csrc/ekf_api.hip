@@ -711,9 +711,14 @@ extern "C" int ekf_set_option(ekf_ctx* c, int opt, int v)
     switch (opt) {
     case EKF_OPT_SPECULATE: if (v < 0 || v > 2) return EKF_ERANGE; break;
     case EKF_OPT_SPIN_LOG2: if (v < 8 || v > 24) return EKF_ERANGE; break;
-    case EKF_OPT_FLUSH_FORM: if (v != 0 && v != 2 && v != 8 && v != 24) return EKF_ERANGE; break;
+    case EKF_OPT_FLUSH_FORM:
+        if (v != 0 && v != 2 && v != 8 && v != 24) return EKF_ERANGE;
+        // a partitioned context stores only its tile rows; only the wave forms walk the rank's
+        // wave tables (the super-tile and tile forms walk every tile of the block)
+        if (c->sh_world > 0 && v != 8) return EKF_EINVAL;
+        break;
     case EKF_OPT_FLUSH_BLOCKS_PER_CU: if (v < 1 || v > 16) return EKF_ERANGE; break;
-    case EKF_OPT_MFMA_REPLAY:
+    case EKF_OPT_MFMA_REPLAY: if (v < 0 || v > 2) return EKF_ERANGE; break;
     case EKF_OPT_ACTIVE_FLUSH:
     case EKF_OPT_SCAN_STAMPS: if (v < 0 || v > 1) return EKF_ERANGE; break;
     case EKF_OPT_TEST_DROP_WG:
@@ -732,7 +737,7 @@ extern "C" int ekf_set_option(ekf_ctx* c, int opt, int v)
         break;
     case EKF_OPT_MFMA_REPLAY:
         c->mfrep_opt = v;
-        c->mfrep = (c->bf && v) ? 1 : 0;
+        c->mfrep = c->bf ? v : 0;
         break;
     case EKF_OPT_SCAN_STAMPS:
         if (v && !c->dbg) {
@@ -909,8 +914,6 @@ static int enqueue_flush(ekf_ctx* c)
     dp.slot0 = (int)(c->unflushed0 % (long long)c->ring.size());
     dp.dbg = c->dbg;
     dp.bf = c->pmode;
-    // the association kernel's RES_ZMAX bound (partitioned contexts write other records)
-    dp.zskip = (c->active_flush && c->sh_world == 0) ? 1 : 0;
     dp.bbase = c->ops_b;
     dp.bslot_bytes = c->bslot_bytes;
     for (int q = 0; q < nst; q++) dp.steps[q] = slot_of(c, c->unflushed0 + q);
@@ -924,6 +927,10 @@ static int enqueue_flush(ekf_ctx* c)
     const int out = c->cfg.pipeline ? 1 - in : in;
     dp.Pin = xview(c, in);
     dp.Pout = xview(c, out);
+    // the association kernel's RES_ZMAX bound (partitioned contexts write other records). A
+    // skipped wave-tile is neither loaded nor stored, so it stays valid only in place: a
+    // double-buffered (pipelined) flush would leave X[out]'s copy from two flushes earlier
+    dp.zskip = (c->active_flush && c->sh_world == 0 && in == out) ? 1 : 0;
     EvPair* pr = prof_begin(c, 1, fs, false);
     if (pr) c->ev_nsteps.push_back(nst);
     HIP_TRY(ekf::launch_downdate(dp, c->cfg.precision, c->dd_grid, fs, pr ? pr->a : nullptr,
@@ -1024,7 +1031,7 @@ extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
             for (int gq = 0; gq < c->G; gq++)
                 st = ekf::commit_fold(st, (unsigned)hs[(size_t)e * c->sync_stride + ekf::SYNC_WG0 + gq],
                                       c->scan_epoch);
-            c->h_res[(size_t)e * ekf::RES_STRIDE + ekf::RES_STATUS] |= st;
+            c->h_res[(size_t)e * ekf::RES_STRIDE + ekf::RES_STATUS] |= st & ekf::DONE_STATUS_MASK;
         }
     if (!out) return EKF_OK;
     for (int e = 0; e < E; e++) {
@@ -1146,7 +1153,12 @@ extern "C" int ekf_download_state(ekf_ctx* c, int e, double* P, double* y, int* 
 {
     if (!c) return EKF_EINVAL;
     if (e < 0 || e >= c->cfg.instances) return EKF_ERANGE;
-    int rc = drain(c);
+    // P drains (the pending downdates are flushed first); the mean, pose and savedLineCount are
+    // committed by every association kernel, so without P the call only waits for the stream and
+    // leaves the flush schedule as it is
+    int rc = EKF_OK;
+    if (P) rc = drain(c);
+    else HIP_TRY(hipStreamSynchronize(c->stream));
     if (rc) return rc;
     const Dims& d = c->d;
     int cb = 0;

@@ -16,6 +16,11 @@ EKF_HD unsigned done_word(unsigned epoch, int status) { return ((epoch & 0xfffff
 // bit 7 of a completion word (not a status bit): the workgroup wrote a nonzero operand row this
 // step (its landmarks bound the downdate's nonzero columns: RES_ZMAX)
 constexpr unsigned DONE_NZ = 128u;
+// bit 6 (not a status bit): a landmark of the workgroup is below the split-fp16 planes' dynamic
+// range this step (PLANE_VAR_MIN); the lead records the step's σ as PLANE_SIGMA_EXACT
+constexpr unsigned DONE_PLOSS = 64u;
+// the status bits of a completion word (the rest are DONE_* flags)
+constexpr int DONE_STATUS_MASK = 0x3f;
 
 // The lead's decision from the G completion words as last seen (words[0] is its own): the OR of
 // the status bits, with EKF_ST_SYNC_TIMEOUT added for every word not (yet) of this epoch. The

@@ -11,9 +11,17 @@ namespace ekf {
 
 enum { PHASE_PREDICT = 1, PHASE_UPDATE = 2, PHASE_BOTH = 3 };
 enum { EKF_ST_SINGULAR = EKF_ST_SINGULAR_S, EKF_ST_CAP = EKF_ST_CAPACITY, EKF_ST_NSYM = EKF_ST_NONSYM,
-       EKF_ST_TIMEOUT_BIT = EKF_ST_SYNC_TIMEOUT, EKF_ST_RANGE_BIT = EKF_ST_RANGE };
+       EKF_ST_TIMEOUT_BIT = EKF_ST_SYNC_TIMEOUT, EKF_ST_RANGE_BIT = EKF_ST_RANGE,
+       EKF_ST_PRECISION_BIT = EKF_ST_PRECISION };
+// fp32 storage: a scan that shrinks an owned landmark's variance trace by more than 2^4 sets
+// EKF_ST_PRECISION: the cancellation leaves fewer than 20 of fp32's 24 significant bits, i.e. a
+// stored result no longer guaranteed to 2^-20 ≈ 1e-6 relative (the P bar) element by element
+constexpr double PREC_CANCEL = 16.0;
 // fp16 storage: a stored variance above 2^14 (a quarter of the fp16 range) raises EKF_ST_RANGE
 constexpr double F16_RANGE_WARN = 16384.0;
+// fp32 storage: a new landmark variance above 2^120 (fp32's largest finite value is ≈2^128) sets
+// EKF_ST_RANGE too
+constexpr double F32_RANGE_WARN = 1.329227995784916e36;   // 2^120
 constexpr int F16_EXP_DEFAULT = 10;
 
 // per-instance synchronisation words of the association kernel (never reset): a monotonic
@@ -106,8 +114,9 @@ struct ScanParams {
                           // (copy live[e] read, the other written and committed with Rs / y)
     int mfrep64;          // fp64 context: pending steps replayed on read by f64 MFMA (the flush's own
                           // instruction: bit-identical chains; EKF_OPT_MFMA_REPLAY)
-    int mfrep;            // split-bf16 context: pending steps replayed on read by bf16 MFMA from
-                          // the operand planes, diagonal blocks kept in Dd
+    int mfrep;            // split-plane context: pending steps replayed on read by MFMA (1 fp32
+                          // MFMA on the fp32 operand rows, 2 split products on the planes),
+                          // diagonal blocks kept in Dd; 0 the per-element forms
     int bf;               // split-plane context (1 EKF_ARITH_BF16X6, 2 EKF_ARITH_F16X3): fp16 storage
                           // rounded once per flush group, also in the on-read replay
     int* psig;            // [Etot] EKF_ARITH_F16X3 plane exponent σ (the lead lowers it when a new

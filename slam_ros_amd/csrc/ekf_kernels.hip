@@ -1484,6 +1484,68 @@ __device__ __forceinline__ void plane_replay(const Slot* pend, int e, size_t ins
     }
 }
 
+// Split-plane contexts, EKF_OPT_MFMA_REPLAY = 1 (default): the same ΔX = Σ_q V_q(rows)·V_q(cols)ᵀ
+// by v_mfma_f32_16x16x4_f32 on the fp32 operand rows V_q themselves (kmax = 16), exact fp32
+// products accumulated in fp32: within a flush group the association kernel reads the landmark
+// block at the precision of the EXACT arithmetic, and the split products enter P only at the
+// group's flush. Same bytes per row and step as the two fp16 planes (64). Lane l
+// loads one 16-byte quarter of a row's operand row: memory lane (row & 31) + 32·b, slots 4a..4a+3
+// with (a, b) = (kk >> 1, kk & 1), kk = l >> 4; chunk c takes slot 4a + c, i.e. k = 2·(4a + c) + b
+// on both operands (a k permutation: every dot product keeps its terms). acc layout as
+// plane_replay's.
+template <int NB, typename RA, typename RB>
+__device__ __forceinline__ void f32_replay(const Slot* pend, int e, size_t opstride, int M, unsigned amask,
+                                           int lane, RA row_a, RB row_b, f32x4v (&acc)[NB])
+{
+#pragma unroll
+    for (int mb = 0; mb < NB; mb++) acc[mb] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    const int kk = lane >> 4, r16 = lane & 15;
+    const int qoff = 32 * (kk & 1) * 8 + 4 * (kk >> 1);   // floats, within a row's 32-row block
+    auto off = [&](int row) __attribute__((always_inline)) {
+        return ((size_t)(row >> 5) * 64 + (row & 31)) * 8 + qoff;
+    };
+    const f32x4v zero = {0.f, 0.f, 0.f, 0.f};
+    const int rb_ = row_b(r16);
+    const bool bok = rb_ >= 0 && rb_ < M;
+    const size_t boff = bok ? off(rb_) : 0;
+    size_t aoff[NB];
+    bool aok[NB];
+#pragma unroll
+    for (int mb = 0; mb < NB; mb++) {
+        const int ra = row_a(mb, r16);
+        aok[mb] = ra >= 0 && ra < M;
+        aoff[mb] = aok[mb] ? off(ra) : 0;
+    }
+    unsigned m = amask;
+    while (m) {
+        // two steps per round trip: both steps' rows issued before either step's MFMAs
+        const int qa = __builtin_ctz(m);
+        m &= m - 1;
+        const int qb = m ? __builtin_ctz(m) : -1;
+        if (qb >= 0) m &= m - 1;
+        const float* va = reinterpret_cast<const float*>(pend[qa].Vop) + (size_t)e * opstride;
+        const float* vb = reinterpret_cast<const float*>(pend[qb >= 0 ? qb : qa].Vop) + (size_t)e * opstride;
+        f32x4v Ba = bok ? *reinterpret_cast<const f32x4v*>(va + boff) : zero;
+        f32x4v Bb = (bok && qb >= 0) ? *reinterpret_cast<const f32x4v*>(vb + boff) : zero;
+        f32x4v Aa[NB], Ab[NB];
+#pragma unroll
+        for (int mb = 0; mb < NB; mb++) {
+            Aa[mb] = aok[mb] ? *reinterpret_cast<const f32x4v*>(va + aoff[mb]) : zero;
+            Ab[mb] = (aok[mb] && qb >= 0) ? *reinterpret_cast<const f32x4v*>(vb + aoff[mb]) : zero;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+            for (int mb = 0; mb < NB; mb++)
+                acc[mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(Aa[mb][c], Ba[c], acc[mb], 0, 0, 0);
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+            for (int mb = 0; mb < NB; mb++)
+                acc[mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ab[mb][c], Bb[c], acc[mb], 0, 0, 0);
+    }
+}
+
 // EKF_ARITH_F16X3: x = 2^σ·v as hi + lo fp16 (hi = fp16(x) round-to-nearest, lo = fp16(x − hi), the
 // remainder exact in fp32): 22 significant bits; (a, b) packed into one dword per part, a low
 __device__ __forceinline__ void split_pack_f16(float a, float b, int sig, unsigned (&o)[2])
@@ -1590,6 +1652,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     const int npl = pf16 ? 2 : 3;
     const int psig = !pf16 ? 0 : p.npend == 0 ? plane_sigma(p.pvmax[e]) : p.psig[e];
     const double rsc = pf16 ? ldexp(1.0, -2 * psig) : 1.0;
+    // the on-read replay of plain pending steps (EKF_OPT_MFMA_REPLAY): 1 fp32 MFMA on the fp32
+    // operand rows (f32_replay: ΔX unscaled), 2 the split products on the planes (plane_replay:
+    // 2^(2σ)·ΔX for EKF_ARITH_F16X3)
+    const bool f32rep = kPlanes && p.mfrep == 1;
+    const double rrsc = f32rep ? 1.0 : rsc;
     // phase timers only in the ST instantiation (EKF_SCAN_STAMPS=1): the product kernel carries
     // no timer code at all (its uniform branches and registers cost ≈2 µs per scan)
     unsigned long long* const pdbg = ST ? p.dbg : nullptr;
@@ -1809,8 +1876,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         // a plane exponent other than this scan's takes the exact forms
         bool m = st && p.mfrep && kPlanes;
         for (int q = 0; q < p.npend; q++) {
-            m &= !sh_ctl[q].x && (!pf16 || sh_psg[q] == psig);
-            rpath |= (sh_ctl[q].x ? 128 : 0) | (pf16 && sh_psg[q] != psig ? 256 : 0);
+            // (the planes of a step written with another exponent: only the plane replay minds)
+            const bool sgx = pf16 && !f32rep && sh_psg[q] != psig;
+            m &= !sh_ctl[q].x && !sgx;
+            rpath |= (sh_ctl[q].x ? 128 : 0) | (sgx ? 256 : 0);
             aug_pend |= sh_ctl[q].z > 0;
             if (sh_ctl[q].y > 0) amask |= 1u << q;
         }
@@ -1845,6 +1914,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     // writes a match's owned rows: U/V history and the MFMA downdate operands
     // F: the line's symmetric operand factor (sym_factor; unused otherwise)
     bool nzr = false;   // this thread wrote a nonzero operand row (DONE_NZ, RES_ZMAX)
+    // the scan's downdate of the owned 2×2 diagonal block, trace (Σ over matches and both rows of
+    // −U·V ≥ 0): with the block after the scan it measures the update's cancellation (EKF_ST_PRECISION)
+    double dsq = 0.0;
     auto store_rows = [&](int t, const double kk[4], const double uu[4], bool vhist, const float F[3]) {
         nzr = nzr || kk[0] != 0.0 || kk[1] != 0.0 || kk[2] != 0.0 || kk[3] != 0.0 || uu[0] != 0.0 ||
               uu[1] != 0.0 || uu[2] != 0.0 || uu[3] != 0.0;
@@ -1869,6 +1941,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     o0 = (double)(float)v0;
                     o1 = (double)(float)v1;
                 }
+                dsq += o0 * v0 + o1 * v1;   // (row pp's diagonal entry falls by it)
                 if (stage_ops) {
                     // staged in LDS: the operand rows (U, V, the bf16 planes) go out once at the end
                     // of the scan as whole 16-byte lane rows
@@ -2182,9 +2255,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     return w >= 0 ? 2 * w + (c & 1) : -1;
                 };
                 f32x4v dacc[1];
-                if (HOT == 2 || (HOT == 0 && pf16))
+                if (f32rep)
+                    f32_replay<1>(p.pend, e, opstride, M, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow, dacc);
+                else if (HOT == 2 || (HOT == 0 && pf16))
                     plane_replay<1, true>(p.pend, e, opstride * 2, M, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow, dacc);
-                if (HOT == 1 || (HOT == 0 && !pf16))
+                else
                     plane_replay<1, false>(p.pend, e, opstride * 3, M, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow, dacc);
                 float* scr = sh_stg;   // (not staged in this mode) 16 × 16 floats
 #pragma unroll
@@ -2200,7 +2275,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                     double* r = sh_wd + pu * SPEC_WD + (pt == pu ? 6 : 14 + 4 * pt);
 #pragma unroll
                     for (int a = 0; a < 4; a++)
-                        r[a] = from_domain<T>(xr[a], pv.ex) - (double)scr[(2 * pu + (a >> 1)) * 16 + 2 * pt + (a & 1)] * rsc;
+                        r[a] = from_domain<T>(xr[a], pv.ex) - (double)scr[(2 * pu + (a >> 1)) * 16 + 2 * pt + (a & 1)] * rrsc;
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_wave_barrier();
@@ -2345,10 +2420,13 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         return w >= 0 ? 2 * w + (c & 1) : -1;
                     };
                     f32x4v dacc[8];
-                    if (HOT == 2 || (HOT == 0 && pf16))
+                    if (f32rep)
+                        f32_replay<8>(p.pend, e, opstride, M, amask, l,
+                                      [&](int mb, int r) { return rbase + 16 * mb + r; }, wrow, dacc);
+                    else if (HOT == 2 || (HOT == 0 && pf16))
                         plane_replay<8, true>(p.pend, e, opstride * 2, M, amask, l,
                                               [&](int mb, int r) { return rbase + 16 * mb + r; }, wrow, dacc);
-                    if (HOT == 1 || (HOT == 0 && !pf16))
+                    else
                         plane_replay<8, false>(p.pend, e, opstride * 3, M, amask, l,
                                                [&](int mb, int r) { return rbase + 16 * mb + r; }, wrow, dacc);
                     float* scr = sh_vpl + (tid & ~63) * 32;
@@ -2383,10 +2461,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                                 if (qs >= 0) patch_block<T>(pv, p.pend[qs], sh_ctl[qs], 2 * j, 2 * sh_spec[t], false, b);
                                 const int c0 = 2 * t;
                                 sh_blk[t][tid] = make_float4(
-                                    (float)(from_domain<T>(b[0], pv.ex) - (double)d0[c0 >> 2][c0 & 3] * rsc),
-                                    (float)(from_domain<T>(b[1], pv.ex) - (double)d0[c0 >> 2][(c0 & 3) + 1] * rsc),
-                                    (float)(from_domain<T>(b[2], pv.ex) - (double)d1[c0 >> 2][c0 & 3] * rsc),
-                                    (float)(from_domain<T>(b[3], pv.ex) - (double)d1[c0 >> 2][(c0 & 3) + 1] * rsc));
+                                    (float)(from_domain<T>(b[0], pv.ex) - (double)d0[c0 >> 2][c0 & 3] * rrsc),
+                                    (float)(from_domain<T>(b[1], pv.ex) - (double)d0[c0 >> 2][(c0 & 3) + 1] * rrsc),
+                                    (float)(from_domain<T>(b[2], pv.ex) - (double)d1[c0 >> 2][c0 & 3] * rrsc),
+                                    (float)(from_domain<T>(b[3], pv.ex) - (double)d1[c0 >> 2][(c0 & 3) + 1] * rrsc));
                             }
                     }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -2721,6 +2799,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                 blk_cached = true;
                 matched = false;
                 m = nextra = status = 0;
+                dsq = 0.0;
                 ops_early = 0;   // (the sequential path rewrites every operand row)
                 __syncthreads();   // sh_extra, sh_vhist reuse
             }
@@ -2946,11 +3025,29 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         // column (|P_ij| <= sqrt(P_ii P_jj)), and downdates only shrink them
                         if (Stor<T>::half && fabs(ldexp(gsum + h, pv.ex)) > F16_RANGE_WARN)
                             status |= EKF_ST_RANGE_BIT;
+                        // fp32 storage: within 2^8 of fp32's range (a diverged filter; SURVEY §8d's
+                        // world reaches P ≈ 1e43 after 200 scans)
+                        if (sizeof(typename Stor<T>::C) == 4 && !Stor<T>::half && !(fabs(gsum + h) <= F32_RANGE_WARN))
+                            status |= EKF_ST_RANGE_BIT;
                     }
             }
         }
     }
     EKF_STAMP(27);
+    // fp32 storage: an update that cancels more than 4 of fp32's 24 significant bits of a
+    // landmark's variance (trace before / after > 2^4: the result not guaranteed to 2^-20, the P
+    // bar), or leaves it non-positive, is flagged EKF_ST_PRECISION; the result still commits (a
+    // diverging filter: SURVEY §8d's world)
+    if constexpr (sizeof(C) == 4 && !Stor<T>::half)
+        if (own && !reset && j < s && dsq > 0.0) {
+            const double ta = Dj[0] + Dj[3];
+            if (!(ta > 0.0) || ta + dsq > PREC_CANCEL * ta) status |= EKF_ST_PRECISION_BIT;
+        }
+    // EKF_ARITH_F16X3: an active landmark whose variance sits below the planes' dynamic range at
+    // this scan's σ (a filter whose largest variance is ≥ 2^28 times its smallest: SURVEY §8d's
+    // world in steady state) makes the step's flush exact (PLANE_SIGMA_EXACT, DONE_PLOSS)
+    if (pf16 && own && !reset && j < s + nadd && ldexp(fmin(Dj[0], Dj[3]), 2 * psig) < PLANE_VAR_MIN)
+        status |= (int)DONE_PLOSS;
     // write back the owned state (reset: Robot.cpp:893-904 zeroes landmark entries of y and P)
     if (own) {
         if (reset) {
@@ -3068,7 +3165,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     if (tid == 0 && g != 0) publish_done(sync, g, p.epoch, wgst);
     int zg = (wgst & (int)DONE_NZ) ? 1 : 0;
     if (g == 0 && (sequential || G > 1)) wgst = lead_collect(sync, G, p.epoch, wgst, p.spin_log2, tid, sh_red, zg);
-    wgst &= ~(int)DONE_NZ;
+    const bool ploss = (wgst & (int)DONE_PLOSS) != 0;
+    wgst &= ~(int)(DONE_NZ | DONE_PLOSS);
     EKF_STAMP(26);
     if (lead) {
         sync[SYNC_WG0] = (int)done_word(p.epoch, wgst);
@@ -3093,7 +3191,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
             res[RES_NADD] = reset ? 0 : nadd;
             res[RES_KSTEPS] = (sizeof(C) == 4) ? m : (m + 1) / 2;
             res[RES_ROLLBACK] = 0;
-            res[RES_PSIG] = psig;
+            res[RES_PSIG] = ploss ? PLANE_SIGMA_EXACT : psig;
             // nonzero operand rows only below zg workgroups' landmarks; new rows below s + nadd
             res[RES_ZMAX] = max(min(zg * SCAN_THREADS, N), reset ? 0 : s + nadd);
             p.saved[e] = reset ? 0 : s + nadd;
@@ -4346,21 +4444,12 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
             // step q of wave-tile t into ring set r: A row blocks, then B row blocks, three planes
             auto load_ops = [&](int r, const Item& t, int q) __attribute__((always_inline)) {
                 const bf16x8* b = pl_base(q) + t.e * pstride + lane;
-#ifdef EKF_XP_BF_HALF_OPS   // timing experiment (results invalid): A planes only, reused as B
-#pragma unroll
-                for (int i = 0; i < WT_R; i++) {
-                    const bf16x8* rb = b + (size_t)op_row(t, 0, i) * NPL * 64;
-#pragma unroll
-                    for (int pl = 0; pl < NPL; pl++) R[r][i][pl] = R[r][WT_R + i][pl] = rb[pl * 64];
-                }
-#else
 #pragma unroll
                 for (int i = 0; i < WT_R + WT_C; i++) {
                     const bf16x8* rb = b + (size_t)(i < WT_R ? op_row(t, 0, i) : op_row(t, 1, i - WT_R)) * NPL * 64;
 #pragma unroll
                     for (int pl = 0; pl < NPL; pl++) R[r][i][pl] = rb[pl * 64];
                 }
-#endif
             };
             auto load_tiles = [&](const Item& t) __attribute__((always_inline)) {
 #pragma unroll
@@ -4412,6 +4501,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                     const int sg = F16 ? rec_of(e, q, RES_PSIG) : 0;
                     if (q == 0) sg0 = sg;
                     else if (sg != prev) smask |= 1u << (q - 1);
+                    if (sg == PLANE_SIGMA_EXACT) smask |= 1u << NS;   // (the whole group exact)
                     prev = sg;
                 }
                 sgl = prev;
@@ -4460,21 +4550,9 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
             if (cur.g >= g_end) return;   // (no live wave-tile: nothing to store, no second pass)
             next_live(cur, nxt);
             load_tiles(cur);
-#ifdef EKF_XP_BF_NO_OPS   // timing experiment (results invalid): operands loaded once, never in the loop
-#pragma unroll
-            for (int q = 0; q < RD; q++) load_ops(q, cur, q);
-#else
 #pragma unroll
             for (int q = 0; q < RD - 1; q++) load_ops(q, cur, q);
-#endif
-#ifdef EKF_XP_FLUSH_STAMPS   // timing experiment: shader cycles per wave-tile section, in-kernel clock
-            unsigned long long xs_b = 0, xs_m = 0, xs_s = 0, xs_n = 0;
-            const unsigned long long xc0 = __builtin_amdgcn_s_memtime(), xr0 = __builtin_amdgcn_s_memrealtime();
-#endif
             while (true) {
-#ifdef EKF_XP_FLUSH_STAMPS
-                const unsigned long long xt0 = __builtin_amdgcn_s_memtime();
-#endif
                 const bool more = nxt.g < g_end;
                 next_live(nxt, nxt2);
                 const Item ldi = more ? nxt : cur;   // the last wave-tile re-reads its own rows
@@ -4491,26 +4569,16 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                     for (int qq = 0; qq < 4; qq++)
 #pragma unroll
                         for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = (float)pref[i][qq][j] * isc;
-#ifndef EKF_XP_BF_NO_TILES   // timing experiment (results invalid): no tile stream after the first
                 if (!LATE && (EKF_F16_TILES_ALWAYS || more)) load_tiles(EKF_F16_TILES_ALWAYS ? ldi : nxt);
-#endif
-#ifdef EKF_XP_TILE_WAIT   // timing experiment: wait for the next wave-tile's tiles right away
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
                 __builtin_amdgcn_sched_barrier(0);
-#ifdef EKF_XP_FLUSH_STAMPS
-                const unsigned long long xt1 = __builtin_amdgcn_s_memtime();
-#endif
 #pragma unroll
                 for (int q = 0; q < NS; q++) {
                     // (EKF_F16_TILES_ALWAYS: unconditional, the last wave-tile re-reads its own)
                     if (LATE && q == TQ && (EKF_F16_TILES_ALWAYS || more)) load_tiles(EKF_F16_TILES_ALWAYS ? ldi : nxt);
                     // ring set of step q + RD − 1 (this wave-tile's, else the next one's)
                     const int ql = q + RD - 1;
-#ifndef EKF_XP_BF_NO_OPS
                     if (ql < NS) load_ops(ql % RD, cur, ql);
                     else load_ops(ql % RD, ldi, ql - NS);
-#endif
                     const int r = q % RD;
                     if constexpr (F16) {
                         // (lo, hi), (hi, lo), (hi, hi): 12 MFMAs beside the 8 plane loads
@@ -4552,36 +4620,17 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
-#ifdef EKF_XP_FLUSH_STAMPS
-                const unsigned long long xt2 = __builtin_amdgcn_s_memtime();
-#endif
                 // back from the last step's domain (−1, −2^x, −2^(x − 2σ): exact)
                 const float osc = F16 ? 1.0f / (isc * ldexpf(1.0f, 2 * (sgl - sg0))) : 1.0f / isc;
 #pragma unroll
                 for (int i = 0; i < WT_N; i++)
 #pragma unroll
                     for (int k = 0; k < 16; k++) acc[i][k] = zero ? 0.0f : acc[i][k] * osc;
-#ifdef EKF_XP_BF_NO_TILES
-                if (acc[0][0] == 1234.5f && acc[3][15] == -1234.5f)   // (never true: keeps the MFMAs live)
-#endif
                 store_tiles(cur, acc, skip);
-#ifdef EKF_XP_FLUSH_STAMPS
-                __builtin_amdgcn_sched_barrier(0);
-                const unsigned long long xt3 = __builtin_amdgcn_s_memtime();
-                xs_b += xt1 - xt0; xs_m += xt2 - xt1; xs_s += xt3 - xt2; xs_n += 1;
-#endif
                 if (!more) break;
                 cur = nxt;
                 nxt = nxt2;
             }
-#ifdef EKF_XP_FLUSH_STAMPS
-            if (p.dbg && lane == 0) {
-                atomicAdd(p.dbg + 24, xs_b); atomicAdd(p.dbg + 25, xs_m);
-                atomicAdd(p.dbg + 26, xs_s); atomicAdd(p.dbg + 27, xs_n);
-                atomicAdd(p.dbg + 28, __builtin_amdgcn_s_memtime() - xc0);
-                atomicAdd(p.dbg + 29, __builtin_amdgcn_s_memrealtime() - xr0);
-            }
-#endif
             // second pass: the skipped wave-tiles through the general loop (their input tiles are
             // as read: the first pass stored them to the sink). Exact arithmetic on the fp32 operand
             // rows there, the split arithmetic elsewhere: both within the fp32 bar (slam_ekf.h)
@@ -4654,13 +4703,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
             load_half(q, cur, q, 1);
         }
         int g = g0;
-#ifdef EKF_XP_FLUSH_STAMPS   // timing experiment: shader cycles per wave-tile section
-        unsigned long long xs_b = 0, xs_m = 0, xs_s = 0, xs_n = 0;
-#endif
         while (true) {
-#ifdef EKF_XP_FLUSH_STAMPS
-            const unsigned long long xt0 = __builtin_amdgcn_s_memtime();
-#endif
             const bool more = g + K < g_end;
             next_item(nxt, nxt2);   // read now, used by the next wave-tile
             // operand rows for the next wave-tile (the last one re-reads its own: no branch
@@ -4676,9 +4719,6 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
             // during the one before it, so these have the whole wave-tile to land
             if (more) load_tiles(nxt);
             __builtin_amdgcn_sched_barrier(0);
-#ifdef EKF_XP_FLUSH_STAMPS
-            const unsigned long long xt1 = __builtin_amdgcn_s_memtime();
-#endif
             if constexpr (AM) {
                 // group-major steps (fp16 storage): the
                 // per-step rounding of one group of accumulators runs on the VALU while the other
@@ -4769,26 +4809,12 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                 __builtin_amdgcn_sched_barrier(0);
             }
             load_half(NS - 1, ldi, NS - 1, 1);
-#ifdef EKF_XP_FLUSH_STAMPS
-            const unsigned long long xt2 = __builtin_amdgcn_s_memtime();
-#endif
             store_tiles(cur, acc);
-#ifdef EKF_XP_FLUSH_STAMPS
-            __builtin_amdgcn_sched_barrier(0);
-            const unsigned long long xt3 = __builtin_amdgcn_s_memtime();
-            xs_b += xt1 - xt0; xs_m += xt2 - xt1; xs_s += xt3 - xt2; xs_n += 1;
-#endif
             if (!more) break;
             g += K;
             cur = nxt;
             nxt = nxt2;
         }
-#ifdef EKF_XP_FLUSH_STAMPS
-        if (p.dbg && lane == 0) {
-            atomicAdd(p.dbg + 24, xs_b); atomicAdd(p.dbg + 25, xs_m);
-            atomicAdd(p.dbg + 26, xs_s); atomicAdd(p.dbg + 27, xs_n);
-        }
-#endif
         return;
     }
 
@@ -4859,7 +4885,8 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_bf24_kernel(DowndateParam
             for (int q = 0; q < NS; q++) {
                 const int* r = p.steps[q].res + (size_t)e * RES_STRIDE;
                 fast = fast && !sload(r + RES_RESET) && sload(r + RES_NADD) == 0 && !sload(r + RES_ROLLBACK);
-                if (F16) fast = fast && sload(r + RES_PSIG) == sload(p.steps[0].res + (size_t)e * RES_STRIDE + RES_PSIG);
+                if (F16) fast = fast && sload(r + RES_PSIG) == sload(p.steps[0].res + (size_t)e * RES_STRIDE + RES_PSIG) &&
+                                sload(r + RES_PSIG) != PLANE_SIGMA_EXACT;
             }
     }
     struct Item {
@@ -5280,6 +5307,7 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f64_wave_kernel(DowndateP
     }
 }
 
+#if !defined(EKF_TU) || EKF_TU == 2   // (a plain kernel: defined in the flush unit only)
 __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams p)
 {
     const Dims d = p.d;
@@ -5377,6 +5405,8 @@ __global__ __launch_bounds__(DD_THREADS) void downdate_f64_kernel(DowndateParams
 // ---------------------------------------------------------------------------------------
 // state transfer / initialisation
 // ---------------------------------------------------------------------------------------
+#endif
+
 template <typename T>
 __device__ __forceinline__ void tile_rc_of(int rem, int& r, int& c)
 {
@@ -5478,6 +5508,7 @@ __global__ void lowrank_kernel(Dims d, const double* __restrict__ diag,
 // ---------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------
+#if !defined(EKF_TU) || EKF_TU == 1
 int scan_blocks_per_cu(int precision)
 {
     int nb = 0;
@@ -5498,6 +5529,9 @@ size_t scan_lds_bytes(int precision)
     return err == hipSuccess ? a.sharedSizeBytes : 0;
 }
 
+#endif
+
+#if !defined(EKF_TU) || EKF_TU == 3
 hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st)
 {
     const unsigned grid = (unsigned)((p.d.N + 255) / 256);   // every landmark
@@ -5507,6 +5541,9 @@ hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st)
     return hipGetLastError();
 }
 
+#endif
+
+#if !defined(EKF_TU) || EKF_TU == 1
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 {
     const dim3 grid(p.G * p.E), block(SCAN_BLOCK);
@@ -5528,6 +5565,9 @@ hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
     return hipGetLastError();
 }
 
+#endif
+
+#if !defined(EKF_TU) || EKF_TU == 2
 hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st, hipEvent_t ev_a,
                            hipEvent_t ev_b)
 {
@@ -5690,6 +5730,9 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     return hipGetLastError();
 }
 
+#endif
+
+#if !defined(EKF_TU) || EKF_TU == 3
 static int grid_for(int64_t work, int block)
 {
     int64_t g = (work + block - 1) / block;
@@ -5749,5 +5792,7 @@ hipError_t launch_lowrank(const Dims& d, int precision, const double* diag, cons
                            rank, (float*)Pll, Rs, tile_rc, ex, t0, t1);
     return hipGetLastError();
 }
+
+#endif
 
 }  // namespace ekf

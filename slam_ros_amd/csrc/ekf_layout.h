@@ -154,6 +154,15 @@ EKF_HD int64_t op_index_pl(int row, int k, int pl, int npl)
 // down to 2^-17 of the largest keep their full 22-bit hi + lo split. An empty map (vmax = 0) keeps
 // PLANE_SIGMA_EMPTY until its first landmark.
 constexpr int PLANE_SIGMA_EMPTY = 0;
+// RES_PSIG of a step whose planes do not carry the instance's dynamic range (EKF_ARITH_F16X3: some
+// active landmark's variance below 2^-4·4^-σ, where the fp16 lo part loses bits relative to that
+// landmark's own scale): the flush runs the instance's group in the exact form (an exponent no
+// plane uses, so it also differs from every other step's)
+constexpr int PLANE_SIGMA_EXACT = -100000;
+// the smallest 4^σ·variance whose rows keep the 22-bit split relative to their own scale: a row
+// value x = 2^σ·V with |x| ~ sqrt(4^σ·var) keeps its lo part normal (|lo| ≈ 2^-11·|x| >= 2^-14)
+// while 4^σ·var >= 2^-4 ... 2^-6; below it the split's error is no longer 2^-22 of the row's scale
+constexpr double PLANE_VAR_MIN = 0.0625;   // 2^-4
 EKF_HD int plane_sigma(double vmax)
 {
     if (!(vmax > 0.0) || vmax > 1e300) return PLANE_SIGMA_EMPTY;

@@ -76,15 +76,17 @@ class GroupedBroadcast:
 
     Buffer reuse is ordered by construction: group gi + 1 overwrites the buffer group gi − 1's
     steps read, and those were issued before it (stream order on the GPU; synchronous on CPU).
-    `host_coll`: the collective runs on host copies (gloo rehearsal of GPU ranks)."""
+    `host_coll`: the collective runs on host copies (gloo rehearsal of GPU ranks). `force`: the
+    collective path even for a world of one (the RCCL device branch on a one-GPU box)."""
 
     def __init__(self, payload, B: int, dist, rank: int, world: int, src: int = 0,
-                 host_coll: bool = False, sync=None):
+                 host_coll: bool = False, sync=None, force: bool = False):
         self.payload, self.B, self.dist = payload, max(1, int(B)), dist
         self.rank, self.world, self.src = rank, world, src
+        self.coll = world > 1 or force
         self.steps_total = payload.shape[0]
         self.host_coll, self.sync = host_coll, sync
-        self.recv = payload.new_empty((2, self.B, payload.shape[1])) if world > 1 else None
+        self.recv = payload.new_empty((2, self.B, payload.shape[1])) if self.coll else None
         self.inflight = {}
         self.issued = []        # group indices in issue order (tests)
 
@@ -93,7 +95,7 @@ class GroupedBroadcast:
             pass
 
     def issue(self, gi: int) -> None:
-        if self.world == 1 or gi * self.B >= self.steps_total:
+        if not self.coll or gi * self.B >= self.steps_total:
             return
         import torch
         B = self.B
@@ -118,7 +120,7 @@ class GroupedBroadcast:
 
     def step_buffer(self, s: int):
         """The payload row step s consumes (a view into the receive area for world > 1)."""
-        if self.world == 1:
+        if not self.coll:
             return self.payload[s]
         gi, k = divmod(s, self.B)
         if k == 0:

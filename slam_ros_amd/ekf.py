@@ -22,7 +22,7 @@ EKF_MAX_LINES = 64
 PREC_F64, PREC_F32, PREC_F16 = 0, 1, 2
 R_INTENDED, R_AS_WRITTEN = 0, 1
 ARITH_EXACT, ARITH_BF16X6, ARITH_F16X3 = 0, 1, 2   # fp32 flush arithmetic (slam_ekf.h EKF_ARITH_*)
-ST_SINGULAR_S, ST_CAPACITY, ST_NONSYM, ST_SYNC_TIMEOUT, ST_RANGE = 1, 2, 4, 8, 16
+ST_SINGULAR_S, ST_CAPACITY, ST_NONSYM, ST_SYNC_TIMEOUT, ST_RANGE, ST_PRECISION = 1, 2, 4, 8, 16, 32
 EXP_AUTO = -1000
 # per-context options (slam_ekf.h EKF_OPT_*, ekf_set_option)
 OPT_SPECULATE, OPT_SPIN_LOG2, OPT_FLUSH_FORM, OPT_FLUSH_BLOCKS_PER_CU = 1, 2, 3, 4

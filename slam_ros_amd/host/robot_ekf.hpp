@@ -66,6 +66,7 @@ public:
         cfg.capacity = N;
         cfg.instances = 1;
         cfg.precision = precision;
+        precision_ = precision;
         cfg.device = device;
         cfg.max_lines = EKF_MAX_LINES;
         int rc = ekf_create(&cfg, &ctx_);
@@ -155,6 +156,7 @@ public:
 
 private:
     ekf_ctx* ctx_ = nullptr;
+    int precision_ = EKF_PREC_F64;
     ekf_result last_{};
     Mirror mirror_ = kFull;
 
@@ -193,8 +195,11 @@ private:
             std::fprintf(stderr, "slam_ekf: landmark capacity exceeded\n");
         if (res.status & EKF_ST_SYNC_TIMEOUT)
             std::fprintf(stderr, "slam_ekf: association exchange timed out\n");
-        if (res.status & EKF_ST_RANGE)   // fp16 storage near its range: re-choose the exponent
+        if ((res.status & EKF_ST_RANGE) && precision_ == EKF_PREC_F16)   // near fp16's range: re-choose the exponent
             report(ekf_rescale(ctx_, 0, EKF_EXP_AUTO), "ekf_rescale");
+        else if (res.status & EKF_ST_RANGE)
+            std::fprintf(stderr, "slam_ekf: landmark variance near the storage range (diverged filter)\n");
+        // (EKF_ST_PRECISION is informational: the update still committed)
         xPos = res.pose[0];
         yPos = res.pose[1];
         thetaPos = res.pose[2];

@@ -69,3 +69,33 @@ def test_two_ranks_equal_one_rank(tmp_path, arith):
         for key in ("P", "y", "saved", "pose"):
             assert np.array_equal(a[key], b[key]), (arith, k, key)
         assert int(a["saved"]) == 246   # s = N − 10 kept: every line matched, no augmentation
+
+
+@pytest.mark.gpu
+def test_rccl_grouped_broadcast_world1(tmp_path):
+    """GroupedBroadcast's device branch (dist.py: the payload rows copied on the stream, RCCL's
+    in-place broadcast into the double-buffered receive area, work.wait() ordering the stream) on
+    the nccl backend, forced at a world of one on the test box's single GPU (--force-collective):
+    over several groups and a partial last one, every instance ends bitwise in the state of the
+    same run fed straight from the payload (the stream ordering and the buffer reuse lose or
+    reorder no scan). The multi-GPU curve is the driver's 8-GPU run."""
+    common = ["--steps", "13", "--warmup", "3", "--preroll", "4", "--capacity", "256", "--instances", "4",
+              "--no-cpu", "--arith", "f16x3", "--flush-interval", "6", "--bcast-every", "5"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0",
+               WORLD_SIZE="1", LOCAL_RANK="0")
+    coll = tmp_path / "coll"
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--force-collective",
+                          "--dist-backend", "nccl", "--dump-state", str(coll)] + common,
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=150)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert "forced through the nccl collective" in r["config"]["parallelism"], r["config"]
+    assert r["all_lines_matched"] is True
+    plain = tmp_path / "plain"
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dump-state", str(plain)] + common,
+                         cwd=ROOT, capture_output=True, text=True, timeout=150)
+    assert out.returncode == 0, out.stderr[-3000:]
+    for k in range(4):
+        a, b = np.load(coll / f"state_{k}.npz"), np.load(plain / f"state_{k}.npz")
+        for key in ("P", "y", "saved", "pose"):
+            assert np.array_equal(a[key], b[key]), (k, key)

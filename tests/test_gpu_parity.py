@@ -708,6 +708,54 @@ def test_f64_wave_flush_equals_tile_kernel(ekf_mod, monkeypatch, N, T, lines, ex
 
 
 @pytest.mark.parametrize("arith", [1, 2])
+def test_active_flush_pipelined_reset_and_upload(ekf_mod, arith):
+    """pipeline = 1 at N <= 192 (one association workgroup: the flush double-buffers the block):
+    a capacity reset inside a group followed by groups without matches, then an upload followed
+    by a group without matches. A wave-tile skipped by the active-map flush would keep the output
+    buffer's copy from two flushes earlier (the pre-reset covariance), so the double-buffered flush
+    never skips: P, y and the matches equal the flush over every wave-tile bit for bit."""
+    N, E, T = 160, 2, 4
+    w = G.make_world(N, active=N - 14)
+    st = G.initial_state(w)
+    a = ekf_mod.Ensemble(N, E, 1, max_lines=8, flush_interval=T, arith=arith, pipeline=True)
+    b = ekf_mod.Ensemble(N, E, 1, max_lines=8, flush_interval=T, arith=arith, pipeline=True,
+                         options={"active_flush": 0})
+    for ens in (a, b):
+        for e in range(E):
+            ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+    rng = np.random.default_rng(5)
+    empty = np.zeros(E, dtype=np.int32)
+    resets = 0
+    for step in range(1, 6 * T + 2):
+        enc, ln, nl = G.make_scan(w, step, instances=E, lines=4)
+        if step in (3, 4):     # new landmarks past N - 10: the capacity reset
+            ln = np.concatenate([ln, G.random_lines(rng, 4)[None].repeat(E, axis=0)], axis=1)
+            nl = np.full(E, ln.shape[1], dtype=np.int32)
+        elif 5 <= step < 5 + 3 * T:
+            nl = empty         # groups without a match (the upload below lands inside them)
+        if step == 5 + 2 * T:  # upload (drains), then a group without matches
+            for ens in (a, b):
+                P, y, s, pose = ens.download_state(0)
+                ens.upload_state(1, P, y, s, pose)
+        ra = a.localize(enc, ln, nl)
+        rb = b.localize(enc, ln, nl)
+        for e in range(E):
+            assert ra[e]["match"] == rb[e]["match"], (step, e)
+            assert ra[e]["status"] & ~ekf_mod.ST_CAPACITY == 0
+            resets += ra[e]["reset"]
+    assert resets > 0
+    for e in range(E):
+        Pa, ya, sa, pa = a.download_state(e)
+        Pb, yb, sb, pb = b.download_state(e)
+        bad = np.argwhere(Pa != Pb)
+        assert bad.size == 0, (e, bad[:12].tolist(), rel(Pa, Pb))
+        np.testing.assert_array_equal(ya, yb)
+        assert sa == sb
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("arith", [1, 2])
 @pytest.mark.parametrize("N,active,T,extra_every", [(1024, 300, 12, 3), (4096, 1500, 20, 4), (512, 100, 8, 0),
                                                      (1024, 1014, 12, 0)])
 def test_active_flush_equals_full_flush(ekf_mod, arith, N, active, T, extra_every):
