@@ -103,8 +103,8 @@ def parse():
     ap.add_argument("--flush-form", type=int, default=0,
                     help="EKF_OPT_FLUSH_FORM (A/B runs): 0 default, 24 the 2 x 4 split flush")
     ap.add_argument("--mfma-replay", type=int, choices=[0, 1, 2], default=1,
-                    help="EKF_OPT_MFMA_REPLAY: 1 fp32 MFMA on the operand rows (default), 2 the split "
-                         "products on the planes, 0 the per-element forms")
+                    help="EKF_OPT_MFMA_REPLAY: 1 the split products on the planes (default), 2 fp32 "
+                         "MFMA on the fp32 operand rows, 0 the per-element forms")
     ap.add_argument("--force-collective", action="store_true",
                     help="run the scan broadcast through the collective even at one rank (RANK=0, "
                          "WORLD_SIZE=1, MASTER_* in the env): the RCCL device branch on a one-GPU box")
@@ -303,11 +303,6 @@ def main():
         arith = ekf.ARITH_EXACT   # the split-bf16 flush serves fp32 operands (fp32 and fp16 storage)
     if args.flush_interval <= 0:
         args.flush_interval = 8 if prec == ekf.PREC_F64 else (8 if arith == ekf.ARITH_EXACT else (20 if arith == ekf.ARITH_F16X3 else 12))
-        if args.world == "survey" and arith != ekf.ARITH_EXACT and prec != ekf.PREC_F64:
-            # SURVEY §8d's wide covariances carry the split arithmetic's per-group P error into the
-            # state through large innovations: at T = 20 y reached 4.5e-8 within one group (bar
-            # 1e-8, profiles/r04_survey_line/), at T = 12 1.9e-10 (tests/test_bench_config.py)
-            args.flush_interval = 12
     ens = ekf.Ensemble(N, E, prec, max_lines=L_LINES, device=local, pipeline=bool(args.pipeline),
                       flush_interval=args.flush_interval, arith=arith,
                       options={"speculate": args.speculate, "flush_form": args.flush_form,

@@ -182,11 +182,12 @@ enum {
     EKF_OPT_FLUSH_FORM = 3,
     /* workgroups per CU of the grid-strided flush forms, 1..16 (8) */
     EKF_OPT_FLUSH_BLOCKS_PER_CU = 4,
-    /* pending steps applied on read by MFMA. 1 (default): split arithmetics by fp32 MFMA on the
-     * fp32 operand rows (exact products: within a flush group the association reads the block at
-     * the EXACT arithmetic's precision; the split products enter P only at the flush), fp64
-     * storage by the flush's own f64 MFMA (bit-identical); 2: split arithmetics by their own split
-     * products on the operand planes (round 4); 0: the per-element replay forms */
+    /* pending steps applied on read by MFMA. 1 (default): split arithmetics by their own split
+     * products on the operand planes (a step whose planes cannot carry the instance's dynamic
+     * range is replayed exactly, PLANE_SIGMA_EXACT), fp64 storage by the flush's own f64 MFMA
+     * (bit-identical); 2: split arithmetics by fp32 MFMA on the fp32 operand rows (exact
+     * products: within a flush group the association reads the block at the EXACT arithmetic's
+     * precision, ≈3 µs per scan more at T = 20); 0: the per-element replay forms */
     EKF_OPT_MFMA_REPLAY = 5,
     /* 1: the association kernel's instrumented instantiation with phase timers
      * (ekf_debug_scan_stamps); 0 (default) the product kernel */

@@ -114,8 +114,8 @@ struct ScanParams {
                           // (copy live[e] read, the other written and committed with Rs / y)
     int mfrep64;          // fp64 context: pending steps replayed on read by f64 MFMA (the flush's own
                           // instruction: bit-identical chains; EKF_OPT_MFMA_REPLAY)
-    int mfrep;            // split-plane context: pending steps replayed on read by MFMA (1 fp32
-                          // MFMA on the fp32 operand rows, 2 split products on the planes),
+    int mfrep;            // split-plane context: pending steps replayed on read by MFMA (1 split
+                          // products on the planes, 2 fp32 MFMA on the fp32 operand rows),
                           // diagonal blocks kept in Dd; 0 the per-element forms
     int bf;               // split-plane context (1 EKF_ARITH_BF16X6, 2 EKF_ARITH_F16X3): fp16 storage
                           // rounded once per flush group, also in the on-read replay

@@ -1484,11 +1484,12 @@ __device__ __forceinline__ void plane_replay(const Slot* pend, int e, size_t ins
     }
 }
 
-// Split-plane contexts, EKF_OPT_MFMA_REPLAY = 1 (default): the same ΔX = Σ_q V_q(rows)·V_q(cols)ᵀ
-// by v_mfma_f32_16x16x4_f32 on the fp32 operand rows V_q themselves (kmax = 16), exact fp32
-// products accumulated in fp32: within a flush group the association kernel reads the landmark
-// block at the precision of the EXACT arithmetic, and the split products enter P only at the
-// group's flush. Same bytes per row and step as the two fp16 planes (64). Lane l
+// Split-plane contexts, EKF_OPT_MFMA_REPLAY = 2: the same ΔX = Σ_q V_q(rows)·V_q(cols)ᵀ by
+// v_mfma_f32_16x16x4_f32 on the fp32 operand rows V_q themselves (kmax = 16), exact fp32 products
+// accumulated in fp32: within a flush group the association kernel reads the landmark block at
+// the precision of the EXACT arithmetic, and the split products enter P only at the group's
+// flush (≈3 µs per scan more than the plane replay at T = 20: 4× the MFMA cycles).
+// Same bytes per row and step as the two fp16 planes (64). Lane l
 // loads one 16-byte quarter of a row's operand row: memory lane (row & 31) + 32·b, slots 4a..4a+3
 // with (a, b) = (kk >> 1, kk & 1), kk = l >> 4; chunk c takes slot 4a + c, i.e. k = 2·(4a + c) + b
 // on both operands (a k permutation: every dot product keeps its terms). acc layout as
@@ -1652,10 +1653,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     const int npl = pf16 ? 2 : 3;
     const int psig = !pf16 ? 0 : p.npend == 0 ? plane_sigma(p.pvmax[e]) : p.psig[e];
     const double rsc = pf16 ? ldexp(1.0, -2 * psig) : 1.0;
-    // the on-read replay of plain pending steps (EKF_OPT_MFMA_REPLAY): 1 fp32 MFMA on the fp32
-    // operand rows (f32_replay: ΔX unscaled), 2 the split products on the planes (plane_replay:
-    // 2^(2σ)·ΔX for EKF_ARITH_F16X3)
-    const bool f32rep = kPlanes && p.mfrep == 1;
+    // the on-read replay of plain pending steps (EKF_OPT_MFMA_REPLAY): 1 the split products on
+    // the planes (plane_replay: 2^(2σ)·ΔX for EKF_ARITH_F16X3), 2 fp32 MFMA on the fp32 operand
+    // rows (f32_replay: ΔX unscaled)
+    const bool f32rep = kPlanes && p.mfrep == 2;
     const double rrsc = f32rep ? 1.0 : rsc;
     // phase timers only in the ST instantiation (EKF_SCAN_STAMPS=1): the product kernel carries
     // no timer code at all (its uniform branches and registers cost ≈2 µs per scan)
@@ -5567,6 +5568,125 @@ hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 
 #endif
 
+// The split-arithmetic flush launchers, one compilation unit each (EKF_TU 4-6: their template
+// instantiations are most of the library's device code)
+hipError_t launch_flush_bf24(const DowndateParams& p, bool half, bool f16, hipStream_t st, hipEvent_t ev_a,
+                             hipEvent_t ev_b);
+hipError_t launch_flush_f16x3(const DowndateParams& p, bool half, hipStream_t st, hipEvent_t ev_a, hipEvent_t ev_b);
+hipError_t launch_flush_bf16x6(const DowndateParams& p, bool half, hipStream_t st, hipEvent_t ev_a, hipEvent_t ev_b);
+
+#if !defined(EKF_TU) || EKF_TU == 4
+hipError_t launch_flush_f16x3(const DowndateParams& p, bool half, hipStream_t st, hipEvent_t ev_a, hipEvent_t ev_b)
+{
+    const unsigned wgrid = (unsigned)(8 * EKF_F16_WAVES * ((p.ncu + 7) / 8));
+#define EKF_F16_CASE(NSV)                                                                               \
+case NSV:                                                                                           \
+    if (half) hipExtLaunchKernelGGL((flush_f32_wave_kernel<_Float16, NSV, true, true>), dim3(wgrid),  \
+                                    dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p);                      \
+    else hipExtLaunchKernelGGL((flush_f32_wave_kernel<float, NSV, true, true>), dim3(wgrid),          \
+                               dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p);                           \
+    break;
+    switch (p.nsteps) {
+        EKF_F16_CASE(2)
+        EKF_F16_CASE(4)
+        EKF_F16_CASE(6)
+        EKF_F16_CASE(8)
+        EKF_F16_CASE(10)
+        EKF_F16_CASE(12)
+        EKF_F16_CASE(14)
+        EKF_F16_CASE(16)
+        EKF_F16_CASE(18)
+        EKF_F16_CASE(20)
+        EKF_F16_CASE(22)
+        EKF_F16_CASE(24)
+    }
+#undef EKF_F16_CASE
+    return hipGetLastError();
+}
+#endif
+
+#if !defined(EKF_TU) || EKF_TU == 5
+hipError_t launch_flush_bf24(const DowndateParams& p, bool half, bool f16, hipStream_t st, hipEvent_t ev_a,
+                             hipEvent_t ev_b)
+{
+    if (!f16) {
+        // EKF_ARITH_BF16X6, EKF_FLUSH_VARIANT=24: the 2 × 4 split-bf16 wave flush (measured 7 %
+        // slower than the 2 × 2 form below at T = 12; kept as an option, bit-identical)
+        const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
+#define EKF_BF24_CASE(NSV)                                                                              \
+    case NSV:                                                                                           \
+        if (half) hipExtLaunchKernelGGL((flush_bf24_kernel<_Float16, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, \
+                                        ev_a, ev_b, 0, p);                                              \
+        else hipExtLaunchKernelGGL((flush_bf24_kernel<float, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, \
+                                   ev_b, 0, p);                                                         \
+        break;
+        switch (p.nsteps) {
+            EKF_BF24_CASE(2)
+            EKF_BF24_CASE(4)
+            EKF_BF24_CASE(6)
+            EKF_BF24_CASE(8)
+            EKF_BF24_CASE(10)
+            EKF_BF24_CASE(12)
+            EKF_BF24_CASE(14)
+            EKF_BF24_CASE(16)
+        }
+#undef EKF_BF24_CASE
+        return hipGetLastError();
+        }
+        // EKF_ARITH_F16X3, EKF_OPT_FLUSH_FORM = 24: the 2 × 4 split-fp16 flush
+        const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));
+#define EKF_F24_CASE(NSV)                                                                               \
+    case NSV:                                                                                           \
+        if (half) hipExtLaunchKernelGGL((flush_bf24_kernel<_Float16, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, st, \
+                                        ev_a, ev_b, 0, p);                                               \
+        else hipExtLaunchKernelGGL((flush_bf24_kernel<float, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, \
+                                   ev_b, 0, p);                                                          \
+        break;
+        switch (p.nsteps) {
+            EKF_F24_CASE(2)
+            EKF_F24_CASE(4)
+            EKF_F24_CASE(6)
+            EKF_F24_CASE(8)
+            EKF_F24_CASE(10)
+            EKF_F24_CASE(12)
+            EKF_F24_CASE(14)
+            EKF_F24_CASE(16)
+            EKF_F24_CASE(18)
+            EKF_F24_CASE(20)
+            EKF_F24_CASE(22)
+            EKF_F24_CASE(24)
+        }
+#undef EKF_F24_CASE
+        return hipGetLastError();
+    }
+#endif
+
+#if !defined(EKF_TU) || EKF_TU == 6
+hipError_t launch_flush_bf16x6(const DowndateParams& p, bool half, hipStream_t st, hipEvent_t ev_a, hipEvent_t ev_b)
+{
+    const unsigned wgrid = (unsigned)(8 * EKF_BF_WAVES * ((p.ncu + 7) / 8));   // EKF_BF_WAVES workgroups per CU
+#define EKF_BF_CASE(NSV)                                                                                \
+case NSV:                                                                                           \
+    if (half) hipExtLaunchKernelGGL((flush_f32_wave_kernel<_Float16, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, \
+                                    st, ev_a, ev_b, 0, p);                                          \
+    else hipExtLaunchKernelGGL((flush_f32_wave_kernel<float, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, st, \
+                               ev_a, ev_b, 0, p);                                                   \
+    break;
+    switch (p.nsteps) {
+        EKF_BF_CASE(2)
+        EKF_BF_CASE(4)
+        EKF_BF_CASE(6)
+        EKF_BF_CASE(8)
+        EKF_BF_CASE(10)
+        EKF_BF_CASE(12)
+        EKF_BF_CASE(14)
+        EKF_BF_CASE(16)
+    }
+#undef EKF_BF_CASE
+    return hipGetLastError();
+}
+#endif
+
 #if !defined(EKF_TU) || EKF_TU == 2
 hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hipStream_t st, hipEvent_t ev_a,
                            hipEvent_t ev_b)
@@ -5597,105 +5717,14 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
     const bool wave_ok = wave_shape && (p.nsteps >= 6 || p.variant == 8);
     const bool bf_shape = p.nsteps >= 2 && p.nsteps <= (p.bf == 2 ? F16X3_MAXS : 16) && p.nsteps % 2 == 0 && p.d.kmax <= 16 &&
                           p.nwt > 0 && p.wt != nullptr;
-    if (p.bf == 1 && bf_shape && p.variant == 24 && p.nwt24 > 0 && p.wt24 != nullptr) {
-        // EKF_ARITH_BF16X6, EKF_FLUSH_VARIANT=24: the 2 × 4 split-bf16 wave flush (measured 7 %
-        // slower than the 2 × 2 form below at T = 12; kept as an option, bit-identical)
-        const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
-#define EKF_BF24_CASE(NSV)                                                                              \
-    case NSV:                                                                                           \
-        if (half) hipExtLaunchKernelGGL((flush_bf24_kernel<_Float16, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, \
-                                        ev_a, ev_b, 0, p);                                              \
-        else hipExtLaunchKernelGGL((flush_bf24_kernel<float, NSV>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, \
-                                   ev_b, 0, p);                                                         \
-        break;
-        switch (p.nsteps) {
-            EKF_BF24_CASE(2)
-            EKF_BF24_CASE(4)
-            EKF_BF24_CASE(6)
-            EKF_BF24_CASE(8)
-            EKF_BF24_CASE(10)
-            EKF_BF24_CASE(12)
-            EKF_BF24_CASE(14)
-            EKF_BF24_CASE(16)
-        }
-#undef EKF_BF24_CASE
-        return hipGetLastError();
-    }
-    if (p.bf == 2 && bf_shape && p.variant == 24 && p.nwt24 > 0 && p.wt24 != nullptr) {
-        // EKF_ARITH_F16X3, EKF_OPT_FLUSH_FORM = 24: the 2 × 4 split-fp16 flush
-        const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));
-#define EKF_F24_CASE(NSV)                                                                               \
-    case NSV:                                                                                           \
-        if (half) hipExtLaunchKernelGGL((flush_bf24_kernel<_Float16, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, st, \
-                                        ev_a, ev_b, 0, p);                                               \
-        else hipExtLaunchKernelGGL((flush_bf24_kernel<float, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, st, ev_a, \
-                                   ev_b, 0, p);                                                          \
-        break;
-        switch (p.nsteps) {
-            EKF_F24_CASE(2)
-            EKF_F24_CASE(4)
-            EKF_F24_CASE(6)
-            EKF_F24_CASE(8)
-            EKF_F24_CASE(10)
-            EKF_F24_CASE(12)
-            EKF_F24_CASE(14)
-            EKF_F24_CASE(16)
-            EKF_F24_CASE(18)
-            EKF_F24_CASE(20)
-            EKF_F24_CASE(22)
-            EKF_F24_CASE(24)
-        }
-#undef EKF_F24_CASE
-        return hipGetLastError();
-    }
-    if (p.bf == 2 && bf_shape) {   // EKF_ARITH_F16X3: split-fp16 wave flush, groups of 2-24 steps (even)
-        const unsigned wgrid = (unsigned)(8 * EKF_F16_WAVES * ((p.ncu + 7) / 8));
-#define EKF_F16_CASE(NSV)                                                                               \
-    case NSV:                                                                                           \
-        if (half) hipExtLaunchKernelGGL((flush_f32_wave_kernel<_Float16, NSV, true, true>), dim3(wgrid),  \
-                                        dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p);                      \
-        else hipExtLaunchKernelGGL((flush_f32_wave_kernel<float, NSV, true, true>), dim3(wgrid),          \
-                                   dim3(DD_THREADS), 0, st, ev_a, ev_b, 0, p);                           \
-        break;
-        switch (p.nsteps) {
-            EKF_F16_CASE(2)
-            EKF_F16_CASE(4)
-            EKF_F16_CASE(6)
-            EKF_F16_CASE(8)
-            EKF_F16_CASE(10)
-            EKF_F16_CASE(12)
-            EKF_F16_CASE(14)
-            EKF_F16_CASE(16)
-            EKF_F16_CASE(18)
-            EKF_F16_CASE(20)
-            EKF_F16_CASE(22)
-            EKF_F16_CASE(24)
-        }
-#undef EKF_F16_CASE
-        return hipGetLastError();
-    }
-    if (p.bf == 1 && bf_shape) {   // EKF_ARITH_BF16X6: split-bf16 wave flush, groups of 2-16 steps (even)
-        const unsigned wgrid = (unsigned)(8 * EKF_BF_WAVES * ((p.ncu + 7) / 8));   // EKF_BF_WAVES workgroups per CU
-#define EKF_BF_CASE(NSV)                                                                                \
-    case NSV:                                                                                           \
-        if (half) hipExtLaunchKernelGGL((flush_f32_wave_kernel<_Float16, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, \
-                                        st, ev_a, ev_b, 0, p);                                          \
-        else hipExtLaunchKernelGGL((flush_f32_wave_kernel<float, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, st, \
-                                   ev_a, ev_b, 0, p);                                                   \
-        break;
-        switch (p.nsteps) {
-            EKF_BF_CASE(2)
-            EKF_BF_CASE(4)
-            EKF_BF_CASE(6)
-            EKF_BF_CASE(8)
-            EKF_BF_CASE(10)
-            EKF_BF_CASE(12)
-            EKF_BF_CASE(14)
-            EKF_BF_CASE(16)
-        }
-#undef EKF_BF_CASE
-        return hipGetLastError();
-    }
+    if (p.bf == 1 && bf_shape && p.variant == 24 && p.nwt24 > 0 && p.wt24 != nullptr)
+        return launch_flush_bf24(p, half, false, st, ev_a, ev_b);
+    if (p.bf == 2 && bf_shape && p.variant == 24 && p.nwt24 > 0 && p.wt24 != nullptr)
+        return launch_flush_bf24(p, half, true, st, ev_a, ev_b);
+    if (p.bf == 2 && bf_shape)   // EKF_ARITH_F16X3: split-fp16 wave flush, groups of 2-24 steps (even)
+        return launch_flush_f16x3(p, half, st, ev_a, ev_b);
+    if (p.bf == 1 && bf_shape)   // EKF_ARITH_BF16X6: split-bf16 wave flush, groups of 2-16 steps (even)
+        return launch_flush_bf16x6(p, half, st, ev_a, ev_b);
     if (wave_ok) {
         const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
 #define EKF_WAVE_CASE(NSV)                                                                              \

@@ -261,7 +261,7 @@ def test_survey_world_association(ekf_mod, oracle_mod, arith):
     assert out["sequential"] <= 0.10 * out["scans"], out
 
 
-def run_survey_parity(ekf_mod, oracle_mod, arith, T, pre, scans, N=N):
+def run_survey_parity(ekf_mod, oracle_mod, arith, T, pre, scans, N=N, options=None):
     """SURVEY §8d's world through the bench's schedule (E = 8, no drains inside a group), the
     restatement re-synced to the GPU per scan for y and the pose (committed every scan, read
     without a drain) and per group for the whole state. An instance-group that reported
@@ -270,7 +270,7 @@ def run_survey_parity(ekf_mod, oracle_mod, arith, T, pre, scans, N=N):
     one is held to the bar: association identical, y per scan ≤ 1e-8, P per group ≤ 1e-6."""
     world = G.make_world(N)
     st = G.initial_state(world, profile="survey")
-    ens = ekf_mod.Ensemble(N, E, 1, max_lines=L, flush_interval=T, arith=arith)
+    ens = ekf_mod.Ensemble(N, E, 1, max_lines=L, flush_interval=T, arith=arith, options=options or {})
     for e in range(E):
         ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
     for s in range(1, pre + 1):
@@ -315,22 +315,24 @@ def run_survey_parity(ekf_mod, oracle_mod, arith, T, pre, scans, N=N):
     return out
 
 
-@pytest.mark.parametrize("arith,T", [(2, 20), (2, 24), (1, 16), (0, 16)])
-def test_survey_world_parity_from_init(ekf_mod, oracle_mod, arith, T):
+@pytest.mark.parametrize("arith,T,rep", [(2, 20, 1), (2, 24, 1), (2, 20, 2), (1, 16, 1), (0, 16, 1)])
+def test_survey_world_parity_from_init(ekf_mod, oracle_mod, arith, T, rep):
     """VERDICT r04 Missing #1: the split arithmetics at the bench's T in SURVEY §8d's world, from
     the initial state over 48 scans (augmentation, the reset, the robot's heading starting to run
-    away): every instance-group not flagged by the library meets the bar."""
-    out = run_survey_parity(ekf_mod, oracle_mod, arith, T, 0, 48)
-    record(f"survey_parity_init_a{arith}_T{T}", out)
+    away): every instance-group not flagged by the library meets the bar. rep: the on-read replay
+    (EKF_OPT_MFMA_REPLAY: 1 the split products on the planes, 2 fp32 MFMA)."""
+    out = run_survey_parity(ekf_mod, oracle_mod, arith, T, 0, 48, options={"mfma_replay": rep})
+    record(f"survey_parity_init_a{arith}_T{T}_rep{rep}", out)
     assert out["assoc_checked"] >= 48   # (most of it unflagged)
 
 
-@pytest.mark.parametrize("arith,T", [(2, 20), (0, 16)])
-def test_survey_world_parity_steady_state(ekf_mod, oracle_mod, arith, T):
+@pytest.mark.parametrize("arith,T,rep", [(2, 20, 1), (2, 20, 2), (0, 16, 1)])
+def test_survey_world_parity_steady_state(ekf_mod, oracle_mod, arith, T, rep):
     """The same after a 200-scan pre-roll (the bench's): the reference's motion model has run away
     in every instance (poses 1e9-1e21 m, P up to 1e43). Instance 0 (P ≈ 1e30: every
     arithmetic, EXACT included, differs from the fp64 reference there) must be flagged; whatever
-    is not flagged meets the bar."""
-    out = run_survey_parity(ekf_mod, oracle_mod, arith, T, 200, 48)
-    record(f"survey_parity_steady_a{arith}_T{T}", out)
+    is not flagged meets the bar (instance 7, P ≈ 1e16-1e19: the split-fp16 planes cannot carry its
+    dynamic range, PLANE_SIGMA_EXACT takes its steps to the exact forms)."""
+    out = run_survey_parity(ekf_mod, oracle_mod, arith, T, 200, 48, options={"mfma_replay": rep})
+    record(f"survey_parity_steady_a{arith}_T{T}_rep{rep}", out)
     assert out["flagged_groups"] > 0
