@@ -93,19 +93,27 @@ enum { EKF_R_INTENDED = 0, EKF_R_AS_WRITTEN = 1 };
  *   products down to 2^-16 relative; the dropped ones are below 2^-24), accumulated in fp32; fp16
  *   storage is scaled out of its exponent on load and rounded to fp16 once per group on store.
  *   Within fp32 rounding of EXACT (the 1e-6 bound of BASELINE holds; fp16: its re-stated 1e-3) but
- *   no longer bit-identical across flush intervals. The association kernel applies pending steps
- *   by the same bf16 MFMAs on the planes and keeps the diagonal blocks in fp64. Groups of an even number of steps (2..16) without
- *   augmented rows or a reset take the split-bf16 flush; a group with augmentation or the reset,
- *   and an odd-sized group (a partial group flushed by a drain), take the EXACT forms
- *   (ekf_flush_kernel_name reports the form a group size runs).
+ *   no longer bit-identical across flush intervals: the state depends on T at the level of fp32
+ *   rounding. The association kernel applies pending steps by the same bf16 MFMAs on the planes
+ *   (EKF_OPT_MFMA_REPLAY) and keeps the diagonal blocks in fp64. Groups of an even number of steps
+ *   (2..16) take the split-bf16 flush, augmentation and resets included: the wave-tiles holding a
+ *   landmark the group added are recomputed by the exact general loop in a second pass, and those
+ *   of an instance whose map was reset in the group are stored as zero; the wave-tiles past every
+ *   step's nonzero operand rows are skipped (EKF_OPT_ACTIVE_FLUSH). An odd-sized group (a partial
+ *   group flushed by a drain) takes the EXACT forms (ekf_flush_kernel_name reports the form).
  * F16X3: the same requirements, schedule and fallbacks as BF16X6, with a two-part fp16 split
  *   instead: every operand row is scaled by 2^σ (σ per instance, from the largest landmark variance
  *   vmax: |2^σ·V| <= 2^12 because each step's downdate V·Vᵀ is bounded by the variances it reduces;
- *   the association kernel lowers σ when a new landmark raises vmax, always at a step that takes the
- *   EXACT forms), split into hi + lo fp16 parts (22 significant bits), and each product runs as three
- *   v_mfma_f32_32x32x16_f16 — (lo, hi), (hi, lo), (hi, hi) — accumulated in fp32, the accumulators
- *   holding P·2^(2σ) (power-of-two scalings, exact). Half the MFMA work and two thirds of the plane
- *   bytes of BF16X6; per product within ≈2^-21 relative (BF16X6: 2^-23), held to the same bar. */
+ *   σ is chosen at the first scan of a flush group and changes mid-group only on a reset or a new
+ *   landmark 64x above the variance it was set for; an instance whose σ changes inside a group,
+ *   or one with a landmark whose variance is below 2^-4·4^-σ (the planes would lose bits relative
+ *   to that landmark's own scale: PLANE_SIGMA_EXACT, a filter spanning more than 2^28 in
+ *   variance), runs that group's flush and on-read replay in the exact forms), split into hi + lo
+ *   fp16 parts (22 significant bits), and each product runs as three v_mfma_f32_32x32x16_f16 —
+ *   (lo, hi), (hi, lo), (hi, hi) — accumulated in fp32, the accumulators holding P·2^(2σ)
+ *   (power-of-two scalings, exact). Half the MFMA work and two thirds of the plane bytes of BF16X6;
+ *   per product within ≈2^-21 of the rows' own scale (BF16X6: 2^-23), held to the same bar per scan
+ *   from identical inputs (tests/test_bench_config.py, SURVEY §8d's world included). */
 enum { EKF_ARITH_EXACT = 0, EKF_ARITH_BF16X6 = 1, EKF_ARITH_F16X3 = 2 };
 
 typedef struct ekf_config {
@@ -125,9 +133,10 @@ typedef struct ekf_config {
                               flush in flight, and the second buffer is not allocated */
     int32_t flush_interval;/* T >= 1: the landmark block is rewritten once per T scans by one
                               rank-2·Σm MFMA pass; scans in between read it with the pending
-                              downdates applied on read. Bit-identical state for every T (the
-                              MFMA chain is an ordered FMA chain); T = 1: once per scan. <= 16
-                              (<= 24 with EKF_ARITH_F16X3) */
+                              downdates applied on read. With EKF_ARITH_EXACT the state is
+                              bit-identical for every T (the MFMA chain is an ordered FMA chain);
+                              the split arithmetics are within fp32 rounding of it instead.
+                              T = 1: once per scan. <= 16 (<= 24 with EKF_ARITH_F16X3) */
     int32_t arith;         /* EKF_ARITH_* (fp32 flush arithmetic); formerly reserved, 0 = EXACT */
     double mahalanobis;    /* MAHALANOBIS gate, Robot.h:15 (0.4) */
     double encoder_noise;  /* ENCODERNOISE, Robot.h:17 (0.024) */

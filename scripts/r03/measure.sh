@@ -1,5 +1,5 @@
 # Bench lines of record for DESIGN §5 (one box): fp16 / fp64 / N=1024 / N=256, the association's
-# bad cases (speculate option 0 and 2) and SURVEY §8d's world, then scripts/assoc_cases.py.
+# bad cases (speculate option 0 and 2) and SURVEY §8d's world, then tests/diag/assoc_cases.py.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${TAG:-r03_measure}
@@ -15,5 +15,5 @@ run n256 --capacity 256
 run spec0 --speculate 0
 run spec2 --speculate 2
 run survey --world survey
-timeout -k 10 600 python scripts/assoc_cases.py --k 24 --w 12 > $O/assoc_cases.txt 2>&1 || { echo "fail assoc_cases" >> $O/status; exit 1; }
+timeout -k 10 600 python tests/diag/assoc_cases.py --k 24 --w 12 > $O/assoc_cases.txt 2>&1 || { echo "fail assoc_cases" >> $O/status; exit 1; }
 echo done >> $O/status

@@ -4508,10 +4508,10 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                 sgl = prev;
                 st_e = e;
             };
-            auto in_scale = [&](const Item& t) __attribute__((always_inline)) {
+            auto in_exp = [&](const Item& t) __attribute__((always_inline)) {
                 int ex = 2 * sg0;
                 if constexpr (HALF) ex -= sload(p.pexp + t.e);
-                return -ldexpf(1.0f, ex);
+                return ex;
             };
             auto touched = [&](const Item& t) __attribute__((always_inline)) {
                 if (t.e != st_e) load_steps(t.e);
@@ -4563,7 +4563,8 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                 const bool skip = skip_of(cur);
                 const bool zero = zero_of(cur);   // (reset instance, untouched: stored as zero)
                 any_skip |= skip;
-                const float isc = in_scale(cur);
+                const int iex = in_exp(cur);
+                const float isc = -ldexpf(1.0f, iex);
 #pragma unroll
                 for (int i = 0; i < WT_N; i++)
 #pragma unroll
@@ -4621,12 +4622,17 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                // back from the last step's domain (−1, −2^x, −2^(x − 2σ): exact)
-                const float osc = F16 ? 1.0f / (isc * ldexpf(1.0f, 2 * (sgl - sg0))) : 1.0f / isc;
+                // back from the last step's domain (−1, −2^x, −2^(x − 2σ): an exact power of two, no
+                // division), as whole-vector products (packed multiplies); a zeroed wave-tile (zero is
+                // uniform) takes no multiply at all
+                const float osc = -ldexpf(1.0f, -iex - (F16 ? 2 * (sgl - sg0) : 0));
+                if (zero) {
 #pragma unroll
-                for (int i = 0; i < WT_N; i++)
+                    for (int i = 0; i < WT_N; i++) acc[i] = f32x16{};
+                } else {
 #pragma unroll
-                    for (int k = 0; k < 16; k++) acc[i][k] = zero ? 0.0f : acc[i][k] * osc;
+                    for (int i = 0; i < WT_N; i++) acc[i] = acc[i] * osc;
+                }
                 store_tiles(cur, acc, skip);
                 if (!more) break;
                 cur = nxt;

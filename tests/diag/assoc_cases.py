@@ -13,7 +13,7 @@ split-bf16 flush, T = 12):
 Per configuration: W warm-up scans, then K measured scans; reports the mean association-kernel time,
 the fraction of (instance, scan) whose speculation failed its verdict or was unresolved (path code
 bits 4/8, slam_ekf.h ekf_debug_result_words) or that ran the sequential path, matches per scan,
-augmented landmarks and resets. usage: python scripts/assoc_cases.py [case ...] [--k K] [--n N]
+augmented landmarks and resets. usage: python tests/diag/assoc_cases.py [case ...] [--k K] [--n N]
 """
 import argparse
 import json
@@ -22,7 +22,7 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from slam_ros_amd import ekf, scan_gen as G  # noqa: E402
 
 ap = argparse.ArgumentParser()

@@ -5,14 +5,14 @@
   B1: fast mode (sparse predict/gating, dense O(n²) update per match), OpenMP build on the host
      threads OMP_NUM_THREADS allows (bit-identical results), and its 1-core build.
 Same synthetic worlds and scans as bench.py (L = m = 8). Prints one JSON line per (mode, N).
-usage: python scripts/cpu_baselines.py [B0|B1|all]"""
+usage: python tests/diag/cpu_baselines.py [B0|B1|all]"""
 import json
 import os
 import platform
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np  # noqa: E402,F401
 
 from oracle import oracle as O  # noqa: E402

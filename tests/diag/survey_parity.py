@@ -5,7 +5,7 @@ scans with instances 0 and 7 checked against the restatement (oracle/, fast mode
 GPU state at every flush-group end. Per group and instance: ‖ΔP‖_F/‖P‖_F, ‖Δy‖/‖y‖, the absolute
 pose and landmark parts of Δy, ‖y‖, the map size and whether the group held a reset.
 
-usage: python scripts/r05/survey_parity.py ARITH:T[:opt=v...][,ARITH:T...] [pre] [scans]
+usage: python tests/diag/survey_parity.py ARITH:T[:opt=v...][,ARITH:T...] [pre] [scans]
 (ARITH in exact, bf16x6, f16x3). One JSON line per configuration.
 """
 import json
