@@ -4551,6 +4551,9 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
             if (cur.g >= g_end) return;   // (no live wave-tile: nothing to store, no second pass)
             next_live(cur, nxt);
             load_tiles(cur);
+            // (the first tiles ahead of every operand load, as in the loop: the wait count at the loop
+            // head then covers the tiles without draining the previous wave-tile's stores)
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int q = 0; q < RD - 1; q++) load_ops(q, cur, q);
             while (true) {
