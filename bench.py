@@ -302,7 +302,15 @@ def main():
     if prec == ekf.PREC_F64:
         arith = ekf.ARITH_EXACT   # the split-bf16 flush serves fp32 operands (fp32 and fp16 storage)
     if args.flush_interval <= 0:
-        args.flush_interval = 8 if prec == ekf.PREC_F64 else (8 if arith == ekf.ARITH_EXACT else (20 if arith == ekf.ARITH_F16X3 else 12))
+        # per capacity: the flush's pass over P is the part T amortises; below
+        # N = 2048 it costs 10-60 µs per launch while every pending step adds replay to every scan
+        # (sweep: scripts/r05/tsweep.sh)
+        if prec == ekf.PREC_F64 or arith == ekf.ARITH_EXACT:
+            args.flush_interval = 8
+        elif arith == ekf.ARITH_F16X3:
+            args.flush_interval = 20 if N > 2048 else (8 if N > 512 else 4)
+        else:
+            args.flush_interval = 12
     ens = ekf.Ensemble(N, E, prec, max_lines=L_LINES, device=local, pipeline=bool(args.pipeline),
                       flush_interval=args.flush_interval, arith=arith,
                       options={"speculate": args.speculate, "flush_form": args.flush_form,
@@ -447,11 +455,14 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": args.precision,
+        "dtype": f"{args.precision} storage, {args.arith if prec != ekf.PREC_F64 else 'exact'} products" if prec != ekf.PREC_F64 else "f64",
         "data": "synthetic (seeded line-landmark world and scans, SURVEY.md §8d)",
         "config": {
-            "workload": f"N={N} landmarks (n={n}), {E} EKF instances/GPU, L=m={L_LINES} matched "
-                        f"lines/scan, s=N-10 active, {args.precision} covariance storage",
+            "workload": (f"N={N} landmarks (n={n}), {E} EKF instances/GPU, L=m={L_LINES} matched "
+                         f"lines/scan, s=N-10 active, {args.precision} covariance storage" if args.world == "bench" else
+                         f"N={N} landmark capacity (n={n}), {E} EKF instances/GPU, L={L_LINES} lines/scan of "
+                         f"SURVEY §8d's world after a {PR}-scan pre-roll (most lines new landmarks, map resets; "
+                         f"the reference's motion model has run away, DESIGN §2.1), {args.precision} covariance storage"),
             "capacity": N, "instances_per_gpu": E, "global_batch": E_total,
             "lines_per_scan": L_LINES,
             "parallelism": (f"ensemble x{world} ({'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} "
@@ -480,6 +491,9 @@ def main():
             "mfma_frac_basis": (f"executed MFMA flops ({mfma_mult} x the algorithmic 2m·n(n+1) per step) "
                                 f"vs the dense {mfma_dtype.split()[0]} MFMA peak {mfma_peak} TF/s"),
             "ideal_ms": max(t_hbm, t_mfma) * 1e3,
+            # north_star's "fraction of the fp32 MFMA roofline", end to end: the algorithmic flops
+            # of every update one GPU completes per second (2m·n(n+1) each) over the dense fp32 peak
+            "fp32_mfma_frac_end_to_end": (value / world) * 2 * L_LINES * n * (n + 1) / (MFMA_F32_PEAK_TFS * 1e12),
             "traffic_source": traffic_src,
             "lib_sha": sha,
         },
