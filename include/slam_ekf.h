@@ -69,8 +69,8 @@ enum {
                               EKF_PREC_F32: a new landmark variance above 2^120, within 2^8 of
                               fp32's range (a diverged filter: the fp64 storage holds it) */
     EKF_ST_PRECISION = 32, /* EKF_PREC_F32: the call's update shrank some landmark's variance (the
-                              trace of its 2x2 block) by more than 2^6, or left it non-positive:
-                              more than 6 of fp32's 24 significant bits cancel, so the stored
+                              trace of its 2x2 block) by more than 2^4, or left it non-positive:
+                              more than 4 of fp32's 24 significant bits cancel, so the stored
                               block is no longer guaranteed to resolve the fp64 reference to the
                               1e-6 bar (informational: the state commits; EKF_PREC_F64 holds any
                               filter). In SURVEY §8d's world the reference's own motion model runs

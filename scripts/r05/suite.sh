@@ -3,7 +3,7 @@
 set -o pipefail
 out=gpurun_out/${TAG:-r05_suite}; mkdir -p $out
 rm -f gpurun_out/bench_config_parity.json
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > $out/pytest.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu ${XFLAG--x} -v --timeout 400 --timeout-method thread > $out/pytest.log 2>&1
 rc=$?
 cp gpurun_out/bench_config_parity.json $out/ 2>/dev/null
 [ $rc -eq 0 ] || exit $rc

@@ -13,11 +13,10 @@ enum { PHASE_PREDICT = 1, PHASE_UPDATE = 2, PHASE_BOTH = 3 };
 enum { EKF_ST_SINGULAR = EKF_ST_SINGULAR_S, EKF_ST_CAP = EKF_ST_CAPACITY, EKF_ST_NSYM = EKF_ST_NONSYM,
        EKF_ST_TIMEOUT_BIT = EKF_ST_SYNC_TIMEOUT, EKF_ST_RANGE_BIT = EKF_ST_RANGE,
        EKF_ST_PRECISION_BIT = EKF_ST_PRECISION };
-// fp32 storage: a scan that shrinks an owned landmark's variance trace by more than 2^6 sets
-// EKF_ST_PRECISION: the cancellation leaves fewer than 18 of fp32's 24 significant bits (2^-18 ≈
-// 4e-6 per element). Measured in SURVEY §8d's world: every group with ratios up to
-// ≈20 met the 1e-6 bar, and the first group over it (the EXACT arithmetic's 1.03e-6) had 3e2
-constexpr double PREC_CANCEL = 64.0;
+// fp32 storage: a scan that shrinks an owned landmark's variance trace by more than 2^4 sets
+// EKF_ST_PRECISION: the cancellation leaves fewer than 20 of fp32's 24 significant bits, i.e. a
+// stored result no longer guaranteed to 2^-20 ≈ 1e-6 relative (the P bar) element by element
+constexpr double PREC_CANCEL = 16.0;
 // fp16 storage: a stored variance above 2^14 (a quarter of the fp16 range) raises EKF_ST_RANGE
 constexpr double F16_RANGE_WARN = 16384.0;
 // fp32 storage: a new landmark variance above 2^120 (fp32's largest finite value is ≈2^128) sets

@@ -3035,10 +3035,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         }
     }
     EKF_STAMP(27);
-    // fp32 storage: an update that cancels more than 6 of fp32's 24 significant bits of a
-    // landmark's variance (trace before / after > PREC_CANCEL = 2^6), or leaves it non-positive, is
-    // flagged EKF_ST_PRECISION; the result still commits (a diverging filter: SURVEY §8d's world,
-    // DESIGN §2.1)
+    // fp32 storage: an update that cancels more than 4 of fp32's 24 significant bits of a
+    // landmark's variance (trace before / after > PREC_CANCEL = 2^4: the result no longer
+    // guaranteed to 2^-20, the P bar), or leaves it non-positive, is flagged EKF_ST_PRECISION; the
+    // result still commits (a diverging filter: SURVEY §8d's world)
     if constexpr (sizeof(C) == 4 && !Stor<T>::half)
         if (own && !reset && j < s && dsq > 0.0) {
             const double ta = Dj[0] + Dj[3];
