@@ -73,8 +73,13 @@ enum {
                               more than 4 of fp32's 24 significant bits cancel, so the stored
                               block is no longer guaranteed to resolve the fp64 reference to the
                               1e-6 bar (informational: the state commits; EKF_PREC_F64 holds any
-                              filter). In SURVEY §8d's world the reference's own motion model runs
-                              away and this is how a diverging instance shows */
+                              filter). Every precision: a gate distance the call evaluated (up to
+                              the winner) lies within the storage precision of the gate of the
+                              threshold (|ΔP_ab| up to eta·sqrt(P_aa·P_bb), eta 2^-16 for F32,
+                              2^-8 F16, 2^-44 F64, first order), so the reference's state may decide
+                              that line differently. In SURVEY §8d's world the reference's own
+                              motion model runs away and this is how a diverging
+                              instance shows */
 };
 
 /* storage precision of the landmark-landmark covariance block (robot rows, mean: always fp64).

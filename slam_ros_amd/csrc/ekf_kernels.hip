@@ -503,7 +503,25 @@ struct Cand {
     double h10, h11, h1l;
     int pass;
     int singular;
+    int amb;   // the decision is within the storage precision of the gate (gate_eta)
 };
+
+// The storage precision of the gate (round 5). P as stored differs from the fp64 reference's by
+// the roundings of its storage and of the flush's products; eta bounds that difference relative
+// to the magnitudes |P_ab| <= sqrt(P_aa·P_bb) of the 5×5 block. With H0 = (0, 0, −1, 1, 0) and
+// ‖H1‖² = 2 + h1l², |ΔS_ab| <= eta·s_a·s_b with s_a = Σ_k |H_ak|·√P_kk, and by Cauchy-Schwarz
+// s0² <= m0 = 2(|p22| + |daa|), s1² <= m1 = ‖H1‖²·tr|P5|, s0·s1 <= (m0 + m1)/2. The filters add
+// these (root-free) bounds to their error bounds (a rejection then
+// holds for every P within eta; the decisions themselves are unchanged, so every path still agrees
+// bit for bit), and the exact evaluation reports a distance within the first-order bound
+// eta·(|w0|·s0 + |w1|·s1)², w = S⁻¹v, of the gate as ambiguous: EKF_ST_PRECISION, the statement
+// that this state does not resolve the reference's decision (SURVEY §8d's run-away world, where
+// S is the difference of terms 1e10 times larger). fp32 storage: 2^-16 (16 × the
+// per-group P bar of 1e-6); fp16: 2^-8; fp64: 2^-44.
+template <typename T> constexpr double gate_eta()
+{
+    return sizeof(T) == 8 ? 0x1p-44 : sizeof(T) == 4 ? 0x1p-16 : 0x1p-8;
+}
 
 // 5×5 block {0,1,2, 3+2j, 4+2j} of the current P: robot 3×3 (R33), robot–landmark columns
 // (Rs, owned), landmark diagonal block (Dj, owned), and H·P·Hᵀ + R for given H row 1.
@@ -587,7 +605,7 @@ __device__ __forceinline__ void sincos_near(double ma, double ma0, double s0, do
 // Exact candidate evaluation in fp64 (Robot.cpp:367-489).
 __device__ __forceinline__ void eval_candidate(const Block5& b, double ma, double mr, double sn,
                                                double cs, const double xp[3], double za, double zr,
-                                               const double Rm[4], double gate, Cand& c)
+                                               const double Rm[4], double gate, double eta, Cand& c)
 {
     c.h10 = -cs;
     c.h11 = -sn;
@@ -612,6 +630,14 @@ __device__ __forceinline__ void eval_candidate(const Block5& b, double ma, doubl
     if (a < g2 * (1.0 - 0x1p-40)) c.pass = 1;
     else if (a > g2 * (1.0 + 0x1p-40)) c.pass = 0;
     else c.pass = !(sqrt(a) > gate);
+    // the storage precision of the gate (gate_eta): |ΔS_ab| <= eta·s_a·s_b with s_a = Σ_k |H_ak|·√P_kk
+    // (H0 = (0, 0, −1, 1, 0), H1 = (h10, h11, 0, h1l, 1) on rows 0, 1, 2, a, b), so to first order
+    // |Δd²| <= eta·(|w0|·s0 + |w1|·s1)², w = S⁻¹v (the roots in fp32, 2^-8 of slack)
+    auto rt = [](double x) { return (double)__builtin_amdgcn_sqrtf((float)fabs(x)); };
+    const double s0 = rt(b.p22) + rt(b.daa);
+    const double s1 = fabs(c.h10) * rt(b.p00) + fabs(c.h11) * rt(b.p11) + fabs(c.h1l) * rt(b.daa) + rt(b.dbb);
+    const double wv = fabs(vs0) * s0 + fabs(vs1) * s1;
+    c.amb = !c.singular && !(fabs(d2 - g2) > eta * (1.0 + 0x1p-8) * wv * wv);
 }
 
 // Certified rejection: true only if the exact evaluation is guaranteed to fail the gate. It
@@ -621,7 +647,7 @@ __device__ __forceinline__ void eval_candidate(const Block5& b, double ma, doubl
 // |S00·S11| + |S01·S10| (so that the reference's LU-based d² is within 1e-9 of q/det).
 __device__ __forceinline__ bool certified_reject(const Block5& b, double ma, double mr, double sn,
                                                  double cs, const double xp[3], double za, double zr,
-                                                 const double Rm[4], double gate)
+                                                 const double Rm[4], double gate, double eta)
 {
     if (!(fabs(ma) <= 8.0) || Rm[1] != Rm[2]) return false;
     const double EPS = 1e-5;
@@ -637,21 +663,27 @@ __device__ __forceinline__ bool certified_reject(const Block5& b, double ma, dou
                        fmax(fmax(fabs(b.p0b), fabs(b.p1b)), fabs(b.p2b))));
     Pm = fmax(Pm, fmax(fmax(fabs(b.daa), fabs(b.dab)), fmax(fabs(b.dba), fabs(b.dbb))));
     const double dh = (2.0 * EPS + ex) * Pm;                   // |Δ hp1[b]|
-    const double dS01 = EPS * (fabs(hp0[0]) + fabs(hp0[1])) + ex * fabs(hp0[3]);
-    const double dS10 = 2.0 * dh;
+    // + the storage precision of the gate (gate_eta)
+    const double m0 = eta * 2.0 * (fabs(b.p22) + fabs(b.daa));
+    const double m1 = eta * (2.0 + (fabs(h1l) + ex) * (fabs(h1l) + ex)) *
+                      (fabs(b.p00) + fabs(b.p11) + fabs(b.p22) + fabs(b.daa) + fabs(b.dbb));
+    const double dS00 = m0;
+    const double dS01 = EPS * (fabs(hp0[0]) + fabs(hp0[1])) + ex * fabs(hp0[3]) + 0.5 * (m0 + m1);
+    const double dS10 = 2.0 * dh + 0.5 * (m0 + m1);
     const double dS11 = dh * (3.0 + fabs(h1l) + ex) + EPS * (fabs(hp1[0]) + fabs(hp1[1])) +
-                        ex * fabs(hp1[3]);
+                        ex * fabs(hp1[3]) + m1;
     const double dv1 = ex;
     const double q = v0 * v0 * S[3] - v0 * v1 * (S[1] + S[2]) + v1 * v1 * S[0];
     const double det = S[0] * S[3] - S[1] * S[2];
     const double mag_det = fabs(S[0] * S[3]) + fabs(S[1] * S[2]);
     const double mag_q = v0 * v0 * fabs(S[3]) + fabs(v0 * v1) * (fabs(S[1]) + fabs(S[2])) +
                          v1 * v1 * fabs(S[0]);
-    const double dq = v0 * v0 * dS11 + fabs(v0) * (fabs(v1) + dv1) * (dS01 + dS10) +
+    const double av1 = fabs(v1) + dv1;
+    const double dq = v0 * v0 * dS11 + fabs(v0) * av1 * (dS01 + dS10) +
                       fabs(v0) * dv1 * fabs(S[1] + S[2]) +
-                      (2.0 * fabs(v1) * dv1 + dv1 * dv1) * fabs(S[0]) + 1e-9 * mag_q;
-    const double ddet = fabs(S[0]) * dS11 + fabs(S[1]) * dS10 + fabs(S[2]) * dS01 +
-                        dS01 * dS10 + 1e-9 * mag_det;
+                      (2.0 * fabs(v1) * dv1 + dv1 * dv1) * fabs(S[0]) + av1 * av1 * dS00 + 1e-9 * mag_q;
+    const double ddet = fabs(S[0]) * dS11 + fabs(S[3]) * dS00 + fabs(S[1]) * dS10 + fabs(S[2]) * dS01 +
+                        dS01 * dS10 + dS00 * dS11 + 1e-9 * mag_det;
     const double det_lo = det - ddet;
     if (!(det_lo > 1e-6 * mag_det)) return false;              // also false for NaN / Inf
     return (q - dq) > gate * gate * (1.0 + 1e-6) * (det + ddet);
@@ -676,7 +708,7 @@ __device__ __forceinline__ bool certified_reject(const Block5& b, double ma, dou
 constexpr double QR_TRIG_EPS = 4e-6;
 __device__ __forceinline__ bool quick_reject(const Block5& b, double ma, double mr, double ma0, double s0,
                                              double c0, const double xp[3], double za, double zr,
-                                             const double Rm[4], double gate)
+                                             const double Rm[4], double gate, double eta)
 {
     // every bound evaluated, the tests combined without branches (bitwise on bools): the same
     // values as the early-exit form, fewer exec-mask instructions on the per-line chain
@@ -686,14 +718,15 @@ __device__ __forceinline__ bool quick_reject(const Block5& b, double ma, double 
     const bool ok = (Rm[1] == Rm[2]) & (tr5 >= 0.0) & (Rm[0] > 1e-5 * 2.0 * tr5) & (Rm[3] > 1e-5 * H2 * tr5) &
                     (fabs(ma0) <= 8.0);
     const double g2 = gate * gate * (1.0 + 1e-6);
-    const double S00 = b.p22 - 2.0 * b.p2a + b.daa + Rm[0];
+    // S00 + its storage precision (gate_eta): |Δ(p22 − 2·p2a + daa)| <= 2·eta·(|p22| + |daa|)
+    const double S00 = b.p22 - 2.0 * b.p2a + b.daa + Rm[0] + 2.0 * eta * (fabs(b.p22) + fabs(b.daa));
     const double x = za - (ma - xp[2]);
     const double cd = fabs(x - 2.0 * EKF_PI * rint(x * (0.5 / EKF_PI)));
     const double a0 = cd - 1e-12 * (1.0 + fabs(x));
     const bool r0 = (S00 > 0.0) & (a0 > 0.0) & (a0 * a0 > g2 * S00);
     const double v1e = zr - (mr - (xp[0] * c0 + xp[1] * s0));
     const double a1 = fabs(v1e) - X * (fabs(ma - ma0) + QR_TRIG_EPS) - 1e-12 * (1.0 + fabs(zr) + fabs(mr) + X);
-    const double S11u = H2 * tr5 * (1.0 + 1e-5) + Rm[3];
+    const double S11u = H2 * tr5 * (1.0 + 1e-5 + eta) + Rm[3];
     const bool r1 = (a1 > 0.0) & (a1 * a1 > g2 * S11u);
     return ok & (r0 | r1);
 }
@@ -706,7 +739,8 @@ __device__ __forceinline__ bool quick_reject(const Block5& b, double ma, double 
 // landmark angle from the fast fp32 path with EPS = 1e-4 allowed. v0 is the exact fp64 value of
 // the evaluation (innovation_angle, no trigonometry), rounded once.
 __device__ __forceinline__ bool certified_reject_f32(const Block5& b, double ma, double mr, const double xp[3],
-                                                     double za, double zr, const double Rm[4], double gate)
+                                                     double za, double zr, const double Rm[4], double gate,
+                                                     double eta)
 {
     if (!(fabs(ma) <= 8.0) || Rm[1] != Rm[2]) return false;
     constexpr float U = 5.9604645e-08f, EPS = 1e-4f;
@@ -743,11 +777,16 @@ __device__ __forceinline__ bool certified_reject_f32(const Block5& b, double ma,
     Pm = fmaxf(Pm, fmaxf(fmaxf(fabsf(daa), fabsf(dab)), fmaxf(fabsf(dba), fabsf(dbb))));
     const float Hs = 1.f + fabsf(h10) + fabsf(h11) + fabsf(h1l);
     const float dh = (2.f * EPS + ex) * Pm;
-    const float dS00 = 12.f * U * (4.f * Pm + fabsf(R0));
-    const float dS01 = EPS * (fabsf(a0) + fabsf(a1)) + ex * fabsf(a3) + 12.f * U * (2.f * Hs * Pm + fabsf(R1));
-    const float dS10 = 2.f * dh + 12.f * U * (2.f * Hs * Pm + fabsf(R2));
+    // + the storage precision of the gate (gate_eta; |h1l| <= ax, 8u for these sums)
+    const float fe = (float)eta * (1.f + 8.f * U);
+    const float m0 = fe * 2.f * (fabsf(p22) + fabsf(daa));
+    const float m1 = fe * (2.f + ax * ax) * (fabsf(p00) + fabsf(p11) + fabsf(p22) + fabsf(daa) + fabsf(dbb));
+    const float dS00 = 12.f * U * (4.f * Pm + fabsf(R0)) + m0;
+    const float dS01 = EPS * (fabsf(a0) + fabsf(a1)) + ex * fabsf(a3) + 12.f * U * (2.f * Hs * Pm + fabsf(R1)) +
+                       0.5f * (m0 + m1);
+    const float dS10 = 2.f * dh + 12.f * U * (2.f * Hs * Pm + fabsf(R2)) + 0.5f * (m0 + m1);
     const float dS11 = dh * (3.f + fabsf(h1l) + ex) + EPS * (fabsf(c0) + fabsf(c1)) + ex * fabsf(c3) +
-                       12.f * U * (Hs * Hs * Pm + fabsf(R3));
+                       12.f * U * (Hs * Hs * Pm + fabsf(R3)) + m1;
     const float dv1 = ex + 8.f * U * ((float)fabs(zr) + (float)fabs(mr) + ax);
     const float q = v0 * v0 * S3 - v0 * v1 * (S1 + S2) + v1 * v1 * S0;
     const float det = S0 * S3 - S1 * S2;
@@ -1574,6 +1613,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
 {
     const Dims d = p.d;
     const int r_mode = HOT ? (int)EKF_R_INTENDED : p.r_mode;   // (HOT: the launch checked it)
+    constexpr double ETA = gate_eta<T>();
     // 1-D grid, instance-minor: block b is workgroup b / E of instance b % E. Workgroups are
     // dealt round-robin over the 8 XCDs, so with 8 instances per launch each instance's
     // workgroups share one XCD (and its L2) in every launch; correctness never depends on it
@@ -2343,9 +2383,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         fill_block5(b5, R33l, w0, w1, w2, wD);
                         double sn, cs;
                         sincos_near(wy.x, wma0, ws0, wc0, sn, cs);
-                        eval_candidate(b5, wy.x, wy.y, sn, cs, xpl, ln.alpha, ln.r, Rm, p.gate, c);
+                        eval_candidate(b5, wy.x, wy.y, sn, cs, xpl, ln.alpha, ln.r, Rm, p.gate, ETA, c);
                         // GSL_EDOM of the winner (the reference evaluated it: Robot.cpp:454)
                         if (c.singular) atomicOr(&sh_rwst, (int)EKF_ST_SINGULAR);
+                        if (c.amb) atomicOr(&sh_rwst, (int)EKF_ST_PRECISION_BIT);
                         okl = c.pass ? 1 : 0;
                         pk[PK_OK] = okl ? 1.0 : 0.0;
                     }
@@ -2667,7 +2708,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                             // the quick filter and the gain rows in one block (independent chains);
                             // the gain rows take effect only if the guessed winner passed (wok,
                             // uniform; otherwise the package words are not written)
-                            deeper = cand && !quick_reject(b5, ybx, yby, ma0, s0f, c0f, xpg, ln.alpha, ln.r, Rm, p.gate);
+                            deeper = cand && !quick_reject(b5, ybx, yby, ma0, s0f, c0f, xpg, ln.alpha, ln.r, Rm, p.gate, ETA);
                             double blk[4];
                             if constexpr (sizeof(typename Stor<T>::C) == 4) {
                                 const float4 bk = sh_blk[i][tid];
@@ -2690,21 +2731,22 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
                         }
                         sub(18);
                     } else {
-                        deeper = cand && !quick_reject(b5, ybx, yby, ma0, s0f, c0f, xpg, ln.alpha, ln.r, Rm, p.gate);
+                        deeper = cand && !quick_reject(b5, ybx, yby, ma0, s0f, c0f, xpg, ln.alpha, ln.r, Rm, p.gate, ETA);
                     }
                     if (deeper) {   // rare: the certified fp32 and fp64 filters, then the exact evaluation
                         deep = 1;
                         bool pass = false;
                         double sn = 0.0, cs = 1.0;
-                        if (!certified_reject_f32(b5, ybx, yby, xpg, ln.alpha, ln.r, Rm, p.gate) &&
+                        if (!certified_reject_f32(b5, ybx, yby, xpg, ln.alpha, ln.r, Rm, p.gate, ETA) &&
                             (deep = 2, exact_sc(), sincos_near(ybx, ma0, s0j, c0j, sn, cs),
-                             !certified_reject(b5, ybx, yby, sn, cs, xpg, ln.alpha, ln.r, Rm, p.gate))) {
+                             !certified_reject(b5, ybx, yby, sn, cs, xpg, ln.alpha, ln.r, Rm, p.gate, ETA))) {
                             deep = 3;
                             Cand c;
-                            eval_candidate(b5, ybx, yby, sn, cs, xpg, ln.alpha, ln.r, Rm, p.gate, c);
+                            eval_candidate(b5, ybx, yby, sn, cs, xpg, ln.alpha, ln.r, Rm, p.gate, ETA, c);
                             // GSL_EDOM counts only for candidates the reference evaluates: the
                             // unmatched ones up to the winner (Robot.cpp:313-498 stops there)
                             if (c.singular && (w < 0 || !wok || j <= w)) status |= EKF_ST_SINGULAR;
+                            if (c.amb && (w < 0 || !wok || j <= w)) status |= EKF_ST_PRECISION_BIT;
                             pass = c.pass;
                         }
                         // the guess must be the first passing unmatched landmark; a guessed
@@ -2818,17 +2860,18 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         line_R(ln, i, r_mode, Rm);
         // gating of the owned candidate (Robot.cpp:313-498); the first passing unmatched j wins
         int best = 0x7fffffff;
-        bool sing = false;
+        bool sing = false, amb = false;
         Cand c;
         if (own && j < s && !matched) {
             Block5 b5;
             fill_block5(b5, R33, rr0, rr1, rr2, Dj);
             double sn, cs;
-            if (!quick_reject(b5, yb.x, yb.y, ma0, s0f, c0f, xp, ln.alpha, ln.r, Rm, p.gate) &&
+            if (!quick_reject(b5, yb.x, yb.y, ma0, s0f, c0f, xp, ln.alpha, ln.r, Rm, p.gate, ETA) &&
                 (exact_sc(), sincos_near(yb.x, ma0, s0j, c0j, sn, cs),
-                 !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate))) {
-                eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, c);
+                 !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, ETA))) {
+                eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, ETA, c);
                 sing = c.singular;
+                amb = c.amb;
                 if (c.pass) best = j;
             }
         }
@@ -2883,6 +2926,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         EKF_STAMP(4);
         // GSL_EDOM counts only for the candidates the reference evaluates (up to the winner)
         if (sing && j <= jstar) status |= EKF_ST_SINGULAR;
+        if (amb && j <= jstar) status |= EKF_ST_PRECISION_BIT;
         if (jstar == 0x7fffffff) {
             // no match (or s == 0): the line goes to extraLines (Robot.cpp:308-310, 492-496)
             if (lead) {
@@ -3286,6 +3330,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
 {
     using C = typename Stor<T>::C;
+    constexpr double ETA = gate_eta<T>();
     const Dims d = p.d;
     const int n = d.n;
     const int j = (int)(blockIdx.x * blockDim.x + threadIdx.x);   // every rank runs every landmark
@@ -3404,16 +3449,17 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
     line_R(ln, p.line, p.r_mode, Rm);
 
     // the gate of one landmark exactly as the sequential path (Robot.cpp:313-498)
-    auto gate_of = [&](Cand& c, bool& pass, bool& sing) {
+    auto gate_of = [&](Cand& c, bool& pass, bool& sing, bool& amb) {
         Block5 b5;
         fill_block5(b5, R33, rr0, rr1, rr2, Dj);
         double sn, cs;
-        pass = sing = false;
-        if (!quick_reject(b5, yb.x, yb.y, ma0, s0f, c0f, xp, ln.alpha, ln.r, Rm, p.gate) &&
+        pass = sing = amb = false;
+        if (!quick_reject(b5, yb.x, yb.y, ma0, s0f, c0f, xp, ln.alpha, ln.r, Rm, p.gate, ETA) &&
             (sincos_near(yb.x, ma0, s0j, c0j, sn, cs),
-             !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate))) {
-            eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, c);
+             !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, ETA))) {
+            eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, ETA, c);
             sing = c.singular;
+            amb = c.amb;
             pass = c.pass;
         }
     };
@@ -3425,9 +3471,9 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
             return;
         }
         Cand c;
-        bool pass, sing;
-        gate_of(c, pass, sing);
-        p.flags[j] = (fl & 1) | (sing ? 2 : 0);
+        bool pass, sing, amb;
+        gate_of(c, pass, sing, amb);
+        p.flags[j] = (fl & 1) | (sing ? 2 : 0) | (amb ? 4 : 0);
         if (pass) atomicMin(ctl + SC_WIN, j);
         return;
     }
@@ -3441,8 +3487,8 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
             if (local_blk(j, jstar)) pll_block(pv, 2 * j, 2 * jstar, blk);
             if (j == jstar) {
                 Cand c;
-                bool pass, sing;
-                gate_of(c, pass, sing);
+                bool pass, sing, amb;
+                gate_of(c, pass, sing, amb);
                 build_package(c, R33, rr0, rr1, rr2, p.pkg);
                 const int m = ctl[SC_M];
                 for (int q = 0; q < m; q++) {   // the winner's V rows of the earlier matches (Robot.cpp:560-568)
@@ -3462,6 +3508,7 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
         const int jstar = ctl[SC_WIN];
         // GSL_EDOM counts only for the candidates the reference evaluates (up to the winner)
         int st = (fl & 2) && j <= jstar ? (int)EKF_ST_SINGULAR : 0;
+        if ((fl & 4) && j <= jstar) st |= EKF_ST_PRECISION_BIT;   // (gate_eta)
         if (p.r_mode == 1 && (p.line == 1 || p.line == 2)) st |= EKF_ST_NSYM;
         if (st) atomicOr(ctl + SC_STATUS, st);
         if (jstar == 0x7fffffff) return;

@@ -5,6 +5,9 @@ passes 2^14 at that exponent, and re-chosen by ekf_rescale.
 
 Parity: per scan from the identical stored state against the CPU restatement (oracle/), P within
 the fp16 bound of tests/test_gpu_parity.py (1e-3 relative Frobenius), association identical.
+EKF_ST_PRECISION may accompany a scan here: with fp16 storage (gate_eta 2^-8) a random line whose
+distance to some landmark lies within ≈1 % of the gate is reported as not resolved by the stored
+state; from the identical stored state the association still agrees, which these tests check.
 """
 import math
 
@@ -81,7 +84,7 @@ def test_large_covariance_updates(ekf_mod, oracle_mod):
         res = ens.localize(enc, lines, [lines.shape[1]])[0]
         m = ref.localize(lines[0], enc[0])
         assert res["match"] == m, (step, res["match"], m)
-        assert res["status"] & ~ekf_mod.ST_RANGE == 0, res["status"]
+        assert res["status"] & ~(ekf_mod.ST_RANGE | ekf_mod.ST_PRECISION) == 0, res["status"]
         P, y, s, pose = ens.download_state(0)
         assert np.all(np.isfinite(P))
         assert rel(P, ref.P_t0) <= P_TOL16, (step, rel(P, ref.P_t0))
@@ -126,7 +129,7 @@ def test_match_free_trajectory_rescales(ekf_mod, oracle_mod):
     assert min(r["exp"] for r in log) <= 4          # 10 → 8 → 6 → 4 as the variances pass 16, 64, 256
     for r in log:
         assert r["match"] == r["m"], r["k"]
-        assert r["status"] & ~ekf_mod.ST_RANGE == 0, (r["k"], r["status"])
+        assert r["status"] & ~(ekf_mod.ST_RANGE | ekf_mod.ST_PRECISION) == 0, (r["k"], r["status"])
         assert r["rel"] <= P_TOL16, (r["k"], r["rel"])
 
 
