@@ -105,6 +105,8 @@ def parse():
     ap.add_argument("--mfma-replay", type=int, choices=[0, 1, 2], default=1,
                     help="EKF_OPT_MFMA_REPLAY: 1 the split products on the planes (default), 2 fp32 "
                          "MFMA on the fp32 operand rows, 0 the per-element forms")
+    ap.add_argument("--scan-threads", type=int, choices=[0, 64, 128, 192], default=0,
+                    help="EKF_OPT_SCAN_THREADS: landmarks per association workgroup, 0 automatic")
     ap.add_argument("--force-collective", action="store_true",
                     help="run the scan broadcast through the collective even at one rank (RANK=0, "
                          "WORLD_SIZE=1, MASTER_* in the env): the RCCL device branch on a one-GPU box")
@@ -314,7 +316,7 @@ def main():
     ens = ekf.Ensemble(N, E, prec, max_lines=L_LINES, device=local, pipeline=bool(args.pipeline),
                       flush_interval=args.flush_interval, arith=arith,
                       options={"speculate": args.speculate, "flush_form": args.flush_form,
-                               "mfma_replay": args.mfma_replay})
+                               "mfma_replay": args.mfma_replay, "scan_threads": args.scan_threads})
     # one real stream for everything (torch's default stream has handle 0, which the C-ABI reads
     # as "the context's own stream"): the payload copies, the RCCL waits (work.wait() orders the
     # current stream) and the EKF kernels are then ordered on the same queue

@@ -8,4 +8,4 @@ rc=$?
 cp gpurun_out/bench_config_parity.json $out/ 2>/dev/null
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || exit 1
-[ "${SWEEP:-1}" = "1" ] && bash scripts/r05/tsweep.sh
+if [ "${SWEEP:-1}" = "1" ]; then bash scripts/r05/tsweep.sh; fi

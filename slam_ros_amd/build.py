@@ -37,11 +37,13 @@ def _stale(target: str, deps: list[str]) -> bool:
 # step on the VALU, which cannot read AGPRs, so the AGPR form paid a read + write copy per
 # element per step (fp16 flush 0.84 -> 0.72 ms at N=4096, T=8; fp32 unchanged or faster)
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-mllvm", "-amdgpu-mfma-vgpr-form"]
-# ekf_kernels.hip is compiled as six units (EKF_TU: 1 association kernels, 2 the exact and fp64
-# flushes, 3 the rest, 4 / 5 / 6 the split-fp16, 2 x 4 and split-bf16 flushes), in parallel with
-# ekf_api.hip: each unit instantiates only the kernels its launchers use
-UNITS = [("ekf_kernels.hip", 4), ("ekf_kernels.hip", 2), ("ekf_kernels.hip", 1), ("ekf_kernels.hip", 5),
-         ("ekf_kernels.hip", 6), ("ekf_kernels.hip", 3), ("ekf_api.hip", 0)]
+# ekf_kernels.hip is compiled as eight units (EKF_TU: 1 association kernels, 2 the exact and fp64
+# flushes, 3 the rest, 4 / 5 / 6 the split-fp16, 2 x 4 and split-bf16 flushes, 7 / 8 the association
+# kernel on 128 / 64 landmarks per workgroup), in parallel with ekf_api.hip: each unit instantiates
+# only the kernels its launchers use
+UNITS = [("ekf_kernels.hip", 4), ("ekf_kernels.hip", 2), ("ekf_kernels.hip", 1), ("ekf_kernels.hip", 7),
+         ("ekf_kernels.hip", 8), ("ekf_kernels.hip", 5), ("ekf_kernels.hip", 6), ("ekf_kernels.hip", 3),
+         ("ekf_api.hip", 0)]
 
 
 def _compile_link(out: str, defines: list[str], verbose: bool = False) -> None:

@@ -99,7 +99,11 @@ struct ekf_ctx {
     int mfrep_opt;            // EKF_OPT_MFMA_REPLAY
     int active_flush;         // EKF_OPT_ACTIVE_FLUSH
     int mfrep;                // split-bf16 contexts: MFMA replay of pending steps (bf && mfrep_opt)
-    int scan_batch;           // instances per association launch (co-residency bound)
+    int scan_batch;           // instances per association launch (co-residency bound), 192 wide
+    int resident;             // association workgroups the device holds at once
+    int nt_opt;               // EKF_OPT_SCAN_THREADS
+    int Gmax;                 // workgroups per instance at the narrowest width (mailbox, sync words)
+    int last_G;               // workgroups per instance of the last association launch
     unsigned scan_epoch;      // association launches so far (mailbox tags)
     double* mbox;
     int* sync;
@@ -404,6 +408,9 @@ static int create_ctx(const ekf_config* cfg, int sh_rank, int sh_world, ekf_ctx*
     c->xinst = (size_t)(c->t1 - c->t0) * ekf::TILE_ELEMS;
     c->op_inst = (size_t)d.nb * 64 * (d.kmax / 2);
     c->G = (d.N + ekf::SCAN_THREADS - 1) / ekf::SCAN_THREADS;
+    c->Gmax = (d.N + 63) / 64;   // EKF_OPT_SCAN_THREADS = 64
+    c->last_G = c->G;
+    c->nt_opt = 0;
     // pipeline: the association kernels of an instance spread over G > 1 cooperating workgroups
     // must never wait on CUs a flush holds, so they are ordered after the flush in flight, and
     // nothing would overlap: such contexts run the sequential schedule (slam_ekf.h)
@@ -478,7 +485,7 @@ static int create_ctx(const ekf_config* cfg, int sh_rank, int sh_world, ekf_ctx*
     c->active_flush = 1;
     c->mfrep = c->bf ? 1 : 0;
     c->dbg = nullptr;
-    ALLOC(c->mbox, sizeof(double) * 2 * c->G * c->mbw * E);
+    ALLOC(c->mbox, sizeof(double) * 2 * c->Gmax * c->mbw * E);
     if (c->sh_world > 0) {
         // the partitioned instance's scan state (replicated on every rank) and a step that applies
         // nothing (rolled back: every flush form skips it), which pads an odd partial group
@@ -497,7 +504,7 @@ static int create_ctx(const ekf_config* cfg, int sh_rank, int sh_world, ekf_ctx*
         c->sh_null.patch = c->ring[0].patch;
         c->sh_null.patch_diag = c->ring[0].patch_diag;
     }
-    c->sync_stride = ((ekf::SYNC_WG0 + c->G + 15) / 16) * 16;
+    c->sync_stride = ((ekf::SYNC_WG0 + c->Gmax + 15) / 16) * 16;
     ALLOC(c->sync, sizeof(int) * c->sync_stride * E);
 #undef ALLOC
     if (hipHostMalloc((void**)&c->h_res, sizeof(int) * ekf::RES_STRIDE * E) != hipSuccess) goto fail;
@@ -661,6 +668,7 @@ static int create_ctx(const ekf_config* cfg, int sh_rank, int sh_world, ekf_ctx*
             goto fail;
         }
         const int resident = prop.multiProcessorCount * per_cu;
+        c->resident = resident;
         c->scan_batch = resident / c->G;
         if (c->scan_batch < 1) {
             rc = EKF_EINVAL;   // one instance does not fit the device
@@ -721,6 +729,7 @@ extern "C" int ekf_set_option(ekf_ctx* c, int opt, int v)
     case EKF_OPT_MFMA_REPLAY: if (v < 0 || v > 2) return EKF_ERANGE; break;
     case EKF_OPT_ACTIVE_FLUSH:
     case EKF_OPT_SCAN_STAMPS: if (v < 0 || v > 1) return EKF_ERANGE; break;
+    case EKF_OPT_SCAN_THREADS: if (v != 0 && v != 64 && v != 128 && v != 192) return EKF_ERANGE; break;
     case EKF_OPT_TEST_DROP_WG:
     case EKF_OPT_TEST_VERDICT_TIMEOUT: if (v < 0 || v > E) return EKF_ERANGE; break;
     default: return EKF_EINVAL;
@@ -755,6 +764,7 @@ extern "C" int ekf_set_option(ekf_ctx* c, int opt, int v)
     case EKF_OPT_TEST_DROP_WG: c->test_drop = v; break;
     case EKF_OPT_TEST_VERDICT_TIMEOUT: c->test_verdict = v; break;
     case EKF_OPT_ACTIVE_FLUSH: c->active_flush = v; break;
+    case EKF_OPT_SCAN_THREADS: c->nt_opt = v; break;
     }
     return EKF_OK;
 }
@@ -772,6 +782,7 @@ extern "C" int ekf_get_option(const ekf_ctx* c, int opt, int* v)
     case EKF_OPT_TEST_DROP_WG: *v = c->test_drop; break;
     case EKF_OPT_TEST_VERDICT_TIMEOUT: *v = c->test_verdict; break;
     case EKF_OPT_ACTIVE_FLUSH: *v = c->active_flush; break;
+    case EKF_OPT_SCAN_THREADS: *v = c->nt_opt; break;
     default: return EKF_EINVAL;
     }
     return EKF_OK;
@@ -817,6 +828,23 @@ static void prof_end(ekf_ctx* c, EvPair* pr, hipStream_t st)
     if (pr) (void)hipEventRecord(pr->b, st);
 }
 
+// Landmarks per association workgroup (EKF_OPT_SCAN_THREADS): the narrow widths exist for the
+// split-fp16 instantiation of the kernel only (launch_scan) and need the instance's workgroups
+// within the speculative path's bound, no pipelined overlap and every instance in one launch.
+// Automatic: 64 up to N = 1024 (measured), else 192.
+static int scan_width(const ekf_ctx* c)
+{
+    constexpr int W = ekf::SCAN_THREADS;
+    if (c->dbg || c->sh_world > 0 || c->cfg.precision == EKF_PREC_F64 || c->cfg.r_mode != EKF_R_INTENDED ||
+        c->d.kmax != 16 || c->pmode != 2)
+        return W;
+    const int nt = c->nt_opt ? c->nt_opt : (c->d.N <= 1024 ? 64 : W);
+    if (nt == W) return W;
+    const int G = (c->d.N + nt - 1) / nt;
+    if (G > ekf::SPEC_GMAX || (G > 1 && c->cfg.pipeline) || G * c->cfg.instances > c->resident) return W;
+    return nt;
+}
+
 static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
                                    const ekf_line* lines, const int* nlines)
 {
@@ -850,7 +878,9 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.nlines = nlines;
     p.dbg = c->dbg;
     p.pexp = c->pexp;
-    p.G = c->G;
+    p.nt = scan_width(c);
+    p.G = (c->d.N + p.nt - 1) / p.nt;
+    c->last_G = p.G;
     p.mbw = c->mbw;
     p.spec = c->spec;
     p.mbox = c->mbox;
@@ -866,9 +896,11 @@ static hipError_t launch_scans(ekf_ctx* c, ekf::ScanParams sp)
     const int E = c->cfg.instances;
     sp.epoch = ++c->scan_epoch;
     hipError_t err = hipSuccess;
-    for (int e0 = 0; err == hipSuccess && e0 < E; e0 += c->scan_batch) {
+    // (scan_width keeps a narrow launch within one batch)
+    const int batch = sp.nt == ekf::SCAN_THREADS ? c->scan_batch : E;
+    for (int e0 = 0; err == hipSuccess && e0 < E; e0 += batch) {
         sp.e0 = e0;
-        sp.E = (E - e0 < c->scan_batch) ? E - e0 : c->scan_batch;
+        sp.E = (E - e0 < batch) ? E - e0 : batch;
         err = ekf::launch_scan(sp, c->cfg.precision, c->stream);
     }
     return err;
@@ -1028,7 +1060,7 @@ extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
     if (c->scan_epoch > 0)
         for (int e = 0; e < E; e++) {
             int st = 0;
-            for (int gq = 0; gq < c->G; gq++)
+            for (int gq = 0; gq < c->last_G; gq++)
                 st = ekf::commit_fold(st, (unsigned)hs[(size_t)e * c->sync_stride + ekf::SYNC_WG0 + gq],
                                       c->scan_epoch);
             c->h_res[(size_t)e * ekf::RES_STRIDE + ekf::RES_STATUS] |= st & ekf::DONE_STATUS_MASK;

@@ -28,6 +28,7 @@ constexpr int F16_EXP_DEFAULT = 10;
 // start counter, then one status word per workgroup, rewritten by every launch
 enum { SYNC_START = 0, SYNC_WG0 = 4 };
 constexpr int MAX_GROUPS = (MAX_CAPACITY + SCAN_THREADS - 1) / SCAN_THREADS;   // workgroups per instance
+constexpr int SPEC_GMAX = 64;  // speculative association: workgroups per instance (<= one wave)
 constexpr int MB_WORDS_FIXED = 26; // mailbox words before the V-history (see ekf_kernels.hip)
 
 // per-instance result record in device memory (ints)
@@ -89,7 +90,8 @@ struct ScanParams {
     Dims d;
     int E;                // instances in this launch (grid.y)
     int e0;               // first instance of this launch
-    int G;                // workgroups per instance (grid.x) = ceil(N / SCAN_THREADS)
+    int G;                // workgroups per instance = ceil(N / nt)
+    int nt;               // landmarks per workgroup: SCAN_THREADS, or 128 / 64 (the F16X3 kernel only)
     int mbw;              // mailbox words per workgroup slot
     double* mbox;         // [E][2][G][mbw] per-line candidate exchange
     int* sync;            // [E][sync_stride]

@@ -928,6 +928,7 @@ __device__ __forceinline__ void publish_done(int* sync, int g, unsigned epoch, i
 
 // Run by every thread of workgroup 0 (the words are polled in parallel, thread k word k); the
 // folded status of all G words (= commit_status) is returned to every thread.
+template <int BLK>   // the workgroup's threads
 __device__ __forceinline__ int lead_collect(int* sync, int G, unsigned epoch, int own_status, int spin,
                                             int tid, int* sh_red, int& zg)
 {
@@ -935,7 +936,7 @@ __device__ __forceinline__ int lead_collect(int* sync, int G, unsigned epoch, in
     int st = tid == 0 ? commit_fold(0, done_word(epoch, own_status), epoch) : 0;
     int z = (tid == 0 && (own_status & (int)DONE_NZ)) ? 1 : 0;
     const bool late0 = (own_status & EKF_ST_TIMEOUT_BIT) != 0;
-    for (int k = 1 + tid; k < G; k += SCAN_BLOCK) {
+    for (int k = 1 + tid; k < G; k += BLK) {
         const unsigned* w = reinterpret_cast<const unsigned*>(&sync[SYNC_WG0 + k]);
         unsigned v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int polls = 0;
@@ -959,7 +960,7 @@ __device__ __forceinline__ int lead_collect(int* sync, int G, unsigned epoch, in
     st = 0;
     z = 0;
 #pragma unroll
-    for (int w = 0; w < SCAN_BLOCK / 64; w++) {
+    for (int w = 0; w < BLK / 64; w++) {
         st |= sh_red[w] & 0xff;
         z = max(z, sh_red[w] >> 8);
     }
@@ -1224,7 +1225,6 @@ constexpr int SPEC_PB64 = EKF_SPEC_PB64;            // ... fp64 operands (pll_sh
 #define EKF_STAGED_DEPTH 1
 #endif
 constexpr int SPEC_QMAX = 16;                       // pending steps staged in LDS (T = 16: up to 15)
-constexpr int SPEC_GMAX = 64;                       // workgroups per instance (<= one wave)
 constexpr int SPEC_WD = 14 + 4 * (SPEC_L - 1);      // winner record: rr, Dj, y, sin/cos, column blocks
 // speculative package: the words of build_package, then the robot 3×3 block and x_pre after the
 // line's update (robot_update), computed once by the replay wave for every landmark wave
@@ -1607,10 +1607,15 @@ __device__ __forceinline__ void split_pack_f16(float a, float b, int sig, unsign
 // ST: phase timers (EKF_OPT_SCAN_STAMPS). HOT (1, 2): the launch guarantees symmetric fp32 operands
 // with kmax = 16 (the bench and every EKF_R_INTENDED fp32/fp16 context with max_lines <= 8): the
 // per-line loops then carry no code for the other operand forms; HOT = 2 also fixes the plane
-// arithmetic to EKF_ARITH_F16X3, HOT = 1 to EKF_ARITH_BF16X6 or none. HOT = 0: decided at run time
-template <typename T, bool ST, int HOT>
-__global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
+// arithmetic to EKF_ARITH_F16X3, HOT = 1 to EKF_ARITH_BF16X6 or none. HOT = 0: decided at run time.
+// NT: landmarks (threads) per workgroup, 192 by default; 128 and 64 (ScanParams::nt) spread a small
+// map's instances over more CUs (the commit's stores and the replay per CU scale with it)
+template <typename T, bool ST, int HOT, int NT = ekf::SCAN_THREADS>
+__global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
 {
+    // (these hide the namespace defaults for the whole kernel body)
+    constexpr int SCAN_THREADS = NT;
+    constexpr int SCAN_BLOCK = NT + 64;
     const Dims d = p.d;
     const int r_mode = HOT ? (int)EKF_R_INTENDED : p.r_mode;   // (HOT: the launch checked it)
     constexpr double ETA = gate_eta<T>();
@@ -1830,7 +1835,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
         if (tid == 0 && g != 0) publish_done(sync, g, p.epoch, 0);
         if (g == 0) {
             int zg_unused = 0;
-            const int st = lead_collect(sync, G, p.epoch, 0, p.spin_log2, tid, sh_red, zg_unused);
+            const int st = lead_collect<SCAN_BLOCK>(sync, G, p.epoch, 0, p.spin_log2, tid, sh_red, zg_unused);
             if (lead) sync[SYNC_WG0] = (int)done_word(p.epoch, st);
             if (lead && !(st & EKF_ST_TIMEOUT_BIT)) {
                 for (int a = 0; a < 9; a++) Rsw[(a / 3) * n + (a % 3)] = R33[a];
@@ -3209,7 +3214,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanParams p)
     EKF_STAMP(25);
     if (tid == 0 && g != 0) publish_done(sync, g, p.epoch, wgst);
     int zg = (wgst & (int)DONE_NZ) ? 1 : 0;
-    if (g == 0 && (sequential || G > 1)) wgst = lead_collect(sync, G, p.epoch, wgst, p.spin_log2, tid, sh_red, zg);
+    if (g == 0 && (sequential || G > 1)) wgst = lead_collect<SCAN_BLOCK>(sync, G, p.epoch, wgst, p.spin_log2, tid, sh_red, zg);
     const bool ploss = (wgst & (int)DONE_PLOSS) != 0;
     wgst &= ~(int)(DONE_NZ | DONE_PLOSS);
     EKF_STAMP(26);
@@ -5565,6 +5570,31 @@ __global__ void lowrank_kernel(Dims d, const double* __restrict__ diag,
 // ---------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------
+// The association kernel on 128 / 64 landmarks per workgroup (ScanParams::nt): its split-fp16
+// instantiation only, one compilation unit per width (EKF_TU 7, 8)
+hipError_t launch_scan_nt128(const ScanParams& p, bool half, hipStream_t st);
+hipError_t launch_scan_nt64(const ScanParams& p, bool half, hipStream_t st);
+
+#if !defined(EKF_TU) || EKF_TU == 7
+hipError_t launch_scan_nt128(const ScanParams& p, bool half, hipStream_t st)
+{
+    const dim3 grid(p.G * p.E), block(128 + 64);
+    if (half) hipLaunchKernelGGL((scan_kernel<_Float16, false, 2, 128>), grid, block, 0, st, p);
+    else hipLaunchKernelGGL((scan_kernel<float, false, 2, 128>), grid, block, 0, st, p);
+    return hipGetLastError();
+}
+#endif
+
+#if !defined(EKF_TU) || EKF_TU == 8
+hipError_t launch_scan_nt64(const ScanParams& p, bool half, hipStream_t st)
+{
+    const dim3 grid(p.G * p.E), block(64 + 64);
+    if (half) hipLaunchKernelGGL((scan_kernel<_Float16, false, 2, 64>), grid, block, 0, st, p);
+    else hipLaunchKernelGGL((scan_kernel<float, false, 2, 64>), grid, block, 0, st, p);
+    return hipGetLastError();
+}
+#endif
+
 #if !defined(EKF_TU) || EKF_TU == 1
 int scan_blocks_per_cu(int precision)
 {
@@ -5603,6 +5633,13 @@ hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st)
 #if !defined(EKF_TU) || EKF_TU == 1
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 {
+    if (p.nt != SCAN_THREADS) {   // (the context picks a narrow width for this instantiation only)
+        if (p.dbg || precision == EKF_PREC_F64 || p.r_mode == 1 || p.d.kmax != 16 || p.bf != 2)
+            return hipErrorInvalidValue;
+        if (p.nt == 128) return launch_scan_nt128(p, precision == EKF_PREC_F16, st);
+        if (p.nt == 64) return launch_scan_nt64(p, precision == EKF_PREC_F16, st);
+        return hipErrorInvalidValue;
+    }
     const dim3 grid(p.G * p.E), block(SCAN_BLOCK);
     if (p.dbg) {   // phase timers (EKF_OPT_SCAN_STAMPS): the instrumented instantiation
         if (precision == EKF_PREC_F64) hipLaunchKernelGGL((scan_kernel<double, true, 0>), grid, block, 0, st, p);

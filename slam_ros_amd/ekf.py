@@ -27,11 +27,12 @@ EXP_AUTO = -1000
 # per-context options (slam_ekf.h EKF_OPT_*, ekf_set_option)
 OPT_SPECULATE, OPT_SPIN_LOG2, OPT_FLUSH_FORM, OPT_FLUSH_BLOCKS_PER_CU = 1, 2, 3, 4
 OPT_MFMA_REPLAY, OPT_SCAN_STAMPS, OPT_TEST_DROP_WG, OPT_TEST_VERDICT_TIMEOUT = 5, 6, 7, 8
-OPT_ACTIVE_FLUSH = 9
+OPT_ACTIVE_FLUSH, OPT_SCAN_THREADS = 9, 10
 OPTIONS = {"speculate": OPT_SPECULATE, "spin_log2": OPT_SPIN_LOG2, "flush_form": OPT_FLUSH_FORM,
            "flush_blocks_per_cu": OPT_FLUSH_BLOCKS_PER_CU, "mfma_replay": OPT_MFMA_REPLAY,
            "scan_stamps": OPT_SCAN_STAMPS, "test_drop_wg": OPT_TEST_DROP_WG,
-           "test_verdict_timeout": OPT_TEST_VERDICT_TIMEOUT, "active_flush": OPT_ACTIVE_FLUSH}
+           "test_verdict_timeout": OPT_TEST_VERDICT_TIMEOUT, "active_flush": OPT_ACTIVE_FLUSH,
+           "scan_threads": OPT_SCAN_THREADS}
 
 LIB_PATH = _build.LIB_PATH
 

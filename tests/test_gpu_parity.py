@@ -529,6 +529,44 @@ def test_hot_scan_kernel_equals_generic(ekf_mod, monkeypatch, prec, arith):
 
 
 @pytest.mark.parametrize("prec", [1, 2])
+@pytest.mark.parametrize("N,T", [(256, 4), (1000, 8), (1024, 20), (2048, 12)])
+def test_narrow_scan_workgroups_identical(ekf_mod, prec, N, T):
+    """EKF_OPT_SCAN_THREADS: the split-fp16 association kernel on 128 and 64 landmarks per
+    workgroup (more workgroups per instance, a partial last one at N = 1000) gives bit-identical
+    results and state to the 192-wide one, on the speculative path and when every guess is wrong
+    (the sequential restart: one cross-workgroup exchange per line), three instances per launch."""
+    E = 3
+    w = G.make_world(N, active=N - 30)
+    st = G.initial_state(w)
+    scans = _spec_scans(w, np.random.default_rng(11), 2 * T + 3)
+    runs = {}
+    for nt in (192, 128, 64):
+        for spec in (1, 2):
+            ens = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=2,
+                                   options={"scan_threads": nt, "speculate": spec})
+            for e in range(E):
+                ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+            results = []
+            for enc, ln in scans:
+                lines = np.stack([ln] * E)
+                r = ens.localize(np.repeat(enc, E, axis=0), lines, [len(ln)] * E)
+                results.append([(x["match"], x["matches"], x["new_landmarks"], x["status"]) for x in r])
+            runs[(nt, spec)] = (results, [ens.download_state(e) for e in range(E)])
+            ens.close()
+    for key, (res, states) in runs.items():
+        ref_res, ref_states = runs[(192, key[1])]
+        assert res == ref_res, key
+        for e in range(E):
+            P, y, s, pose = states[e]
+            P0, y0, s0, pose0 = ref_states[e]
+            bad = np.argwhere(P != P0)
+            assert bad.size == 0, (key, e, bad[:8].tolist(), rel(P, P0))
+            np.testing.assert_array_equal(y, y0)
+            np.testing.assert_array_equal(pose, pose0)
+            assert s == s0
+
+
+@pytest.mark.parametrize("prec", [1, 2])
 @pytest.mark.parametrize("N,T,lines,extra_every", [(80, 8, 6, 3), (80, 2, 8, 0), (64, 6, 6, 4),
                                                   (1024, 8, 8, 0), (1024, 4, 6, 5)])
 def test_wave_flush_equals_drained(ekf_mod, monkeypatch, prec, N, T, lines, extra_every):
