@@ -831,18 +831,28 @@ static void prof_end(ekf_ctx* c, EvPair* pr, hipStream_t st)
 // Landmarks per association workgroup (EKF_OPT_SCAN_THREADS): the narrow widths exist for the
 // split-fp16 instantiation of the kernel only (launch_scan) and need the instance's workgroups
 // within the speculative path's bound, no pipelined overlap and every instance in one launch.
-// Automatic: 64 up to N = 1024 (measured), else 192.
+// Automatic: the narrowest of 64 and 128 that fits (measured, DESIGN §4.1: N = 256 / 1024 / 2048
+// +8 / +9 / +5 % updates/s at 64, N = 4096 with 8 instances +1.4 % at 128).
+// Symmetric fp32 operands (sym_factor: every EKF_R_INTENDED fp32 / fp16 context; U = −2^x·V
+// exactly): the association kernel stores the V rows only and every reader of U rows scales them
+// (ScanParams / DowndateParams::usym). The partitioned instance stores both.
+static int usym_of(const ekf_ctx* c)
+{
+    return c->sh_world == 0 && c->cfg.precision != EKF_PREC_F64 && c->cfg.r_mode == EKF_R_INTENDED;
+}
+
 static int scan_width(const ekf_ctx* c)
 {
     constexpr int W = ekf::SCAN_THREADS;
     if (c->dbg || c->sh_world > 0 || c->cfg.precision == EKF_PREC_F64 || c->cfg.r_mode != EKF_R_INTENDED ||
         c->d.kmax != 16 || c->pmode != 2)
         return W;
-    const int nt = c->nt_opt ? c->nt_opt : (c->d.N <= 1024 ? 64 : W);
-    if (nt == W) return W;
-    const int G = (c->d.N + nt - 1) / nt;
-    if (G > ekf::SPEC_GMAX || (G > 1 && c->cfg.pipeline) || G * c->cfg.instances > c->resident) return W;
-    return nt;
+    auto fits = [&](int nt) {
+        const int G = (c->d.N + nt - 1) / nt;
+        return G <= ekf::SPEC_GMAX && !(G > 1 && c->cfg.pipeline) && G * c->cfg.instances <= c->resident;
+    };
+    if (c->nt_opt) return c->nt_opt != W && fits(c->nt_opt) ? c->nt_opt : W;
+    return fits(64) ? 64 : fits(128) ? 128 : W;
 }
 
 static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
@@ -879,6 +889,7 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.dbg = c->dbg;
     p.pexp = c->pexp;
     p.nt = scan_width(c);
+    p.usym = usym_of(c);
     p.G = (c->d.N + p.nt - 1) / p.nt;
     c->last_G = p.G;
     p.mbw = c->mbw;
@@ -938,6 +949,7 @@ static int enqueue_flush(ekf_ctx* c)
     dp.wt24 = c->wt24;
     dp.nwt24 = c->nwt24;
     dp.pexp = c->pexp;
+    dp.usym = usym_of(c);
     dp.sink = c->sink;
     dp.ubase = c->ops_u;
     dp.vbase = c->ops_v;

@@ -92,6 +92,7 @@ struct ScanParams {
     int e0;               // first instance of this launch
     int G;                // workgroups per instance = ceil(N / nt)
     int nt;               // landmarks per workgroup: SCAN_THREADS, or 128 / 64 (the F16X3 kernel only)
+    int usym;             // symmetric fp32 operands, U = −2^x·V: the U rows are not stored (Slot::Uop)
     int mbw;              // mailbox words per workgroup slot
     double* mbox;         // [E][2][G][mbw] per-line candidate exchange
     int* sync;            // [E][sync_stride]
@@ -198,6 +199,7 @@ struct DowndateParams {
     const WtEntry* wt64;  // [nwt64] f64 wave-tiles of 1 × WT64_C tiles (tile[0..1], rows[0] = A row block)
     int nwt64;
     const int* pexp;      // [E] fp16 storage exponent
+    int usym;             // the steps' U rows are −2^pexp·V (not stored): read V and scale
     void* sink;           // one scratch tile (8 KB): the wave flushes' stores of slots outside the triangle
     const void* ubase;    // operand rows of ring slot i at ubase / vbase + i·slot_bytes; the
     const void* vbase;    // group's step q is slot (slot0 + q) mod nslots (= steps[q].Uop / .Vop)

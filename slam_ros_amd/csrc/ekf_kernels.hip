@@ -101,6 +101,21 @@ __device__ __forceinline__ double from_domain(typename Stor<T>::C x, int ex)
 
 // the storage exponent of instance e (0 unless fp16)
 template <typename T>
+__device__ __forceinline__ int storage_exp(const int* pexp, int e);
+
+// A flush's U operand rows of instance e: as stored, or (DowndateParams::usym: symmetric operands,
+// U = −2^x·V exactly) the V rows times us_of(). Either way the same fp32 values reach the MFMAs.
+template <typename TS>
+__device__ __forceinline__ float us_of(const DowndateParams& p, int e)
+{
+    return p.usym ? -ldexpf(1.0f, storage_exp<TS>(p.pexp, e)) : 1.0f;
+}
+__device__ __forceinline__ const float* u_rows_flush(const DowndateParams& p, const Slot& sq, int e, size_t opstride)
+{
+    return reinterpret_cast<const float*>(p.usym ? sq.Vop : sq.Uop) + e * opstride;
+}
+
+template <typename T>
 __device__ __forceinline__ int storage_exp(const int* pexp, int e)
 {
     if constexpr (Stor<T>::half) return pexp[e];
@@ -177,7 +192,16 @@ struct PllView {
     const int4* ctl;  // per pending step {reset, ks, nadd, s0} of instance e (LDS copy)
     int rnd;          // fp16: round after every pending step, as the exact flush does (0 under
                       // the split-bf16 flush, which rounds once per group)
+    int usym;         // symmetric operands: U = us·V, the U rows not stored (ScanParams::usym)
+    float us;         // −2^ex if usym, else 1 (U rows read as stored)
 };
+
+// Step q's U rows as stored, or its V rows (scaled by v.us on use) for symmetric operands
+template <typename T>
+__device__ __forceinline__ const float* u_rows_f32(const PllView<T>& v, const Slot& sq)
+{
+    return reinterpret_cast<const float*>(v.usym ? sq.Vop : sq.Uop) + v.e * v.opstride;
+}
 
 // fp16 rounding of a replayed element (identity for fp32 / fp64 storage)
 template <typename T>
@@ -286,8 +310,9 @@ __device__ __forceinline__ void pll_shared_step(const PllView<T>& v, const Slot&
     using C = typename Stor<T>::C;
     if constexpr (sizeof(C) == 4) {
         const int kh = v.kmax / 2;
-        const float* U = reinterpret_cast<const float*>(sq.Uop) + v.e * v.opstride;
+        const float* U = u_rows_f32(v, sq);
         const float* V = reinterpret_cast<const float*>(sq.Vop) + v.e * v.opstride;
+        const float us = v.us;
         auto row = [&](int r) { return ((size_t)(r >> 5) * 64 + (r & 31)) * kh; };
         const float* uo = U + row(i0);
         const float* vo = V + row(i0);
@@ -296,10 +321,10 @@ __device__ __forceinline__ void pll_shared_step(const PllView<T>& v, const Slot&
         for (int b = 0; b < B; b++) xc[b] = (swap[b] ? U : V) + row(j0[b]);
         for (int s0 = 0; s0 < ks; s0 += 4) {
             // [row, row + 1] × [k half 0, k half 1] of the owned U and V rows
-            const f32x4v ue0 = *reinterpret_cast<const f32x4v*>(uo + s0);
-            const f32x4v ue1 = *reinterpret_cast<const f32x4v*>(uo + kh + s0);
-            const f32x4v uo0 = *reinterpret_cast<const f32x4v*>(uo + 32 * kh + s0);
-            const f32x4v uo1 = *reinterpret_cast<const f32x4v*>(uo + 33 * kh + s0);
+            const f32x4v ue0 = *reinterpret_cast<const f32x4v*>(uo + s0) * us;
+            const f32x4v ue1 = *reinterpret_cast<const f32x4v*>(uo + kh + s0) * us;
+            const f32x4v uo0 = *reinterpret_cast<const f32x4v*>(uo + 32 * kh + s0) * us;
+            const f32x4v uo1 = *reinterpret_cast<const f32x4v*>(uo + 33 * kh + s0) * us;
             const f32x4v ve0 = *reinterpret_cast<const f32x4v*>(vo + s0);
             const f32x4v ve1 = *reinterpret_cast<const f32x4v*>(vo + kh + s0);
             const f32x4v vo0 = *reinterpret_cast<const f32x4v*>(vo + 32 * kh + s0);
@@ -311,7 +336,8 @@ __device__ __forceinline__ void pll_shared_step(const PllView<T>& v, const Slot&
                 const f32x4v co0 = *reinterpret_cast<const f32x4v*>(xc[b] + 32 * kh + s0);
                 const f32x4v co1 = *reinterpret_cast<const f32x4v*>(xc[b] + 33 * kh + s0);
                 const bool sw = swap[b];
-                const f32x4v ae0 = sw ? ce0 : ue0, ae1 = sw ? ce1 : ue1, ao0 = sw ? co0 : uo0, ao1 = sw ? co1 : uo1;
+                const f32x4v ae0 = sw ? ce0 * us : ue0, ae1 = sw ? ce1 * us : ue1, ao0 = sw ? co0 * us : uo0,
+                             ao1 = sw ? co1 * us : uo1;
                 const f32x4v be0 = sw ? ve0 : ce0, be1 = sw ? ve1 : ce1, bo0 = sw ? vo0 : co0, bo1 = sw ? vo1 : co1;
 #pragma unroll
                 for (int s = 0; s < 4; s++) {
@@ -398,8 +424,7 @@ __device__ __forceinline__ void pll_blocks(const PllView<T>& v, int i0, const in
                 const float* vb[B];
 #pragma unroll
                 for (int b = 0; b < B; b++) {
-                    ua[b] = reinterpret_cast<const float*>(sq.Uop) + v.e * v.opstride +
-                            ((size_t)(a0[b] >> 5) * 64 + (a0[b] & 31)) * kh;   // row a0; a0+1 at +kh
+                    ua[b] = u_rows_f32(v, sq) + ((size_t)(a0[b] >> 5) * 64 + (a0[b] & 31)) * kh;   // row a0; a0+1 at +kh
                     vb[b] = reinterpret_cast<const float*>(sq.Vop) + v.e * v.opstride +
                             ((size_t)(b0[b] >> 5) * 64 + (b0[b] & 31)) * kh;
                 }
@@ -407,10 +432,10 @@ __device__ __forceinline__ void pll_blocks(const PllView<T>& v, int i0, const in
                     f32x4v ae0[B], ae1[B], ao0[B], ao1[B], be0[B], be1[B], bo0[B], bo1[B];
 #pragma unroll
                     for (int b = 0; b < B; b++) {
-                        ae0[b] = *reinterpret_cast<const f32x4v*>(ua[b] + s0);
-                        ae1[b] = *reinterpret_cast<const f32x4v*>(ua[b] + kh + s0);
-                        ao0[b] = *reinterpret_cast<const f32x4v*>(ua[b] + 32 * kh + s0);
-                        ao1[b] = *reinterpret_cast<const f32x4v*>(ua[b] + 33 * kh + s0);
+                        ae0[b] = *reinterpret_cast<const f32x4v*>(ua[b] + s0) * v.us;
+                        ae1[b] = *reinterpret_cast<const f32x4v*>(ua[b] + kh + s0) * v.us;
+                        ao0[b] = *reinterpret_cast<const f32x4v*>(ua[b] + 32 * kh + s0) * v.us;
+                        ao1[b] = *reinterpret_cast<const f32x4v*>(ua[b] + 33 * kh + s0) * v.us;
                         be0[b] = *reinterpret_cast<const f32x4v*>(vb[b] + s0);
                         be1[b] = *reinterpret_cast<const f32x4v*>(vb[b] + kh + s0);
                         bo0[b] = *reinterpret_cast<const f32x4v*>(vb[b] + 32 * kh + s0);
@@ -1286,13 +1311,12 @@ __device__ __forceinline__ void staged_blocks(const PllView<T>& v, int j, const 
     // (power-of-two scaling; fma(a, b, c) == fma(b, a, c)).
     auto load_rows = [&](int q, f32x4v (&Ux)[4][2]) {
         const Slot& sq = v.pend[q];
-        const float* ou = reinterpret_cast<const float*>(sq.Uop) + v.e * v.opstride +
-                          ((size_t)(i0 >> 5) * 64 + (i0 & 31)) * kh;
+        const float* ou = u_rows_f32(v, sq) + ((size_t)(i0 >> 5) * 64 + (i0 & 31)) * kh;
 #pragma unroll
         for (int rh = 0; rh < 4; rh++) {
             const int roff = (rh & 1) * kh + (rh >> 1) * 32 * kh;
 #pragma unroll
-            for (int h = 0; h < 2; h++) Ux[rh][h] = *reinterpret_cast<const f32x4v*>(ou + roff + 4 * h);
+            for (int h = 0; h < 2; h++) Ux[rh][h] = *reinterpret_cast<const f32x4v*>(ou + roff + 4 * h) * v.us;
         }
     };
     const float vscale = -ldexpf(1.0f, -v.ex);   // V_own = U_own · (−2^−x), exact
@@ -1876,6 +1900,8 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
     pv.e = e;
     pv.ex = storage_exp<T>(p.pexp, e);
     pv.opstride = opstride;
+    pv.usym = p.usym;
+    pv.us = p.usym ? -ldexpf(1.0f, pv.ex) : 1.0f;
     pv.npend = p.npend;
     pv.pend = p.pend;
     pv.ctl = sh_ctl;
@@ -1994,8 +2020,10 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                     if constexpr (kPlanes)
                         *reinterpret_cast<f32x2v*>(sh_vpl + tid * 32 + pp * 16 + 2 * t) = f32x2v{(float)v0, (float)v1};
                 } else {
-                    Uop[op_index_f32(lr, 2 * t, d.kmax)] = to_domain<T>(-o0, pv.ex);
-                    Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = to_domain<T>(-o1, pv.ex);
+                    if (!p.usym) {   // (symmetric operands: U = −2^x·V, read from V)
+                        Uop[op_index_f32(lr, 2 * t, d.kmax)] = to_domain<T>(-o0, pv.ex);
+                        Uop[op_index_f32(lr, 2 * t + 1, d.kmax)] = to_domain<T>(-o1, pv.ex);
+                    }
                     Vop[op_index_f32(lr, 2 * t, d.kmax)] = (C)v0;
                     Vop[op_index_f32(lr, 2 * t + 1, d.kmax)] = (C)v1;
                 }
@@ -2020,6 +2048,7 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
     auto store_ops_half = [&](int half, int mm) {   // mm: the matches
         if constexpr (kPlanes) {
             const float us = -ldexpf(1.0f, pv.ex);
+            const bool su = !p.usym;   // (usym: U = us·V is not stored; the readers scale V)
 #pragma unroll
             for (int pp = 0; pp < 2; pp++) {
                 const f32x4v* src = reinterpret_cast<const f32x4v*>(sh_vpl + tid * 32 + pp * 16) + 2 * half;
@@ -2035,7 +2064,7 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                     const size_t o = op_index_f32(2 * j + pp, h, d.kmax) + 4 * half;   // k = h: s = 0
                     const f32x4v vh = {v[h], v[2 + h], v[4 + h], v[6 + h]};
                     *reinterpret_cast<f32x4v*>(Vop + o) = vh;
-                    *reinterpret_cast<f32x4v*>(Uop + o) = vh * us;
+                    if (su) *reinterpret_cast<f32x4v*>(Uop + o) = vh * us;
                 }
             }
         }
@@ -2272,10 +2301,10 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                     float* dst = sh_stg + ((t * SPEC_QMAX + q) * 2) * 32;
                     if (piece < 8) {   // U: row half rh, 4 k
                         const int half = piece & 1, rh = piece >> 1;
-                        const float* base = reinterpret_cast<const float*>(p.pend[q].Uop) + e * opstride + rowb;
+                        const float* base = u_rows_f32(pv, p.pend[q]) + rowb;
                         const int roff = (rh & 1) * kh + (rh >> 1) * 32 * kh;
                         *reinterpret_cast<f32x4v*>(dst + rh * 8 + half * 4) =
-                            *reinterpret_cast<const f32x4v*>(base + roff + half * 4);
+                            *reinterpret_cast<const f32x4v*>(base + roff + half * 4) * pv.us;
                     } else {           // V: rows of pair pr, k-pairs 2kc, 2kc + 1, interleaved
                         const int pr = (piece - 8) >> 2, kc = (piece - 8) & 3;
                         const float* base = reinterpret_cast<const float*>(p.pend[q].Vop) + e * opstride + rowb;
@@ -3121,7 +3150,7 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
             for (int k = 2 * m; k < d.kmax; k++)
 #pragma unroll
                 for (int pp = 0; pp < 2; pp++) {
-                    Uop[op_index_f32(2 * j + pp, k, d.kmax)] = (C)(-0.0f);
+                    if (!p.usym) Uop[op_index_f32(2 * j + pp, k, d.kmax)] = (C)(-0.0f);
                     Vop[op_index_f32(2 * j + pp, k, d.kmax)] = (C)0.0f;
                 }
         }
@@ -3356,6 +3385,8 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
     pv.e = 0;
     pv.ex = storage_exp<T>(p.pexp, 0);
     pv.opstride = (size_t)d.nb * 64 * (d.kmax / 2);
+    pv.usym = 0;   // (the partitioned instance stores its U rows)
+    pv.us = 1.0f;
     pv.npend = p.npend;
     pv.pend = p.pend;
     pv.ctl = sh_ctl;
@@ -3838,8 +3869,9 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_sb_kernel(DowndateParams
     // [buf][A/B][block][s4][lane] float4: 2 × 2 × 4 × 2 × 64 × 16 B = 32 KB
     __shared__ f32x4 lds[2][2][DD_SB][2][64];
     // staging: thread t moves float4 i = t + 256 j (j < 4): lane, s4, block, A/B
+    const float us = us_of<TS>(p, e);
     auto fetch = [&](int q, int k0, f32x4 reg[4]) {
-        const float* U = reinterpret_cast<const float*>(p.steps[q].Uop) + e * opstride;
+        const float* U = u_rows_flush(p, p.steps[q], e, opstride);
         const float* V = reinterpret_cast<const float*>(p.steps[q].Vop) + e * opstride;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -3848,7 +3880,7 @@ __global__ __launch_bounds__(DD_THREADS) void flush_f32_sb_kernel(DowndateParams
             const int rb = (ab ? sb.y : sb.x) * DD_SB + blk;
             if (rb < d.nb) {
                 const float* src = (ab ? V : U) + ((size_t)rb * 64 + ln) * kh + k0 + 4 * s4;
-                reg[j] = *reinterpret_cast<const f32x4*>(src);
+                reg[j] = *reinterpret_cast<const f32x4*>(src) * (ab ? 1.0f : us);
             }
         }
     };
@@ -4035,10 +4067,11 @@ __global__ __launch_bounds__(DD_THREADS, 2) void flush_f32_persist2_kernel(Downd
 #pragma unroll
         for (int c = 0; c < PST_MAXC; c++) {
             const int qc = ((t.flags >> (8 * c)) & 15) ? c : 0;   // absent steps re-read step 0
-            const float* U = reinterpret_cast<const float*>(p.steps[qc].Uop) + t.e * opstride;
+            const float* U = u_rows_flush(p, p.steps[qc], t.e, opstride);
             const float* V = reinterpret_cast<const float*>(p.steps[qc].Vop) + t.e * opstride;
-            opreg[c][0] = *reinterpret_cast<const f32x4*>(U + (size_t)rA0 * 64 * kh + in_blk);
-            opreg[c][1] = *reinterpret_cast<const f32x4*>(U + (size_t)rA1 * 64 * kh + in_blk);
+            const float us = us_of<TS>(p, t.e);
+            opreg[c][0] = *reinterpret_cast<const f32x4*>(U + (size_t)rA0 * 64 * kh + in_blk) * us;
+            opreg[c][1] = *reinterpret_cast<const f32x4*>(U + (size_t)rA1 * 64 * kh + in_blk) * us;
             opreg[c][2] = *reinterpret_cast<const f32x4*>(V + (size_t)rB * 64 * kh + in_blk);
         }
 #pragma unroll
@@ -4248,14 +4281,15 @@ __device__ __forceinline__ void wt_general(const DowndateParams& p, int e, const
         const int reset = sload(r + RES_RESET);
         const int kc = reset ? 0 : sload(r + RES_KSTEPS);
         if (kc > 0) {
-            const float* U = reinterpret_cast<const float*>(p.steps[q].Uop) + e * opstride + lofs;
+            const float* U = u_rows_flush(p, p.steps[q], e, opstride) + lofs;
             const float* V = reinterpret_cast<const float*>(p.steps[q].Vop) + e * opstride + lofs;
+            const float us = us_of<TS>(p, e);
             f32x4 a[WT_R][2], b[WT_C][2];
 #pragma unroll
             for (int rr = 0; rr < WT_R; rr++) {
                 const float* src = U + (size_t)op_row(0, rr) * 64 * kh;
-                a[rr][0] = *reinterpret_cast<const f32x4*>(src);
-                a[rr][1] = *reinterpret_cast<const f32x4*>(src + 4);
+                a[rr][0] = *reinterpret_cast<const f32x4*>(src) * us;
+                a[rr][1] = *reinterpret_cast<const f32x4*>(src + 4) * us;
             }
 #pragma unroll
             for (int c = 0; c < WT_C; c++) {
@@ -4460,7 +4494,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
     auto op_base = [&](int q, int side) __attribute__((always_inline)) {
         int sl = p.slot0 + q;
         if (sl >= p.nslots) sl -= p.nslots;
-        return reinterpret_cast<const float*>(reinterpret_cast<const char*>(side ? p.vbase : p.ubase) +
+        return reinterpret_cast<const float*>(reinterpret_cast<const char*>(side || p.usym ? p.vbase : p.ubase) +
                                               (size_t)sl * (size_t)p.slot_bytes);
     };
 
@@ -4720,9 +4754,10 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
         auto load_half = [&](int slot, const Item& t, int q, int h) __attribute__((always_inline)) {
             const float* U = op_base(q, 0) + t.e * opstride + lofs + 4 * h;
             const float* V = op_base(q, 1) + t.e * opstride + lofs + 4 * h;
+            const float us = us_of<TS>(p, t.e);
 #pragma unroll
             for (int r = 0; r < WT_R; r++)
-                opA[slot][r][h] = *reinterpret_cast<const f32x4*>(U + (size_t)op_row(t, 0, r) * 64 * kh);
+                opA[slot][r][h] = *reinterpret_cast<const f32x4*>(U + (size_t)op_row(t, 0, r) * 64 * kh) * us;
 #pragma unroll
             for (int c = 0; c < WT_C; c++)
                 opB[slot][c][h] = *reinterpret_cast<const f32x4*>(V + (size_t)op_row(t, 1, c) * 64 * kh);
@@ -4822,7 +4857,7 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                             const float* base = op_base(lq, isA ? 0 : 1) + ldi.e * opstride + lofs + 4 * h;
                             const f32x4 v = *reinterpret_cast<const f32x4*>(
                                 base + (size_t)op_row(ldi, isA ? 0 : 1, isA ? o : o - WT_R) * 64 * kh);
-                            if (isA) opA[lq][o][h] = v;
+                            if (isA) opA[lq][o][h] = v * us_of<TS>(p, ldi.e);
                             else opB[lq][o - WT_R][h] = v;
                         }
                         __builtin_amdgcn_sched_barrier(0);
