@@ -1724,9 +1724,11 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
     const double rsc = pf16 ? ldexp(1.0, -2 * psig) : 1.0;
     // the on-read replay of plain pending steps (EKF_OPT_MFMA_REPLAY): 1 the split products on
     // the planes (plane_replay: 2^(2σ)·ΔX for EKF_ARITH_F16X3), 2 fp32 MFMA on the fp32 operand
-    // rows (f32_replay: ΔX unscaled)
-    const bool f32rep = kPlanes && p.mfrep == 2;
-    const double rrsc = f32rep ? 1.0 : rsc;
+    // rows (f32_replay: ΔX unscaled); 1 also takes f32_replay when a pending step's planes were
+    // written at another exponent or could not carry the instance's range (PLANE_SIGMA_EXACT),
+    // instead of the exact per-element forms (below; the flush still takes the exact forms)
+    bool f32rep = kPlanes && p.mfrep == 2;
+    double rrsc = f32rep ? 1.0 : rsc;
     // phase timers only in the ST instantiation (EKF_SCAN_STAMPS=1): the product kernel carries
     // no timer code at all (its uniform branches and registers cost ≈2 µs per scan)
     unsigned long long* const pdbg = ST ? p.dbg : nullptr;
@@ -1947,11 +1949,15 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
         // added at step q* starts from q*'s patch (its V rows are zero before), below; a reset or
         // a plane exponent other than this scan's takes the exact forms
         bool m = st && p.mfrep && kPlanes;
+        if (pf16 && p.mfrep == 1) {
+            for (int q = 0; q < p.npend; q++) f32rep |= sh_psg[q] != psig;
+            rrsc = f32rep ? 1.0 : rsc;
+        }
         for (int q = 0; q < p.npend; q++) {
             // (the planes of a step written with another exponent: only the plane replay minds)
             const bool sgx = pf16 && !f32rep && sh_psg[q] != psig;
             m &= !sh_ctl[q].x && !sgx;
-            rpath |= (sh_ctl[q].x ? 128 : 0) | (sgx ? 256 : 0);
+            rpath |= (sh_ctl[q].x ? 128 : 0) | (pf16 && sh_psg[q] != psig ? 256 : 0);
             aug_pend |= sh_ctl[q].z > 0;
             if (sh_ctl[q].y > 0) amask |= 1u << q;
         }
