@@ -141,7 +141,9 @@ def find_traffic(explicit, sha, cfg):
             tj = json.load(open(pth))
         except (OSError, ValueError):
             continue
-        if all(tj.get(k, "bench" if k == "world" else None) == v for k, v in cfg.items()):
+        # (precision: "f32", or the round-5 files' dtype label "f32 storage, f16x3 products")
+        got = dict(tj, precision=str(tj.get("precision", "")).split()[0] if tj.get("precision") else None)
+        if all(got.get(k, "bench" if k == "world" else None) == v for k, v in cfg.items()):
             if tj.get("lib_sha") == sha:
                 return tj, os.path.relpath(pth, ROOT)
             if why.startswith("no counter"):

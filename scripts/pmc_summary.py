@@ -73,7 +73,7 @@ def main(tag, out=None):
     c = ctr[match[0]]
     hbm = 2 * c.get("FETCH_SIZE", 0) * 1024 + c.get("WRITE_SIZE", 0) * 1024
     cfg = b["config"]
-    tj = {"capacity": cfg["capacity"], "instances": cfg["instances_per_gpu"], "precision": b["dtype"],
+    tj = {"capacity": cfg["capacity"], "instances": cfg["instances_per_gpu"], "precision": str(b["dtype"]).split()[0],
           "flush_interval": cfg["flush_interval"], "pipeline": cfg["pipeline"], "kernel": kern,
           "hbm_bytes_per_launch": hbm, "fetch_bytes_corrected": 2 * c.get("FETCH_SIZE", 0) * 1024,
           "write_bytes": c.get("WRITE_SIZE", 0) * 1024,
