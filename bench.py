@@ -308,11 +308,11 @@ def main():
     if args.flush_interval <= 0:
         # per capacity: the flush's pass over P is the part T amortises; below
         # N = 2048 it costs 10-60 µs per launch while every pending step adds replay to every scan
-        # (sweep: scripts/r05/tsweep.sh)
+        # (sweeps: scripts/r05/tsweep2.sh)
         if prec == ekf.PREC_F64 or arith == ekf.ARITH_EXACT:
             args.flush_interval = 8
         elif arith == ekf.ARITH_F16X3:
-            args.flush_interval = 20 if N > 2048 else (8 if N > 512 else 4)
+            args.flush_interval = 20 if N > 2048 else (12 if N > 512 else 8)
         else:
             args.flush_interval = 12
     ens = ekf.Ensemble(N, E, prec, max_lines=L_LINES, device=local, pipeline=bool(args.pipeline),
