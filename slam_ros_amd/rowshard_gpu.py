@@ -53,12 +53,15 @@ class ShardedInstance:
         self.max_lines = max_lines
         # the library's phases and torch's work (the all-reduce, host staging) on one dedicated stream:
         # the exchange buffer's writes, the sum and the reads are ordered on one queue (torch's
-        # default stream has handle 0, which the C-ABI reads as "the context's own stream")
+        # default stream has handle 0, which the C-ABI reads as "the context's own stream"). The
+        # caller's current stream is left alone: every torch operation here runs inside
+        # `with torch.cuda.stream(self.stream)`.
         self.stream = torch.cuda.Stream(dev)
-        torch.cuda.set_stream(self.stream)
         self.ens.set_stream(self.stream.cuda_stream)
-        words = int(self.lib.ekf_shard_buffer_words(self.h))
-        self.buf = torch.zeros(words, dtype=torch.float64, device=dev)
+        self.words = int(self.lib.ekf_shard_buffer_words(self.h))
+        with torch.cuda.stream(self.stream):
+            # + one word: the number of ranks whose phase failed, summed with every exchange
+            self.buf = torch.zeros(self.words + 1, dtype=torch.float64, device=dev)
         self.host_coll = dist.get_backend(group) != "nccl"
         r0, r1 = ctypes.c_int32(), ctypes.c_int32()
         E._check(self.lib.ekf_shard_tiles(self.h, ctypes.byref(r0), ctypes.byref(r1)), "ekf_shard_tiles")
@@ -71,7 +74,9 @@ class ShardedInstance:
     def upload_state(self, P, y, saved, pose):
         self.ens.upload_state(0, P, y, saved, pose)
 
-    def _sum(self):
+    def _sum(self, failed: bool):
+        """The exchange (on self.stream), carrying this rank's failure flag in the last word."""
+        self.buf[self.words].fill_(1.0 if failed else 0.0)
         if self.host_coll:
             t = self.buf.cpu()
             dist.all_reduce(t, group=self.group)
@@ -86,12 +91,28 @@ class ShardedInstance:
         L = ln.shape[0]
         enc = np.ascontiguousarray(np.asarray(enc, dtype=np.float64).reshape(3))
         bp = ctypes.c_void_p(self.buf.data_ptr())
-        E._check(lib.ekf_shard_begin(h, E._dp(enc), ln.ctypes.data_as(ctypes.c_void_p), L, bp), "ekf_shard_begin")
-        self._sum()
-        for i in range(L):
-            E._check(lib.ekf_shard_line(h, i, bp), "ekf_shard_line")
-            self._sum()
-            E._check(lib.ekf_shard_apply(h, i, bp), "ekf_shard_apply")
+        # A phase that fails on one rank must not leave the others waiting in an exchange: every
+        # rank runs the whole exchange sequence, a failed one without further library calls, and
+        # the summed flag word of the last exchange tells every rank alike whether to abandon the
+        # scan (ekf_shard_abort) and raise.
+        err = None
+        with torch.cuda.stream(self.stream):
+            rc = lib.ekf_shard_begin(h, E._dp(enc), ln.ctypes.data_as(ctypes.c_void_p), L, bp)
+            err = err or (rc and (rc, "ekf_shard_begin"))
+            self._sum(bool(err))
+            for i in range(L):
+                if not err:
+                    rc = lib.ekf_shard_line(h, i, bp)
+                    err = rc and (rc, "ekf_shard_line")
+                self._sum(bool(err))
+                if not err:
+                    rc = lib.ekf_shard_apply(h, i, bp)
+                    err = rc and (rc, "ekf_shard_apply")
+            failed = float(self.buf[self.words].item())   # (synchronises the stream once per scan)
+        if failed > 0:
+            lib.ekf_shard_abort(h)
+            rc, what = err if err else (0, "a peer rank's phase")
+            raise E.EkfError(f"{what} failed on {int(failed)} of {self.world} ranks (rc {rc}); scan abandoned")
         E._check(lib.ekf_shard_end(h, ctypes.byref(self._res)), "ekf_shard_end")
         r = self._res[0]
         self.last = dict(matches=r.matches, new_landmarks=r.new_landmarks, saved=r.saved, reset=r.reset,
