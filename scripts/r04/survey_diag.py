@@ -21,6 +21,8 @@ ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=8, flush_interval=T, arith=ekf.
 for e in range(E):
     ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
 bits = Counter()
+per_inst = {e: Counter() for e in range(E)}
+flags = Counter()
 words = Counter()
 per_pos = {}
 saved = []
@@ -33,6 +35,10 @@ for s in range(1, pre + scans + 1):
     for e in range(E):
         dw = int(ens.result_words(e)[9])
         words[dw] += 1
+        if dw & 16:
+            per_inst[e]["sequential"] += 1
+        if r[e]["status"] & (ekf.ST_PRECISION | ekf.ST_RANGE):
+            flags[e] += 1
         for b in (1, 2, 4, 8, 16, 32, 64, 128, 256):
             if dw & b:
                 bits[b] += 1
@@ -40,5 +46,7 @@ for s in range(1, pre + scans + 1):
     saved.append([x["saved"] for x in r])
 print(json.dumps({"T": T, "preroll": pre, "scans": scans, "instances": E, "bits": dict(bits), "words": dict(words),
                   "per_group_position": {k: dict(v) for k, v in sorted(per_pos.items())},
-                  "saved_first": saved[0], "saved_last": saved[-1]}), flush=True)
+                  "saved_first": saved[0], "saved_last": saved[-1],
+                  "sequential_per_instance": {e: c["sequential"] for e, c in per_inst.items()},
+                  "flagged_scans_per_instance": dict(flags)}), flush=True)
 ens.close()
