@@ -321,6 +321,27 @@ int ekf_shard_end(ekf_ctx* ctx, ekf_result* out);
 /* Abandons the open scan (before ekf_shard_end nothing of the committed state has been written),
  * e.g. after a failed exchange; a phase that fails abandons it too. */
 int ekf_shard_abort(ekf_ctx* ctx);
+/* The speculative association of a partitioned instance: the per-line exchanges replaced by one.
+ *   ekf_shard_begin(enc, lines, L, buf); SUM buf over ranks
+ *   ekf_shard_speculate(buf, cols)          every line's first passing landmark at the scan's start
+ *                                           (its guess, found by every rank alike), the rank's
+ *                                           blocks of every guessed column into cols
+ *                                           (ekf_shard_spec_buffer_words doubles, [L][N][4])
+ *   SUM cols over ranks
+ *   ekf_shard_run(cols, next)               lines 0 .. L−1 as the per-line phases compute them, each
+ *                                           winner's column from cols; stops at the first line
+ *                                           whose first passing landmark is not its guess and
+ *                                           writes that line (or L) as a double to next, device
+ *                                           memory of the caller (asynchronous, stream-ordered)
+ *   ekf_shard_resume(line)                  the host's copy of next (every rank reads the same)
+ *   for each line i from next: ekf_shard_line, SUM buf, ekf_shard_apply (the per-line protocol)
+ *   ekf_shard_end(out)
+ * Bit-identical to the per-line protocol; every rank stops at the same line (replicated state).
+ * EKF_OPT_SPECULATE = 2 (test hook) makes every line guess landmark 0. */
+size_t ekf_shard_spec_buffer_words(const ekf_ctx* ctx);
+int ekf_shard_speculate(ekf_ctx* ctx, const double* buf, double* cols);
+int ekf_shard_run(ekf_ctx* ctx, const double* cols, double* next_line);
+int ekf_shard_resume(ekf_ctx* ctx, int line);
 
 /* Introspection for the benchmark's roofline accounting. */
 size_t ekf_landmark_block_bytes(const ekf_ctx* ctx); /* stored bytes of P_ll per instance */

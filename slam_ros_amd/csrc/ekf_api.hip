@@ -62,6 +62,7 @@ struct ekf_ctx {
     int* sh_flags = nullptr;
     int* sh_ctl = nullptr;
     int sh_L = 0, sh_line = 0, sh_open = 0;   // sh_open: 1 during a scan; sh_line: the next line expected
+    int sh_diag = 0;                           // begin's exchange consumed (SH_DIAG ran) in this scan
     ekf::Slot sh_null;        // a step that applies nothing (pads an odd partial group to the wave flush)
     double* pose;
     double* xpre;
@@ -1520,7 +1521,7 @@ extern "C" int ekf_state_dim(const ekf_ctx* c) { return c ? c->d.n : 0; }
 // winner's column after each line. Everything is stream-ordered on the context stream: no host
 // round trip until ekf_shard_end.
 
-static ekf::ShardParams shard_params(ekf_ctx* c, int phase, double* buf)
+static ekf::ShardParams shard_params(ekf_ctx* c, int phase, double* buf, double* cols = nullptr)
 {
     ekf::ShardParams p;
     memset(&p, 0, sizeof(p));
@@ -1549,6 +1550,7 @@ static ekf::ShardParams shard_params(ekf_ctx* c, int phase, double* buf)
     p.pkg = c->sh_pkg;
     p.ctl = c->sh_ctl;
     p.col = buf;
+    p.cols = cols;
     p.enc = c->d_enc;
     p.lines = c->d_lines;
     p.pexp = c->pexp;
@@ -1589,6 +1591,7 @@ extern "C" int ekf_shard_begin(ekf_ctx* c, const double enc[3], const ekf_line* 
     c->sh_line = 0;
     c->sh_L = nlines;
     c->sh_open = 1;
+    c->sh_diag = 0;
     SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_BEGIN, buf), c->cfg.precision, c->stream));
     return EKF_OK;
 }
@@ -1597,8 +1600,10 @@ extern "C" int ekf_shard_line(ekf_ctx* c, int line, double* buf)
 {
     if (!c || c->sh_open != 1 || !buf || line != c->sh_line) return EKF_EINVAL;
     if (line < 0 || line >= c->sh_L) return EKF_ERANGE;
-    if (line == 0)   // the summed diagonal blocks of begin's exchange
+    if (!c->sh_diag) {   // the summed diagonal blocks of begin's exchange
         SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_DIAG, buf), c->cfg.precision, c->stream));
+        c->sh_diag = 1;
+    }
     SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_GATE, buf), c->cfg.precision, c->stream));
     SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_COLUMN, buf), c->cfg.precision, c->stream));
     return EKF_OK;
@@ -1611,6 +1616,44 @@ extern "C" int ekf_shard_apply(ekf_ctx* c, int line, const double* buf)
     SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_APPLY, b), c->cfg.precision, c->stream));
     SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_ROBOT, b), c->cfg.precision, c->stream));
     c->sh_line++;
+    return EKF_OK;
+}
+
+extern "C" size_t ekf_shard_spec_buffer_words(const ekf_ctx* c)
+{
+    return (c && c->sh_world > 0) ? 4 * (size_t)c->d.N * (size_t)c->d.max_lines : 0;
+}
+
+extern "C" int ekf_shard_speculate(ekf_ctx* c, const double* buf, double* cols)
+{
+    if (!c || c->sh_open != 1 || !buf || !cols || c->sh_line != 0 || c->sh_L == 0) return EKF_EINVAL;
+    double* b = const_cast<double*>(buf);   // (read only by SH_DIAG)
+    if (!c->sh_diag) {
+        SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_DIAG, b), c->cfg.precision, c->stream));
+        c->sh_diag = 1;
+    }
+    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_GUESS, b), c->cfg.precision, c->stream));
+    if (c->spec == 2)   // test hook (EKF_OPT_SPECULATE = 2): every line guesses landmark 0
+        SH_TRY(hipMemsetAsync(c->sh_ctl + ekf::SC_GUESS, 0, sizeof(int) * c->d.max_lines, c->stream));
+    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_SPEC_COLS, b, cols), c->cfg.precision, c->stream));
+    return EKF_OK;
+}
+
+extern "C" int ekf_shard_run(ekf_ctx* c, const double* cols, double* next_line)
+{
+    if (!c || c->sh_open != 1 || !cols || !next_line || !c->sh_diag || c->sh_line != 0 || c->sh_L == 0)
+        return EKF_EINVAL;
+    ekf::ShardParams p = shard_params(c, ekf::SH_GATE, nullptr, const_cast<double*>(cols));
+    p.next_out = next_line;
+    SH_TRY(ekf::launch_shard_run(p, c->cfg.precision, c->stream));
+    c->sh_line = -1;   // until ekf_shard_resume
+    return EKF_OK;
+}
+
+extern "C" int ekf_shard_resume(ekf_ctx* c, int line)
+{
+    if (!c || c->sh_open != 1 || c->sh_line != -1 || line < 0 || line > c->sh_L) return EKF_EINVAL;
+    c->sh_line = line;
     return EKF_OK;
 }
 

@@ -145,11 +145,15 @@ struct ScanParams {
 // A scan runs the sequential association (Robot.cpp:298-641) as phases over ALL landmarks; the only
 // exchanges are sums of [N][4] buffers in which every rank fills the 2×2 blocks its tiles hold:
 // the diagonal blocks once per scan, the winner's column once per matched line.
-enum { SH_BEGIN = 0, SH_DIAG = 1, SH_GATE = 2, SH_COLUMN = 3, SH_APPLY = 4, SH_ROBOT = 5, SH_END = 6 };
+enum { SH_BEGIN = 0, SH_DIAG = 1, SH_GATE = 2, SH_COLUMN = 3, SH_APPLY = 4, SH_ROBOT = 5, SH_END = 6,
+       // speculative association of the partitioned instance (ekf_shard_speculate / ekf_shard_run):
+       // every line's first passing landmark at the scan's start (the guesses), the rank's blocks of
+       // all guessed columns, and (shard_run_kernel) the winner's package without its column
+       SH_GUESS = 7, SH_SPEC_COLS = 8, SH_PACKAGE = 9 };
 constexpr int SH_REC = 20;   // doubles per landmark: rr0..2 (6), yb (2), Dj (4), ma0, s0j, c0j, s0f, c0f, spare
 // device control words of the running scan (no host round trip between phases)
-enum { SC_WIN = 0, SC_STATUS = 1, SC_M = 2, SC_NEXTRA = 3, SC_S = 4, SC_MATCH = 8,
-       SC_EXTRA = 8 + EKF_MAX_LINES, SC_WORDS = 8 + 2 * EKF_MAX_LINES };
+enum { SC_WIN = 0, SC_STATUS = 1, SC_M = 2, SC_NEXTRA = 3, SC_S = 4, SC_NEXT = 5, SC_MATCH = 8,
+       SC_EXTRA = 8 + EKF_MAX_LINES, SC_GUESS = 8 + 2 * EKF_MAX_LINES, SC_WORDS = 8 + 3 * EKF_MAX_LINES };
 struct ShardParams {
     Dims d;
     int phase;
@@ -172,12 +176,17 @@ struct ShardParams {
     double* pkg;          // [MB words + 4·max_lines] the line's gain package
     int* ctl;             // [SC_WORDS]
     double* col;          // [N][4] the exchange buffer (caller's device memory)
+    double* cols;         // [L][N][4] the guessed columns' exchange buffer (speculative path)
+    double* next_out;     // shard_run_kernel: the line it stopped at, as a double (caller's device memory)
     const double* enc;    // [3]
     const ekf_line* lines;// [max_lines]
     const int* pexp;
     int reset_margin;
 };
 hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st);
+// lines [ctl[SC_NEXT], L) of the speculative path in one workgroup (shard_run_kernel)
+hipError_t launch_shard_run(const ShardParams& p, int precision, hipStream_t st);
+constexpr int SHR_THREADS = 1024;  // shard_run_kernel's workgroup (1024: 0.385 vs 0.41 ms per scan at 512, 28 VGPRs spilled)
 
 // One pass over the landmark block applying nsteps steps in order (each: reset, or rank-2m
 // downdate then its augmented rows). Pout may equal Pin (in place).

@@ -3366,37 +3366,19 @@ __device__ __forceinline__ void shard_predict(const double pose[3], const double
         }
 }
 
+// One phase of the partitioned instance's scan for landmark j (every rank runs every landmark):
+// shard_kernel runs one phase over a grid, shard_run_kernel the per-line phases of the
+// speculative path in one workgroup (its ctl, robot and package words in LDS).
 template <typename T>
-__global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
+__device__ __forceinline__ void shard_step(const ShardParams& p, const int phase, const int line, const int j,
+                                           const PllView<T>& pv)
 {
     using C = typename Stor<T>::C;
     constexpr double ETA = gate_eta<T>();
     const Dims d = p.d;
     const int n = d.n;
-    const int j = (int)(blockIdx.x * blockDim.x + threadIdx.x);   // every rank runs every landmark
     const bool own = j < d.N;
     int* ctl = p.ctl;
-    __shared__ int4 sh_ctl[PMAX];
-    if ((int)threadIdx.x < p.npend) {
-        const int* r = p.pend[threadIdx.x].res;
-        sh_ctl[threadIdx.x] = make_int4(r[RES_RESET], r[RES_KSTEPS], r[RES_NADD], r[RES_SAVED_IN]);
-    }
-    __syncthreads();
-    PllView<T> pv;
-    pv.X = reinterpret_cast<const T*>(p.Pread);
-    pv.nb = d.nb;
-    pv.kmax = d.kmax;
-    pv.M = d.M;
-    pv.max_lines = d.max_lines;
-    pv.e = 0;
-    pv.ex = storage_exp<T>(p.pexp, 0);
-    pv.opstride = (size_t)d.nb * 64 * (d.kmax / 2);
-    pv.usym = 0;   // (the partitioned instance stores its U rows)
-    pv.us = 1.0f;
-    pv.npend = p.npend;
-    pv.pend = p.pend;
-    pv.ctl = sh_ctl;
-    pv.rnd = 1;
     // block (j, w) of the landmark block is this rank's if the tile that stores it is
     auto local_blk = [&](int ja, int wb) {
         const int ba = (2 * ja) >> 5, bb = (2 * wb) >> 5;
@@ -3407,12 +3389,12 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
     const int b0 = 3 + 2 * j;
     double* rc = p.rec + (size_t)j * SH_REC;
     double R33[9], xp[3];
-    if (p.phase != SH_BEGIN) {
+    if (phase != SH_BEGIN) {
 #pragma unroll
         for (int a = 0; a < 9; a++) R33[a] = p.rob[a];
         xp[0] = p.rob[9]; xp[1] = p.rob[10]; xp[2] = p.rob[11];
     }
-    if (p.phase == SH_ROBOT) {
+    if (phase == SH_ROBOT) {
         // after line `line` (one thread): the robot block and x_pre after its match (Robot.cpp:560-602),
         // the match list, and the winner word reset for the next line's gate
         if (j == 0) {
@@ -3422,11 +3404,11 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
 #pragma unroll
                 for (int a = 0; a < 9; a++) p.rob[a] = R33[a];
                 p.rob[9] = xp[0]; p.rob[10] = xp[1]; p.rob[11] = xp[2];
-                ctl[SC_MATCH + p.line] = jstar;
+                ctl[SC_MATCH + line] = jstar;
                 ctl[SC_M] += 1;
             } else {
-                ctl[SC_MATCH + p.line] = -1;
-                ctl[SC_EXTRA + ctl[SC_NEXTRA]] = p.line;
+                ctl[SC_MATCH + line] = -1;
+                ctl[SC_EXTRA + ctl[SC_NEXTRA]] = line;
                 ctl[SC_NEXTRA] += 1;
             }
             ctl[SC_WIN] = 0x7fffffff;
@@ -3434,7 +3416,7 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
         return;
     }
 
-    if (p.phase == SH_BEGIN) {
+    if (phase == SH_BEGIN) {
         // the committed robot block and pose, predicted (every thread the same), every landmark's
         // strip columns predicted (Robot.cpp:242) and scan-start angle; the rank's diagonal blocks
         // with the pending steps applied into the exchange buffer (zero where another rank's)
@@ -3452,6 +3434,8 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
             ctl[SC_M] = 0;
             ctl[SC_NEXTRA] = 0;
             ctl[SC_S] = s;
+            ctl[SC_NEXT] = 0;
+            for (int i = 0; i < EKF_MAX_LINES; i++) ctl[SC_GUESS + i] = 0x7fffffff;
         }
         if (!own) return;
         double2 rr0 = *reinterpret_cast<const double2*>(p.Rs + b0);
@@ -3474,7 +3458,7 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
         return;
     }
     if (!own) return;
-    if (p.phase == SH_DIAG) {   // the summed diagonal blocks (every rank contributed its own)
+    if (phase == SH_DIAG) {   // the summed diagonal blocks (every rank contributed its own)
         const double4 dj = *reinterpret_cast<const double4*>(p.col + 4 * (size_t)j);
         rc[8] = dj.x; rc[9] = dj.y; rc[10] = dj.z; rc[11] = dj.w;
         return;
@@ -3486,9 +3470,9 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
     const double ma0 = rc[12], s0j = rc[13], c0j = rc[14];
     const double s0f = rc[15], c0f = rc[16];
     int fl = p.flags[j];
-    const ekf_line ln = p.lines[p.line < 0 ? 0 : p.line];
+    ekf_line ln = p.lines[line < 0 ? 0 : line];
     double Rm[4];
-    line_R(ln, p.line, p.r_mode, Rm);
+    line_R(ln, line, p.r_mode, Rm);
 
     // the gate of one landmark exactly as the sequential path (Robot.cpp:313-498)
     auto gate_of = [&](Cand& c, bool& pass, bool& sing, bool& amb) {
@@ -3506,7 +3490,48 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
         }
     };
 
-    if (p.phase == SH_GATE) {
+    if (phase == SH_GUESS) {
+        // every line's first passing landmark at the scan's start (no line applied yet): the
+        // speculative path fetches these columns in one exchange; shard_run_kernel checks each
+        // line's real winner against its guess
+        if (!(j < s)) return;
+        for (int i = 0; i < p.L; i++) {
+            ln = p.lines[i];
+            line_R(ln, i, p.r_mode, Rm);
+            Cand c;
+            bool pass, sing, amb;
+            gate_of(c, pass, sing, amb);
+            if (pass) atomicMin(ctl + SC_GUESS + i, j);
+        }
+        return;
+    }
+    if (phase == SH_SPEC_COLS) {
+        // the rank's blocks of every guessed column, pending steps applied (SH_COLUMN's blocks)
+        for (int i = 0; i < p.L; i++) {
+            const int w = ctl[SC_GUESS + i];
+            double blk[4] = {0, 0, 0, 0};
+            if (w != 0x7fffffff && local_blk(j, w)) pll_block(pv, 2 * j, 2 * w, blk);
+            *reinterpret_cast<double4*>(p.cols + 4 * ((size_t)i * d.N + j)) = make_double4(blk[0], blk[1], blk[2], blk[3]);
+        }
+        return;
+    }
+    if (phase == SH_PACKAGE) {   // (the winner's thread) SH_COLUMN's package, without the column
+        Cand c;
+        bool pass, sing, amb;
+        gate_of(c, pass, sing, amb);
+        build_package(c, R33, rr0, rr1, rr2, p.pkg);
+        const int m = ctl[SC_M];
+        for (int q = 0; q < m; q++) {
+            const double* h = p.hist + ((size_t)j * d.max_lines + q) * 8 + 4;
+            p.pkg[MB_VH + 4 * q + 0] = h[0];
+            p.pkg[MB_VH + 4 * q + 1] = h[1];
+            p.pkg[MB_VH + 4 * q + 2] = h[2];
+            p.pkg[MB_VH + 4 * q + 3] = h[3];
+        }
+        return;
+    }
+
+    if (phase == SH_GATE) {
         // the first passing unmatched landmark of the line: every rank finds the same one
         if (!(j < s) || (fl & 1)) {
             p.flags[j] = fl & 1;
@@ -3520,7 +3545,7 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
         return;
     }
 
-    if (p.phase == SH_COLUMN) {
+    if (phase == SH_COLUMN) {
         // the winner's gain package (its thread) and the rank's blocks of its column, with the
         // pending steps applied, into the exchange buffer (zero where another rank's)
         const int jstar = ctl[SC_WIN];
@@ -3546,12 +3571,12 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
         return;
     }
 
-    if (p.phase == SH_APPLY) {
+    if (phase == SH_APPLY) {
         const int jstar = ctl[SC_WIN];
         // GSL_EDOM counts only for the candidates the reference evaluates (up to the winner)
         int st = (fl & 2) && j <= jstar ? (int)EKF_ST_SINGULAR : 0;
         if ((fl & 4) && j <= jstar) st |= EKF_ST_PRECISION_BIT;   // (gate_eta)
-        if (p.r_mode == 1 && (p.line == 1 || p.line == 2)) st |= EKF_ST_NSYM;
+        if (p.r_mode == 1 && (line == 1 || line == 2)) st |= EKF_ST_NSYM;
         if (st) atomicOr(ctl + SC_STATUS, st);
         if (jstar == 0x7fffffff) return;
         const double4 cb = *reinterpret_cast<const double4*>(p.col + 4 * (size_t)j);   // summed over ranks
@@ -3705,6 +3730,82 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
         for (int q = 0; q < nextra; q++) res[RES_EXTRA + q] = ctl[SC_EXTRA + q];
         p.saved[0] = reset ? 0 : s + nadd;
     }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
+{
+    __shared__ int4 sh_ctl[PMAX];
+    if ((int)threadIdx.x < p.npend) {
+        const int* r = p.pend[threadIdx.x].res;
+        sh_ctl[threadIdx.x] = make_int4(r[RES_RESET], r[RES_KSTEPS], r[RES_NADD], r[RES_SAVED_IN]);
+    }
+    __syncthreads();
+    const Dims d = p.d;
+    PllView<T> pv;
+    pv.X = reinterpret_cast<const T*>(p.Pread);
+    pv.nb = d.nb;
+    pv.kmax = d.kmax;
+    pv.M = d.M;
+    pv.max_lines = d.max_lines;
+    pv.e = 0;
+    pv.ex = storage_exp<T>(p.pexp, 0);
+    pv.opstride = (size_t)d.nb * 64 * (d.kmax / 2);
+    pv.usym = 0;   // (the partitioned instance stores its U rows)
+    pv.us = 1.0f;
+    pv.npend = p.npend;
+    pv.pend = p.pend;
+    pv.ctl = sh_ctl;
+    pv.rnd = 1;
+    shard_step<T>(p, p.phase, p.line, (int)(blockIdx.x * blockDim.x + threadIdx.x), pv);
+}
+
+// The speculative path's lines (ekf_shard_run): one workgroup runs lines 0 .. L − 1 of
+// the sequential association exactly as the per-line phases do (gate of every landmark, the
+// winner's package, gain rows, robot update), taking each winner's column from the exchanged
+// guessed columns (p.cols) instead of a per-line exchange. A line whose first passing landmark is
+// not its guess stops the run there (*next_out = that line): the caller continues with the
+// per-line phases from the state after the lines before it. Every rank holds the same replicated
+// state, so every rank stops at the same line.
+template <typename T>
+__global__ __launch_bounds__(SHR_THREADS) void shard_run_kernel(ShardParams p)
+{
+    __shared__ int sh_cw[SC_WORDS];
+    __shared__ double sh_rob[12];
+    __shared__ double sh_pkg[MB_WORDS_FIXED + 4 * EKF_MAX_LINES];
+    const int tid = threadIdx.x;
+    for (int k = tid; k < SC_WORDS; k += SHR_THREADS) sh_cw[k] = p.ctl[k];
+    if (tid < 12) sh_rob[tid] = p.rob[tid];
+    __syncthreads();
+    ShardParams q = p;
+    q.ctl = sh_cw;
+    q.rob = sh_rob;
+    q.pkg = sh_pkg;
+    PllView<T> pv = {};   // (unused by the per-line phases)
+    const int N = p.d.N;
+    int i = 0;
+    for (; i < p.L; i++) {
+        for (int j = tid; j < N; j += SHR_THREADS) shard_step<T>(q, SH_GATE, i, j, pv);
+        __syncthreads();
+        const int w = sh_cw[SC_WIN];
+        if (w != 0x7fffffff && w != sh_cw[SC_GUESS + i]) break;   // (uniform)
+        if (w != 0x7fffffff) {
+            if (tid == w % SHR_THREADS) shard_step<T>(q, SH_PACKAGE, i, w, pv);
+            q.col = p.cols + 4 * (size_t)i * N;
+            __syncthreads();
+        }
+        for (int j = tid; j < N; j += SHR_THREADS) shard_step<T>(q, SH_APPLY, i, j, pv);
+        __syncthreads();
+        if (tid == 0) shard_step<T>(q, SH_ROBOT, i, 0, pv);
+        __syncthreads();
+    }
+    if (tid == 0) {
+        sh_cw[SC_NEXT] = i;
+        *p.next_out = (double)i;
+    }
+    __syncthreads();
+    for (int k = tid; k < SC_WORDS; k += SHR_THREADS) p.ctl[k] = sh_cw[k];
+    if (tid < 12) p.rob[tid] = sh_rob[tid];
 }
 
 #pragma clang fp contract(fast)
@@ -5660,6 +5761,14 @@ size_t scan_lds_bytes(int precision)
 #endif
 
 #if !defined(EKF_TU) || EKF_TU == 3
+hipError_t launch_shard_run(const ShardParams& p, int precision, hipStream_t st)
+{
+    if (precision == EKF_PREC_F64) hipLaunchKernelGGL(shard_run_kernel<double>, dim3(1), dim3(SHR_THREADS), 0, st, p);
+    else if (precision == EKF_PREC_F32) hipLaunchKernelGGL(shard_run_kernel<float>, dim3(1), dim3(SHR_THREADS), 0, st, p);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st)
 {
     const unsigned grid = (unsigned)((p.d.N + 255) / 256);   // every landmark

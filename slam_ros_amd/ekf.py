@@ -46,7 +46,8 @@ EXPORTED = [
     "ekf_state_dim", "ekf_profile_enable", "ekf_profile_read", "ekf_profile_flushes",
     "ekf_flush_kernel_name", "ekf_debug_scan_stamps", "ekf_debug_result_words",
     "ekf_shard_create", "ekf_shard_tiles", "ekf_shard_buffer_words", "ekf_shard_begin", "ekf_shard_line",
-    "ekf_shard_apply", "ekf_shard_end", "ekf_shard_abort",
+    "ekf_shard_apply", "ekf_shard_end", "ekf_shard_abort", "ekf_shard_spec_buffer_words",
+    "ekf_shard_speculate", "ekf_shard_run", "ekf_shard_resume",
 ]
 
 
@@ -139,6 +140,10 @@ def load_library(path: str = ""):
         "ekf_shard_apply": (ctypes.c_int, [vp, ctypes.c_int, vp]),
         "ekf_shard_end": (ctypes.c_int, [vp, vp]),
         "ekf_shard_abort": (ctypes.c_int, [vp]),
+        "ekf_shard_spec_buffer_words": (sz, [vp]),
+        "ekf_shard_speculate": (ctypes.c_int, [vp, vp, vp]),
+        "ekf_shard_run": (ctypes.c_int, [vp, vp, vp]),
+        "ekf_shard_resume": (ctypes.c_int, [vp, ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

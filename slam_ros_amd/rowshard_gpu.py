@@ -39,7 +39,8 @@ class ShardedInstance:
     """One instance over the ranks of the default process group (or `group`)."""
 
     def __init__(self, capacity: int, precision: int = E.PREC_F32, max_lines: int = 8,
-                 flush_interval: int = 4, r_mode: int = E.R_INTENDED, group=None, device: int | None = None):
+                 flush_interval: int = 4, r_mode: int = E.R_INTENDED, group=None, device: int | None = None,
+                 speculate: bool = True, options: dict | None = None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -47,7 +48,7 @@ class ShardedInstance:
         dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         torch.cuda.set_device(dev)
         self.ens = E.Ensemble(capacity, 1, precision, max_lines=max_lines, flush_interval=flush_interval,
-                              r_mode=r_mode, device=dev.index, shard=(self.rank, self.world))
+                              r_mode=r_mode, device=dev.index, shard=(self.rank, self.world), options=options or {})
         self.lib = E.load_library()
         self.h = self.ens.handle
         self.max_lines = max_lines
@@ -59,9 +60,14 @@ class ShardedInstance:
         self.stream = torch.cuda.Stream(dev)
         self.ens.set_stream(self.stream.cuda_stream)
         self.words = int(self.lib.ekf_shard_buffer_words(self.h))
+        self.speculate = speculate
+        self.swords = int(self.lib.ekf_shard_spec_buffer_words(self.h))
         with torch.cuda.stream(self.stream):
             # + one word: the number of ranks whose phase failed, summed with every exchange
             self.buf = torch.zeros(self.words + 1, dtype=torch.float64, device=dev)
+            self.cols = torch.zeros(self.swords + 1, dtype=torch.float64, device=dev)
+            self.agree = torch.zeros(2, dtype=torch.float64, device=dev)
+        self.spec_runs = []   # per scan: the line the speculative run stopped at (L: all lines)
         self.host_coll = dist.get_backend(group) != "nccl"
         r0, r1 = ctypes.c_int32(), ctypes.c_int32()
         E._check(self.lib.ekf_shard_tiles(self.h, ctypes.byref(r0), ctypes.byref(r1)), "ekf_shard_tiles")
@@ -74,15 +80,16 @@ class ShardedInstance:
     def upload_state(self, P, y, saved, pose):
         self.ens.upload_state(0, P, y, saved, pose)
 
-    def _sum(self, failed: bool):
+    def _sum(self, failed: bool, buf=None):
         """The exchange (on self.stream), carrying this rank's failure flag in the last word."""
-        self.buf[self.words].fill_(1.0 if failed else 0.0)
+        buf = self.buf if buf is None else buf
+        buf[-1].fill_(1.0 if failed else 0.0)
         if self.host_coll:
-            t = self.buf.cpu()
+            t = buf.cpu()
             dist.all_reduce(t, group=self.group)
-            self.buf.copy_(t)
+            buf.copy_(t)
         else:
-            dist.all_reduce(self.buf, group=self.group)
+            dist.all_reduce(buf, group=self.group)
 
     def localize(self, lines, enc) -> list[int]:
         """Robot::localize on the partitioned instance; returns the matched landmark per line."""
@@ -100,7 +107,41 @@ class ShardedInstance:
             rc = lib.ekf_shard_begin(h, E._dp(enc), ln.ctypes.data_as(ctypes.c_void_p), L, bp)
             err = err or (rc and (rc, "ekf_shard_begin"))
             self._sum(bool(err))
-            for i in range(L):
+            first, abandon = 0, False
+            if self.speculate and L > 0:
+                # one exchange of every guessed column, then the lines in one workgroup up to the
+                # first wrong guess (ekf_shard_run, synchronous; the replicated state makes every
+                # rank stop at the same line). A small agreement exchange (max of the failure flag
+                # and of the stopping line) keeps the ranks' exchange sequences equal even when
+                # one rank's run fails.
+                cp_ = ctypes.c_void_p(self.cols.data_ptr())
+                if not err:
+                    rc = lib.ekf_shard_speculate(h, bp, cp_)
+                    err = rc and (rc, "ekf_shard_speculate")
+                self._sum(bool(err), self.cols)
+                # stream-ordered: the run writes its stopping line into agree[1]; agree[0] carries
+                # the failure flag of the columns' exchange; one host read after the agreement
+                self.agree[0:1].copy_(self.cols[-1:])
+                self.agree[1].fill_(float(L))
+                if not err:
+                    rc = lib.ekf_shard_run(h, cp_, ctypes.c_void_p(self.agree.data_ptr() + 8))
+                    err = rc and (rc, "ekf_shard_run")
+                if err:
+                    self.agree[0].fill_(1.0)
+                if self.host_coll:
+                    t = self.agree.cpu()
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                    self.agree.copy_(t)
+                else:
+                    dist.all_reduce(self.agree, op=dist.ReduceOp.MAX, group=self.group)
+                ag = self.agree.cpu()
+                abandon = bool(ag[0] > 0)
+                first = L if abandon else int(ag[1])
+                if not abandon:
+                    rc = lib.ekf_shard_resume(h, first)
+                    err = err or (rc and (rc, "ekf_shard_resume"))
+                self.spec_runs.append(first)
+            for i in range(first, L):
                 if not err:
                     rc = lib.ekf_shard_line(h, i, bp)
                     err = rc and (rc, "ekf_shard_line")
@@ -109,6 +150,8 @@ class ShardedInstance:
                     rc = lib.ekf_shard_apply(h, i, bp)
                     err = rc and (rc, "ekf_shard_apply")
             failed = float(self.buf[self.words].item())   # (synchronises the stream once per scan)
+        if abandon and failed == 0:
+            failed = 1.0
         if failed > 0:
             lib.ekf_shard_abort(h)
             rc, what = err if err else (0, "a peer rank's phase")

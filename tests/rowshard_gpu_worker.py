@@ -24,6 +24,9 @@ ap.add_argument("--precision", type=int, default=E.PREC_F32)
 ap.add_argument("--active", type=int, default=0, help="active landmarks (0: N - 10)")
 ap.add_argument("--extra-every", type=int, default=0, help="two unmatched lines every k scans")
 ap.add_argument("--backend", default="gloo")
+ap.add_argument("--per-line", action="store_true", help="the per-line protocol only (no speculative run)")
+ap.add_argument("--dup-every", type=int, default=0, help="line 1 repeats line 0 every k scans")
+ap.add_argument("--wrong-guess", action="store_true", help="EKF_OPT_SPECULATE = 2: every line guesses landmark 0")
 args = ap.parse_args()
 
 dist.init_process_group(args.backend)
@@ -31,7 +34,8 @@ rank = dist.get_rank()
 torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) if args.backend == "nccl" else 0)
 w = G.make_world(args.N, active=args.active or args.N - 10)
 st = G.initial_state(w)
-inst = R.ShardedInstance(args.N, args.precision, max_lines=8, flush_interval=args.T)
+inst = R.ShardedInstance(args.N, args.precision, max_lines=8, flush_interval=args.T, speculate=not args.per_line,
+                         options={"speculate": 2} if args.wrong_guess else None)
 inst.init_lowrank(st.diag, st.U, st.y, st.saved, st.pose)
 matches, times = [], []
 rng = np.random.default_rng(11)
@@ -40,6 +44,9 @@ for step in range(1, args.scans + 1):
     ln = lines[0, :nl[0]]
     if args.extra_every and step % args.extra_every == 0:
         ln = np.concatenate([ln, G.random_lines(rng, 2)])
+    if args.dup_every and step % args.dup_every == 0:
+        ln = ln.copy()
+        ln[1] = ln[0]
     dist.barrier()
     t0 = time.perf_counter()
     matches.append(inst.localize(ln, enc[0]) + [-2] * (8 - len(ln)))
@@ -47,7 +54,7 @@ for step in range(1, args.scans + 1):
 P, y, saved, pose = inst.download_state()
 np.savez(os.path.join(args.out, f"rank{rank}.npz"), P=P, y=y, saved=saved, pose=pose, matches=np.array(matches),
          tile_rows=np.array(inst.tile_rows), block_bytes=inst.landmark_block_bytes(), times=np.array(times),
-         status=inst.status())
+         status=inst.status(), spec_runs=np.array(inst.spec_runs))
 inst.close()
 dist.barrier()
 dist.destroy_process_group()

@@ -4,7 +4,12 @@ context (ekf_shard_create) storing its share of the packed tiles, against a sing
 same library on the same scans. Exact arithmetic: every association, the robot rows, the mean, the
 pose and savedLineCount on every rank, and the landmark block — the sum of the ranks' tiles — are
 bit-identical, augmentation and the capacity reset included; each rank stores at most 0.55 of the
-single context's landmark-block bytes. The per-scan wall time of the two-rank run is recorded."""
+single context's landmark-block bytes. The per-scan wall time of the two-rank run is recorded.
+Both protocols (slam_ekf.h): the speculative one (one exchange of every guessed column, the lines
+in one workgroup up to the first wrong guess; the default) and the per-line one (one exchange per
+line), with scans whose line 1 repeats line 0, and with every guess wrong (EKF_OPT_SPECULATE = 2:
+the run stops at the first line whose winner is not landmark 0 and the per-line protocol finishes
+the scan from the state after the lines before it)."""
 import os
 import socket
 import subprocess
@@ -25,28 +30,38 @@ def free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("prec,N,T,scans,active,extra_every",
-                         [(1, 1024, 4, 9, 0, 0), (1, 1000, 6, 8, 0, 0), (0, 512, 4, 6, 0, 0),
-                          (1, 1024, 4, 9, 1000, 3), (1, 256, 4, 6, 0, 3), (0, 480, 4, 7, 400, 2)])
-def test_two_rank_shard_equals_single_context(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_every):
+@pytest.mark.parametrize("prec,N,T,scans,active,extra_every,dup,mode",
+                         [(1, 1024, 4, 9, 0, 0, 0, "spec"), (1, 1000, 6, 8, 0, 0, 3, "spec"), (0, 512, 4, 6, 0, 0, 2, "spec"),
+                          (1, 1024, 4, 9, 1000, 3, 0, "spec"), (1, 256, 4, 6, 0, 3, 0, "spec"),
+                          (0, 480, 4, 7, 400, 2, 3, "wrong"), (1, 1024, 4, 9, 1000, 3, 2, "wrong"),
+                          (1, 1024, 4, 9, 1000, 3, 2, "perline"), (0, 512, 4, 6, 0, 0, 0, "perline")])
+def test_two_rank_shard_equals_single_context(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_every,
+                                              dup, mode):
     """(active, extra_every): every extra_every-th scan carries two unmatched lines — augmented
-    landmarks landing on either rank, and (active = N − 10) the capacity reset."""
-    run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_every, world=2, backend="gloo")
+    landmarks landing on either rank, and (active = N − 10) the capacity reset; dup: line 1 repeats
+    line 0 every dup-th scan; mode: the speculative protocol, the same with every guess wrong, or
+    the per-line protocol only."""
+    run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_every, world=2, backend="gloo",
+                dup=dup, mode=mode)
 
 
-@pytest.mark.parametrize("prec,N,T,scans,active,extra_every", [(1, 1024, 4, 9, 1000, 3), (0, 512, 4, 6, 0, 0)])
-def test_rccl_device_sum_world1(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_every):
-    """The nccl (RCCL) backend's path: the exchange buffer all-reduced in place on the device, on
+@pytest.mark.parametrize("prec,N,T,scans,active,extra_every,dup,mode",
+                         [(1, 1024, 4, 9, 1000, 3, 3, "spec"), (0, 512, 4, 6, 0, 0, 0, "wrong"),
+                          (1, 1024, 4, 9, 1000, 3, 0, "perline")])
+def test_rccl_device_sum_world1(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_every, dup, mode):
+    """The nccl (RCCL) backend's path: the exchange buffers all-reduced in place on the device, on
     the context's stream, with no host staging. One GPU holds one RCCL rank, so this runs a world of
     one (the partition is the whole block); the two-rank protocol itself is covered over gloo."""
-    run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_every, world=1, backend="nccl")
+    run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_every, world=1, backend="nccl",
+                dup=dup, mode=mode)
 
 
 def rel(a, b):
     return float(np.linalg.norm(a - b) / np.linalg.norm(b))
 
 
-def run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_every, world, backend):
+def run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_every, world, backend, dup=0,
+                mode="spec"):
     w = G.make_world(N, active=active or N - 10)
     st = G.initial_state(w)
     one = ekf_mod.Ensemble(N, 1, prec, max_lines=8, flush_interval=T)
@@ -62,6 +77,9 @@ def run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_
         ln = lines[0, :nl[0]]
         if extra_every and step % extra_every == 0:
             ln = np.concatenate([ln, G.random_lines(rng, 2)])
+        if dup and step % dup == 0:
+            ln = ln.copy()
+            ln[1] = ln[0]
         la = np.zeros((1, 8, 6))
         la[0, :len(ln)] = ln
         r = one.localize(enc, la, np.array([len(ln)], dtype=np.int32))
@@ -79,7 +97,8 @@ def run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "tests", "rowshard_gpu_worker.py"), "--out", str(tmp_path), "--N", str(N),
            "--T", str(T), "--scans", str(scans), "--precision", str(prec), "--active", str(active),
-           "--extra-every", str(extra_every), "--backend", backend]
+           "--extra-every", str(extra_every), "--backend", backend, "--dup-every", str(dup)] + \
+        {"spec": [], "wrong": ["--wrong-guess"], "perline": ["--per-line"]}[mode]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-3000:]
     Psum = np.zeros_like(P)
@@ -98,6 +117,13 @@ def run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_
         if world == 2:
             assert int(d["block_bytes"]) <= (0.55 if N >= 1000 else 0.65) * block_bytes, (r, int(d["block_bytes"]), block_bytes)
         times = d["times"]
+        spec_runs = [int(x) for x in d["spec_runs"]]
+    if mode == "perline":
+        assert spec_runs == []
+    else:
+        assert len(spec_runs) == scans
+        if mode == "wrong":   # guesses of landmark 0: the runs stop early
+            assert sum(x < 8 - (extra_every > 0) * 2 for x in spec_runs) >= scans // 2, spec_runs
     np.testing.assert_array_equal(Psum[3:, 3:], P[3:, 3:])
     # the assembled partitioned state against the restatement: a trajectory of `scans` updates
     # never re-synced, so k times the per-scan bar (tests/test_bench_config.py) on P; the state
@@ -113,7 +139,8 @@ def run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_
     assert rows[0][0] == 0 and rows[-1][1] == (2 * N + 31) // 32
     assert all(rows[r][1] == rows[r + 1][0] for r in range(world - 1))
     from tests.test_bench_config import record
-    record(f"rowshard_{backend}{world}_N{N}_T{T}_p{prec}", {"scan_ms_median": float(np.median(times)) * 1e3,
+    record(f"rowshard_{backend}{world}_N{N}_T{T}_p{prec}_{mode}_d{dup}",
+           {"scan_ms_median": float(np.median(times)) * 1e3, "spec_runs": spec_runs,
                                             "tile_rows": [[int(a), int(b)] for a, b in rows],
                                             "block_bytes_single": int(block_bytes),
                                             "p_rel_err_vs_oracle": rp, "y_rel_err_vs_oracle": ry})
