@@ -940,3 +940,58 @@ def test_bf16_2x4_flush_equals_2x2(ekf_mod, monkeypatch, prec, N, T, extra_every
             assert rel(ya, yb) <= 1e-10, (e, rel(ya, yb))
         else:
             assert np.array_equal(Pa, Pb) and np.array_equal(ya, yb), e
+
+
+def _gate_case(ekf_mod, oracle_mod, prec, p22, p2a, daa, delta):
+    """One landmark at (alpha 0.3, r 2.0) seen from the pose (0, 0, 0) without motion (the encoder
+    equals the pose: F = I, Q = 0, Robot.cpp:136-286), its angle variance p22 / daa / covariance
+    p2a, and one line at Mahalanobis distance² = 0.16·(1 + delta) from it (v1 = 0, S01 = 0: d² =
+    v0²/S00 with S00 = p22 − 2·p2a + daa + R00 from the STORED block). Returns (status, match,
+    the restatement's match)."""
+    N = 16
+    n = 3 + 2 * N
+    P = np.zeros((n, n))
+    P[0, 0] = P[1, 1] = 1e-3
+    P[2, 2] = p22
+    P[3, 3] = daa
+    P[4, 4] = 1e-3
+    P[2, 3] = P[3, 2] = p2a
+    for k in range(5, n):
+        P[k, k] = 1e-3
+    y = np.zeros(n)
+    y[3], y[4] = 0.3, 2.0
+    ens = ekf_mod.Ensemble(N, 1, prec, max_lines=8)
+    ens.upload_state(0, P, y, 1, [0.0, 0.0, 0.0])
+    Ps = ens.download_state(0)[0]
+    R00 = 1e-3
+    S00 = Ps[2, 2] - 2.0 * Ps[2, 3] + Ps[3, 3] + R00
+    v0 = np.sqrt(0.16 * (1.0 + delta) * S00)
+    line = np.array([[0.3 + v0, 2.0, R00, 0.0, 0.0, 1e-3]])
+    ref = oracle_mod.OracleRobot(N)
+    ref.set_state(*ens.download_state(0))
+    r = ens.localize(np.zeros((1, 3)), line[None], [1])[0]
+    m = ref.localize(line, np.zeros(3))
+    ens.close()
+    return r["status"], r["match"][0], m[0]
+
+
+@pytest.mark.parametrize("prec", [1, 2])
+def test_gate_storage_precision_flag(ekf_mod, oracle_mod, prec):
+    """EKF_ST_PRECISION from the gate (gate_eta): a distance within the stored state's
+    precision of the 0.4 gate (Robot.cpp:489) is reported, both where S00 is the difference of
+    terms 1e7 times larger (the robot and landmark angles correlated to 1 − 1e-7: a run-away
+    filter) and, without cancellation, within 1e-7 of the threshold; a clear decision is not, and
+    matches the restatement from the same stored state."""
+    ST = ekf_mod.ST_PRECISION
+    # cancellation: flagged on either side of the gate
+    for delta in (0.05, -0.05):
+        st, _, _ = _gate_case(ekf_mod, oracle_mod, prec, 1e4, 1e4 - 1e-3, 1e4, delta)
+        assert st & ST, (prec, delta, st)
+    # no cancellation, clear decisions: not flagged, the reference's decision
+    for delta, want in ((0.05, -1), (-0.05, 0)):
+        st, got, ref = _gate_case(ekf_mod, oracle_mod, prec, 1e-3, 0.0, 1e-3, delta)
+        assert not (st & ST), (prec, delta, st)
+        assert got == ref == want, (prec, delta, got, ref)
+    if prec == 1:   # (fp16 storage: eta 2^-8 flags ±1 % already)
+        st, _, _ = _gate_case(ekf_mod, oracle_mod, prec, 1e-3, 0.0, 1e-3, 1e-7)
+        assert st & ST, st
