@@ -25,12 +25,12 @@ def rel(a, b):
 
 
 @pytest.mark.parametrize("prec,T,spec", [(1, 4, "1"), (1, 1, "0"), (0, 3, "1"), (2, 4, "1")])
-def test_timeout_rolls_back_the_instance(ekf_mod, oracle_mod, prec, T, spec, hook="test_drop_wg"):
-    N, E = 1024, 3   # G = 6 workgroups per instance
+def test_timeout_rolls_back_the_instance(ekf_mod, oracle_mod, prec, T, spec, hook="test_drop_wg", arith=0, nt=0):
+    N, E = 1024, 3   # G = 6 workgroups per instance (16 / 8 with 64 / 128 landmarks per workgroup)
     w = G.make_world(N)
     st = G.initial_state(w)
-    ens = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T,
-                           options={hook: 2, "spin_log2": 12, "speculate": int(spec)})
+    ens = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=arith,
+                           options={hook: 2, "spin_log2": 12, "speculate": int(spec), "scan_threads": nt})
     for e in range(E):
         ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
     before = ens.download_state(1)
@@ -67,6 +67,15 @@ def test_verdict_timeout_of_one_workgroup_rolls_back(ekf_mod, oracle_mod, prec, 
     sequential path and the lead must not commit without its completion word: the
     instance's calls roll back, the other instances proceed."""
     test_timeout_rolls_back_the_instance(ekf_mod, oracle_mod, prec, T, "1", hook="test_verdict_timeout")
+
+
+@pytest.mark.parametrize("prec,nt,hook", [(1, 64, "test_drop_wg"), (1, 128, "test_drop_wg"), (2, 64, "test_drop_wg"),
+                                          (1, 64, "test_verdict_timeout")])
+def test_timeout_rolls_back_narrow_workgroups(ekf_mod, oracle_mod, prec, nt, hook):
+    """The same with the split-fp16 association kernel on 64 / 128 landmarks per workgroup
+    (EKF_OPT_SCAN_THREADS): more workgroups per instance in the exchanges, the collection and the
+    completion words (sized for the narrowest width)."""
+    test_timeout_rolls_back_the_instance(ekf_mod, oracle_mod, prec, 4, "1", hook=hook, arith=2, nt=nt)
 
 
 def test_environment_is_not_read(ekf_mod, monkeypatch):
