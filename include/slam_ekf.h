@@ -216,11 +216,11 @@ enum {
      * landmark with a nonzero operand row or new row in the group (unchanged by it: a partly
      * filled map streams only its active part); 0: every wave-tile */
     EKF_OPT_ACTIVE_FLUSH = 9,
-    /* landmarks per association workgroup: 0 automatic (default), 192, or 128 / 64 (more
-     * workgroups per instance, each with fewer landmarks, on more CUs: contexts whose association
-     * runs the split-fp16 (EKF_ARITH_F16X3) kernel, symmetric fp32 / fp16 storage, max_lines <= 8,
-     * when an instance then needs at most 64 workgroups and the instances still fit the device in
-     * one launch; otherwise 192). Identical results for every value. */
+    /* landmarks per association workgroup: 0 automatic (default: the narrowest that fits), 192,
+     * or 128 / 64 (more workgroups per instance, each with fewer landmarks, on more CUs: fp32 /
+     * fp16 storage with EKF_R_INTENDED and max_lines <= 8, every flush arithmetic, when an
+     * instance then needs at most 64 workgroups and the instances still fit the device in one
+     * launch; otherwise 192). Identical results for every value. */
     EKF_OPT_SCAN_THREADS = 10,
 };
 int ekf_set_option(ekf_ctx* ctx, int option, int value);

@@ -830,7 +830,8 @@ static void prof_end(ekf_ctx* c, EvPair* pr, hipStream_t st)
 }
 
 // Landmarks per association workgroup (EKF_OPT_SCAN_THREADS): the narrow widths exist for the
-// split-fp16 instantiation of the kernel only (launch_scan) and need the instance's workgroups
+// HOT instantiations of the kernel only (symmetric fp32 / fp16 operands, kmax = 16, every flush
+// arithmetic; launch_scan) and need the instance's workgroups
 // within the speculative path's bound, no pipelined overlap and every instance in one launch.
 // Automatic: the narrowest of 64 and 128 that fits (measured, DESIGN §4.1: N = 256 / 1024 / 2048
 // +8 / +9 / +5 % updates/s at 64, N = 4096 with 8 instances +1.4 % at 128).
@@ -846,7 +847,7 @@ static int scan_width(const ekf_ctx* c)
 {
     constexpr int W = ekf::SCAN_THREADS;
     if (c->dbg || c->sh_world > 0 || c->cfg.precision == EKF_PREC_F64 || c->cfg.r_mode != EKF_R_INTENDED ||
-        c->d.kmax != 16 || c->pmode != 2)
+        c->d.kmax != 16)
         return W;
     auto fits = [&](int nt) {
         const int G = (c->d.N + nt - 1) / nt;

@@ -5712,27 +5712,38 @@ __global__ void lowrank_kernel(Dims d, const double* __restrict__ diag,
 // ---------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------
-// The association kernel on 128 / 64 landmarks per workgroup (ScanParams::nt): its split-fp16
-// instantiation only, one compilation unit per width (EKF_TU 7, 8)
-hipError_t launch_scan_nt128(const ScanParams& p, bool half, hipStream_t st);
-hipError_t launch_scan_nt64(const ScanParams& p, bool half, hipStream_t st);
+// The association kernel on 128 / 64 landmarks per workgroup (ScanParams::nt): its HOT
+// instantiations (symmetric fp32 operands, kmax = 16; HOT = 2 split-fp16, 1 the others), one
+// compilation unit per width (EKF_TU 7, 8)
+hipError_t launch_scan_nt128(const ScanParams& p, bool half, bool f16x3, hipStream_t st);
+hipError_t launch_scan_nt64(const ScanParams& p, bool half, bool f16x3, hipStream_t st);
 
 #if !defined(EKF_TU) || EKF_TU == 7
-hipError_t launch_scan_nt128(const ScanParams& p, bool half, hipStream_t st)
+hipError_t launch_scan_nt128(const ScanParams& p, bool half, bool f16x3, hipStream_t st)
 {
     const dim3 grid(p.G * p.E), block(128 + 64);
-    if (half) hipLaunchKernelGGL((scan_kernel<_Float16, false, 2, 128>), grid, block, 0, st, p);
-    else hipLaunchKernelGGL((scan_kernel<float, false, 2, 128>), grid, block, 0, st, p);
+    if (f16x3) {
+        if (half) hipLaunchKernelGGL((scan_kernel<_Float16, false, 2, 128>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((scan_kernel<float, false, 2, 128>), grid, block, 0, st, p);
+    } else {
+        if (half) hipLaunchKernelGGL((scan_kernel<_Float16, false, 1, 128>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((scan_kernel<float, false, 1, 128>), grid, block, 0, st, p);
+    }
     return hipGetLastError();
 }
 #endif
 
 #if !defined(EKF_TU) || EKF_TU == 8
-hipError_t launch_scan_nt64(const ScanParams& p, bool half, hipStream_t st)
+hipError_t launch_scan_nt64(const ScanParams& p, bool half, bool f16x3, hipStream_t st)
 {
     const dim3 grid(p.G * p.E), block(64 + 64);
-    if (half) hipLaunchKernelGGL((scan_kernel<_Float16, false, 2, 64>), grid, block, 0, st, p);
-    else hipLaunchKernelGGL((scan_kernel<float, false, 2, 64>), grid, block, 0, st, p);
+    if (f16x3) {
+        if (half) hipLaunchKernelGGL((scan_kernel<_Float16, false, 2, 64>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((scan_kernel<float, false, 2, 64>), grid, block, 0, st, p);
+    } else {
+        if (half) hipLaunchKernelGGL((scan_kernel<_Float16, false, 1, 64>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((scan_kernel<float, false, 1, 64>), grid, block, 0, st, p);
+    }
     return hipGetLastError();
 }
 #endif
@@ -5783,11 +5794,11 @@ hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st)
 #if !defined(EKF_TU) || EKF_TU == 1
 hipError_t launch_scan(const ScanParams& p, int precision, hipStream_t st)
 {
-    if (p.nt != SCAN_THREADS) {   // (the context picks a narrow width for this instantiation only)
-        if (p.dbg || precision == EKF_PREC_F64 || p.r_mode == 1 || p.d.kmax != 16 || p.bf != 2)
-            return hipErrorInvalidValue;
-        if (p.nt == 128) return launch_scan_nt128(p, precision == EKF_PREC_F16, st);
-        if (p.nt == 64) return launch_scan_nt64(p, precision == EKF_PREC_F16, st);
+    if (p.nt != SCAN_THREADS) {   // (the context picks a narrow width for the HOT instantiations only)
+        if (p.dbg || precision == EKF_PREC_F64 || p.r_mode == 1 || p.d.kmax != 16) return hipErrorInvalidValue;
+        const bool half = precision == EKF_PREC_F16, f16x3 = p.bf == 2;
+        if (p.nt == 128) return launch_scan_nt128(p, half, f16x3, st);
+        if (p.nt == 64) return launch_scan_nt64(p, half, f16x3, st);
         return hipErrorInvalidValue;
     }
     const dim3 grid(p.G * p.E), block(SCAN_BLOCK);

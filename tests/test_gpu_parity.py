@@ -528,13 +528,16 @@ def test_hot_scan_kernel_equals_generic(ekf_mod, monkeypatch, prec, arith):
         np.testing.assert_array_equal(runs[("0", "2")][1][0], runs[("0", "1")][1][0])
 
 
-@pytest.mark.parametrize("prec", [1, 2])
+@pytest.mark.parametrize("prec,arith", [(1, 2), (2, 2), (1, 0), (1, 1), (2, 1)])
 @pytest.mark.parametrize("N,T", [(256, 4), (1000, 8), (1024, 20), (2048, 12)])
-def test_narrow_scan_workgroups_identical(ekf_mod, prec, N, T):
-    """EKF_OPT_SCAN_THREADS: the split-fp16 association kernel on 128 and 64 landmarks per
-    workgroup (more workgroups per instance, a partial last one at N = 1000) gives bit-identical
-    results and state to the 192-wide one, on the speculative path and when every guess is wrong
-    (the sequential restart: one cross-workgroup exchange per line), three instances per launch."""
+def test_narrow_scan_workgroups_identical(ekf_mod, prec, arith, N, T):
+    """EKF_OPT_SCAN_THREADS: the association kernel on 128 and 64 landmarks per workgroup (more
+    workgroups per instance, a partial last one at N = 1000) gives bit-identical results and state
+    to the 192-wide one, in every flush arithmetic, on the speculative path and when every guess is
+    wrong (the sequential restart: one cross-workgroup exchange per line), three instances per
+    launch."""
+    if arith != 2 and T > 16:
+        T = 16   # (EKF_ARITH_EXACT / BF16X6: T <= 16)
     E = 3
     w = G.make_world(N, active=N - 30)
     st = G.initial_state(w)
@@ -542,7 +545,7 @@ def test_narrow_scan_workgroups_identical(ekf_mod, prec, N, T):
     runs = {}
     for nt in (192, 128, 64):
         for spec in (1, 2):
-            ens = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=2,
+            ens = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=arith,
                                    options={"scan_threads": nt, "speculate": spec})
             for e in range(E):
                 ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
