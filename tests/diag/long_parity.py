@@ -5,7 +5,7 @@ pose re-synced to the GPU's after every scan (the per-scan contract, DESIGN §2.
 at every flush-group end; association compared on every scan. A second restatement of instance 0
 is never re-synced (the drift of a whole trajectory). One JSON line.
 
-usage: python tests/diag/long_parity.py [pre] [scans] [T]
+usage: python tests/diag/long_parity.py [pre] [scans] [T] [precision f32|f16|f64]
 """
 import json
 import os
@@ -32,9 +32,12 @@ def main():
     pre = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     scans = int(sys.argv[2]) if len(sys.argv) > 2 else 240
     T = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    precision = sys.argv[4] if len(sys.argv) > 4 else "f32"
+    prec = {"f32": ekf.PREC_F32, "f16": ekf.PREC_F16, "f64": ekf.PREC_F64}[precision]
+    arith = ekf.ARITH_EXACT if prec == ekf.PREC_F64 else ekf.ARITH_F16X3
     w = G.make_world(N)
     st = G.initial_state(w)
-    ens = ekf.Ensemble(N, E, ekf.PREC_F32, max_lines=L, flush_interval=T, arith=ekf.ARITH_F16X3)
+    ens = ekf.Ensemble(N, E, prec, max_lines=L, flush_interval=T, arith=arith)
     for e in range(E):
         ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
     for s in range(1, pre + 1):
@@ -65,7 +68,8 @@ def main():
                 p_group.append(rel(P, refs[e].P_t0))
                 refs[e].set_state(P, y, saved, pose)
     P0, y0, _, _ = ens.download_state(0)
-    out = {"config": f"N={N} E={E} L={L} f32 storage f16x3 T={T}, bench world, pre-roll {pre}",
+    out = {"config": f"N={N} E={E} L={L} {precision} storage {'exact' if arith == ekf.ARITH_EXACT else 'f16x3'} "
+                     f"T={T}, bench world, pre-roll {pre}",
            "scans": scans, "groups": len(p_group) // len(CHECK), "instances_checked": list(CHECK),
            "assoc_differences": assoc_diff, "status_bits": status,
            "y_per_scan_max": max(y_scan), "y_per_scan_median": float(np.median(y_scan)),
