@@ -332,7 +332,9 @@ int ekf_shard_abort(ekf_ctx* ctx);
  *                                           winner's column from cols; stops at the first line
  *                                           whose first passing landmark is not its guess and
  *                                           writes that line (or L) as a double to next, device
- *                                           memory of the caller (asynchronous, stream-ordered)
+ *                                           memory of the caller (asynchronous, stream-ordered;
+ *                                           L + 1 when its cooperating workgroups' exchange timed
+ *                                           out: abandon the scan, ekf_shard_abort)
  *   ekf_shard_resume(line)                  the host's copy of next (every rank reads the same)
  *   for each line i from next: ekf_shard_line, SUM buf, ekf_shard_apply (the per-line protocol)
  *   ekf_shard_end(out)

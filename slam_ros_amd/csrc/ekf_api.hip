@@ -1584,16 +1584,19 @@ extern "C" int ekf_shard_begin(ekf_ctx* c, const double enc[3], const ekf_line* 
 {
     if (!c || c->sh_world <= 0 || !enc || !buf || (nlines > 0 && !lines) || c->sh_open) return EKF_EINVAL;
     if (nlines < 0 || nlines > c->d.max_lines) return EKF_ERANGE;
-    std::vector<ekf_line> pad(c->d.max_lines);
-    memset(pad.data(), 0, sizeof(ekf_line) * pad.size());
-    for (int i = 0; i < nlines; i++) pad[i] = lines[i];
-    int rc = stage_inputs(c, enc, pad.data(), &nlines);
-    if (rc) return rc;
     c->sh_line = 0;
     c->sh_L = nlines;
     c->sh_open = 1;
     c->sh_diag = 0;
-    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_BEGIN, buf), c->cfg.precision, c->stream));
+    // the inputs travel as kernel arguments of the first phase, which stores them for the later
+    // ones (stream-ordered: no host staging copy, no wait for the previous scan)
+    ekf::ShardParams p = shard_params(c, ekf::SH_BEGIN, buf);
+    for (int k = 0; k < 3; k++) p.enc_v[k] = enc[k];
+    for (int i = 0; i < c->d.max_lines; i++) {
+        if (i < nlines) p.lines_v[i] = lines[i];
+        else memset(&p.lines_v[i], 0, sizeof(ekf_line));
+    }
+    SH_TRY(ekf::launch_shard(p, c->cfg.precision, c->stream));
     return EKF_OK;
 }
 
@@ -1629,11 +1632,10 @@ extern "C" int ekf_shard_speculate(ekf_ctx* c, const double* buf, double* cols)
 {
     if (!c || c->sh_open != 1 || !buf || !cols || c->sh_line != 0 || c->sh_L == 0) return EKF_EINVAL;
     double* b = const_cast<double*>(buf);   // (read only by SH_DIAG)
-    if (!c->sh_diag) {
-        SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_DIAG, b), c->cfg.precision, c->stream));
-        c->sh_diag = 1;
-    }
-    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_GUESS, b), c->cfg.precision, c->stream));
+    ekf::ShardParams pg = shard_params(c, ekf::SH_GUESS, b);
+    pg.diag_first = !c->sh_diag;   // (SH_DIAG fused into the guesses' launch)
+    c->sh_diag = 1;
+    SH_TRY(ekf::launch_shard(pg, c->cfg.precision, c->stream));
     if (c->spec == 2)   // test hook (EKF_OPT_SPECULATE = 2): every line guesses landmark 0
         SH_TRY(hipMemsetAsync(c->sh_ctl + ekf::SC_GUESS, 0, sizeof(int) * c->d.max_lines, c->stream));
     SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_SPEC_COLS, b, cols), c->cfg.precision, c->stream));
@@ -1646,6 +1648,12 @@ extern "C" int ekf_shard_run(ekf_ctx* c, const double* cols, double* next_line)
         return EKF_EINVAL;
     ekf::ShardParams p = shard_params(c, ekf::SH_GATE, nullptr, const_cast<double*>(cols));
     p.next_out = next_line;
+    // the run's workgroups exchange through the association kernel's mailbox (unused by a
+    // partitioned context: ⌈N/64⌉ ≥ shard_run_workgroups(N) slots per parity)
+    p.mbox = c->mbox;
+    p.mbw = c->mbw;
+    p.epoch = ++c->scan_epoch;
+    p.spin_log2 = c->spin_log2;
     SH_TRY(ekf::launch_shard_run(p, c->cfg.precision, c->stream));
     c->sh_line = -1;   // until ekf_shard_resume
     return EKF_OK;

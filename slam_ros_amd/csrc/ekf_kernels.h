@@ -182,11 +182,29 @@ struct ShardParams {
     const ekf_line* lines;// [max_lines]
     const int* pexp;
     int reset_margin;
+    double enc_v[3];      // SH_BEGIN: the scan's encoder pose and lines (kernel arguments; it stores
+    ekf_line lines_v[EKF_MAX_LINES];   // them to enc / lines for the later phases)
+    int diag_first;       // SH_GUESS: take the summed diagonal blocks first (SH_DIAG in the same launch)
+    double* mbox;         // shard_run_kernel: the workgroups' mailbox (2 parities × G slots of mbw words)
+    int mbw;
+    unsigned epoch;       // its tag epoch (one per launch)
+    int spin_log2;        // its bounded waits
 };
 hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st);
-// lines [ctl[SC_NEXT], L) of the speculative path in one workgroup (shard_run_kernel)
+// lines [ctl[SC_NEXT], L) of the speculative path on shard_run_workgroups(N) cooperating
+// workgroups (shard_run_kernel)
 hipError_t launch_shard_run(const ShardParams& p, int precision, hipStream_t st);
-constexpr int SHR_THREADS = 1024;  // shard_run_kernel's workgroup (1024: 0.385 vs 0.41 ms per scan at 512, 28 VGPRs spilled)
+constexpr int SH_THREADS = 64;     // shard_kernel's workgroup
+#ifndef EKF_SHR_THREADS
+#define EKF_SHR_THREADS 128
+#endif
+constexpr int SHR_THREADS = EKF_SHR_THREADS;   // shard_run_kernel's workgroup: landmarks per workgroup
+constexpr int SHR_GMAX = 64;       // ... and at most this many workgroups (more landmarks per thread past it)
+inline int shard_run_workgroups(int N)
+{
+    const int g = (N + SHR_THREADS - 1) / SHR_THREADS;
+    return g < 1 ? 1 : (g > SHR_GMAX ? SHR_GMAX : g);
+}
 
 // One pass over the landmark block applying nsteps steps in order (each: reset, or rank-2m
 // downdate then its augmented rows). Pout may equal Pin (in place).

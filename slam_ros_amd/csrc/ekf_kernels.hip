@@ -3424,8 +3424,14 @@ __device__ __forceinline__ void shard_step(const ShardParams& p, const int phase
 #pragma unroll
         for (int a = 0; a < 9; a++) R33[a] = p.Rs[(a / 3) * n + (a % 3)];
         double F3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-        shard_predict(p.pose, p.enc, p.enc_noise, F3, R33, xp);
+        shard_predict(p.pose, p.enc_v, p.enc_noise, F3, R33, xp);
         if (j == 0) {
+            // the scan's inputs, handed over as kernel arguments (no host staging copy), for the
+            // later phases
+            double* enc = const_cast<double*>(p.enc);
+            enc[0] = p.enc_v[0]; enc[1] = p.enc_v[1]; enc[2] = p.enc_v[2];
+            ekf_line* lines = const_cast<ekf_line*>(p.lines);
+            for (int i = 0; i < d.max_lines; i++) lines[i] = p.lines_v[i];
 #pragma unroll
             for (int a = 0; a < 9; a++) p.rob[a] = R33[a];
             p.rob[9] = xp[0]; p.rob[10] = xp[1]; p.rob[11] = xp[2];
@@ -3458,10 +3464,12 @@ __device__ __forceinline__ void shard_step(const ShardParams& p, const int phase
         return;
     }
     if (!own) return;
-    if (phase == SH_DIAG) {   // the summed diagonal blocks (every rank contributed its own)
+    if (phase == SH_DIAG || (phase == SH_GUESS && p.diag_first)) {
+        // the summed diagonal blocks (every rank contributed its own); the guesses may follow in
+        // the same launch (this thread's landmark only)
         const double4 dj = *reinterpret_cast<const double4*>(p.col + 4 * (size_t)j);
         rc[8] = dj.x; rc[9] = dj.y; rc[10] = dj.z; rc[11] = dj.w;
-        return;
+        if (phase == SH_DIAG) return;
     }
     const int s = ctl[SC_S];
     double2 rr0 = make_double2(rc[0], rc[1]), rr1 = make_double2(rc[2], rc[3]), rr2 = make_double2(rc[4], rc[5]);
@@ -3733,12 +3741,12 @@ __device__ __forceinline__ void shard_step(const ShardParams& p, const int phase
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
+__global__ __launch_bounds__(SH_THREADS) void shard_kernel(ShardParams p)
 {
     __shared__ int4 sh_ctl[PMAX];
-    if ((int)threadIdx.x < p.npend) {
-        const int* r = p.pend[threadIdx.x].res;
-        sh_ctl[threadIdx.x] = make_int4(r[RES_RESET], r[RES_KSTEPS], r[RES_NADD], r[RES_SAVED_IN]);
+    for (int q = threadIdx.x; q < p.npend; q += blockDim.x) {
+        const int* r = p.pend[q].res;
+        sh_ctl[q] = make_int4(r[RES_RESET], r[RES_KSTEPS], r[RES_NADD], r[RES_SAVED_IN]);
     }
     __syncthreads();
     const Dims d = p.d;
@@ -3760,22 +3768,33 @@ __global__ __launch_bounds__(256) void shard_kernel(ShardParams p)
     shard_step<T>(p, p.phase, p.line, (int)(blockIdx.x * blockDim.x + threadIdx.x), pv);
 }
 
-// The speculative path's lines (ekf_shard_run): one workgroup runs lines 0 .. L − 1 of
+// The speculative path's lines (ekf_shard_run): G cooperating workgroups run lines 0 .. L − 1 of
 // the sequential association exactly as the per-line phases do (gate of every landmark, the
 // winner's package, gain rows, robot update), taking each winner's column from the exchanged
-// guessed columns (p.cols) instead of a per-line exchange. A line whose first passing landmark is
-// not its guess stops the run there (*next_out = that line): the caller continues with the
-// per-line phases from the state after the lines before it. Every rank holds the same replicated
-// state, so every rank stops at the same line.
+// guessed columns (p.cols) instead of a per-line exchange between ranks. Landmark j belongs to
+// thread j mod SHR_THREADS of workgroup ⌊j / SHR_THREADS⌋ mod G for the whole run (its records,
+// U/V history and flags are only ever touched by that thread). Every workgroup holds its own
+// copy of the control words, the robot block and the package in LDS and updates them itself
+// (SH_ROBOT: the same bits in every workgroup). Per line one exchange among the workgroups, the
+// scan kernel's sequential-path mailbox: each publishes its first passing landmark and, when it has
+// one, that landmark's package (built before the exchange), then polls every workgroup's tag; all
+// take the smallest landmark and its package, the reference's first passing one
+// (Robot.cpp:313-498). A line whose winner is not its guess stops the run there (*next_out = that
+// line; L + 1 when a workgroup's exchange timed out: the scan is abandoned): the caller continues
+// with the per-line phases from the state after the lines before it. Every rank holds the same
+// replicated state, so every rank stops at the same line.
 template <typename T>
 __global__ __launch_bounds__(SHR_THREADS) void shard_run_kernel(ShardParams p)
 {
     __shared__ int sh_cw[SC_WORDS];
     __shared__ double sh_rob[12];
     __shared__ double sh_pkg[MB_WORDS_FIXED + 4 * EKF_MAX_LINES];
-    const int tid = threadIdx.x;
+    __shared__ int sh_best[SHR_GMAX];
+    __shared__ int sh_to;
+    const int tid = threadIdx.x, g = blockIdx.x, G = gridDim.x;
     for (int k = tid; k < SC_WORDS; k += SHR_THREADS) sh_cw[k] = p.ctl[k];
     if (tid < 12) sh_rob[tid] = p.rob[tid];
+    if (tid == 0) sh_to = 0;
     __syncthreads();
     ShardParams q = p;
     q.ctl = sh_cw;
@@ -3783,29 +3802,62 @@ __global__ __launch_bounds__(SHR_THREADS) void shard_run_kernel(ShardParams p)
     q.pkg = sh_pkg;
     PllView<T> pv = {};   // (unused by the per-line phases)
     const int N = p.d.N;
-    int i = 0;
+    const int stride = G * SHR_THREADS;
+    int status = 0, i = 0;
     for (; i < p.L; i++) {
-        for (int j = tid; j < N; j += SHR_THREADS) shard_step<T>(q, SH_GATE, i, j, pv);
+        for (int j = g * SHR_THREADS + tid; j < N; j += stride) shard_step<T>(q, SH_GATE, i, j, pv);
         __syncthreads();
-        const int w = sh_cw[SC_WIN];
-        if (w != 0x7fffffff && w != sh_cw[SC_GUESS + i]) break;   // (uniform)
-        if (w != 0x7fffffff) {
-            if (tid == w % SHR_THREADS) shard_step<T>(q, SH_PACKAGE, i, w, pv);
-            q.col = p.cols + 4 * (size_t)i * N;
-            __syncthreads();
+        const int lw = sh_cw[SC_WIN];   // this workgroup's first passing landmark
+        const int m = sh_cw[SC_M];
+        if (lw != 0x7fffffff && lw % SHR_THREADS == tid) shard_step<T>(q, SH_PACKAGE, i, lw, pv);
+        __syncthreads();
+        // to the mailbox (parity i & 1: a workgroup one line ahead never overwrites a slot that
+        // another still reads), drained and ordered by the barrier before the tagged word
+        double* slot = p.mbox + ((size_t)(i & 1) * G + g) * p.mbw;
+        const int npk = MB_VH + 4 * m;
+        if (lw != 0x7fffffff)
+            for (int k = 1 + tid; k < npk; k += SHR_THREADS) mb_store(slot + k, sh_pkg[k]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) mb_tag(slot, p.epoch, (unsigned)(i + 1), (unsigned)(lw == 0x7fffffff ? 0 : lw + 1));
+        for (int k = tid; k < G; k += SHR_THREADS) {
+            const int bq = mb_poll(p.mbox, i & 1, G, k, p.mbw, p.epoch, (unsigned)(i + 1), status, p.spin_log2);
+            if (bq < 0) sh_to = 1;
+            sh_best[k] = bq <= 0 ? 0x7fffffff : bq - 1;
         }
-        for (int j = tid; j < N; j += SHR_THREADS) shard_step<T>(q, SH_APPLY, i, j, pv);
+        __syncthreads();
+        if (sh_to) break;   // (uniform in the workgroup)
+        int w = 0x7fffffff, gw = 0;
+        for (int k = 0; k < G; k++)
+            if (sh_best[k] < w) {
+                w = sh_best[k];
+                gw = k;
+            }
+        if (w != 0x7fffffff && w != sh_cw[SC_GUESS + i]) break;   // (uniform)
+        if (w != 0x7fffffff && gw != g) {
+            const double* ws = p.mbox + ((size_t)(i & 1) * G + gw) * p.mbw;
+            for (int k = 1 + tid; k < npk; k += SHR_THREADS) sh_pkg[k] = mb_load(ws + k);
+        }
+        if (tid == 0) sh_cw[SC_WIN] = w;
+        q.col = p.cols + 4 * (size_t)i * N;
+        __syncthreads();
+        for (int j = g * SHR_THREADS + tid; j < N; j += stride) shard_step<T>(q, SH_APPLY, i, j, pv);
         __syncthreads();
         if (tid == 0) shard_step<T>(q, SH_ROBOT, i, 0, pv);
         __syncthreads();
     }
-    if (tid == 0) {
+    if (g == 0 && tid == 0) {
         sh_cw[SC_NEXT] = i;
-        *p.next_out = (double)i;
+        *p.next_out = sh_to ? (double)(p.L + 1) : (double)i;
     }
     __syncthreads();
-    for (int k = tid; k < SC_WORDS; k += SHR_THREADS) p.ctl[k] = sh_cw[k];
-    if (tid < 12) p.rob[tid] = sh_rob[tid];
+    // the status bits of every workgroup's landmarks (each copy started from the same word)
+    if (tid == 0) atomicOr(p.ctl + SC_STATUS, sh_cw[SC_STATUS] | (sh_to ? (int)EKF_ST_TIMEOUT_BIT : 0));
+    if (g == 0) {
+        for (int k = tid; k < SC_WORDS; k += SHR_THREADS)
+            if (k != SC_STATUS) p.ctl[k] = sh_cw[k];
+        if (tid < 12) p.rob[tid] = sh_rob[tid];
+    }
 }
 
 #pragma clang fp contract(fast)
@@ -5774,17 +5826,19 @@ size_t scan_lds_bytes(int precision)
 #if !defined(EKF_TU) || EKF_TU == 3
 hipError_t launch_shard_run(const ShardParams& p, int precision, hipStream_t st)
 {
-    if (precision == EKF_PREC_F64) hipLaunchKernelGGL(shard_run_kernel<double>, dim3(1), dim3(SHR_THREADS), 0, st, p);
-    else if (precision == EKF_PREC_F32) hipLaunchKernelGGL(shard_run_kernel<float>, dim3(1), dim3(SHR_THREADS), 0, st, p);
+    const unsigned G = (unsigned)shard_run_workgroups(p.d.N);
+    if (precision == EKF_PREC_F64) hipLaunchKernelGGL(shard_run_kernel<double>, dim3(G), dim3(SHR_THREADS), 0, st, p);
+    else if (precision == EKF_PREC_F32) hipLaunchKernelGGL(shard_run_kernel<float>, dim3(G), dim3(SHR_THREADS), 0, st, p);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
 hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st)
 {
-    const unsigned grid = (unsigned)((p.d.N + 255) / 256);   // every landmark
-    if (precision == EKF_PREC_F64) hipLaunchKernelGGL(shard_kernel<double>, dim3(grid), dim3(256), 0, st, p);
-    else if (precision == EKF_PREC_F32) hipLaunchKernelGGL(shard_kernel<float>, dim3(grid), dim3(256), 0, st, p);
+    // every landmark, one per thread, spread over ⌈N/64⌉ CUs
+    const unsigned grid = (unsigned)((p.d.N + SH_THREADS - 1) / SH_THREADS);
+    if (precision == EKF_PREC_F64) hipLaunchKernelGGL(shard_kernel<double>, dim3(grid), dim3(SH_THREADS), 0, st, p);
+    else if (precision == EKF_PREC_F32) hipLaunchKernelGGL(shard_kernel<float>, dim3(grid), dim3(SH_THREADS), 0, st, p);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }

@@ -63,10 +63,16 @@ class ShardedInstance:
         self.speculate = speculate
         self.swords = int(self.lib.ekf_shard_spec_buffer_words(self.h))
         with torch.cuda.stream(self.stream):
-            # + one word: the number of ranks whose phase failed, summed with every exchange
+            # + one word: the number of ranks whose phase failed, summed with every exchange. The
+            # flag words stay zero while no phase fails (a sum of zeros), so they are written only
+            # after a failure (self._dirty). The agreement pair [failure flag, stopping line] is the
+            # columns' flag word and the word after it: the columns' sum leaves their flag in place
+            # and ekf_shard_run writes its stopping line next to it, with no copy in between.
             self.buf = torch.zeros(self.words + 1, dtype=torch.float64, device=dev)
-            self.cols = torch.zeros(self.swords + 1, dtype=torch.float64, device=dev)
-            self.agree = torch.zeros(2, dtype=torch.float64, device=dev)
+            self._cols = torch.zeros(self.swords + 2, dtype=torch.float64, device=dev)
+            self.cols = self._cols[: self.swords + 1]
+            self.agree = self._cols[self.swords:]
+        self._dirty = False
         self.spec_runs = []   # per scan: the line the speculative run stopped at (L: all lines)
         self.host_coll = dist.get_backend(group) != "nccl"
         r0, r1 = ctypes.c_int32(), ctypes.c_int32()
@@ -83,7 +89,9 @@ class ShardedInstance:
     def _sum(self, failed: bool, buf=None):
         """The exchange (on self.stream), carrying this rank's failure flag in the last word."""
         buf = self.buf if buf is None else buf
-        buf[-1].fill_(1.0 if failed else 0.0)
+        if failed:
+            buf[-1].fill_(1.0)
+            self._dirty = True
         if self.host_coll:
             t = buf.cpu()
             dist.all_reduce(t, group=self.group)
@@ -104,14 +112,18 @@ class ShardedInstance:
         # scan (ekf_shard_abort) and raise.
         err = None
         with torch.cuda.stream(self.stream):
+            if self._dirty:   # (a failed scan left nonzero flag words)
+                self.buf[-1].fill_(0.0)
+                self.agree.fill_(0.0)
+                self._dirty = False
             rc = lib.ekf_shard_begin(h, E._dp(enc), ln.ctypes.data_as(ctypes.c_void_p), L, bp)
             err = err or (rc and (rc, "ekf_shard_begin"))
             self._sum(bool(err))
             first, abandon = 0, False
             if self.speculate and L > 0:
-                # one exchange of every guessed column, then the lines in one workgroup up to the
-                # first wrong guess (ekf_shard_run, synchronous; the replicated state makes every
-                # rank stop at the same line). A small agreement exchange (max of the failure flag
+                # one exchange of every guessed column, then the lines on cooperating workgroups up
+                # to the first wrong guess (ekf_shard_run, stream-ordered; the replicated state
+                # makes every rank stop at the same line). A small agreement exchange (max of the failure flag
                 # and of the stopping line) keeps the ranks' exchange sequences equal even when
                 # one rank's run fails.
                 cp_ = ctypes.c_void_p(self.cols.data_ptr())
@@ -119,15 +131,15 @@ class ShardedInstance:
                     rc = lib.ekf_shard_speculate(h, bp, cp_)
                     err = rc and (rc, "ekf_shard_speculate")
                 self._sum(bool(err), self.cols)
-                # stream-ordered: the run writes its stopping line into agree[1]; agree[0] carries
-                # the failure flag of the columns' exchange; one host read after the agreement
-                self.agree[0:1].copy_(self.cols[-1:])
-                self.agree[1].fill_(float(L))
+                # stream-ordered: the run writes its stopping line into agree[1]; agree[0] is the
+                # columns' summed failure flag; one host read after the agreement
                 if not err:
                     rc = lib.ekf_shard_run(h, cp_, ctypes.c_void_p(self.agree.data_ptr() + 8))
                     err = rc and (rc, "ekf_shard_run")
                 if err:
                     self.agree[0].fill_(1.0)
+                    self.agree[1].fill_(float(L))
+                    self._dirty = True
                 if self.host_coll:
                     t = self.agree.cpu()
                     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
@@ -135,7 +147,8 @@ class ShardedInstance:
                 else:
                     dist.all_reduce(self.agree, op=dist.ReduceOp.MAX, group=self.group)
                 ag = self.agree.cpu()
-                abandon = bool(ag[0] > 0)
+                # (a stopping line past L: the run's workgroups timed out on some rank)
+                abandon = bool(ag[0] > 0) or int(ag[1]) > L
                 first = L if abandon else int(ag[1])
                 if not abandon:
                     rc = lib.ekf_shard_resume(h, first)
@@ -149,10 +162,16 @@ class ShardedInstance:
                 if not err:
                     rc = lib.ekf_shard_apply(h, i, bp)
                     err = rc and (rc, "ekf_shard_apply")
-            failed = float(self.buf[self.words].item())   # (synchronises the stream once per scan)
+            if first < L or not (self.speculate and L > 0):
+                # the last exchange was a per-line (or begin's) sum: its flag word
+                failed = float(self.buf[self.words].item())
+            else:
+                # every line on the speculative run: the agreement carried every failure flag
+                failed = float(ag[0]) if ag[0] > 0 else 0.0
         if abandon and failed == 0:
             failed = 1.0
         if failed > 0:
+            self._dirty = True
             lib.ekf_shard_abort(h)
             rc, what = err if err else (0, "a peer rank's phase")
             raise E.EkfError(f"{what} failed on {int(failed)} of {self.world} ranks (rc {rc}); scan abandoned")
