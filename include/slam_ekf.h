@@ -340,6 +340,18 @@ int ekf_shard_abort(ekf_ctx* ctx);
  *   ekf_shard_end(out)
  * Bit-identical to the per-line protocol; every rank stops at the same line (replicated state).
  * EKF_OPT_SPECULATE = 2 (test hook) makes every line guess landmark 0. */
+/* The same scan as one call, with the exchanges on the library's own RCCL communicator (RCCL is
+ * loaded on first use; EKF_EDEVICE if it is not available): rank 0 gets an id with
+ * ekf_rccl_unique_id, the host hands it to every rank, and each attaches with its (rank, world)
+ * of ekf_shard_create. ekf_shard_localize then runs begin, SUM, speculate, SUM, run, MAX, resume /
+ * the per-line phases and end on the context's stream, with two host reads (the agreement pair
+ * and the results), and is bit-identical to the sequence above (Robot::localize,
+ * Robot.cpp:126-904). A phase failing on any rank, or a run whose workgroups timed out, abandons
+ * the scan on every rank alike (the error, or EKF_EDEVICE on the ranks where nothing failed);
+ * a failed collective returns EKF_EDEVICE. */
+int ekf_rccl_unique_id(unsigned char out[128]);
+int ekf_shard_attach_rccl(ekf_ctx* ctx, const unsigned char id[128], int rank, int world);
+int ekf_shard_localize(ekf_ctx* ctx, const double enc[3], const ekf_line* lines, int nlines, ekf_result* out);
 size_t ekf_shard_spec_buffer_words(const ekf_ctx* ctx);
 int ekf_shard_speculate(ekf_ctx* ctx, const double* buf, double* cols);
 int ekf_shard_run(ekf_ctx* ctx, const double* cols, double* next_line);

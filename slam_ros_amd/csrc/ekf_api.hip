@@ -21,9 +21,13 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <new>
 #include <vector>
+
+#include <rccl/rccl.h>   // (types only: the library loads RCCL on first use, ekf_rccl_unique_id)
 
 #include "../../include/slam_ekf.h"
 #include "ekf_kernels.h"
@@ -85,6 +89,11 @@ struct ekf_ctx {
     double* d_enc;
     ekf_line* d_lines;
     int* d_nlines;
+    void* rccl_comm;          // ekf_shard_attach_rccl: the partitioned instance's own communicator
+    double* sh_xbuf;          // ... and ekf_shard_localize's exchange buffers (device): [N][4] + flag,
+    double* sh_xcols;         // [L][N][4] + flag + stopping line
+    double* h_agree;          // pinned: the agreement pair and a flag word
+    int sh_dirty;             // a failed scan left nonzero flag words
     int* h_res;
     double* h_pose;
     int dd_grid;
@@ -188,7 +197,7 @@ static void free_all(ekf_ctx* c)
                                c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->wt24, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->pexp, c->sink, c->mbox,
                                c->sync, c->Ust, c->Vst, c->dense, c->psig, c->pvmax,
                                c->sh_rob, c->sh_rec, c->sh_hist, c->sh_pkg, c->sh_flags, c->sh_ctl,
-                               c->sh_null.res};
+                               c->sh_null.res, c->sh_xbuf, c->sh_xcols};
     ptrs.push_back(c->ops_u);
     ptrs.push_back(c->ops_v);
     ptrs.push_back(c->ops_b);
@@ -199,6 +208,7 @@ static void free_all(ekf_ctx* c)
     }
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (c->h_agree) (void)hipHostFree(c->h_agree);
     if (c->h_res) (void)hipHostFree(c->h_res);
     if (c->h_pose) (void)hipHostFree(c->h_pose);
     for (auto& v : c->ev)
@@ -688,11 +698,14 @@ fail:
     return rc;
 }
 
+static void rccl_destroy(ekf_ctx* c);
+
 extern "C" int ekf_destroy(ekf_ctx* c)
 {
     if (!c) return EKF_EINVAL;
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->dstream);
+    rccl_destroy(c);
     free_all(c);
     delete c;
     return EKF_OK;
@@ -1689,6 +1702,162 @@ extern "C" int ekf_shard_abort(ekf_ctx* c)
     c->sh_open = 0;
     HIP_TRY(hipStreamSynchronize(c->stream));
     return EKF_OK;
+}
+
+// The partitioned instance's scan as one call (ekf_shard_localize): the protocol above with the
+// exchanges on the library's own RCCL communicator (ekf_shard_attach_rccl), so a C++ host (the
+// drop-in Robot over ranks) needs no collective library of its own and a scan costs one call, two
+// host reads (the agreement pair, then the results) and no host staging. RCCL is loaded on first
+// use (dlopen): the library itself does not depend on it.
+namespace {
+struct RcclApi {
+    ncclResult_t (*get_unique_id)(ncclUniqueId*);
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int);
+    ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+    ncclResult_t (*comm_destroy)(ncclComm_t);
+    const char* (*error_string)(ncclResult_t);
+};
+const RcclApi* rccl_api()
+{
+    static RcclApi api;
+    static int state = 0;   // 0 not tried, 1 loaded, -1 unavailable (one thread: the context's)
+    if (state == 0) {
+        state = -1;
+        void* h = nullptr;
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+            if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+        if (h) {
+            api.get_unique_id = (decltype(api.get_unique_id))dlsym(h, "ncclGetUniqueId");
+            api.comm_init_rank = (decltype(api.comm_init_rank))dlsym(h, "ncclCommInitRank");
+            api.all_reduce = (decltype(api.all_reduce))dlsym(h, "ncclAllReduce");
+            api.comm_destroy = (decltype(api.comm_destroy))dlsym(h, "ncclCommDestroy");
+            api.error_string = (decltype(api.error_string))dlsym(h, "ncclGetErrorString");
+            if (api.get_unique_id && api.comm_init_rank && api.all_reduce && api.comm_destroy && api.error_string)
+                state = 1;
+        }
+        if (state != 1) fprintf(stderr, "slam_ekf: RCCL (librccl.so) not available\n");
+    }
+    return state == 1 ? &api : nullptr;
+}
+}  // namespace
+
+static void rccl_destroy(ekf_ctx* c)
+{
+    const RcclApi* r = c->rccl_comm ? rccl_api() : nullptr;
+    if (r) (void)r->comm_destroy((ncclComm_t)c->rccl_comm);
+    c->rccl_comm = nullptr;
+}
+
+extern "C" int ekf_rccl_unique_id(unsigned char out[128])
+{
+    const RcclApi* r = rccl_api();
+    if (!out) return EKF_EINVAL;
+    if (!r) return EKF_EDEVICE;
+    ncclUniqueId id;
+    if (r->get_unique_id(&id) != ncclSuccess) return EKF_EDEVICE;
+    static_assert(sizeof(id) == 128, "ncclUniqueId");
+    memcpy(out, &id, sizeof(id));
+    return EKF_OK;
+}
+
+extern "C" int ekf_shard_attach_rccl(ekf_ctx* c, const unsigned char id[128], int rank, int world)
+{
+    if (!c || c->sh_world <= 0 || !id || rank != c->sh_rank || world != c->sh_world || c->sh_open) return EKF_EINVAL;
+    const RcclApi* r = rccl_api();
+    if (!r) return EKF_EDEVICE;
+    HIP_TRY(hipSetDevice(c->device));
+    rccl_destroy(c);
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof(uid));
+    ncclComm_t comm;
+    const ncclResult_t e = r->comm_init_rank(&comm, world, uid, rank);
+    if (e != ncclSuccess) {
+        fprintf(stderr, "slam_ekf: ncclCommInitRank: %s\n", r->error_string(e));
+        return EKF_EDEVICE;
+    }
+    c->rccl_comm = comm;
+    const size_t words = 4 * (size_t)c->d.N, swords = words * (size_t)c->d.max_lines;
+    if (!c->sh_xbuf) {
+        HIP_TRY(hipMalloc((void**)&c->sh_xbuf, sizeof(double) * (words + 1)));
+        HIP_TRY(hipMalloc((void**)&c->sh_xcols, sizeof(double) * (swords + 2)));
+        HIP_TRY(hipHostMalloc((void**)&c->h_agree, sizeof(double) * 4));
+        HIP_TRY(hipMemset(c->sh_xbuf, 0, sizeof(double) * (words + 1)));
+        HIP_TRY(hipMemset(c->sh_xcols, 0, sizeof(double) * (swords + 2)));
+    }
+    c->sh_dirty = 0;
+    return EKF_OK;
+}
+
+extern "C" int ekf_shard_localize(ekf_ctx* c, const double enc[3], const ekf_line* lines, int nlines, ekf_result* out)
+{
+    if (!c || c->sh_world <= 0 || !c->rccl_comm || !enc || (nlines > 0 && !lines) || c->sh_open) return EKF_EINVAL;
+    if (nlines < 0 || nlines > c->d.max_lines) return EKF_ERANGE;
+    const RcclApi* r = rccl_api();
+    const int L = nlines;
+    const size_t words = 4 * (size_t)c->d.N, swords = words * (size_t)c->d.max_lines;
+    double* buf = c->sh_xbuf;
+    double* cols = c->sh_xcols;
+    double* agree = cols + swords;   // [failure flag (the columns' flag word), stopping line]
+    ncclComm_t comm = (ncclComm_t)c->rccl_comm;
+    auto sum = [&](double* b, size_t n, ncclRedOp_t op) {
+        return r->all_reduce(b, b, n, ncclFloat64, op, comm, c->stream) == ncclSuccess;
+    };
+    // a phase that fails on one rank must not leave the others waiting in an exchange: every rank
+    // runs the whole exchange sequence, a failed one without further phases, and the summed flag
+    // words tell every rank alike whether to abandon the scan
+    static const double one_l[2] = {1.0, 0.0};
+    auto flag = [&](double* w) {
+        c->sh_dirty = 1;
+        return hipMemcpyAsync(w, one_l, sizeof(double), hipMemcpyHostToDevice, c->stream) == hipSuccess;
+    };
+    if (c->sh_dirty) {
+        HIP_TRY(hipMemsetAsync(buf + words, 0, sizeof(double), c->stream));
+        HIP_TRY(hipMemsetAsync(agree, 0, 2 * sizeof(double), c->stream));
+        c->sh_dirty = 0;
+    }
+    int err = ekf_shard_begin(c, enc, lines, L, buf);
+    if (err && !flag(buf + words)) return EKF_EDEVICE;
+    if (!sum(buf, words + 1, ncclSum)) return EKF_EDEVICE;
+    int first = 0;
+    bool abandon = false, spec_all = false;
+    if (c->spec && L > 0) {
+        if (!err) err = ekf_shard_speculate(c, buf, cols);
+        if (err && !flag(agree)) return EKF_EDEVICE;
+        if (!sum(cols, swords + 1, ncclSum)) return EKF_EDEVICE;
+        if (!err) err = ekf_shard_run(c, cols, agree + 1);
+        if (err) {
+            const double v[2] = {1.0, (double)L};
+            HIP_TRY(hipMemcpyAsync(agree, v, sizeof(v), hipMemcpyHostToDevice, c->stream));
+            c->sh_dirty = 1;
+        }
+        if (!sum(agree, 2, ncclMax)) return EKF_EDEVICE;
+        HIP_TRY(hipMemcpyAsync(c->h_agree, agree, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        abandon = c->h_agree[0] > 0.0 || c->h_agree[1] > (double)L;   // (past L: a run timed out)
+        first = abandon ? L : (int)c->h_agree[1];
+        if (!abandon && !err) err = ekf_shard_resume(c, first);
+        spec_all = first == L;
+    }
+    for (int i = first; i < L; i++) {
+        if (!err) err = ekf_shard_line(c, i, buf);
+        if (err && !flag(buf + words)) return EKF_EDEVICE;
+        if (!sum(buf, words + 1, ncclSum)) return EKF_EDEVICE;
+        if (!err) err = ekf_shard_apply(c, i, buf);
+    }
+    double failed;
+    if (spec_all) {
+        failed = c->h_agree[0];   // (the agreement carried every failure flag)
+    } else {
+        HIP_TRY(hipMemcpyAsync(c->h_agree + 2, buf + words, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        failed = c->h_agree[2];
+    }
+    if (abandon || failed > 0.0 || err) {
+        c->sh_dirty = 1;
+        (void)ekf_shard_abort(c);
+        return err ? err : EKF_EDEVICE;   // (a peer's phase failed, or the run's exchange timed out)
+    }
+    return ekf_shard_end(c, out);
 }
 
 extern "C" int ekf_profile_enable(ekf_ctx* c, int enable)

@@ -3464,17 +3464,24 @@ __device__ __forceinline__ void shard_step(const ShardParams& p, const int phase
         return;
     }
     if (!own) return;
-    if (phase == SH_DIAG || (phase == SH_GUESS && p.diag_first)) {
+    const bool fused_diag = phase == SH_GUESS && p.diag_first;
+    double4 dj = make_double4(0, 0, 0, 0);
+    if (phase == SH_DIAG || fused_diag) {
         // the summed diagonal blocks (every rank contributed its own); the guesses may follow in
-        // the same launch (this thread's landmark only)
-        const double4 dj = *reinterpret_cast<const double4*>(p.col + 4 * (size_t)j);
-        rc[8] = dj.x; rc[9] = dj.y; rc[10] = dj.z; rc[11] = dj.w;
+        // the same launch, which reads them from the sum (its grid row 0 stores them)
+        dj = *reinterpret_cast<const double4*>(p.col + 4 * (size_t)j);
+        if (phase == SH_DIAG || line == 0) {
+            rc[8] = dj.x; rc[9] = dj.y; rc[10] = dj.z; rc[11] = dj.w;
+        }
         if (phase == SH_DIAG) return;
     }
     const int s = ctl[SC_S];
     double2 rr0 = make_double2(rc[0], rc[1]), rr1 = make_double2(rc[2], rc[3]), rr2 = make_double2(rc[4], rc[5]);
     double2 yb = make_double2(rc[6], rc[7]);
     double Dj[4] = {rc[8], rc[9], rc[10], rc[11]};
+    if (fused_diag) {
+        Dj[0] = dj.x; Dj[1] = dj.y; Dj[2] = dj.z; Dj[3] = dj.w;
+    }
     const double ma0 = rc[12], s0j = rc[13], c0j = rc[14];
     const double s0f = rc[15], c0f = rc[16];
     int fl = p.flags[j];
@@ -3502,20 +3509,19 @@ __device__ __forceinline__ void shard_step(const ShardParams& p, const int phase
         // every line's first passing landmark at the scan's start (no line applied yet): the
         // speculative path fetches these columns in one exchange; shard_run_kernel checks each
         // line's real winner against its guess
+        // (one line per grid row)
         if (!(j < s)) return;
-        for (int i = 0; i < p.L; i++) {
-            ln = p.lines[i];
-            line_R(ln, i, p.r_mode, Rm);
-            Cand c;
-            bool pass, sing, amb;
-            gate_of(c, pass, sing, amb);
-            if (pass) atomicMin(ctl + SC_GUESS + i, j);
-        }
+        Cand c;
+        bool pass, sing, amb;
+        gate_of(c, pass, sing, amb);
+        if (pass) atomicMin(ctl + SC_GUESS + line, j);
         return;
     }
     if (phase == SH_SPEC_COLS) {
-        // the rank's blocks of every guessed column, pending steps applied (SH_COLUMN's blocks)
-        for (int i = 0; i < p.L; i++) {
+        // the rank's blocks of the guessed column of line `line` (one line per grid row), pending
+        // steps applied (SH_COLUMN's blocks)
+        {
+            const int i = line;
             const int w = ctl[SC_GUESS + i];
             double blk[4] = {0, 0, 0, 0};
             if (w != 0x7fffffff && local_blk(j, w)) pll_block(pv, 2 * j, 2 * w, blk);
@@ -3765,7 +3771,9 @@ __global__ __launch_bounds__(SH_THREADS) void shard_kernel(ShardParams p)
     pv.pend = p.pend;
     pv.ctl = sh_ctl;
     pv.rnd = 1;
-    shard_step<T>(p, p.phase, p.line, (int)(blockIdx.x * blockDim.x + threadIdx.x), pv);
+    // (SH_GUESS, SH_SPEC_COLS: grid row y = the line)
+    shard_step<T>(p, p.phase, (p.phase == SH_SPEC_COLS || p.phase == SH_GUESS) ? (int)blockIdx.y : p.line,
+                  (int)(blockIdx.x * blockDim.x + threadIdx.x), pv);
 }
 
 // The speculative path's lines (ekf_shard_run): G cooperating workgroups run lines 0 .. L − 1 of
@@ -5836,9 +5844,11 @@ hipError_t launch_shard_run(const ShardParams& p, int precision, hipStream_t st)
 hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st)
 {
     // every landmark, one per thread, spread over ⌈N/64⌉ CUs
-    const unsigned grid = (unsigned)((p.d.N + SH_THREADS - 1) / SH_THREADS);
-    if (precision == EKF_PREC_F64) hipLaunchKernelGGL(shard_kernel<double>, dim3(grid), dim3(SH_THREADS), 0, st, p);
-    else if (precision == EKF_PREC_F32) hipLaunchKernelGGL(shard_kernel<float>, dim3(grid), dim3(SH_THREADS), 0, st, p);
+    // (the guesses and the guessed columns: one grid row per line)
+    const bool per_line = p.phase == SH_SPEC_COLS || p.phase == SH_GUESS;
+    const dim3 grid((unsigned)((p.d.N + SH_THREADS - 1) / SH_THREADS), per_line ? (unsigned)max(p.L, 1) : 1u);
+    if (precision == EKF_PREC_F64) hipLaunchKernelGGL(shard_kernel<double>, grid, dim3(SH_THREADS), 0, st, p);
+    else if (precision == EKF_PREC_F32) hipLaunchKernelGGL(shard_kernel<float>, grid, dim3(SH_THREADS), 0, st, p);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }

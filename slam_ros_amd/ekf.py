@@ -48,6 +48,7 @@ EXPORTED = [
     "ekf_shard_create", "ekf_shard_tiles", "ekf_shard_buffer_words", "ekf_shard_begin", "ekf_shard_line",
     "ekf_shard_apply", "ekf_shard_end", "ekf_shard_abort", "ekf_shard_spec_buffer_words",
     "ekf_shard_speculate", "ekf_shard_run", "ekf_shard_resume",
+    "ekf_rccl_unique_id", "ekf_shard_attach_rccl", "ekf_shard_localize",
 ]
 
 
@@ -143,6 +144,9 @@ def load_library(path: str = ""):
         "ekf_shard_spec_buffer_words": (sz, [vp]),
         "ekf_shard_speculate": (ctypes.c_int, [vp, vp, vp]),
         "ekf_shard_run": (ctypes.c_int, [vp, vp, vp]),
+        "ekf_rccl_unique_id": (ctypes.c_int, [vp]),
+        "ekf_shard_attach_rccl": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int]),
+        "ekf_shard_localize": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, vp]),
         "ekf_shard_resume": (ctypes.c_int, [vp, ctypes.c_int]),
     }
     for name, (res, args) in sig.items():

@@ -40,7 +40,7 @@ class ShardedInstance:
 
     def __init__(self, capacity: int, precision: int = E.PREC_F32, max_lines: int = 8,
                  flush_interval: int = 4, r_mode: int = E.R_INTENDED, group=None, device: int | None = None,
-                 speculate: bool = True, options: dict | None = None):
+                 speculate: bool = True, options: dict | None = None, native: bool = False):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -79,6 +79,20 @@ class ShardedInstance:
         E._check(self.lib.ekf_shard_tiles(self.h, ctypes.byref(r0), ctypes.byref(r1)), "ekf_shard_tiles")
         self.tile_rows = (r0.value, r1.value)
         self._res = (E.EkfResult * 1)()
+        # native: the whole scan in one library call (ekf_shard_localize) on the library's own RCCL
+        # communicator; rank 0's id reaches the others through the process group (host objects)
+        self.native = native
+        if native:
+            if not speculate:
+                E._check(self.lib.ekf_set_option(self.h, E.OPT_SPECULATE, 0), "ekf_set_option")
+            uid = (ctypes.c_ubyte * 128)()
+            if self.rank == 0:
+                E._check(self.lib.ekf_rccl_unique_id(uid), "ekf_rccl_unique_id")
+            box = [bytes(uid)]
+            dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                       group=group)
+            uid = (ctypes.c_ubyte * 128).from_buffer_copy(box[0])
+            E._check(self.lib.ekf_shard_attach_rccl(self.h, uid, self.rank, self.world), "ekf_shard_attach_rccl")
 
     def init_lowrank(self, diag, U, y, saved, pose):
         self.ens.init_lowrank(0, diag, U, y, saved, pose)
@@ -105,6 +119,10 @@ class ShardedInstance:
         ln = np.ascontiguousarray(np.asarray(lines, dtype=np.float64).reshape(-1, LINE_FIELDS))
         L = ln.shape[0]
         enc = np.ascontiguousarray(np.asarray(enc, dtype=np.float64).reshape(3))
+        if self.native:
+            E._check(lib.ekf_shard_localize(h, enc.ctypes.data_as(ctypes.c_void_p), ln.ctypes.data_as(ctypes.c_void_p),
+                                            L, ctypes.byref(self._res)), "ekf_shard_localize")
+            return self._finish()
         bp = ctypes.c_void_p(self.buf.data_ptr())
         # A phase that fails on one rank must not leave the others waiting in an exchange: every
         # rank runs the whole exchange sequence, a failed one without further library calls, and
@@ -176,6 +194,9 @@ class ShardedInstance:
             rc, what = err if err else (0, "a peer rank's phase")
             raise E.EkfError(f"{what} failed on {int(failed)} of {self.world} ranks (rc {rc}); scan abandoned")
         E._check(lib.ekf_shard_end(h, ctypes.byref(self._res)), "ekf_shard_end")
+        return self._finish()
+
+    def _finish(self) -> list[int]:
         r = self._res[0]
         self.last = dict(matches=r.matches, new_landmarks=r.new_landmarks, saved=r.saved, reset=r.reset,
                          status=r.status, pose=np.array(r.pose[:]))

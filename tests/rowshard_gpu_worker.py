@@ -27,6 +27,7 @@ ap.add_argument("--backend", default="gloo")
 ap.add_argument("--per-line", action="store_true", help="the per-line protocol only (no speculative run)")
 ap.add_argument("--dup-every", type=int, default=0, help="line 1 repeats line 0 every k scans")
 ap.add_argument("--wrong-guess", action="store_true", help="EKF_OPT_SPECULATE = 2: every line guesses landmark 0")
+ap.add_argument("--native", action="store_true", help="the whole scan in one library call on its own RCCL communicator")
 args = ap.parse_args()
 
 dist.init_process_group(args.backend)
@@ -35,7 +36,7 @@ torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) if args.backend == 
 w = G.make_world(args.N, active=args.active or args.N - 10)
 st = G.initial_state(w)
 inst = R.ShardedInstance(args.N, args.precision, max_lines=8, flush_interval=args.T, speculate=not args.per_line,
-                         options={"speculate": 2} if args.wrong_guess else None)
+                         options={"speculate": 2} if args.wrong_guess else None, native=args.native)
 inst.init_lowrank(st.diag, st.U, st.y, st.saved, st.pose)
 matches, times = [], []
 rng = np.random.default_rng(11)

@@ -47,11 +47,15 @@ def test_two_rank_shard_equals_single_context(ekf_mod, oracle_mod, tmp_path, pre
 
 @pytest.mark.parametrize("prec,N,T,scans,active,extra_every,dup,mode",
                          [(1, 1024, 4, 9, 1000, 3, 3, "spec"), (0, 512, 4, 6, 0, 0, 0, "wrong"),
-                          (1, 1024, 4, 9, 1000, 3, 0, "perline")])
+                          (1, 1024, 4, 9, 1000, 3, 0, "perline"),
+                          (1, 1024, 4, 9, 1000, 3, 3, "native"), (0, 480, 4, 7, 400, 2, 3, "native-wrong"),
+                          (1, 512, 4, 6, 0, 0, 2, "native-perline"), (1, 4096, 4, 6, 0, 0, 0, "native")])
 def test_rccl_device_sum_world1(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_every, dup, mode):
     """The nccl (RCCL) backend's path: the exchange buffers all-reduced in place on the device, on
     the context's stream, with no host staging. One GPU holds one RCCL rank, so this runs a world of
-    one (the partition is the whole block); the two-rank protocol itself is covered over gloo."""
+    one (the partition is the whole block); the two-rank protocol itself is covered over gloo.
+    native*: the whole scan as one library call (ekf_shard_localize) on the library's own RCCL
+    communicator (ekf_shard_attach_rccl), every protocol variant."""
     run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_every, world=1, backend="nccl",
                 dup=dup, mode=mode)
 
@@ -98,7 +102,8 @@ def run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_
            os.path.join(ROOT, "tests", "rowshard_gpu_worker.py"), "--out", str(tmp_path), "--N", str(N),
            "--T", str(T), "--scans", str(scans), "--precision", str(prec), "--active", str(active),
            "--extra-every", str(extra_every), "--backend", backend, "--dup-every", str(dup)] + \
-        {"spec": [], "wrong": ["--wrong-guess"], "perline": ["--per-line"]}[mode]
+        {"spec": [], "wrong": ["--wrong-guess"], "perline": ["--per-line"], "native": ["--native"],
+         "native-wrong": ["--native", "--wrong-guess"], "native-perline": ["--native", "--per-line"]}[mode]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-3000:]
     Psum = np.zeros_like(P)
@@ -118,8 +123,8 @@ def run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_
             assert int(d["block_bytes"]) <= (0.55 if N >= 1000 else 0.65) * block_bytes, (r, int(d["block_bytes"]), block_bytes)
         times = d["times"]
         spec_runs = [int(x) for x in d["spec_runs"]]
-    if mode == "perline":
-        assert spec_runs == []
+    if mode == "perline" or mode.startswith("native"):
+        assert spec_runs == []   # (the native call does not report its stopping lines)
     else:
         assert len(spec_runs) == scans
         if mode == "wrong":   # guesses of landmark 0: the runs stop early
