@@ -1065,6 +1065,8 @@ static int stage_inputs(ekf_ctx* c, const double* enc, const ekf_line* lines, co
     return EKF_OK;
 }
 
+static void fill_results(const ekf_ctx* c, ekf_result* out);
+
 extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
 {
     if (!c) return EKF_EINVAL;
@@ -1092,7 +1094,15 @@ extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
                                       c->scan_epoch);
             c->h_res[(size_t)e * ekf::RES_STRIDE + ekf::RES_STATUS] |= st & ekf::DONE_STATUS_MASK;
         }
-    if (!out) return EKF_OK;
+    fill_results(c, out);
+    return EKF_OK;
+}
+
+// ekf_result of every instance from the host copies of the last step's records and poses
+static void fill_results(const ekf_ctx* c, ekf_result* out)
+{
+    const int E = c->cfg.instances;
+    if (!out) return;
     for (int e = 0; e < E; e++) {
         const int* r = c->h_res + (size_t)e * ekf::RES_STRIDE;
         ekf_result& o = out[e];
@@ -1109,7 +1119,6 @@ extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
         for (int i = 0; i < EKF_MAX_LINES; i++)
             o.match[i] = (i < o.nlines) ? r[ekf::RES_MATCH + i] : -1;
     }
-    return EKF_OK;
 }
 
 extern "C" int ekf_localize(ekf_ctx* c, const double* enc, const ekf_line* lines,
@@ -1682,8 +1691,18 @@ extern "C" int ekf_shard_resume(ekf_ctx* c, int line)
 extern "C" int ekf_shard_end(ekf_ctx* c, ekf_result* out)
 {
     if (!c || c->sh_open != 1 || c->sh_line != c->sh_L) return EKF_EINVAL;
-    // (with no line, begin's exchange is not consumed: the end needs no diagonal block)
-    SH_TRY(ekf::launch_shard(shard_params(c, ekf::SH_END, nullptr), c->cfg.precision, c->stream));
+    // (with no line, begin's exchange is not consumed: the end needs no diagonal block). The
+    // phase also writes the step's record and pose into the pinned host buffers (one instance),
+    // so the result needs no copy: only the wait for this kernel, not for a flush behind it
+    ekf::ShardParams p = shard_params(c, ekf::SH_END, nullptr);
+    int* rh = nullptr;
+    double* ph = nullptr;
+    HIP_TRY(hipHostGetDevicePointer((void**)&rh, c->h_res, 0));
+    HIP_TRY(hipHostGetDevicePointer((void**)&ph, c->h_pose, 0));
+    p.res_host = rh;
+    p.pose_host = ph;
+    SH_TRY(ekf::launch_shard(p, c->cfg.precision, c->stream));
+    HIP_TRY(hipEventRecord(c->ev_scan, c->stream));
     c->sh_open = 0;
     // the step joins the deferred flush of the rank's tiles
     c->nsteps++;
@@ -1691,7 +1710,9 @@ extern "C" int ekf_shard_end(ekf_ctx* c, ekf_result* out)
         const int rc = enqueue_flush(c);
         if (rc) return rc;
     }
-    return ekf_read_results(c, out);
+    HIP_TRY(hipEventSynchronize(c->ev_scan));
+    fill_results(c, out);
+    return EKF_OK;
 }
 
 extern "C" int ekf_shard_abort(ekf_ctx* c)

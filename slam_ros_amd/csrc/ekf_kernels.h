@@ -30,6 +30,8 @@ enum { SYNC_START = 0, SYNC_WG0 = 4 };
 constexpr int MAX_GROUPS = (MAX_CAPACITY + SCAN_THREADS - 1) / SCAN_THREADS;   // workgroups per instance
 constexpr int SPEC_GMAX = 64;  // speculative association: workgroups per instance (<= one wave)
 constexpr int MB_WORDS_FIXED = 26; // mailbox words before the V-history (see ekf_kernels.hip)
+constexpr int SH_MAX_LINES = 8;     // a partitioned context's lines per scan (ekf_shard_create)
+constexpr int SH_PKG_WORDS = MB_WORDS_FIXED + 4 * SH_MAX_LINES;   // one gain package of its scan
 
 // per-instance result record in device memory (ints)
 enum {
@@ -185,6 +187,9 @@ struct ShardParams {
     double enc_v[3];      // SH_BEGIN: the scan's encoder pose and lines (kernel arguments; it stores
     ekf_line lines_v[EKF_MAX_LINES];   // them to enc / lines for the later phases)
     int diag_first;       // SH_GUESS: take the summed diagonal blocks first (SH_DIAG in the same launch)
+    double* pkg_slot;     // SH_GATE (shard_run_kernel): a passing landmark's package into this slot
+    int* res_host;        // SH_END: the step's record and pose also into pinned host memory (device
+    double* pose_host;    // pointers; nullptr: not)
     double* mbox;         // shard_run_kernel: the workgroups' mailbox (2 parities × G slots of mbw words)
     int mbw;
     unsigned epoch;       // its tag epoch (one per launch)

@@ -3555,7 +3555,21 @@ __device__ __forceinline__ void shard_step(const ShardParams& p, const int phase
         bool pass, sing, amb;
         gate_of(c, pass, sing, amb);
         p.flags[j] = (fl & 1) | (sing ? 2 : 0) | (amb ? 4 : 0);
-        if (pass) atomicMin(ctl + SC_WIN, j);
+        if (pass) {
+            atomicMin(ctl + SC_WIN, j);
+            if (p.pkg_slot) {   // (shard_run_kernel) SH_PACKAGE's package from this evaluation
+                double* slot = p.pkg_slot + (size_t)threadIdx.x * SH_PKG_WORDS;
+                build_package(c, R33, rr0, rr1, rr2, slot);
+                const int m = ctl[SC_M];
+                for (int q = 0; q < m; q++) {
+                    const double* h = p.hist + ((size_t)j * d.max_lines + q) * 8 + 4;
+                    slot[MB_VH + 4 * q + 0] = h[0];
+                    slot[MB_VH + 4 * q + 1] = h[1];
+                    slot[MB_VH + 4 * q + 2] = h[2];
+                    slot[MB_VH + 4 * q + 3] = h[3];
+                }
+            }
+        }
         return;
     }
 
@@ -3743,6 +3757,11 @@ __device__ __forceinline__ void shard_step(const ShardParams& p, const int phase
         for (int i = 0; i < p.L; i++) res[RES_MATCH + i] = ctl[SC_MATCH + i];
         for (int q = 0; q < nextra; q++) res[RES_EXTRA + q] = ctl[SC_EXTRA + q];
         p.saved[0] = reset ? 0 : s + nadd;
+        if (p.res_host) {   // (the host reads them after this kernel, without a copy)
+            for (int w = 0; w < RES_STRIDE; w++) p.res_host[w] = res[w];
+            p.pose_host[0] = pose[0]; p.pose_host[1] = pose[1]; p.pose_host[2] = pose[2];
+            __threadfence_system();
+        }
     }
 }
 
@@ -3799,6 +3818,7 @@ __global__ __launch_bounds__(SHR_THREADS) void shard_run_kernel(ShardParams p)
     __shared__ double sh_pkg[MB_WORDS_FIXED + 4 * EKF_MAX_LINES];
     __shared__ int sh_best[SHR_GMAX];
     __shared__ int sh_to;
+    __shared__ double sh_slot[SHR_THREADS][SH_PKG_WORDS];   // each thread's package of its passing landmark
     const int tid = threadIdx.x, g = blockIdx.x, G = gridDim.x;
     for (int k = tid; k < SC_WORDS; k += SHR_THREADS) sh_cw[k] = p.ctl[k];
     if (tid < 12) sh_rob[tid] = p.rob[tid];
@@ -3811,20 +3831,29 @@ __global__ __launch_bounds__(SHR_THREADS) void shard_run_kernel(ShardParams p)
     PllView<T> pv = {};   // (unused by the per-line phases)
     const int N = p.d.N;
     const int stride = G * SHR_THREADS;
+    // one landmark per thread: every passing landmark builds its package during the gate (the
+    // owner's slot is the package); otherwise the owner rebuilds it after the gate (SH_PACKAGE)
+    const bool fused = N <= stride;
+    q.pkg_slot = fused ? &sh_slot[0][0] : nullptr;   // (only SH_GATE reads it: its thread's row)
     int status = 0, i = 0;
     for (; i < p.L; i++) {
         for (int j = g * SHR_THREADS + tid; j < N; j += stride) shard_step<T>(q, SH_GATE, i, j, pv);
         __syncthreads();
         const int lw = sh_cw[SC_WIN];   // this workgroup's first passing landmark
         const int m = sh_cw[SC_M];
-        if (lw != 0x7fffffff && lw % SHR_THREADS == tid) shard_step<T>(q, SH_PACKAGE, i, lw, pv);
-        __syncthreads();
+        const double* lpk = sh_pkg;
+        if (fused) {
+            if (lw != 0x7fffffff) lpk = sh_slot[lw % SHR_THREADS];
+        } else {
+            if (lw != 0x7fffffff && lw % SHR_THREADS == tid) shard_step<T>(q, SH_PACKAGE, i, lw, pv);
+            __syncthreads();
+        }
         // to the mailbox (parity i & 1: a workgroup one line ahead never overwrites a slot that
         // another still reads), drained and ordered by the barrier before the tagged word
         double* slot = p.mbox + ((size_t)(i & 1) * G + g) * p.mbw;
         const int npk = MB_VH + 4 * m;
         if (lw != 0x7fffffff)
-            for (int k = 1 + tid; k < npk; k += SHR_THREADS) mb_store(slot + k, sh_pkg[k]);
+            for (int k = 1 + tid; k < npk; k += SHR_THREADS) mb_store(slot + k, lpk[k]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) mb_tag(slot, p.epoch, (unsigned)(i + 1), (unsigned)(lw == 0x7fffffff ? 0 : lw + 1));
@@ -3845,6 +3874,8 @@ __global__ __launch_bounds__(SHR_THREADS) void shard_run_kernel(ShardParams p)
         if (w != 0x7fffffff && gw != g) {
             const double* ws = p.mbox + ((size_t)(i & 1) * G + gw) * p.mbw;
             for (int k = 1 + tid; k < npk; k += SHR_THREADS) sh_pkg[k] = mb_load(ws + k);
+        } else if (w != 0x7fffffff && fused) {
+            for (int k = 1 + tid; k < npk; k += SHR_THREADS) sh_pkg[k] = lpk[k];
         }
         if (tid == 0) sh_cw[SC_WIN] = w;
         q.col = p.cols + 4 * (size_t)i * N;
