@@ -149,3 +149,51 @@ def run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_
                                             "tile_rows": [[int(a), int(b)] for a, b in rows],
                                             "block_bytes_single": int(block_bytes),
                                             "p_rel_err_vs_oracle": rp, "y_rel_err_vs_oracle": ry})
+
+
+def test_one_call_scan_in_process(ekf_mod, oracle_mod):
+    """ekf_shard_localize straight through the C-ABI, without torch.distributed: its argument
+    checks (no communicator attached: EKF_EINVAL; a rank or world other than the context's:
+    EKF_EINVAL; more lines than the context takes: EKF_ERANGE), then a world of one attached to
+    the library's own RCCL communicator, its scans against one context of the same library
+    (bit-identical state and associations) and the restatement (associations)."""
+    import ctypes
+    N, T, scans = 512, 4, 6
+    lib = ekf_mod.load_library()
+    w = G.make_world(N)
+    st = G.initial_state(w)
+    one = ekf_mod.Ensemble(N, 1, 1, max_lines=8, flush_interval=T)
+    sh = ekf_mod.Ensemble(N, 1, 1, max_lines=8, flush_interval=T, shard=(0, 1))
+    for ens in (one, sh):
+        ens.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
+    ref = oracle_mod.OracleRobot(N, mode=oracle_mod.FAST)
+    ref.set_state(*one.download_state(0))
+    res = (ekf_mod.EkfResult * 1)()
+    enc0 = np.zeros(3)
+    ln0 = np.zeros((8, 6))
+    dp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    assert lib.ekf_shard_localize(sh.handle, dp(enc0), dp(ln0), 1, ctypes.byref(res)) == 1   # no communicator
+    assert lib.ekf_shard_localize(one.handle, dp(enc0), dp(ln0), 1, ctypes.byref(res)) == 1  # not partitioned
+    uid = (ctypes.c_ubyte * 128)()
+    assert lib.ekf_rccl_unique_id(uid) == 0
+    assert lib.ekf_shard_attach_rccl(sh.handle, uid, 1, 1) == 1   # rank outside the context's world
+    assert lib.ekf_shard_attach_rccl(sh.handle, uid, 0, 2) == 1   # not the context's world
+    assert lib.ekf_shard_attach_rccl(sh.handle, uid, 0, 1) == 0
+    big = np.zeros((9, 6))
+    assert lib.ekf_shard_localize(sh.handle, dp(enc0), dp(big), 9, ctypes.byref(res)) == 4   # ERANGE
+    for step in range(1, scans + 1):
+        enc, lines, nl = G.make_scan(w, step, instances=1, lines=8)
+        ln = np.ascontiguousarray(lines[0, :nl[0]])
+        r1 = one.localize(enc, lines, nl)[0]
+        e = np.ascontiguousarray(enc[0])
+        assert lib.ekf_shard_localize(sh.handle, dp(e), dp(ln), len(ln), ctypes.byref(res)) == 0
+        m = list(res[0].match[: res[0].nlines])
+        assert m == list(r1["match"][: len(ln)]), step
+        assert ref.localize(ln, enc[0]) == m, step
+    P1, y1, s1, p1 = one.download_state(0)
+    P2, y2, s2, p2 = sh.download_state(0)
+    np.testing.assert_array_equal(P2, P1)
+    np.testing.assert_array_equal(y2, y1)
+    assert s1 == s2
+    one.close()
+    sh.close()
