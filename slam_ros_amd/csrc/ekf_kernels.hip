@@ -3757,8 +3757,17 @@ __device__ __forceinline__ void shard_step(const ShardParams& p, const int phase
         for (int i = 0; i < p.L; i++) res[RES_MATCH + i] = ctl[SC_MATCH + i];
         for (int q = 0; q < nextra; q++) res[RES_EXTRA + q] = ctl[SC_EXTRA + q];
         p.saved[0] = reset ? 0 : s + nadd;
-        if (p.res_host) {   // (the host reads them after this kernel, without a copy)
-            for (int w = 0; w < RES_STRIDE; w++) p.res_host[w] = res[w];
+        if (p.res_host) {
+            // the words ekf_result takes, for the host to read after this kernel without a copy
+            // (each store crosses to host memory: only these, not the whole record)
+            int* rh = p.res_host;
+            rh[RES_NLINES] = res[RES_NLINES];
+            rh[RES_STATUS] = res[RES_STATUS];
+            rh[RES_M] = res[RES_M];
+            rh[RES_NEXTRA] = res[RES_NEXTRA];
+            rh[RES_SAVED] = res[RES_SAVED];
+            rh[RES_RESET] = res[RES_RESET];
+            for (int i = 0; i < p.L; i++) rh[RES_MATCH + i] = res[RES_MATCH + i];
             p.pose_host[0] = pose[0]; p.pose_host[1] = pose[1]; p.pose_host[2] = pose[2];
             __threadfence_system();
         }
