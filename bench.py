@@ -117,7 +117,12 @@ def parse():
                          "--steps); its per-group error does not depend on the count")
     ap.add_argument("--traffic-json", default="",
                     help="HBM traffic file (default: the newest profiles/*/traffic.json)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.force_collective and not args.no_cpu:
+        # the parity leg replays the timed steps from the broadcast's receive groups, which the
+        # forced collective has already retired (it is a test of the RCCL branch, not a line)
+        ap.error("--force-collective needs --no-cpu")
+    return args
 
 
 def lib_sha(path):

@@ -26,7 +26,7 @@ for c in cfgs:
     if prec == ekf.PREC_F64:
         arith = ekf.ARITH_EXACT
     ens = ekf.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=arith,
-                       options={"scan_stamps": 1})
+                       options={"scan_stamps": 1, **({"scan_threads": int(os.environ["PROBE_NT"])} if os.environ.get("PROBE_NT") else {})})
     for e in range(E):
         ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
     base = ens.scan_stamps()

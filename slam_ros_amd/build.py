@@ -46,14 +46,14 @@ UNITS = [("ekf_kernels.hip", 4), ("ekf_kernels.hip", 2), ("ekf_kernels.hip", 1),
          ("ekf_api.hip", 0)]
 
 
-def _compile_link(out: str, defines: list[str], verbose: bool = False) -> None:
+def _compile_link(out: str, defines: list[str], verbose: bool = False, csrc: str = CSRC) -> None:
     objdir = out + ".objs"
     os.makedirs(objdir, exist_ok=True)
     procs, objs = [], []
     for src, tu in UNITS:
         obj = os.path.join(objdir, f"{os.path.splitext(src)[0]}_{tu}.o")
         cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, *[f"-D{d}" for d in defines],
-               *([f"-DEKF_TU={tu}"] if tu else []), "-c", os.path.join(CSRC, src), "-o", obj]
+               *([f"-DEKF_TU={tu}"] if tu else []), "-c", os.path.join(csrc, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append(subprocess.Popen(cmd))
@@ -67,9 +67,9 @@ def _compile_link(out: str, defines: list[str], verbose: bool = False) -> None:
     shutil.rmtree(objdir, ignore_errors=True)
 
 
-def build_variant(out: str, defines: list[str]) -> str:
-    """An A/B build of the same sources with extra -D flags (scripts only; SLAM_EKF_LIB)."""
-    _compile_link(out, defines)
+def build_variant(out: str, defines: list[str], csrc: str = CSRC) -> str:
+    """An A/B build with extra -D flags, or of a patched copy of csrc/ (scripts only; SLAM_EKF_LIB)."""
+    _compile_link(out, defines, csrc=csrc)
     return out
 
 

@@ -1085,8 +1085,10 @@ extern "C" int ekf_read_results(ekf_ctx* c, ekf_result* out)
     HIP_TRY(hipStreamSynchronize(c->stream));
     // every workgroup's completion word of the last association launch (commit_fold: a word of
     // another launch — a workgroup that never ran or never finished — reads as a timeout, not as
-    // the status bits an earlier launch left in it)
-    if (c->scan_epoch > 0)
+    // the status bits an earlier launch left in it). A partitioned context never launches the
+    // association kernel (scan_epoch counts its shard runs, which write no completion words): its
+    // status bits are already in the record SH_END wrote
+    if (c->scan_epoch > 0 && c->sh_world <= 0)
         for (int e = 0; e < E; e++) {
             int st = 0;
             for (int gq = 0; gq < c->last_G; gq++)
@@ -1798,12 +1800,25 @@ extern "C" int ekf_shard_attach_rccl(ekf_ctx* c, const unsigned char id[128], in
     }
     c->rccl_comm = comm;
     const size_t words = 4 * (size_t)c->d.N, swords = words * (size_t)c->d.max_lines;
-    if (!c->sh_xbuf) {
-        HIP_TRY(hipMalloc((void**)&c->sh_xbuf, sizeof(double) * (words + 1)));
-        HIP_TRY(hipMalloc((void**)&c->sh_xcols, sizeof(double) * (swords + 2)));
-        HIP_TRY(hipHostMalloc((void**)&c->h_agree, sizeof(double) * 4));
-        HIP_TRY(hipMemset(c->sh_xbuf, 0, sizeof(double) * (words + 1)));
-        HIP_TRY(hipMemset(c->sh_xcols, 0, sizeof(double) * (swords + 2)));
+    if (!c->sh_xbuf || !c->sh_xcols || !c->h_agree) {
+        // all three or none: a failure part way frees what was allocated, so a later attach
+        // allocates again instead of finding one pointer set and the others null
+        auto drop = [c]() {
+            if (c->sh_xbuf) (void)hipFree(c->sh_xbuf);
+            if (c->sh_xcols) (void)hipFree(c->sh_xcols);
+            if (c->h_agree) (void)hipHostFree(c->h_agree);
+            c->sh_xbuf = c->sh_xcols = c->h_agree = nullptr;
+        };
+        drop();
+        if (hipMalloc((void**)&c->sh_xbuf, sizeof(double) * (words + 1)) != hipSuccess ||
+            hipMalloc((void**)&c->sh_xcols, sizeof(double) * (swords + 2)) != hipSuccess ||
+            hipHostMalloc((void**)&c->h_agree, sizeof(double) * 4) != hipSuccess ||
+            hipMemset(c->sh_xbuf, 0, sizeof(double) * (words + 1)) != hipSuccess ||
+            hipMemset(c->sh_xcols, 0, sizeof(double) * (swords + 2)) != hipSuccess) {
+            drop();
+            rccl_destroy(c);
+            return EKF_EDEVICE;
+        }
     }
     c->sh_dirty = 0;
     return EKF_OK;
@@ -1856,6 +1871,7 @@ extern "C" int ekf_shard_localize(ekf_ctx* c, const double enc[3], const ekf_lin
         HIP_TRY(hipStreamSynchronize(c->stream));
         abandon = c->h_agree[0] > 0.0 || c->h_agree[1] > (double)L;   // (past L: a run timed out)
         first = abandon ? L : (int)c->h_agree[1];
+        // (host bookkeeping only, on the agreed line: it fails on every rank alike or on none)
         if (!abandon && !err) err = ekf_shard_resume(c, first);
         spec_all = first == L;
     }
@@ -1869,6 +1885,13 @@ extern "C" int ekf_shard_localize(ekf_ctx* c, const double enc[3], const ekf_lin
     if (spec_all) {
         failed = c->h_agree[0];   // (the agreement carried every failure flag)
     } else {
+        if (L > first) {
+            // the last line's apply ran after its exchange: one more word, the MAX over the ranks
+            // of the summed flags and of every rank's failure since, so that a rank whose apply
+            // failed does not abandon the scan alone while its peers commit it
+            if (err && !flag(buf + words)) return EKF_EDEVICE;
+            if (!sum(buf + words, 1, ncclMax)) return EKF_EDEVICE;
+        }
         HIP_TRY(hipMemcpyAsync(c->h_agree + 2, buf + words, sizeof(double), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         failed = c->h_agree[2];

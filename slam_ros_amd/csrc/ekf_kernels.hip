@@ -1089,6 +1089,22 @@ __device__ __forceinline__ void build_package(const Cand& c, const double R33[9]
 // `uq_of(q)` / `vq_of(q)` return the landmark's U rows and jstar's V rows of the scan's match q.
 // MAXQ > 0: at most MAXQ earlier matches (the speculative path). (Applying all MAXQ rows
 // branch-free on zeroed rows measured slower: DESIGN.md §10.)
+// One earlier match q's correction of a landmark's block of a later match's column (Robot.cpp:560-568
+// in order): blk −= U_q(own rows)·V_q(column rows)ᵀ, four independent fused chains. Every path that
+// corrects a block (gain_rows, all at once; the speculative landmark waves, one match at a time)
+// runs this sequence per element, so they agree bit for bit.
+__device__ __forceinline__ void correct_block(double blk[4], const double4& uq, const double4& vh)
+{
+    blk[0] = fma(-uq.x, vh.x, blk[0]);
+    blk[1] = fma(-uq.x, vh.z, blk[1]);
+    blk[2] = fma(-uq.z, vh.x, blk[2]);
+    blk[3] = fma(-uq.z, vh.z, blk[3]);
+    blk[0] = fma(-uq.y, vh.y, blk[0]);
+    blk[1] = fma(-uq.y, vh.w, blk[1]);
+    blk[2] = fma(-uq.w, vh.y, blk[2]);
+    blk[3] = fma(-uq.w, vh.w, blk[3]);
+}
+
 template <int MAXQ, typename UQ, typename VQ>
 __device__ __forceinline__ void gain_rows(const double* pk, int t, UQ uq_of, VQ vq_of, double blk[4],
                                           double2& rr0, double2& rr1, double2& rr2, double2& yb,
@@ -1098,14 +1114,7 @@ __device__ __forceinline__ void gain_rows(const double* pk, int t, UQ uq_of, VQ 
     // rows of match q + 1 loaded before match q's products (LDS latency off the chain). t is the
     // scan's match count, the same on every lane: a scalar loop
     auto correct = [&](const double4& uq, const double4& vh) __attribute__((always_inline)) {
-        blk[0] = fma(-uq.x, vh.x, blk[0]);
-        blk[1] = fma(-uq.x, vh.z, blk[1]);
-        blk[2] = fma(-uq.z, vh.x, blk[2]);
-        blk[3] = fma(-uq.z, vh.z, blk[3]);
-        blk[0] = fma(-uq.y, vh.y, blk[0]);
-        blk[1] = fma(-uq.y, vh.w, blk[1]);
-        blk[2] = fma(-uq.w, vh.y, blk[2]);
-        blk[3] = fma(-uq.w, vh.w, blk[3]);
+        correct_block(blk, uq, vh);
     };
     // matches in pairs (both pairs' rows loaded together: one LDS round trip per two matches),
     // then the odd one; the products in q order either way
@@ -1693,7 +1702,6 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
     __shared__ unsigned long long sh_listsb[SPEC_GMAX * SPEC_L];   // the B words (count > 4)
     __shared__ int sh_glist[SPEC_L][SPEC_K + 1];
     __shared__ int sh_spec[SPEC_L];
-    __shared__ int sh_addq[SPEC_L];   // per guessed winner: the latest pending step that added it, or -1
     __shared__ int sh_psg[PMAX];      // pending steps' plane exponents (EKF_ARITH_F16X3)
     __shared__ int sh_flag;
     __shared__ int sh_ready;
@@ -1701,6 +1709,13 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
     __shared__ int sh_vto;    // a verdict poll of this workgroup timed out
     __shared__ int sh_first[SPEC_L];   // per line the first guessed candidate (speculative path)
     if (tid < SPEC_L) sh_first[tid] = 0x7fffffff;
+    // the replay wave's line counter and status words: set before the first barrier below, since
+    // on the MFMA-replay path the landmark waves reach their polls with no barrier after the records
+    if (tid == 0) {
+        sh_ready = 0;
+        sh_rwst = 0;
+        sh_vto = 0;
+    }
     __shared__ double sh_wd[SPEC_L * SPEC_WD];
     __shared__ double4 sh_wh[SPEC_L][SPEC_L][2];
     __shared__ double sh_pk[SPEC_L][PKW];
@@ -1995,10 +2010,13 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
     // the scan's downdate of the owned 2×2 diagonal block, trace (Σ over matches and both rows of
     // −U·V ≥ 0): with the block after the scan it measures the update's cancellation (EKF_ST_PRECISION)
     double dsq = 0.0;
-    auto store_rows = [&](int t, const double kk[4], const double uu[4], bool vhist, const float F[3]) {
+    // uhist: keep the U rows for later corrections (the sequential path; the speculative landmark
+    // waves apply each match to the later blocks at once and keep only the last one, in registers)
+    auto store_rows = [&](int t, const double kk[4], const double uu[4], bool vhist, const float F[3], bool uhist) {
         nzr = nzr || kk[0] != 0.0 || kk[1] != 0.0 || kk[2] != 0.0 || kk[3] != 0.0 || uu[0] != 0.0 ||
               uu[1] != 0.0 || uu[2] != 0.0 || uu[3] != 0.0;
-        if (t < HIST_LDS)
+        if (!uhist) {
+        } else if (t < HIST_LDS)
             sh_uhist[t][tid] = make_double4(uu[0], uu[1], uu[2], uu[3]);
         else
             *reinterpret_cast<double4*>(Ust + ((size_t)t * n + b0) * 2) = make_double4(uu[0], uu[1], uu[2], uu[3]);
@@ -2251,13 +2269,16 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                 const int w = t < L ? sh_spec[t] : -1;
                 cols[t] = w >= 0 ? w : j;
             }
-            if (tid < SPEC_L) {   // (read after the records' barrier)
-                const int w = tid < L ? sh_spec[tid] : -1;
-                int qa = -1;
-                if (mf && aug_pend && w >= 0)
+            // per guessed winner t (lane t of every wave): the latest pending step that added it,
+            // or -1; read with __shfl, so that no wave waits for another's (the MFMA-replay path
+            // has no barrier between the records and the waves' replays)
+            int addq_l = -1;
+            if (mf && aug_pend) {
+                const int lt = tid & 63;
+                const int w = lt < L ? sh_spec[lt] : -1;
+                if (w >= 0)
                     for (int q = 0; q < p.npend; q++)
-                        if (w >= sh_ctl[q].w && w < sh_ctl[q].w + sh_ctl[q].z) qa = q;
-                sh_addq[tid] = qa;
+                        if (w >= sh_ctl[q].w && w < sh_ctl[q].w + sh_ctl[q].z) addq_l = q;
             }
             C srow[SPEC_L + 1][4];
             if ((staged || m64) && own) staged_blocks_load<T>(pv, j, cols, srow);
@@ -2320,12 +2341,19 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                     }
                 }
             }
-            if (tid == SCAN_BLOCK - 1) {
-                sh_ready = 0;
-                sh_rwst = 0;
-                sh_vto = 0;
-            }
-            __syncthreads();
+            // the guessed winners' addition steps of this lane's mutual block (the replay wave), and of
+            // every guessed column (the landmark waves): shuffles with the whole wave active
+            const int qs_pair = mf && aug_pend ? max(__shfl(addq_l, pu, 64), __shfl(addq_l, pt, 64)) : -1;
+            int addq_t[SPEC_L];
+#pragma unroll
+            for (int t = 0; t < SPEC_L; t++) addq_t[t] = mf && aug_pend ? __shfl(addq_l, t, 64) : -1;
+            // MFMA replay (mf): no barrier here. Each wave reads only what it wrote itself or what
+            // an earlier barrier published — the replay wave its winners' records (sh_wd), the
+            // landmark waves their owned rows' blocks — so the landmark waves replay the pending
+            // steps while the replay wave loads the records and replays the winners' mutual blocks,
+            // and its chain starts without waiting for them (the packages and the winners' V rows
+            // then reach the landmark waves through sh_ready, release / acquire)
+            if (!mf) __syncthreads();
             if (mf && tid >= SCAN_THREADS) {
               if constexpr (kPlanes) {
                 // the winners' mutual blocks: X minus the pending steps' ΔX of the 16 winner rows
@@ -2351,7 +2379,7 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                 if (lane_r < L * (L + 1) / 2 && sh_spec[pu] >= 0 && sh_spec[pt] >= 0) {
                     const bool swap = ((2 * sh_spec[pu]) >> 5) > ((2 * sh_spec[pt]) >> 5);
                     C xr[4] = {pacc[0], swap ? pacc[2] : pacc[1], swap ? pacc[1] : pacc[2], pacc[3]};
-                    const int qs = max(sh_addq[pu], sh_addq[pt]);   // (as for the landmark waves' blocks)
+                    const int qs = qs_pair;   // (as for the landmark waves' blocks)
                     if (qs >= 0) patch_block<T>(pv, p.pend[qs], sh_ctl[qs], 2 * sh_spec[pu], 2 * sh_spec[pt], false, xr);
                     double* r = sh_wd + pu * SPEC_WD + (pt == pu ? 6 : 14 + 4 * pt);
 #pragma unroll
@@ -2539,7 +2567,7 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                         for (int t = 0; t < SPEC_L; t++)
                             if (t < L && sh_spec[t] >= 0) {
                                 C b[4] = {srow[t][0], srow[t][1], srow[t][2], srow[t][3]};
-                                const int qs = max(qj, sh_addq[t]);
+                                const int qs = max(qj, addq_t[t]);
                                 if (qs >= 0) patch_block<T>(pv, p.pend[qs], sh_ctl[qs], 2 * j, 2 * sh_spec[t], false, b);
                                 const int c0 = 2 * t;
                                 sh_blk[t][tid] = make_float4(
@@ -2766,7 +2794,7 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                                 rr0 = g0; rr1 = g1; rr2 = g2; yb = gy;
                                 Dj[0] = gD[0]; Dj[1] = gD[1]; Dj[2] = gD[2]; Dj[3] = gD[3];
                                 const float F[3] = {(float)pk[PK_F], (float)pk[PK_F + 1], (float)pk[PK_F + 2]};
-                                store_rows(m, kk, uu, false, F);
+                                store_rows(m, kk, uu, false, F, true);
                             }
                         }
                         sub(18);
@@ -3024,7 +3052,7 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                          blk, rr0, rr1, rr2, yb, Dj, kk, uu);
             float F[3] = {0.f, 0.f, 0.f};
             if (sym) sym_factor(sh_pkg, F);
-            store_rows(m, kk, uu, true, F);
+            store_rows(m, kk, uu, true, F, true);
         }
         robot_update(R33, xp, sh_pkg);
         if (j == jstar) matched = true;
@@ -3827,11 +3855,12 @@ __global__ __launch_bounds__(SHR_THREADS) void shard_run_kernel(ShardParams p)
     __shared__ double sh_pkg[MB_WORDS_FIXED + 4 * EKF_MAX_LINES];
     __shared__ int sh_best[SHR_GMAX];
     __shared__ int sh_to;
+    __shared__ int sh_bad;   // workgroup 0: some workgroup timed out, never arrived or stopped elsewhere
     __shared__ double sh_slot[SHR_THREADS][SH_PKG_WORDS];   // each thread's package of its passing landmark
     const int tid = threadIdx.x, g = blockIdx.x, G = gridDim.x;
     for (int k = tid; k < SC_WORDS; k += SHR_THREADS) sh_cw[k] = p.ctl[k];
     if (tid < 12) sh_rob[tid] = p.rob[tid];
-    if (tid == 0) sh_to = 0;
+    if (tid == 0) sh_to = sh_bad = 0;
     __syncthreads();
     ShardParams q = p;
     q.ctl = sh_cw;
@@ -3894,9 +3923,27 @@ __global__ __launch_bounds__(SHR_THREADS) void shard_run_kernel(ShardParams p)
         if (tid == 0) shard_step<T>(q, SH_ROBOT, i, 0, pv);
         __syncthreads();
     }
-    if (g == 0 && tid == 0) {
-        sh_cw[SC_NEXT] = i;
-        *p.next_out = sh_to ? (double)(p.L + 1) : (double)i;
+    // every workgroup's outcome to workgroup 0: its stopping line and whether one of its exchanges
+    // timed out, one self-tagged word each (parity-0 slot, last word: the list words' region, which
+    // the association kernel of a partitioned context never uses). Workgroup 0 decides the stopping
+    // line over all G of them, so a workgroup that timed out — its landmarks then missed the line it
+    // broke at, possibly the last one, which workgroup 0 completed — or never arrived makes the run
+    // report L + 1, and the scan is abandoned on every rank
+    if (tid == 0)
+        mb_store_tagged(p.mbox + (size_t)g * p.mbw + p.mbw - 1, p.epoch,
+                        ((unsigned long long)i << 1) | (sh_to ? 1ull : 0ull));
+    if (g == 0) {
+        for (int k = tid; k < G; k += SHR_THREADS) {
+            int st = sh_to ? (int)EKF_ST_TIMEOUT_BIT : 0;   // (timed out already: no second wait)
+            const unsigned long long w =
+                mb_wait_tagged(p.mbox + (size_t)k * p.mbw + p.mbw - 1, p.epoch, st, p.spin_log2);
+            if (st || (w & 1ull) || (int)(w >> 1) != i) atomicOr(&sh_bad, 1);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            sh_cw[SC_NEXT] = i;
+            *p.next_out = (sh_to || sh_bad) ? (double)(p.L + 1) : (double)i;
+        }
     }
     __syncthreads();
     // the status bits of every workgroup's landmarks (each copy started from the same word)

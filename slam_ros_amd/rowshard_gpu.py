@@ -180,6 +180,20 @@ class ShardedInstance:
                 if not err:
                     rc = lib.ekf_shard_apply(h, i, bp)
                     err = rc and (rc, "ekf_shard_apply")
+            if first < L:
+                # the last line's apply ran after its exchange: one more word, the MAX over the ranks
+                # of the summed flags and of every rank's failure since, so that a rank whose apply
+                # failed does not abandon the scan alone while its peers commit it
+                fw = self.buf[self.words:self.words + 1]
+                if err:
+                    fw.fill_(1.0)
+                    self._dirty = True
+                if self.host_coll:
+                    t = fw.cpu()
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                    fw.copy_(t)
+                else:
+                    dist.all_reduce(fw, op=dist.ReduceOp.MAX, group=self.group)
             if first < L or not (self.speculate and L > 0):
                 # the last exchange was a per-line (or begin's) sum: its flag word
                 failed = float(self.buf[self.words].item())
