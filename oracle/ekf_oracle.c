@@ -40,6 +40,13 @@ struct oracle_robot {
     int status;
     double gate_margin; /* min |sqrt(|d²|) − MAHALANOBIS| over the candidates the last localize
                            evaluated (test instrumentation: SURVEY §8d's gate-margin rejection) */
+    /* Test instrumentation: where a stored state of relative precision pred_eta could not resolve
+     * this restatement's decisions (the conditions the GPU library reports as EKF_ST_PRECISION /
+     * EKF_ST_RANGE, computed here from the restatement's own fp64 state): ORACLE_PRED_* bits of
+     * the last localize. pred_eta = 0 disables it. */
+    double pred_eta;
+    double pred_cancel;  /* the cancellation ratio above which an update is predicted (16: 4 bits) */
+    int pred;
     double pose[3]; /* xPos, yPos, thetaPos */
     double* P;      /* P_t0, n*n */
     double* y;      /* y, n */
@@ -194,6 +201,9 @@ oracle_robot* oracle_create(int capacity, double x, double y, double theta, int 
     o->P[0 * n + 0] = 0.05;
     o->P[1 * n + 1] = 0.05;
     o->P[2 * n + 2] = 0.0;
+    o->pred_eta = 0.0;
+    o->pred_cancel = 16.0;
+    o->pred = 0;
     return o;
 }
 
@@ -210,6 +220,12 @@ int oracle_capacity(const oracle_robot* o) { return o->N; }
 int oracle_saved(const oracle_robot* o) { return o->saved; }
 int oracle_status(const oracle_robot* o) { return o->status; }
 double oracle_gate_margin(const oracle_robot* o) { return o->gate_margin; }
+void oracle_set_pred(oracle_robot* o, double eta, double cancel)
+{
+    o->pred_eta = eta;
+    o->pred_cancel = cancel;
+}
+int oracle_pred_flags(const oracle_robot* o) { return o->pred; }
 int oracle_threads(void)
 {
 #ifdef _OPENMP
@@ -332,6 +348,8 @@ int oracle_localize(oracle_robot* o, const oracle_line* lines, int L, const doub
     double* y = o->y;
     o->status = 0;
     o->gate_margin = INFINITY;
+    o->pred = 0;
+    const int s_in = o->saved;   /* the landmarks this scan can update (before any augmentation) */
 
     /* Robot.cpp:130-148 (SIMULATIONOFF branch; `rot` unused) */
     const double x_t0[3] = {o->pose[0], o->pose[1], o->pose[2]};
@@ -442,6 +460,20 @@ int oracle_localize(oracle_robot* o, const oracle_line* lines, int L, const doub
             oracle_dgemm(0, 0, 1, 1, 2, 1.0, vS, 2, z, 1, 0.0, &d2, 1);
 
             if (fabs(sqrt(fabs(d2)) - MAHALANOBIS) < o->gate_margin) o->gate_margin = fabs(sqrt(fabs(d2)) - MAHALANOBIS);
+            if (o->pred_eta > 0.0) {
+                /* The gate distance against a state within pred_eta of this one: |ΔS_ab| <=
+                 * eta·s_a·s_b with s_a = Σ_k |H_ak|·√P_kk over rows 0, 1, 2, l0, l1 (H0 = (0, 0, −1,
+                 * 1, 0), H1 = (h10, h11, 0, h1l, 1)), so to first order |Δd²| <= eta·(|w0|·s0 +
+                 * |w1|·s1)², w = S⁻¹v: a distance that close to the gate is not resolved (the
+                 * reference's own evaluation order: Robot.cpp:313-489, every candidate up to the
+                 * winner) */
+                const double* Pd = P_pre;
+                const double s0 = sqrt(fabs(Pd[(size_t)2 * n + 2])) + sqrt(fabs(Pd[(size_t)l0 * n + l0]));
+                const double s1 = fabs(h10) * sqrt(fabs(Pd[0])) + fabs(h11) * sqrt(fabs(Pd[(size_t)n + 1])) +
+                                  fabs(h1l) * sqrt(fabs(Pd[(size_t)l0 * n + l0])) + sqrt(fabs(Pd[(size_t)l1 * n + l1]));
+                const double wv = fabs(vS[0]) * s0 + fabs(vS[1]) * s1;
+                if (fabs(d2 - MAHALANOBIS * MAHALANOBIS) <= o->pred_eta * wv * wv) o->pred |= ORACLE_PRED_GATE;
+            }
             if (sqrt(fabs(d2)) > MAHALANOBIS) {                  /* Robot.cpp:489-498 */
                 if (j == s - 1) { extra[nextra++] = i; break; }
                 continue;
@@ -514,6 +546,18 @@ int oracle_localize(oracle_robot* o, const oracle_line* lines, int L, const doub
         o->pose[1] = y[1];
         o->pose[2] = oracle_normalize_radian(y[2]);
     }
+    int canc = 0;   /* (a scan that ends in the map reset updates no landmark it keeps) */
+    if (o->pred_eta > 0.0 && matchesNum > 0) {
+        /* An update that shrinks a landmark's variance trace by more than pred_cancel (more than
+         * log2 of it of the stored precision's bits cancel) or leaves it non-positive: P still
+         * holds the state before the scan (the landmark block is not predicted), P_pre after */
+        for (int j = 0; j < s_in; j++) {
+            const size_t a = (size_t)(3 + 2 * j), b = a + 1;
+            const double tb = P[a * n + a] + P[b * n + b];
+            const double ta = P_pre[a * n + a] + P_pre[b * n + b];
+            if (!(ta > 0.0) || tb > o->pred_cancel * ta) { canc = 1; break; }
+        }
+    }
     /* P_t0 ← P_pre (Robot.cpp:572 per match / :713 no match) */
     ORACLE_PAR_ROWS
     for (int r = 0; r < n; r++) memcpy(P + (size_t)r * n, P_pre + (size_t)r * n, sizeof(double) * (size_t)n);
@@ -538,6 +582,9 @@ int oracle_localize(oracle_robot* o, const oracle_line* lines, int L, const doub
         oracle_dgemm(0, 0, 2, 2, 2, 1.0, Gl, 2, R, 2, 0.0, GlR, 2);
         oracle_dgemm(0, 1, 2, 2, 2, 1.0, GlR, 2, Gl, 2, 0.0, GlRGl, 2);
         for (int q = 0; q < 4; q++) Pll[q] += GlRGl[q];
+        if (o->pred_eta > 0.0)   /* fp32 storage's range, with 2x of slack (the library's bound: 2^120) */
+            for (int q = 0; q < 4; q++)
+                if (!(fabs(Pll[q]) <= 0x1p119)) o->pred |= ORACLE_PRED_RANGE;
         const int l0 = 3 + 2 * s;
         P[(size_t)l0 * n + l0] = Pll[0];
         P[(size_t)l0 * n + l0 + 1] = Pll[1];
@@ -553,6 +600,7 @@ int oracle_localize(oracle_robot* o, const oracle_line* lines, int L, const doub
     }
 
     /* reset (Robot.cpp:893-904) */
+    if (canc && !(o->saved > N - 10)) o->pred |= ORACLE_PRED_CANCEL;
     if (o->saved > N - 10) {
         o->saved = 0;
         for (int i = 3; i < n; ++i) y[i] = 0;

@@ -63,6 +63,15 @@ int oracle_saved(const oracle_robot* o);
 int oracle_status(const oracle_robot* o);
 /* min |sqrt(|d²|) − 0.4| over the candidates the last localize evaluated (INFINITY: none) */
 double oracle_gate_margin(const oracle_robot* o);
+/* Test instrumentation (not in the reference): the decisions of the last localize that a stored
+ * state within relative precision eta of this one could not resolve — a gate distance within
+ * eta·(|w0|·s0 + |w1|·s1)² of the gate (ORACLE_PRED_GATE), an update that shrinks some landmark's
+ * variance trace by more than `cancel` or to <= 0 (ORACLE_PRED_CANCEL), a new landmark variance
+ * past 2^119 (ORACLE_PRED_RANGE). The GPU library reports the same conditions on its own state as
+ * EKF_ST_PRECISION / EKF_ST_RANGE; the tests check its flags against these. eta = 0: off. */
+enum { ORACLE_PRED_GATE = 1, ORACLE_PRED_CANCEL = 2, ORACLE_PRED_RANGE = 4 };
+void oracle_set_pred(oracle_robot* o, double eta, double cancel);
+int oracle_pred_flags(const oracle_robot* o);
 /* threads the O(n^2) loops run on: 1 in libekf_oracle.so, the OpenMP team in libekf_oracle_omp.so */
 int oracle_threads(void);   /* OR of GSL-like error codes seen in last call */
 void oracle_pose(const oracle_robot* o, double pose[3]);

@@ -23,6 +23,9 @@ FAITHFUL, FAST = 0, 1
 R_INTENDED, R_AS_WRITTEN = 0, 1
 
 
+PRED_GATE, PRED_CANCEL, PRED_RANGE = 1, 2, 4   # oracle_pred_flags bits (ekf_oracle.h)
+
+
 class OracleLine(ctypes.Structure):
     _fields_ = [("alpha", ctypes.c_double), ("r", ctypes.c_double), ("R", ctypes.c_double * 4)]
 
@@ -66,6 +69,9 @@ def lib(omp: bool = False):
         L.oracle_threads.argtypes = []
         L.oracle_gate_margin.restype = d
         L.oracle_gate_margin.argtypes = [vp]
+        L.oracle_set_pred.argtypes = [vp, d, d]
+        L.oracle_pred_flags.restype = i
+        L.oracle_pred_flags.argtypes = [vp]
         _libs[omp] = L
     return _libs[omp]
 
@@ -183,6 +189,16 @@ class OracleRobot:
     def gate_margin(self) -> float:
         """min |sqrt(|d²|) − 0.4| over the candidates the last localize evaluated."""
         return float(self._lib.oracle_gate_margin(self._h))
+
+    def set_prediction(self, eta: float, cancel: float = 16.0):
+        """Test instrumentation: predict, from this restatement's own fp64 state, the decisions a
+        stored state within relative precision eta cannot resolve (oracle_set_pred)."""
+        self._lib.oracle_set_pred(self._h, float(eta), float(cancel))
+
+    @property
+    def pred_flags(self) -> int:
+        """PRED_* bits of the last localize (0: every decision resolved at the set precision)."""
+        return int(self._lib.oracle_pred_flags(self._h))
 
     def set_state(self, P=None, y=None, saved: int = 0, pose=None):
         Pc = None if P is None else np.ascontiguousarray(P, dtype=np.float64)

@@ -201,3 +201,57 @@ def test_synthetic_scans_associate_to_truth(oracle_mod):
         enc, lines, _ = G.make_scan(w, step)
         pick = np.random.default_rng(7 + step).choice(w.active, size=8, replace=False)
         assert r.localize(lines[0], enc[0]) == list(pick)
+
+
+def test_precision_predictions(oracle_mod):
+    """The restatement's test instrumentation (oracle_set_pred): from its own fp64 state it names the
+    decisions a stored state of relative precision eta could not resolve — the conditions the
+    library reports as EKF_ST_PRECISION / EKF_ST_RANGE, checked against them in
+    tests/test_bench_config.py. Constructed cases for each bit, and none in the bench world."""
+    N = 30
+    w = G.make_world(N, active=10)
+    st = G.initial_state(w)
+    P0 = st.dense_P()
+    # bench world: every decision far from the gate, no large cancellation
+    r = oracle_mod.OracleRobot(N)
+    r.set_state(P0, st.y, st.saved, st.pose)
+    r.set_prediction(3 * 2.0 ** -16)
+    enc, lines, _ = G.make_scan(w, 1, lines=4)
+    r.localize(lines[0], enc[0])
+    assert r.pred_flags == 0
+    # cancellation: landmark 0's variance 1e-2 observed with R = 1e-8 → its trace shrinks ≈ 1e6-fold
+    P = P0.copy()
+    P[3, 3] = P[4, 4] = 1e-2
+    r.set_state(P, st.y, st.saved, st.pose)
+    z = np.array([[st.y[3], st.y[4], 1e-8, 0, 0, 1e-8]])
+    assert r.localize(z, [0.0, 0.0, 0.0]) == [0]
+    assert r.pred_flags & oracle_mod.PRED_CANCEL
+    # the same update at eta = 0: no prediction at all
+    r.set_prediction(0.0)
+    r.set_state(P, st.y, st.saved, st.pose)
+    r.localize(z, [0.0, 0.0, 0.0])
+    assert r.pred_flags == 0
+    # gate: a distance just inside the 0.4 gate (d² = 0.16 − 1e-9) is within any eta of it
+    r.set_prediction(2.0 ** -16)
+    r.set_state(P0, st.y, st.saved, st.pose)
+    Rv = 1e-4
+    S00 = P0[2, 2] - 2 * P0[2, 3] + P0[3, 3] + Rv   # innovation_cov's S[0] (Robot.cpp:397-405)
+    S = np.zeros((2, 2))
+    h10, h11 = -math.cos(st.y[3]), -math.sin(st.y[3])
+    H = np.zeros((2, P0.shape[0]))
+    H[0, 2], H[0, 3] = -1.0, 1.0
+    H[1, 0], H[1, 1], H[1, 3], H[1, 4] = h10, h11, 0.0, 1.0
+    S = H @ P0 @ H.T + np.diag([Rv, Rv])
+    # v = (v0, 0): d² = v0² (S⁻¹)_00
+    v0 = math.sqrt((0.16 - 1e-9) / np.linalg.inv(S)[0, 0])
+    h0 = oracle_mod.normalize_radian(st.y[3] - 0.0)
+    z = np.array([[h0 + v0, st.y[4], Rv, 0, 0, Rv]])
+    assert S00 > 0
+    r.localize(z, [0.0, 0.0, 0.0])
+    assert r.pred_flags & oracle_mod.PRED_GATE
+    # range: a new landmark (an empty map) whose variance passes fp32's range (R = 1e37)
+    r.set_prediction(2.0 ** -16)
+    r.set_state(P0, st.y, 0, st.pose)
+    far = np.array([[0.123, 55.0, 1e37, 0, 0, 1e37]])
+    assert r.localize(far, [0.0, 0.0, 0.0]) == [-1]
+    assert r.pred_flags & oracle_mod.PRED_RANGE
