@@ -526,6 +526,7 @@ struct Cand {
     double Si[4];
     double v[2];
     double h10, h11, h1l;
+    double w0, w1, d2;   // S⁻¹v and the distance (cand_amb)
     int pass;
     int singular;
     int amb;   // the decision is within the storage precision of the gate (gate_eta)
@@ -627,7 +628,11 @@ __device__ __forceinline__ void sincos_near(double ma, double ma0, double s0, do
     }
 }
 
-// Exact candidate evaluation in fp64 (Robot.cpp:367-489).
+__device__ __forceinline__ int cand_amb(const Block5& b, const Cand& c, double gate, double eta);
+
+// Exact candidate evaluation in fp64 (Robot.cpp:367-489). AMB = false leaves c.amb for cand_amb
+// (the replay wave evaluates it after it has published the line's package)
+template <bool AMB = true>
 __device__ __forceinline__ void eval_candidate(const Block5& b, double ma, double mr, double sn,
                                                double cs, const double xp[3], double za, double zr,
                                                const double Rm[4], double gate, double eta, Cand& c)
@@ -655,14 +660,22 @@ __device__ __forceinline__ void eval_candidate(const Block5& b, double ma, doubl
     if (a < g2 * (1.0 - 0x1p-40)) c.pass = 1;
     else if (a > g2 * (1.0 + 0x1p-40)) c.pass = 0;
     else c.pass = !(sqrt(a) > gate);
-    // the storage precision of the gate (gate_eta): |ΔS_ab| <= eta·s_a·s_b with s_a = Σ_k |H_ak|·√P_kk
-    // (H0 = (0, 0, −1, 1, 0), H1 = (h10, h11, 0, h1l, 1) on rows 0, 1, 2, a, b), so to first order
-    // |Δd²| <= eta·(|w0|·s0 + |w1|·s1)², w = S⁻¹v (the roots in fp32, 2^-8 of slack)
+    c.w0 = vs0;
+    c.w1 = vs1;
+    c.d2 = d2;
+    c.amb = AMB ? cand_amb(b, c, gate, eta) : 0;
+}
+
+// The storage precision of the gate (gate_eta): |ΔS_ab| <= eta·s_a·s_b with s_a = Σ_k |H_ak|·√P_kk
+// (H0 = (0, 0, −1, 1, 0), H1 = (h10, h11, 0, h1l, 1) on rows 0, 1, 2, a, b), so to first order
+// |Δd²| <= eta·(|w0|·s0 + |w1|·s1)², w = S⁻¹v (the roots in fp32, 2^-8 of slack)
+__device__ __forceinline__ int cand_amb(const Block5& b, const Cand& c, double gate, double eta)
+{
     auto rt = [](double x) { return (double)__builtin_amdgcn_sqrtf((float)fabs(x)); };
     const double s0 = rt(b.p22) + rt(b.daa);
     const double s1 = fabs(c.h10) * rt(b.p00) + fabs(c.h11) * rt(b.p11) + fabs(c.h1l) * rt(b.daa) + rt(b.dbb);
-    const double wv = fabs(vs0) * s0 + fabs(vs1) * s1;
-    c.amb = !c.singular && !(fabs(d2 - g2) > eta * (1.0 + 0x1p-8) * wv * wv);
+    const double wv = fabs(c.w0) * s0 + fabs(c.w1) * s1;
+    return !c.singular && !(fabs(c.d2 - gate * gate) > eta * (1.0 + 0x1p-8) * wv * wv);
 }
 
 // Certified rejection: true only if the exact evaluation is guaranteed to fail the gate. It
@@ -1039,10 +1052,10 @@ __device__ __forceinline__ void fill_block5(Block5& b5, const double R33[9], dou
 // gets the same products whichever orientation is stored (staged_blocks). The scan's own fp64
 // chain (gain_rows: W, K, y, the eager robot-strip and diagonal-block downdates, the corrections
 // of later lines) keeps K·S·Kᵀ; only the stored operands take this form.
-__device__ __forceinline__ void sym_factor(const double* pk, float F[3])
+__device__ __forceinline__ void sym_factor_S(const double S[4], float F[3])
 {
-    const float a = (float)pk[MB_S], b = 0.5f * ((float)pk[MB_S + 1] + (float)pk[MB_S + 2]);
-    const float c = (float)pk[MB_S + 3];
+    const float a = (float)S[0], b = 0.5f * ((float)S[1] + (float)S[2]);
+    const float c = (float)S[3];
     // v_rsq_f32 (1 ulp): F need not be correctly rounded, only the same on every thread
     F[0] = F[1] = F[2] = 0.f;
     if (a > 0.f) {
@@ -1054,6 +1067,12 @@ __device__ __forceinline__ void sym_factor(const double* pk, float F[3])
     } else {
         F[2] = c > 0.f ? c * __builtin_amdgcn_rsqf(c) : 0.f;
     }
+}
+
+__device__ __forceinline__ void sym_factor(const double* pk, float F[3])
+{
+    const double S[4] = {pk[MB_S], pk[MB_S + 1], pk[MB_S + 2], pk[MB_S + 3]};
+    sym_factor_S(S, F);
 }
 
 // The uniform gain package of a match from the matching landmark's state: S, S⁻¹, v, H row 1
@@ -1105,6 +1124,14 @@ __device__ __forceinline__ void correct_block(double blk[4], const double4& uq, 
     blk[3] = fma(-uq.w, vh.w, blk[3]);
 }
 
+// The package words the landmark rows of a match read (Robot.cpp:522-589): S, S⁻¹, v, H row 1 and
+// the robot rows of U = K·S
+struct PkCore {
+    double S[4], Si[4], v[2], h[3], Ur[6];
+};
+__device__ __forceinline__ void gain_core(const PkCore& P, const double blk[4], double2& rr0, double2& rr1,
+                                          double2& rr2, double2& yb, double Dj[4], double kk[4], double uu[4]);
+
 template <int MAXQ, typename UQ, typename VQ>
 __device__ __forceinline__ void gain_rows(const double* pk, int t, UQ uq_of, VQ vq_of, double blk[4],
                                           double2& rr0, double2& rr1, double2& rr2, double2& yb,
@@ -1128,10 +1155,31 @@ __device__ __forceinline__ void gain_rows(const double* pk, int t, UQ uq_of, VQ 
         correct(ub, vb);
     }
     if (q < tu) correct(uq_of(q), vq_of(q));
-    const double S0 = pk[MB_S], S1 = pk[MB_S + 1], S2 = pk[MB_S + 2], S3 = pk[MB_S + 3];
-    const double Si0 = pk[MB_SI], Si1 = pk[MB_SI + 1], Si2 = pk[MB_SI + 2], Si3 = pk[MB_SI + 3];
-    const double v0 = pk[MB_V], v1 = pk[MB_V + 1];
-    const double h10 = pk[MB_H], h11 = pk[MB_H + 1], h1l = pk[MB_H + 2];
+    PkCore P;
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        P.S[a] = pk[MB_S + a];
+        P.Si[a] = pk[MB_SI + a];
+    }
+    P.v[0] = pk[MB_V];
+    P.v[1] = pk[MB_V + 1];
+    P.h[0] = pk[MB_H];
+    P.h[1] = pk[MB_H + 1];
+    P.h[2] = pk[MB_H + 2];
+#pragma unroll
+    for (int a = 0; a < 6; a++) P.Ur[a] = pk[MB_UR + a];
+    gain_core(P, blk, rr0, rr1, rr2, yb, Dj, kk, uu);
+}
+
+// The gain rows from the corrected block (gain_rows without the earlier matches' corrections),
+// the package's words in registers: every path computes them with this one expression set
+__device__ __forceinline__ void gain_core(const PkCore& P, const double blk[4], double2& rr0, double2& rr1,
+                                          double2& rr2, double2& yb, double Dj[4], double kk[4], double uu[4])
+{
+    const double S0 = P.S[0], S1 = P.S[1], S2 = P.S[2], S3 = P.S[3];
+    const double Si0 = P.Si[0], Si1 = P.Si[1], Si2 = P.Si[2], Si3 = P.Si[3];
+    const double v0 = P.v[0], v1 = P.v[1];
+    const double h10 = P.h[0], h11 = P.h[1], h1l = P.h[2];
 #pragma unroll
     for (int pp = 0; pp < 2; pp++) {
         const double pb0 = pp ? rr0.y : rr0.x;
@@ -1149,9 +1197,7 @@ __device__ __forceinline__ void gain_rows(const double* pk, int t, UQ uq_of, VQ 
         const double dyv = k0 * v0 + k1 * v1;   // y += K·v (Robot.cpp:585-589)
         if (pp) yb.y += dyv; else yb.x += dyv;
     }
-    double Ur[6];
-#pragma unroll
-    for (int q = 0; q < 6; q++) Ur[q] = pk[MB_UR + q];
+    const double* Ur = P.Ur;
     // eager downdate of the robot-strip columns and the diagonal block (Robot.cpp:568)
     rr0.x -= Ur[0] * kk[0] + Ur[1] * kk[1];
     rr0.y -= Ur[0] * kk[2] + Ur[1] * kk[3];
@@ -1500,7 +1546,11 @@ typedef __bf16 bf16x8r __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8r __attribute__((ext_vector_type(8)));
 // F16 (EKF_ARITH_F16X3): two fp16 planes (hi, lo of 2^σ·V), three products (lo, hi), (hi, lo),
 // (hi, hi) on v_mfma_f32_16x16x32_f16; acc then holds 2^(2σ)·ΔX (the caller scales it back)
-template <int NB, bool F16, typename RA, typename RB>
+// BATCH pairs of pending steps per memory round trip: every operand load of the BATCH pairs is
+// issued before the first of their MFMAs (the replay wave's 16 winner rows: a few loads per pair,
+// latency-bound; the landmark waves' 128 rows keep BATCH = 1). The MFMAs run in the same order for
+// every BATCH, so the accumulators are the same bits.
+template <int NB, bool F16, int BATCH = 1, typename RA, typename RB>
 __device__ __forceinline__ void plane_replay(const Slot* pend, int e, size_t inst_bf, int M, unsigned amask,
                                              int lane, RA row_a, RB row_b, f32x4v (&acc)[NB])
 {
@@ -1517,40 +1567,49 @@ __device__ __forceinline__ void plane_replay(const Slot* pend, int e, size_t ins
     for (int mb = 0; mb < NB; mb++) ra_[mb] = row_a(mb, r16);
     unsigned m = amask;
     while (m) {
-        const int qa = __builtin_ctz(m);
-        m &= m - 1;
-        const int qb = m ? __builtin_ctz(m) : -1;
-        if (qb >= 0) m &= m - 1;
-        const unsigned short* pa = reinterpret_cast<const unsigned short*>(pend[qa].Bop) + (size_t)e * inst_bf;
-        const unsigned short* pb = qb >= 0 ? reinterpret_cast<const unsigned short*>(pend[qb].Bop) + (size_t)e * inst_bf : pa;
-        const unsigned short* pq = (kg >= 2) ? pb : pa;
-        const bool none = kg >= 2 && qb < 0;
-        PV B[NPL], A[NB][NPL];
+        int qa[BATCH];
+        PV B[BATCH][NPL], A[BATCH][NB][NPL];
 #pragma unroll
-        for (int pl = 0; pl < NPL; pl++)
-            B[pl] = (!none && rb_ >= 0 && rb_ < M) ? *reinterpret_cast<const PV*>(pq + op_index_pl(rb_, h, pl, NPL)) : zero;
-#pragma unroll
-        for (int mb = 0; mb < NB; mb++)
+        for (int bb = 0; bb < BATCH; bb++) {
+            qa[bb] = m ? __builtin_ctz(m) : -1;
+            if (m) m &= m - 1;
+            const int qb = m ? __builtin_ctz(m) : -1;
+            if (qb >= 0) m &= m - 1;
+            const int q0 = qa[bb] >= 0 ? qa[bb] : 0;
+            const unsigned short* pa = reinterpret_cast<const unsigned short*>(pend[q0].Bop) + (size_t)e * inst_bf;
+            const unsigned short* pb = qb >= 0 ? reinterpret_cast<const unsigned short*>(pend[qb].Bop) + (size_t)e * inst_bf : pa;
+            const unsigned short* pq = (kg >= 2) ? pb : pa;
+            const bool none = qa[bb] < 0 || (kg >= 2 && qb < 0);
 #pragma unroll
             for (int pl = 0; pl < NPL; pl++)
-                A[mb][pl] = (!none && ra_[mb] >= 0 && ra_[mb] < M)
-                                ? *reinterpret_cast<const PV*>(pq + op_index_pl(ra_[mb], h, pl, NPL)) : zero;
-        if constexpr (F16) {
+                B[bb][pl] = (!none && rb_ >= 0 && rb_ < M) ? *reinterpret_cast<const PV*>(pq + op_index_pl(rb_, h, pl, NPL)) : zero;
 #pragma unroll
-            for (int pp = 0; pp < 3; pp++) {
-                const int a = pp == 0 ? 1 : 0, b = pp == 1 ? 1 : 0;   // (lo, hi), (hi, lo), (hi, hi)
+            for (int mb = 0; mb < NB; mb++)
 #pragma unroll
-                for (int mb = 0; mb < NB; mb++)
-                    acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[mb][a], B[b], acc[mb], 0, 0, 0);
-            }
-        } else {
+                for (int pl = 0; pl < NPL; pl++)
+                    A[bb][mb][pl] = (!none && ra_[mb] >= 0 && ra_[mb] < M)
+                                        ? *reinterpret_cast<const PV*>(pq + op_index_pl(ra_[mb], h, pl, NPL)) : zero;
+        }
 #pragma unroll
-            for (int pp = 0; pp < 6; pp++) {
-                const int a = (0x102010 >> (4 * (5 - pp))) & 0xf;   // (mid, mid), (hi, lo), (lo, hi),
-                const int b = (0x120100 >> (4 * (5 - pp))) & 0xf;   // (hi, mid), (mid, hi), (hi, hi)
+        for (int bb = 0; bb < BATCH; bb++) {
+            if (qa[bb] < 0) break;   // (uniform)
+            if constexpr (F16) {
 #pragma unroll
-                for (int mb = 0; mb < NB; mb++)
-                    acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mb][a], B[b], acc[mb], 0, 0, 0);
+                for (int pp = 0; pp < 3; pp++) {
+                    const int a = pp == 0 ? 1 : 0, b = pp == 1 ? 1 : 0;   // (lo, hi), (hi, lo), (hi, hi)
+#pragma unroll
+                    for (int mb = 0; mb < NB; mb++)
+                        acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[bb][mb][a], B[bb][b], acc[mb], 0, 0, 0);
+                }
+            } else {
+#pragma unroll
+                for (int pp = 0; pp < 6; pp++) {
+                    const int a = (0x102010 >> (4 * (5 - pp))) & 0xf;   // (mid, mid), (hi, lo), (lo, hi),
+                    const int b = (0x120100 >> (4 * (5 - pp))) & 0xf;   // (hi, mid), (mid, hi), (hi, hi)
+#pragma unroll
+                    for (int mb = 0; mb < NB; mb++)
+                        acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[bb][mb][a], B[bb][b], acc[mb], 0, 0, 0);
+                }
             }
         }
     }
@@ -2367,9 +2426,9 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                 if (f32rep)
                     f32_replay<1>(p.pend, e, opstride, M, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow, dacc);
                 else if (HOT == 2 || (HOT == 0 && pf16))
-                    plane_replay<1, true>(p.pend, e, opstride * 2, M, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow, dacc);
+                    plane_replay<1, true, 4>(p.pend, e, opstride * 2, M, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow, dacc);
                 else
-                    plane_replay<1, false>(p.pend, e, opstride * 3, M, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow, dacc);
+                    plane_replay<1, false, 4>(p.pend, e, opstride * 3, M, amask, lane_r, [&](int, int r) { return wrow(r); }, wrow, dacc);
                 float* scr = sh_stg;   // (not staged in this mode) 16 × 16 floats
 #pragma unroll
                 for (int i = 0; i < 4; i++) scr[(4 * (lane_r >> 4) + i) * 16 + (lane_r & 15)] = dacc[0][i];
@@ -2443,18 +2502,16 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                     double* pk = sh_pk[t];
                     int okl = 1;
                     Cand c;
+                    Block5 b5;
                     if (u == t) {
                         const ekf_line ln = lnu;
                         double Rm[4];
                         line_R(ln, t, r_mode, Rm);
-                        Block5 b5;
                         fill_block5(b5, R33l, w0, w1, w2, wD);
                         double sn, cs;
                         sincos_near(wy.x, wma0, ws0, wc0, sn, cs);
-                        eval_candidate(b5, wy.x, wy.y, sn, cs, xpl, ln.alpha, ln.r, Rm, p.gate, ETA, c);
-                        // GSL_EDOM of the winner (the reference evaluated it: Robot.cpp:454)
-                        if (c.singular) atomicOr(&sh_rwst, (int)EKF_ST_SINGULAR);
-                        if (c.amb) atomicOr(&sh_rwst, (int)EKF_ST_PRECISION_BIT);
+                        // (its storage-precision margin and GSL_EDOM status after the package is out)
+                        eval_candidate<false>(b5, wy.x, wy.y, sn, cs, xpl, ln.alpha, ln.r, Rm, p.gate, ETA, c);
                         okl = c.pass ? 1 : 0;
                         pk[PK_OK] = okl ? 1.0 : 0.0;
                     }
@@ -2470,14 +2527,10 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
 #pragma unroll
                         for (int a = 0; a < 9; a++) pkl[PK_R33 + a] = R33l[a];
                         pkl[PK_XP + 0] = xpl[0]; pkl[PK_XP + 1] = xpl[1]; pkl[PK_XP + 2] = xpl[2];
-                        if (sym) {   // once per line for every landmark's operand stores
-                            float F[3];
-                            sym_factor(pkl, F);
-                            pkl[PK_F + 0] = F[0]; pkl[PK_F + 1] = F[1]; pkl[PK_F + 2] = F[2];
-                        }
-                        // (the robot rows of K stay in registers: only robot_update, here, reads them)
+                        // (the robot rows of K stay in registers: only robot_update, here, reads them;
+                        // the symmetric operand factor is the landmark waves' own, from S)
 #pragma unroll
-                        for (int a = MB_S; a < PKW; a++)
+                        for (int a = MB_S; a < PK_F; a++)
                             if (a < MB_KR || a >= MB_KR + 6) pk[a] = pkl[a];
                     }
                     // the package is complete: to the other lanes of this wave, and to the
@@ -2486,6 +2539,12 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                     __builtin_amdgcn_wave_barrier();
                     if (u == 0) __hip_atomic_store(&sh_ready, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if (u == t) {
+                        // GSL_EDOM of the winner (the reference evaluated it: Robot.cpp:454) and the
+                        // gate's storage precision (gate_eta), off the line's chain
+                        if (c.singular) atomicOr(&sh_rwst, (int)EKF_ST_SINGULAR);
+                        if (cand_amb(b5, c, p.gate, ETA)) atomicOr(&sh_rwst, (int)EKF_ST_PRECISION_BIT);
+                    }
                     if (!ok) continue;   // (ml counts matches: unchanged)
                     if (u != t) {   // (lane t has them)
 #pragma unroll
@@ -2793,7 +2852,8 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                             if (wok) {
                                 rr0 = g0; rr1 = g1; rr2 = g2; yb = gy;
                                 Dj[0] = gD[0]; Dj[1] = gD[1]; Dj[2] = gD[2]; Dj[3] = gD[3];
-                                const float F[3] = {(float)pk[PK_F], (float)pk[PK_F + 1], (float)pk[PK_F + 2]};
+                                float F[3];
+                                sym_factor(pk, F);   // (the same bits as the replay wave's S gives)
                                 store_rows(m, kk, uu, false, F, true);
                             }
                         }
