@@ -125,6 +125,17 @@ def parse():
     return args
 
 
+def build_info(sha, loaded):
+    """How the loaded library came to be on this machine: slam_ros_amd/build.py's last_build()
+    ("compiled" / "reused" by build() here, or "prebuilt": shipped, build() never ran on this copy),
+    and whether that record describes the library this process loaded."""
+    from slam_ros_amd import build as B
+    rec = B.last_build()
+    loaded_default = os.path.abspath(loaded) == os.path.abspath(B.LIB_PATH)
+    return {"build_mode": rec.get("mode"), "source_sha": rec.get("source_sha"),
+            "record_matches_loaded": loaded_default and rec.get("lib_sha") == sha}
+
+
 def lib_sha(path):
     h = hashlib.sha256()
     with open(path, "rb") as f:
@@ -439,8 +450,12 @@ def main():
     steps_per_launch = dom["steps_per_launch"] if dom else args.flush_interval
     alg_bytes = E * n * (n + 1) * bpe   # one read + write of the packed block per flush
     alg_flops = steps_per_launch * E * 2 * L_LINES * n * (n + 1)
-    bf_form = bool(dom and (dom["kernel"].endswith(", true>") or dom["kernel"].startswith("flush_bf24_kernel")))
-    f16_form = bool(dom and dom["kernel"].endswith(", true, true>"))
+    kname = dom["kernel"] if dom else ""
+    # split-fp16 forms: the 2 x 2 wave form <.., true, true>, the 2 x 4 form <.., true> of
+    # flush_bf24_kernel, the quad form flush_f16q_kernel; split-bf16: the other <.., true> forms
+    f16_form = (kname.endswith(", true, true>") or kname.startswith("flush_f16q_kernel")
+                or (kname.startswith("flush_bf24_kernel") and kname.endswith(", true>")))
+    bf_form = not f16_form and (kname.endswith(", true>") or kname.startswith("flush_bf24_kernel"))
     # the MFMA roof of the instruction the flush executes: the split-bf16 flush runs six bf16
     # products per fp32 product (executed flops = 6 x algorithmic, dense bf16 peak); the exact
     # forms run v_mfma_f32_32x32x2_f32 (fp32 and fp16 storage) or v_mfma_f64_16x16x4_f64
@@ -458,7 +473,8 @@ def main():
     gbs = alg_bytes / (dd_ms * 1e-3) / 1e9 if dd_ms > 0 else None
     tfs = alg_flops / (dd_ms * 1e-3) / 1e12 if dd_ms > 0 else None    # fp32-equivalent (algorithmic)
     xtfs = mfma_mult * tfs if tfs else None                             # executed, in mfma_dtype
-    sha = lib_sha(ekf.LIB_PATH)
+    lib_file = ekf.loaded_path or ekf.LIB_PATH
+    sha = lib_sha(lib_file)
     tj, traffic_src = find_traffic(args.traffic_json, sha, {
         "capacity": N, "instances": E, "precision": args.precision, "flush_interval": args.flush_interval,
         "pipeline": bool(args.pipeline), "kernel": dom["kernel"] if dom else None, "world": args.world})
@@ -518,6 +534,7 @@ def main():
             "traffic_source": traffic_src,
             "lib_sha": sha,
         },
+        "build": build_info(sha, lib_file),
         "kernel_ms": {"scan": scan_ms, "flush": dd_ms, "flush_launches": prof["launches"]},
         "all_lines_matched": all_matched,
         "cpu_baseline": None,

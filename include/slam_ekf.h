@@ -192,7 +192,8 @@ enum {
     EKF_OPT_SPIN_LOG2 = 2,
     /* fp32 / fp16 flush form, all bit-identical within an arithmetic: 0 automatic (default),
      * 2 the super-tile form for every group, 8 the wave form also for groups of 2 and 4 steps,
-     * 24 the split-bf16 flush on 2 x 4 wave-tiles */
+     * 24 the split-bf16 flush on 2 x 4 wave-tiles, 44 the split-fp16 flush on groups of 2 x 2
+     * wave-tiles sharing their operand planes through LDS (groups of 6 or more steps) */
     EKF_OPT_FLUSH_FORM = 3,
     /* workgroups per CU of the grid-strided flush forms, 1..16 (8) */
     EKF_OPT_FLUSH_BLOCKS_PER_CU = 4,

@@ -5,9 +5,13 @@ it is missing. Built in-tree so the .so travels to the GPU box with the reposito
 """
 from __future__ import annotations
 
+import hashlib
+import json
 import os
 import shutil
+import socket
 import subprocess
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -26,23 +30,62 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm required to build libslam_ekf.so)")
 
 
-def _stale(target: str, deps: list[str]) -> bool:
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(p) > t for p in deps)
+def _file_sha(path: str) -> str:   # (bench.py's lib_sha)
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()[:16]
+
+
+def _sha(paths: list[str]) -> str:
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            for blk in iter(lambda: f.read(1 << 20), b""):
+                h.update(blk)
+    return h.hexdigest()[:16]
+
+
+# Build provenance: the library carries a sidecar record of the sources it was
+# compiled from (LIB_PATH + ".json": source_sha over the sources, headers and this file, lib_sha of
+# the binary). build() reuses the library only when both hashes match — not by file times, which a
+# copy of the tree does not keep reliably — and writes what it did to lib/last_build.json
+# ("compiled" or "reused", host, time), which bench.py reports as build_mode.
+RECORD = LIB_PATH + ".json"
+LAST_BUILD = os.path.join(LIB_DIR, "last_build.json")
+
+
+def _record() -> dict:
+    try:
+        with open(RECORD) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
+def last_build() -> dict:
+    """The last build() on this copy of the tree, or {"mode": "prebuilt"} when build() never ran
+    here (the library as shipped, with its own record)."""
+    try:
+        with open(LAST_BUILD) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        rec = _record()
+        return {"mode": "prebuilt", "source_sha": rec.get("source_sha"), "lib_sha": rec.get("lib_sha")}
 
 
 # MFMA accumulators in VGPRs (not AGPRs): the fp16 flush rounds every accumulator after each
 # step on the VALU, which cannot read AGPRs, so the AGPR form paid a read + write copy per
 # element per step (fp16 flush 0.84 -> 0.72 ms at N=4096, T=8; fp32 unchanged or faster)
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-mllvm", "-amdgpu-mfma-vgpr-form"]
-# ekf_kernels.hip is compiled as eight units (EKF_TU: 1 association kernels, 2 the exact and fp64
+# ekf_kernels.hip is compiled as nine units (EKF_TU: 1 association kernels, 2 the exact and fp64
 # flushes, 3 the rest, 4 / 5 / 6 the split-fp16, 2 x 4 and split-bf16 flushes, 7 / 8 the association
-# kernel on 128 / 64 landmarks per workgroup), in parallel with ekf_api.hip: each unit instantiates
+# kernel on 128 / 64 landmarks per workgroup, 9 the split-fp16 quad flush), in parallel with ekf_api.hip: each unit instantiates
 # only the kernels its launchers use
 UNITS = [("ekf_kernels.hip", 4), ("ekf_kernels.hip", 2), ("ekf_kernels.hip", 1), ("ekf_kernels.hip", 7),
-         ("ekf_kernels.hip", 8), ("ekf_kernels.hip", 5), ("ekf_kernels.hip", 6), ("ekf_kernels.hip", 3),
+         ("ekf_kernels.hip", 8), ("ekf_kernels.hip", 5), ("ekf_kernels.hip", 6), ("ekf_kernels.hip", 3), ("ekf_kernels.hip", 9),
          ("ekf_api.hip", 0)]
 
 
@@ -77,12 +120,24 @@ def build(force: bool = False, verbose: bool = False) -> str:
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
     deps.append(os.path.join(ROOT, "include", "slam_ekf.h"))
     deps.append(os.path.abspath(__file__))   # compile flags live here
-    if not force and not _stale(LIB_PATH, deps):
-        return LIB_PATH
-    os.makedirs(LIB_DIR, exist_ok=True)
-    tmp = LIB_PATH + ".tmp"
-    _compile_link(tmp, [], verbose)
-    os.replace(tmp, LIB_PATH)
+    src = _sha(deps)
+    rec = _record()
+    reuse = (not force and os.path.exists(LIB_PATH) and rec.get("source_sha") == src
+             and rec.get("lib_sha") == _file_sha(LIB_PATH))
+    if not reuse:
+        os.makedirs(LIB_DIR, exist_ok=True)
+        tmp = LIB_PATH + ".tmp"
+        _compile_link(tmp, [], verbose)
+        os.replace(tmp, LIB_PATH)
+        rec = {"source_sha": src, "lib_sha": _file_sha(LIB_PATH), "built_on": socket.gethostname(),
+               "built_at": time.strftime("%Y-%m-%dT%H:%M:%S")}
+        with open(RECORD, "w") as f:
+            json.dump(rec, f)
+    last = {"mode": "reused" if reuse else "compiled", "source_sha": src, "lib_sha": rec["lib_sha"],
+            "host": socket.gethostname(), "at": time.strftime("%Y-%m-%dT%H:%M:%S")}
+    with open(LAST_BUILD, "w") as f:
+        json.dump(last, f)
+    print(f"libslam_ekf.so: {last['mode']} (source {src}, library {rec['lib_sha']})")
     return LIB_PATH
 
 

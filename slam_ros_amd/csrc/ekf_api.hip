@@ -86,6 +86,8 @@ struct ekf_ctx {
     int nwt64;
     int* wt24;                // split-bf16 wave-tiles of 2 × 4 tiles (wr | wc << 16), panel order
     int nwt24;
+    ekf::WtEntry* wtq;        // split-fp16 quad form: groups of 2 × 2 wave-tiles (four entries each)
+    int nwtq;
     double* d_enc;
     ekf_line* d_lines;
     int* d_nlines;
@@ -194,7 +196,7 @@ int ekf_abi_version(void) { return SLAM_EKF_ABI_VERSION; }
 static void free_all(ekf_ctx* c)
 {
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->cur, c->pose, c->xpre, c->saved, c->D,
-                               c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->wt24, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->pexp, c->sink, c->mbox,
+                               c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->wt24, c->wtq, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->pexp, c->sink, c->mbox,
                                c->sync, c->Ust, c->Vst, c->dense, c->psig, c->pvmax,
                                c->sh_rob, c->sh_rec, c->sh_hist, c->sh_pkg, c->sh_flags, c->sh_ctl,
                                c->sh_null.res, c->sh_xbuf, c->sh_xcols};
@@ -650,6 +652,46 @@ static int create_ctx(const ekf_config* cfg, int sh_rank, int sh_world, ekf_ctx*
         if (hipMalloc((void**)&c->wt24, sizeof(int) * w24.size()) != hipSuccess) goto fail;
         if (hipMemcpy(c->wt24, w24.data(), sizeof(int) * w24.size(), hipMemcpyHostToDevice) != hipSuccess)
             goto fail;
+        // the split-fp16 quad form's groups of 2 × 2 wave-tiles holding a stored tile (group column
+        // >= group row), in panels of 8 group columns walked row by row; entry 2a + b of a group is
+        // its wave-tile (2R + a, 2C + b). Wave-tiles wholly below the diagonal or past the block stay
+        // in their group (the group's operand rows are loaded alike): no valid tile, indices of a
+        // stored tile of the group, rows clamped to the block. A partitioned context has none.
+        if (c->sh_world <= 0) {
+            std::vector<ekf::WtEntry> wq;
+            const int ngr = (nwr + 1) / 2, ngc = (nwc + 1) / 2;
+            for (int pc = 0; pc < ngc; pc += 8)
+                for (int R = 0; R < ngr; R++)
+                    for (int Cg = pc; Cg < pc + 8 && Cg < ngc; Cg++) {
+                        if (Cg < R) continue;
+                        // a stored tile of the group: its first tile row, last tile column in the block
+                        const long long any = ekf::tile_index(4 * R, std::min(4 * Cg + 3, d.nb - 1), d.nb);
+                        for (int a = 0; a < 2; a++)
+                            for (int b = 0; b < 2; b++) {
+                                const int wr = 2 * R + a, wc = 2 * Cg + b;
+                                ekf::WtEntry v;
+                                memset(&v, 0, sizeof(v));
+                                for (int r = 0; r < ekf::WT_R; r++)
+                                    for (int cc = 0; cc < ekf::WT_C; cc++) {
+                                        const int i = r * ekf::WT_C + cc;
+                                        const int bi = wr * ekf::WT_R + r, bj = wc * ekf::WT_C + cc;
+                                        const bool ok = bi < d.nb && bj < d.nb && bi <= bj;
+                                        v.tile[i] = (int)(ok ? ekf::tile_index(bi, bj, d.nb) : any);
+                                        v.valid |= (ok ? 1 : 0) << i;
+                                    }
+                                for (int r = 0; r < ekf::WT_R; r++)
+                                    v.rows[0] |= std::min(wr * ekf::WT_R + r, d.nb - 1) << (16 * r);
+                                for (int cc = 0; cc < ekf::WT_C; cc++)
+                                    v.rows[1] |= std::min(wc * ekf::WT_C + cc, d.nb - 1) << (16 * cc);
+                                v.rc = wr | (wc << 16);
+                                wq.push_back(v);
+                            }
+                    }
+            c->nwtq = (int)wq.size();
+            if (hipMalloc((void**)&c->wtq, sizeof(ekf::WtEntry) * wq.size()) != hipSuccess) goto fail;
+            if (hipMemcpy(c->wtq, wq.data(), sizeof(ekf::WtEntry) * wq.size(), hipMemcpyHostToDevice) != hipSuccess)
+                goto fail;
+        }
     }
     {
         hipDeviceProp_t prop;
@@ -734,7 +776,7 @@ extern "C" int ekf_set_option(ekf_ctx* c, int opt, int v)
     case EKF_OPT_SPECULATE: if (v < 0 || v > 2) return EKF_ERANGE; break;
     case EKF_OPT_SPIN_LOG2: if (v < 8 || v > 24) return EKF_ERANGE; break;
     case EKF_OPT_FLUSH_FORM:
-        if (v != 0 && v != 2 && v != 8 && v != 24) return EKF_ERANGE;
+        if (v != 0 && v != 2 && v != 8 && v != 24 && v != 44) return EKF_ERANGE;
         // a partitioned context stores only its tile rows; only the wave forms walk the rank's
         // wave tables (the super-tile and tile forms walk every tile of the block)
         if (c->sh_world > 0 && v != 8) return EKF_EINVAL;
@@ -963,6 +1005,8 @@ static int enqueue_flush(ekf_ctx* c)
     dp.nwt64 = c->nwt64;
     dp.wt24 = c->wt24;
     dp.nwt24 = c->nwt24;
+    dp.wtq = c->wtq;
+    dp.nwtq = c->nwtq;
     dp.pexp = c->pexp;
     dp.usym = usym_of(c);
     dp.sink = c->sink;
@@ -1970,19 +2014,20 @@ extern "C" const char* ekf_flush_kernel_name(const ekf_ctx* c, int nsteps)
     const bool half = c->cfg.precision == EKF_PREC_F16;
     if (c->pmode == EKF_ARITH_F16X3 && nsteps >= 2 && nsteps <= ekf::F16X3_MAXS && nsteps % 2 == 0) {
         struct Names {
-            char n[2][2][ekf::F16X3_MAXS / 2 + 1][64];
+            char n[3][2][ekf::F16X3_MAXS / 2 + 1][64];
             Names()
             {
-                for (int f = 0; f < 2; f++)
+                static const char* fmt[3] = {"flush_f32_wave_kernel<%s, %d, true, true>", "flush_bf24_kernel<%s, %d, true>",
+                                             "flush_f16q_kernel<%s, %d>"};
+                for (int f = 0; f < 3; f++)
                     for (int h = 0; h < 2; h++)
                         for (int k = 0; k <= ekf::F16X3_MAXS / 2; k++)
-                            snprintf(n[f][h][k], sizeof n[f][h][k],
-                                     f ? "flush_bf24_kernel<%s, %d, true>" : "flush_f32_wave_kernel<%s, %d, true, true>",
-                                     h ? "_Float16" : "float", 2 * k);
+                            snprintf(n[f][h][k], sizeof n[f][h][k], fmt[f], h ? "_Float16" : "float", 2 * k);
             }
         };
         static const Names f16n;   // (initialised once, thread-safe)
-        return f16n.n[c->dd_variant == 24 ? 1 : 0][half ? 1 : 0][nsteps / 2];
+        const int form = c->dd_variant == 24 ? 1 : (c->dd_variant == 44 && nsteps >= 6 && c->nwtq > 0) ? 2 : 0;
+        return f16n.n[form][half ? 1 : 0][nsteps / 2];
     }
     if (c->bf && nsteps >= 2 && nsteps <= 16 && nsteps % 2 == 0 && c->dd_variant == 24) {
         static const char* b24[2][9] = {

@@ -245,6 +245,8 @@ struct DowndateParams {
     int zskip;            // split-plane wave flush: skip wave-tiles past every step's RES_ZMAX
     const int* wt24;      // [nwt24] split-bf16 wave-tiles of 2 × 4 tiles (wr | wc << 16), panel order
     int nwt24;
+    const WtEntry* wtq;   // [nwtq] the split-fp16 quad form's groups of 2 × 2 wave-tiles (four entries each)
+    int nwtq;
     Slot steps[PMAX];
 };
 

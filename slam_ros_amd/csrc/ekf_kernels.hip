@@ -1291,12 +1291,6 @@ constexpr int SPEC_K = 8;
 // and a more bit (36); B = local indices 4..7, written and read only when the count exceeds 4
 constexpr int LW_CNT = 32, LW_MORE = 36;
 constexpr int SPEC_PB = 2;                          // guessed columns per pass over the pending steps
-#ifndef EKF_F16_TILES_ALWAYS
-#define EKF_F16_TILES_ALWAYS 0
-#endif
-#ifndef EKF_F64_TILES_ALWAYS
-#define EKF_F64_TILES_ALWAYS 0
-#endif
 #ifndef EKF_SPEC_PB64
 #define EKF_SPEC_PB64 4
 #endif
@@ -4687,18 +4681,9 @@ __device__ __forceinline__ void wt_general(const DowndateParams& p, int e, const
 // planes, Slot::Bop). With U = −V the accumulators hold −X (negated on load and store, exact), so
 // both operands are V planes: of the wave-tile's row blocks (A) and column blocks (B). Operands
 // stream through a ring of RD step-sets, RD − 1 steps ahead, across wave-tile boundaries.
-#ifndef EKF_BF_WAVES
-#define EKF_BF_WAVES 1   // split-bf16 flush: waves per SIMD (2: ≤ 256 registers, ring depth 2; measured equal)
-#endif
-#ifndef EKF_F16_WAVES
-#define EKF_F16_WAVES 1  // split-fp16 flush: waves per SIMD (2: ≤ 256 registers, ring depth 2; measured equal)
-#endif
-#ifndef EKF_F16_TILES_LATE
-#define EKF_F16_TILES_LATE 1   // split-fp16 flush: deep operand ring, next tiles issued late (below)
-#endif
-#ifndef EKF_F16_RDMAX
-#define EKF_F16_RDMAX 8
-#endif
+// split-plane flushes: one wave per SIMD (two at <= 256 registers and a ring of 2 measured equal;
+// scripts/xp/f16_wave_switches.patch restores that and the other A/B switches of this form)
+constexpr int F16_RDMAX = 8;   // split-fp16 flush: the deepest operand ring (step-sets)
 // the largest divisor of ns not above rmax (at least 2)
 constexpr int ring_depth(int ns, int rmax)
 {
@@ -4708,7 +4693,7 @@ constexpr int ring_depth(int ns, int rmax)
     return r;
 }
 template <typename TS, int NS, bool BF = false, bool F16 = false>
-__global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVES) : 1) void flush_f32_wave_kernel(DowndateParams p)
+__global__ __launch_bounds__(DD_THREADS, 1) void flush_f32_wave_kernel(DowndateParams p)
 {
     static_assert(NS >= 2 && NS % 2 == 0 && NS <= PMAX, "even step count");
     static_assert(BF || NS <= 8, "fp32 wave flush: at most 8 steps (operands of every step in registers)");
@@ -4817,14 +4802,11 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
             // planes: BF16X6 hi, mid, lo bf16 (six products); F16X3 hi, lo fp16 of 2^σ·V (three)
             constexpr int NPL = F16 ? 2 : 3;
             typedef typename std::conditional<F16, f16x8r, bf16x8r>::type bf16x8;
-            constexpr int WAVES = F16 ? EKF_F16_WAVES : EKF_BF_WAVES;
             // operand ring depth (divides NS: a ring slot keeps its step index across wave-tiles).
-            // F16 with late tiles: the deepest ring of at most EKF_F16_RDMAX step-sets, and the next
-            // wave-tile's tiles issued RD − 1 steps before its start (below)
-            constexpr int RD = WAVES > 1 ? 2
-                               : (F16 && EKF_F16_TILES_LATE) ? ring_depth(NS, EKF_F16_RDMAX)
-                               : (NS % 4 == 0 ? 4 : (NS % 3 == 0 ? 3 : 2));
-            constexpr bool LATE = F16 && EKF_F16_TILES_LATE && WAVES == 1 && RD >= 3;
+            // F16: the deepest ring of at most F16_RDMAX step-sets, and the next wave-tile's tiles
+            // issued RD − 1 steps before its start (late, below)
+            constexpr int RD = F16 ? ring_depth(NS, F16_RDMAX) : (NS % 4 == 0 ? 4 : (NS % 3 == 0 ? 3 : 2));
+            constexpr bool LATE = F16 && RD >= 3;
             // vmcnt retires in issue order, so every operand wait after the tile loads also waits for
             // them: issued at step TQ, the first such wait comes RD − 1 steps later, and so does
             // the next wave-tile's first use of them
@@ -4974,12 +4956,11 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
                     for (int qq = 0; qq < 4; qq++)
 #pragma unroll
                         for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = (float)pref[i][qq][j] * isc;
-                if (!LATE && (EKF_F16_TILES_ALWAYS || more)) load_tiles(EKF_F16_TILES_ALWAYS ? ldi : nxt);
+                if (!LATE && more) load_tiles(nxt);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int q = 0; q < NS; q++) {
-                    // (EKF_F16_TILES_ALWAYS: unconditional, the last wave-tile re-reads its own)
-                    if (LATE && q == TQ && (EKF_F16_TILES_ALWAYS || more)) load_tiles(EKF_F16_TILES_ALWAYS ? ldi : nxt);
+                    if (LATE && q == TQ && more) load_tiles(nxt);
                     // ring set of step q + RD − 1 (this wave-tile's, else the next one's)
                     const int ql = q + RD - 1;
                     if (ql < NS) load_ops(ql % RD, cur, ql);
@@ -5240,6 +5221,405 @@ __global__ __launch_bounds__(DD_THREADS, BF ? (F16 ? EKF_F16_WAVES : EKF_BF_WAVE
             t = n;
         }
         wt_general<TS, NS>(p, t.e, t.w, lane);
+    }
+}
+
+// Split-fp16 flush, quad form (EKF_ARITH_F16X3, EKF_OPT_FLUSH_FORM = 44; groups of >= 6 steps).
+// The 2 × 2 wave form streams each wave's 8 KB of operand planes per step through L1/L2 into
+// registers beside its 12 MFMAs, and that stream, not HBM, paces it. Here a
+// workgroup's four MFMA waves take the four wave-tiles of a 2 × 2 group (p.wtq: four entries per
+// group in panel order, entry 2a + b the wave-tile (2R + a, 2C + b); positions wholly below the
+// diagonal or past the block are entries with no stored tile) and share the group's operand row
+// blocks: its 4 A blocks (tile rows) and 4 B blocks (tile columns), both planes, 16 KB per step —
+// half of what the four waves read alone. Loader waves (EKF_Q_LOADERS, no MFMA work) move them by
+// LDS-DMA (global_load_lds_dwordx4, 1 KB per wave-instruction, no register staging) into a ring
+// of D step slots, D − 1 steps ahead of the MFMA waves; one barrier per step: before it each loader
+// waits (its own vmcnt, counted) for the step after the current one to land, and each MFMA wave
+// for its own LDS reads of the current step; after it the MFMA waves read the next step's planes
+// into the second of two register sets while the current step's 12 MFMAs run, and the loaders
+// refill the slot just consumed. The MFMA waves' vector memory queue then holds only their own tile
+// loads (issued EKF_Q_TQ steps into a group for the next one) and stores, so an operand wait never
+// waits for a tile. Per accumulator the chain is the 2 × 2 form's (the same three products per
+// step, in the same order, on the same planes): bit-identical. As there: −P in the accumulators
+// (fp16 storage scaled out of its exponent), the second pass through wt_general for wave-tiles
+// whose steps add rows or whose σ changes, reset instances stored as zero, and a group whose
+// columns all lie past every step's RES_ZMAX skipped whole (dead).
+#ifndef EKF_Q_DEPTH
+#define EKF_Q_DEPTH 8      // quad flush: operand ring slots (16 KB each) = steps in flight
+#endif
+#ifndef EKF_Q_LOADERS
+#define EKF_Q_LOADERS 2    // quad flush: LDS-DMA loader waves beside the four MFMA waves
+#endif
+#ifndef EKF_Q_TQ
+#define EKF_Q_TQ 1         // quad flush: the step of a group at which the next group's tiles are issued
+#endif
+constexpr int Q_WAVES = 4 + EKF_Q_LOADERS;
+constexpr int Q_SLOT = 16 * 1024;   // one step: 8 row blocks × 2 planes × 64 lanes × 16 B
+template <typename TS, int NS>
+__global__ __launch_bounds__(64 * Q_WAVES, 1) void flush_f16q_kernel(DowndateParams p)
+{
+    constexpr int D = EKF_Q_DEPTH < NS ? EKF_Q_DEPTH : NS;
+    constexpr int PPL = 16 / EKF_Q_LOADERS;   // plane pieces per loader wave and step
+    // (vmcnt holds at most 63 outstanding instructions)
+    static_assert(16 % EKF_Q_LOADERS == 0 && D >= 3 && PPL * (D - 2) <= 63, "quad flush: ring");
+    static_assert(NS >= 6 && NS % 2 == 0 && EKF_Q_TQ < NS, "quad flush: step count");
+    constexpr bool HALF = sizeof(TS) == 2;
+    constexpr int NPL = 2;
+    typedef f16x8r f16x8;
+    // the only LDS object: a second one beside a DMA target can make the compiler drain vmcnt
+    // before LDS reads (cdna_hip_programming.md §5)
+    __shared__ __attribute__((aligned(1024))) char ring[D * Q_SLOT];
+
+    const Dims d = p.d;
+    const int ngr = p.nwtq >> 2;   // groups per instance
+    const int total = p.E * ngr;
+    const int per = (total + 7) / 8;   // groups per XCD (a contiguous range)
+    const int xcd = blockIdx.x & 7;
+    const int K = (int)(gridDim.x >> 3);
+    const int g_end = min(total, (xcd + 1) * per);
+    const int gs = xcd * per + (int)(blockIdx.x >> 3);
+    if (gs >= g_end) return;   // (the whole workgroup)
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    const size_t inst_elems = (size_t)d.ntiles * TILE_ELEMS;
+    const TS* Pin = reinterpret_cast<const TS*>(p.Pin);
+    TS* Pout = reinterpret_cast<TS*>(p.Pout);
+    TS* sink = reinterpret_cast<TS*>(p.sink);
+
+    // the plain loop needs every step of the workgroup's instances to be a downdate without a
+    // rollback (the 2 × 2 form's fast_rows), decided alike by every wave
+    bool fast_rows = true;
+    {
+        const int e_lo = gs / ngr, e_hi = (g_end - 1) / ngr;
+        for (int e = e_lo; e <= e_hi; e++)
+#pragma unroll
+            for (int q = 0; q < NS; q++)
+                fast_rows = fast_rows && !sload(p.steps[q].res + (size_t)e * RES_STRIDE + RES_ROLLBACK);
+    }
+    struct Grp {
+        int e, gi, g;   // instance, group of the instance, flat index (gs + k·K)
+    };
+    auto first_grp = [&](Grp& t) __attribute__((always_inline)) {
+        t.e = gs / ngr;
+        t.gi = gs - t.e * ngr;
+        t.g = gs;
+    };
+    auto next_grp = [&](const Grp& c, Grp& t) __attribute__((always_inline)) {
+        int gi = c.gi + K, e = c.e;
+        while (gi >= ngr) {
+            gi -= ngr;
+            e++;
+        }
+        t.e = e;
+        t.gi = gi;
+        t.g = c.g + K;
+    };
+    typedef int i32x8 __attribute__((ext_vector_type(8)));
+    static_assert(sizeof(WtEntry) == sizeof(i32x8), "one scalar dwordx8 per entry");
+    auto load_entry = [&](int li, WtEntry& w) __attribute__((always_inline)) {
+        const i32x8 v = sload(reinterpret_cast<const i32x8*>(p.wtq + li));
+#pragma unroll
+        for (int i = 0; i < WT_N; i++) w.tile[i] = v[i];
+        w.valid = v[WT_N];
+        w.rows[0] = v[WT_N + 1];
+        w.rows[1] = v[WT_N + 2];
+        w.rc = v[WT_N + 3];
+    };
+    if (!fast_rows) {   // every wave-tile through the general loop (no LDS, no barriers)
+        if (wv >= 4) return;
+        Grp t;
+        first_grp(t);
+        for (int g = gs; g < g_end; g += K) {
+            if (g != gs) {
+                Grp n;
+                next_grp(t, n);
+                t = n;
+            }
+            WtEntry w;
+            load_entry(4 * t.gi + wv, w);
+            wt_general<TS, NS>(p, t.e, w, lane);
+        }
+        return;
+    }
+
+    // per instance (the 2 × 2 form's bookkeeping): added landmarks [u_lo, u_hi), σ of the first and
+    // last step, σ changes (smask), a reset (rz), the landmarks past every step's RES_ZMAX (zl)
+    auto rec_of = [&](int e, int q, int w) __attribute__((always_inline)) {
+        return sload(p.steps[q].res + (size_t)e * RES_STRIDE + w);
+    };
+    int st_e = -1, u_lo = 0, u_hi = 0, sg0 = 0, sgl = 0, zl = 0;
+    unsigned smask = 0;
+    bool rz = false;
+    auto load_steps = [&](int e) __attribute__((always_inline)) {
+        u_lo = 0x7fffffff;
+        u_hi = 0;
+        smask = 0;
+        rz = false;
+        zl = 0;
+        int prev = 0;
+#pragma unroll
+        for (int q = 0; q < NS; q++) {
+            zl = max(zl, rec_of(e, q, RES_ZMAX));
+            if (rec_of(e, q, RES_RESET)) {
+                u_lo = 0x7fffffff;
+                u_hi = 0;
+                smask = 0;
+                rz = true;
+                continue;
+            }
+            const int na = rec_of(e, q, RES_NADD), s0 = rec_of(e, q, RES_SAVED_IN);
+            if (na > 0) {
+                u_lo = min(u_lo, s0);
+                u_hi = max(u_hi, s0 + na);
+            }
+            const int sg = rec_of(e, q, RES_PSIG);
+            if (q == 0) sg0 = sg;
+            else if (sg != prev) smask |= 1u << (q - 1);
+            if (sg == PLANE_SIGMA_EXACT) smask |= 1u << NS;
+            prev = sg;
+        }
+        sgl = prev;
+        st_e = e;
+    };
+    // a group whose columns all lie past zl (its first wave-tile column, entry 0's): unchanged by
+    // the group's steps, skipped by every wave alike
+    auto dead = [&](const Grp& t) __attribute__((always_inline)) {
+        if (!p.zskip || t.e >= p.E) return false;
+        if (t.e != st_e) load_steps(t.e);
+        const int rc = sload(&p.wtq[4 * t.gi].rc);
+        return !rz && (rc >> 16) * WT_C * 16 >= zl;
+    };
+    auto next_live = [&](const Grp& c, Grp& t) __attribute__((always_inline)) {
+        next_grp(c, t);
+        while (t.g < g_end && dead(t)) {
+            const Grp u = t;
+            next_grp(u, t);
+        }
+    };
+    auto barrier = [&]() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    Grp cur, nxt, nxt2;
+    first_grp(cur);
+    while (cur.g < g_end && dead(cur)) {
+        const Grp u = cur;
+        next_grp(u, cur);
+    }
+    if (cur.g >= g_end) return;   // (uniform: no live group)
+    next_live(cur, nxt);
+
+    if (wv >= 4) {
+        // loader wave: plane pieces LW·PPL .. LW·PPL + PPL − 1 of every step; piece 2·blk + pl is
+        // plane pl of row block blk: blocks 0-3 the group's tile rows (entry 0's A rows, then entry
+        // 3's), 4-7 its tile columns (entry 0's B rows, then entry 3's)
+        const size_t pstride = (size_t)d.nb * NPL * 64;
+        auto pl_base = [&](int q) __attribute__((always_inline)) {
+            int sl = p.slot0 + q;
+            if (sl >= p.nslots) sl -= p.nslots;
+            return reinterpret_cast<const f16x8*>(reinterpret_cast<const char*>(p.bbase) +
+                                                  (size_t)sl * (size_t)p.bslot_bytes);
+        };
+        auto run = [&](auto lwc) __attribute__((always_inline)) {
+            constexpr int LW = decltype(lwc)::value;
+            struct Rows {
+                int w[4];   // entry 0 rows[0], entry 3 rows[0], entry 0 rows[1], entry 3 rows[1]
+            };
+            auto rows_of = [&](const Grp& t, Rows& r) __attribute__((always_inline)) {
+                const int li = 4 * t.gi;
+                r.w[0] = sload(&p.wtq[li].rows[0]);
+                r.w[1] = sload(&p.wtq[li + 3].rows[0]);
+                r.w[2] = sload(&p.wtq[li].rows[1]);
+                r.w[3] = sload(&p.wtq[li + 3].rows[1]);
+            };
+            // step q of group t into ring slot sl
+            auto issue = [&](int sl, const Grp& t, const Rows& r, int q) __attribute__((always_inline)) {
+                const f16x8* b = pl_base(q) + (size_t)t.e * pstride + lane;
+#pragma unroll
+                for (int i = 0; i < PPL; i++) {
+                    const int pc = LW * PPL + i, blk = pc >> 1, pl = pc & 1;
+                    const int row = (r.w[blk >> 1] >> (16 * (blk & 1))) & 0xffff;
+                    __builtin_amdgcn_global_load_lds(
+                        (const void*)(b + ((size_t)row * NPL + pl) * 64),
+                        (__attribute__((address_space(3))) void*)(ring + sl * Q_SLOT + pc * 1024), 16, 0, 0);
+                }
+            };
+            Rows rc, rn;
+            rows_of(cur, rc);
+#pragma unroll
+            for (int s = 0; s < D; s++) issue(s, cur, rc, s);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPL * (D - 1)) : "memory");
+            barrier();
+            int sb = 0;   // ring slot of the group's step 0
+            while (true) {
+                const bool more = nxt.g < g_end;
+                next_live(nxt, nxt2);
+                const Grp ldi = more ? nxt : cur;   // (the last group re-reads its own rows)
+                rows_of(ldi, rn);
+#pragma unroll
+                for (int q = 0; q < NS; q++) {
+                    // step s + 1 landed (the pieces of the D − 2 steps after it may be in flight)
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPL * (D - 2)) : "memory");
+                    barrier();
+                    // step s + D into the slot of step s, which every MFMA wave has read
+                    const int sl = (sb + q) % D;
+                    if (q + D < NS) issue(sl, cur, rc, q + D);
+                    else issue(sl, ldi, rn, q + D - NS);
+                }
+                if (!more) break;
+                sb = (sb + NS) % D;
+                cur = nxt;
+                nxt = nxt2;
+                rc = rn;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        };
+        if (wv == 4) run(std::integral_constant<int, 0>{});
+#if EKF_Q_LOADERS >= 2
+        else if (wv == 5) run(std::integral_constant<int, 1>{});
+#endif
+#if EKF_Q_LOADERS >= 4
+        else if (wv == 6) run(std::integral_constant<int, 2>{});
+        else if (wv == 7) run(std::integral_constant<int, 3>{});
+#endif
+        return;
+    }
+
+    // MFMA wave (a, b) = (wv >> 1, wv & 1): wave-tile entry 4·gi + wv; its A blocks 2a, 2a + 1
+    // and B blocks 2b, 2b + 1 of the group
+    const int qa = wv >> 1, qb = wv & 1;
+    auto tile_ptr = [&](int e, const WtEntry& w, int i) __attribute__((always_inline)) {
+        return (size_t)e * inst_elems + (size_t)w.tile[i] * TILE_ELEMS;
+    };
+    using Raw = typename std::conditional<HALF, f16x4, f32x4>::type;
+    Raw pref[WT_N][4];
+    f32x16 acc[WT_N];
+    f16x8 op[2][4][NPL];   // [register set][A 2a, A 2a + 1, B 2b, B 2b + 1][hi, lo]
+    auto load_tiles = [&](int e, const WtEntry& w) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < WT_N; i++) {
+            const Raw* tl = reinterpret_cast<const Raw*>(Pin + tile_ptr(e, w, i));
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) pref[i][qq] = __builtin_nontemporal_load(tl + lane + qq * 64);
+        }
+    };
+    // every slot is stored, the invalid ones to the sink tile (no branch around a store)
+    auto store_tiles = [&](int e, const WtEntry& w, bool skip) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < WT_N; i++) {
+            TS* tl = ((w.valid >> i) & 1) && !skip ? Pout + tile_ptr(e, w, i) : sink;
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) tile_st(tl, lane, qq, acc[i]);
+        }
+    };
+    const char* rbase = ring + lane * 16;
+    const int aoff = (2 * (2 * qa)) * 1024, boff = (2 * (4 + 2 * qb)) * 1024;
+    auto read_step = [&](int set, int sl) __attribute__((always_inline)) {
+        const char* s = rbase + sl * Q_SLOT;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int pl = 0; pl < NPL; pl++)
+                op[set][i][pl] = *reinterpret_cast<const f16x8*>(s + (i < 2 ? aoff : boff) + (2 * (i & 1) + pl) * 1024);
+    };
+    auto touched = [&](int e, const WtEntry& w) __attribute__((always_inline)) {
+        if (e != st_e) load_steps(e);
+        const int ra = (w.rc & 0xffff) * WT_R * 16, ca = (w.rc >> 16) * WT_C * 16;
+        return (u_lo < ra + WT_R * 16 && u_hi > ra) || (u_lo < ca + WT_C * 16 && u_hi > ca);
+    };
+    auto skip_of = [&](int e, const WtEntry& w) __attribute__((always_inline)) {
+        return touched(e, w) || (!rz && smask != 0);
+    };
+    // the group's accumulators from its prefetched tiles, −2^iex·P (iex: 2σ of its first step, less
+    // the fp16 storage exponent)
+    auto in_exp = [&](int e) __attribute__((always_inline)) {
+        if (e != st_e) load_steps(e);
+        int ex = 2 * sg0;
+        if constexpr (HALF) ex -= sload(p.pexp + e);
+        return ex;
+    };
+    auto init_acc = [&](int e) __attribute__((always_inline)) {
+        const float isc = -ldexpf(1.0f, in_exp(e));
+#pragma unroll
+        for (int i = 0; i < WT_N; i++)
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[i][4 * qq + j] = (float)pref[i][qq][j] * isc;
+    };
+    WtEntry wc, wn;
+    load_entry(4 * cur.gi + wv, wc);
+    load_tiles(cur.e, wc);
+    init_acc(cur.e);
+    bool any_skip = false;
+    barrier();
+    read_step(0, 0);
+    int sb = 0;
+    while (true) {
+        const bool more = nxt.g < g_end;
+        next_live(nxt, nxt2);
+        if (more) load_entry(4 * nxt.gi + wv, wn);
+        const bool skip = skip_of(cur.e, wc);
+        const bool zero = rz && !touched(cur.e, wc);
+        any_skip |= skip;
+        const int iex = in_exp(cur.e);
+        const int sgl_c = sgl, sg0_c = sg0;
+#pragma unroll
+        for (int q = 0; q < NS; q++) {
+            if (q == EKF_Q_TQ && more) load_tiles(nxt.e, wn);
+            barrier();
+            // the next step's planes (this group's, else the next group's first) into the other set
+            read_step((q + 1) & 1, (sb + q + 1) % D);
+            // (the reads ahead of the MFMAs: left to itself the scheduler sinks them below, and the
+            // next step then waits for them)
+            __builtin_amdgcn_sched_barrier(0);
+            const int st = q & 1;
+            // (lo, hi), (hi, lo), (hi, hi) per accumulator, as the 2 × 2 form
+#pragma unroll
+            for (int pp = 0; pp < 3; pp++) {
+                const int pa = pp == 0 ? 1 : 0, pb = pp == 1 ? 1 : 0;
+#pragma unroll
+                for (int rr = 0; rr < WT_R; rr++)
+#pragma unroll
+                    for (int c = 0; c < WT_C; c++)
+                        acc[rr * WT_C + c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+                            op[st][rr][pa], op[st][2 + c][pb], acc[rr * WT_C + c], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const float osc = -ldexpf(1.0f, -iex - 2 * (sgl_c - sg0_c));
+        if (zero) {
+#pragma unroll
+            for (int i = 0; i < WT_N; i++) acc[i] = f32x16{};
+        } else {
+#pragma unroll
+            for (int i = 0; i < WT_N; i++) acc[i] = acc[i] * osc;
+        }
+        store_tiles(cur.e, wc, skip);
+        if (!more) break;
+        sb = (sb + NS) % D;
+        cur = nxt;
+        nxt = nxt2;
+        wc = wn;
+        // (here, behind the stores on every path to it: the wait for the tiles then counts the
+        // stores instead of draining them, as a merge with the first group's path would)
+        init_acc(cur.e);
+    }
+    // second pass: the skipped wave-tiles through the general loop (their input tiles as read: the
+    // first pass stored them to the sink)
+    if (any_skip) {
+        Grp t;
+        first_grp(t);
+        for (int g = gs; g < g_end; g += K) {
+            if (g != gs) {
+                Grp n;
+                next_grp(t, n);
+                t = n;
+            }
+            if (dead(t)) continue;
+            WtEntry w;
+            load_entry(4 * t.gi + wv, w);
+            if (skip_of(t.e, w)) wt_general<TS, NS>(p, t.e, w, lane);
+        }
     }
 }
 
@@ -5629,13 +6009,7 @@ __global__ __launch_bounds__(DD_THREADS, 1) void flush_f64_wave_kernel(DowndateP
             next_item(nxt, nxt2);
             const Item ldi = more ? nxt : cur;   // the last wave-tile re-reads its own (no branch)
             to_acc(pref, acc);
-#if EKF_F64_TILES_ALWAYS
-            // unconditional (the last wave-tile re-reads its own tiles): a conditional prefetch
-            // makes the wait-count merge at the loop head drain every outstanding access
-            load_tiles(ldi, pref);
-#else
             if (more) load_tiles(nxt, pref);
-#endif
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int q = 0; q < NS; q++) {
@@ -6039,11 +6413,41 @@ hipError_t launch_flush_bf24(const DowndateParams& p, bool half, bool f16, hipSt
                              hipEvent_t ev_b);
 hipError_t launch_flush_f16x3(const DowndateParams& p, bool half, hipStream_t st, hipEvent_t ev_a, hipEvent_t ev_b);
 hipError_t launch_flush_bf16x6(const DowndateParams& p, bool half, hipStream_t st, hipEvent_t ev_a, hipEvent_t ev_b);
+hipError_t launch_flush_f16q(const DowndateParams& p, bool half, hipStream_t st, hipEvent_t ev_a, hipEvent_t ev_b);
+
+#if !defined(EKF_TU) || EKF_TU == 9
+hipError_t launch_flush_f16q(const DowndateParams& p, bool half, hipStream_t st, hipEvent_t ev_a, hipEvent_t ev_b)
+{
+    const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one workgroup per CU
+#define EKF_F16Q_CASE(NSV)                                                                              \
+    case NSV:                                                                                           \
+        if (half) hipExtLaunchKernelGGL((flush_f16q_kernel<_Float16, NSV>), dim3(wgrid), dim3(64 * Q_WAVES), 0, st, \
+                                        ev_a, ev_b, 0, p);                                              \
+        else hipExtLaunchKernelGGL((flush_f16q_kernel<float, NSV>), dim3(wgrid), dim3(64 * Q_WAVES), 0, st, ev_a, \
+                                   ev_b, 0, p);                                                         \
+        break;
+    switch (p.nsteps) {
+        EKF_F16Q_CASE(6)
+        EKF_F16Q_CASE(8)
+        EKF_F16Q_CASE(10)
+        EKF_F16Q_CASE(12)
+        EKF_F16Q_CASE(14)
+        EKF_F16Q_CASE(16)
+        EKF_F16Q_CASE(18)
+        EKF_F16Q_CASE(20)
+        EKF_F16Q_CASE(22)
+        EKF_F16Q_CASE(24)
+        default: return hipErrorInvalidValue;
+    }
+#undef EKF_F16Q_CASE
+    return hipGetLastError();
+}
+#endif
 
 #if !defined(EKF_TU) || EKF_TU == 4
 hipError_t launch_flush_f16x3(const DowndateParams& p, bool half, hipStream_t st, hipEvent_t ev_a, hipEvent_t ev_b)
 {
-    const unsigned wgrid = (unsigned)(8 * EKF_F16_WAVES * ((p.ncu + 7) / 8));
+    const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
 #define EKF_F16_CASE(NSV)                                                                               \
 case NSV:                                                                                           \
     if (half) hipExtLaunchKernelGGL((flush_f32_wave_kernel<_Float16, NSV, true, true>), dim3(wgrid),  \
@@ -6129,7 +6533,7 @@ hipError_t launch_flush_bf24(const DowndateParams& p, bool half, bool f16, hipSt
 #if !defined(EKF_TU) || EKF_TU == 6
 hipError_t launch_flush_bf16x6(const DowndateParams& p, bool half, hipStream_t st, hipEvent_t ev_a, hipEvent_t ev_b)
 {
-    const unsigned wgrid = (unsigned)(8 * EKF_BF_WAVES * ((p.ncu + 7) / 8));   // EKF_BF_WAVES workgroups per CU
+    const unsigned wgrid = (unsigned)(8 * ((p.ncu + 7) / 8));   // one 4-wave workgroup per CU
 #define EKF_BF_CASE(NSV)                                                                                \
 case NSV:                                                                                           \
     if (half) hipExtLaunchKernelGGL((flush_f32_wave_kernel<_Float16, NSV, true>), dim3(wgrid), dim3(DD_THREADS), 0, \
@@ -6186,6 +6590,8 @@ hipError_t launch_downdate(const DowndateParams& p, int precision, int grid, hip
         return launch_flush_bf24(p, half, false, st, ev_a, ev_b);
     if (p.bf == 2 && bf_shape && p.variant == 24 && p.nwt24 > 0 && p.wt24 != nullptr)
         return launch_flush_bf24(p, half, true, st, ev_a, ev_b);
+    if (p.bf == 2 && bf_shape && p.variant == 44 && p.nsteps >= 6 && p.nwtq > 0 && p.wtq != nullptr)
+        return launch_flush_f16q(p, half, st, ev_a, ev_b);   // the quad form (groups of 6-24 steps)
     if (p.bf == 2 && bf_shape)   // EKF_ARITH_F16X3: split-fp16 wave flush, groups of 2-24 steps (even)
         return launch_flush_f16x3(p, half, st, ev_a, ev_b);
     if (p.bf == 1 && bf_shape)   // EKF_ARITH_BF16X6: split-bf16 wave flush, groups of 2-16 steps (even)

@@ -81,12 +81,13 @@ class EkfError(RuntimeError):
 
 
 _lib = None
+loaded_path = None   # the file load_library() loaded
 
 
 def load_library(path: str = ""):
     """Load libslam_ekf.so (never builds implicitly on a GPU box: fail loudly instead).
     SLAM_EKF_LIB selects another build of the same library (A/B experiments)."""
-    global _lib
+    global _lib, loaded_path
     if _lib is not None:
         return _lib
     path = path or os.environ.get("SLAM_EKF_LIB") or LIB_PATH
@@ -94,6 +95,7 @@ def load_library(path: str = ""):
         raise EkfError(f"{path} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`"
                        " (HIP extension required; there is no CPU fallback)")
     L = ctypes.CDLL(path)
+    loaded_path = path
     vp, i32, d, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_double, ctypes.c_size_t
     dp = ctypes.POINTER(ctypes.c_double)
     ip = ctypes.POINTER(ctypes.c_int32)

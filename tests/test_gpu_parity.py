@@ -945,6 +945,51 @@ def test_bf16_2x4_flush_equals_2x2(ekf_mod, monkeypatch, prec, N, T, extra_every
             assert np.array_equal(Pa, Pb) and np.array_equal(ya, yb), e
 
 
+@pytest.mark.parametrize("prec,N,T,extra_every,active", [(1, 1024, 20, 0, 0), (1, 1000, 12, 0, 0), (2, 512, 10, 0, 0),
+                                                         (1, 200, 8, 3, 0), (1, 100, 16, 0, 0), (2, 2048, 24, 0, 0),
+                                                         (1, 1024, 12, 3, 300), (2, 4096, 20, 4, 1500),
+                                                         (1, 64, 6, 2, 0), (1, 256, 8, 2, 240), (2, 256, 14, 3, 240),
+                                                         (1, 4096, 20, 0, 0)])
+def test_f16_quad_flush_equals_2x2(ekf_mod, prec, N, T, extra_every, active):
+    """The split-fp16 flush on groups of 2 × 2 wave-tiles whose operand planes loader waves move into
+    an LDS ring by DMA (flush_f16q_kernel, EKF_OPT_FLUSH_FORM = 44) and the 2 × 2 wave form (default)
+    run the same three products per accumulator and step in the same order on the same planes, and
+    send the same wave-tiles (new rows, σ changes) through the general loop: equal state for plain
+    groups, groups with augmented rows, fp32 and fp16 storage, partly filled maps (whole dead groups
+    skipped; a dead wave-tile in a live group recomputed unchanged), block sizes that are not
+    multiples of the group, step counts whose ring does not divide them (14, 6)."""
+    E = 3
+    if not active:
+        active = N - 12 - 2 * ((3 * T + 1) // extra_every) if extra_every else N - 10
+    w = G.make_world(N, active=active)
+    st = G.initial_state(w)
+    a = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=2, options={"flush_form": 44})
+    b = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T, arith=2)
+    assert a.flush_kernel_name(T).startswith("flush_f16q_kernel"), a.flush_kernel_name(T)
+    assert b.flush_kernel_name(T).startswith("flush_f32_wave_kernel"), b.flush_kernel_name(T)
+    for ens in (a, b):
+        for e in range(E):
+            ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+    rng = np.random.default_rng(5)
+    for step in range(1, 3 * T + 2):
+        enc, ln, nl = G.make_scan(w, step, instances=E, lines=6 if extra_every else 8)
+        if extra_every and step % extra_every == 0:
+            ex = G.random_lines(rng, 2)[None].repeat(E, axis=0)
+            ln = np.concatenate([ln, ex], axis=1)
+            nl = np.full(E, ln.shape[1], dtype=np.int32)
+        ra, rb = a.localize(enc, ln, nl), b.localize(enc, ln, nl)
+        for e in range(E):
+            assert ra[e]["match"] == rb[e]["match"], (step, e)
+            assert ra[e]["status"] == rb[e]["status"], (step, e)
+    for e in range(E):
+        Pa, ya, sa, pa = a.download_state(e)
+        Pb, yb, sb, pb = b.download_state(e)
+        assert sa == sb, e
+        assert np.array_equal(Pa, Pb) and np.array_equal(ya, yb), (e, rel(Pa, Pb))
+    a.close()
+    b.close()
+
+
 def _gate_case(ekf_mod, oracle_mod, prec, p22, p2a, daa, delta):
     """One landmark at (alpha 0.3, r 2.0) seen from the pose (0, 0, 0) without motion (the encoder
     equals the pose: F = I, Q = 0, Robot.cpp:136-286), its angle variance p22 / daa / covariance
