@@ -1527,6 +1527,53 @@ __device__ __forceinline__ void staged_pair_block(const PllView<T>& v, int wa, i
     }
 }
 
+// fp64 MFMA-replay contexts (plain pending steps, kmax = 16): the guessed winners' operand rows of
+// up to M64_QMAX pending steps staged in LDS as doubles, [winner t][step q][U, V][row][kk][s] (k =
+// 16·kk + s for s < 4: pll_blocks' fp64 k order), 32 KB for eight winners and eight steps.
+constexpr int M64_QMAX = 8;
+__device__ __forceinline__ int m64_stage_index(int t, int q, int uv, int rr, int kk)
+{
+    return ((((t * M64_QMAX + q) * 2 + uv) * 2 + rr) * 4 + kk) * 4;
+}
+
+// Block (2·wa, 2·wb) with the pending steps applied when both landmarks are guessed winners (guess
+// indices ta, tb), from the fp64 stage: per element pll_blocks' chain (per step the k-steps s <
+// ks, k-chunks kk, one fma per element and k), operand for operand. acc: the stored block in its
+// stored orientation (pair_block_load).
+template <typename T>
+__device__ __forceinline__ void m64_pair_block(const PllView<T>& v, int wa, int ta, int wb, int tb, const double* stg,
+                                               typename Stor<T>::C (&acc)[4], double (&out)[4])
+{
+    const int i0 = 2 * wa, jb = 2 * wb;
+    const bool swap = (i0 >> 5) > (jb >> 5);   // stored orientation: (jb, i0)
+    const int tA = swap ? tb : ta, tB = swap ? ta : tb;
+    for (int q = 0; q < v.npend; q++) {
+        const int ks = v.ctl[q].y;   // (no reset, no augmented rows on this path)
+        if (ks <= 0) continue;
+        const double* cu = stg + m64_stage_index(tA, q, 0, 0, 0);
+        const double* cv = stg + m64_stage_index(tB, q, 1, 0, 0);
+        for (int s = 0; s < ks; s++)
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                const double x0 = cu[kk * 4 + s], x1 = cu[16 + kk * 4 + s];
+                const double y0 = cv[kk * 4 + s], y1 = cv[16 + kk * 4 + s];
+                acc[0] = fma(x0, y0, (double)acc[0]);
+                acc[1] = fma(x0, y1, (double)acc[1]);
+                acc[2] = fma(x1, y0, (double)acc[2]);
+                acc[3] = fma(x1, y1, (double)acc[3]);
+            }
+#pragma unroll
+        for (int k = 0; k < 4; k++) acc[k] = vround<T>(v, acc[k]);
+    }
+    if (swap) {
+        out[0] = from_domain<T>(acc[0], v.ex); out[1] = from_domain<T>(acc[2], v.ex);
+        out[2] = from_domain<T>(acc[1], v.ex); out[3] = from_domain<T>(acc[3], v.ex);
+    } else {
+        out[0] = from_domain<T>(acc[0], v.ex); out[1] = from_domain<T>(acc[1], v.ex);
+        out[2] = from_domain<T>(acc[2], v.ex); out[3] = from_domain<T>(acc[3], v.ex);
+    }
+}
+
 // Split-bf16 contexts (ScanParams::mfrep): the pending steps' share of the blocks a scan reads,
 // ΔX = Σ_q V_q(rows)·V_q(cols)ᵀ over the active pending steps (amask: ks > 0; rolled-back steps
 // have ks = 0), by v_mfma_f32_16x16x32_bf16 on the operand planes the association kernels wrote
@@ -2338,12 +2385,41 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
             int pu = 0, pt = 0;   // replay-wave lane → mutual block (pu, pt), pt <= pu
             C pacc[4] = {0, 0, 0, 0};
             const int lane_r = tid - SCAN_THREADS;
-            if (staged && tid >= SCAN_THREADS && lane_r < L * (L + 1) / 2) {
+            // fp64 MFMA-replay contexts: the winners' mutual blocks from their U and V rows of every
+            // pending step staged in LDS (m64s, below) instead of a memory round trip per step
+            const bool m64s = m64 && p.npend <= M64_QMAX;
+            if ((staged || m64s) && tid >= SCAN_THREADS && lane_r < L * (L + 1) / 2) {
                 pt = lane_r;
                 while (pt > pu) { pt -= pu + 1; pu++; }
                 if (sh_spec[pu] >= 0 && sh_spec[pt] >= 0) pair_block_load<T>(pv, sh_spec[pu], sh_spec[pt], pacc);
             }
-            if (!staged && tid < L * (L + 1) / 2) {
+            if constexpr (sizeof(C) == 8)
+                if (m64s) {
+                    // rows 2w, 2w + 1 of U_q and V_q of every guessed winner w and pending step q,
+                    // all loads in flight together: pieces of 4 doubles (k = 16·kk + s, s < 4, as
+                    // pll_blocks reads them), [t][q][U, V][row][kk][s] (m64_stage_index), in history
+                    // slots 1.. (unused until the line loop's second match; slot 0 holds the
+                    // landmark waves' diagonal blocks meanwhile, the fp32 stage is not allocated here)
+                    static_assert((HIST_LDS - 1) * SCAN_THREADS * sizeof(double4) >= SPEC_L * M64_QMAX * 64 * sizeof(double),
+                                  "fp64 winners' stage");
+                    double* stg64 = reinterpret_cast<double*>(&sh_uhist[1][0]);
+                    typedef double d64x2 __attribute__((ext_vector_type(2)));
+                    const int nld = L * p.npend * 16;
+                    for (int k = tid; k < nld; k += SCAN_BLOCK) {
+                        const int piece = k & 15, tq = k >> 4, q = tq % p.npend, t = tq / p.npend;
+                        const int w = sh_spec[t];
+                        if (w < 0 || sh_ctl[q].y <= 0) continue;
+                        const int uv = piece >> 3, rr = (piece >> 2) & 1, kk = piece & 3;
+                        const int r = 2 * w + rr;
+                        const double* base = reinterpret_cast<const double*>(uv ? p.pend[q].Vop : p.pend[q].Uop) + e * opstride;
+                        const d64x2* src = reinterpret_cast<const d64x2*>(
+                            base + ((size_t)(r >> 5) * 64 + (r & 15)) * 8 + ((r >> 4) & 1) * 4 + 128 * kk);
+                        d64x2* dst = reinterpret_cast<d64x2*>(stg64 + m64_stage_index(t, q, uv, rr, kk));
+                        dst[0] = src[0];
+                        dst[1] = src[1];
+                    }
+                }
+            if (!staged && !m64s && tid < L * (L + 1) / 2) {
                 int u = 0, t = tid;
                 while (t > u) { t -= u + 1; u++; }
                 const int wu = sh_spec[u], wt = sh_spec[t];
@@ -2443,12 +2519,16 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
               }
-            } else if (staged && tid >= SCAN_THREADS) {
+            } else if ((staged || m64s) && tid >= SCAN_THREADS) {
                 // the winners' mutual blocks from the staged rows, by the replay wave itself
                 // (only it reads them): the landmark waves go straight on
                 if (lane_r < L * (L + 1) / 2 && sh_spec[pu] >= 0 && sh_spec[pt] >= 0) {
                     double bk[4];
-                    staged_pair_block<T>(pv, sh_spec[pu], pu, sh_spec[pt], pt, sh_stg, pacc, bk);
+                    if constexpr (sizeof(C) == 8)
+                        m64_pair_block<T>(pv, sh_spec[pu], pu, sh_spec[pt], pt,
+                                          reinterpret_cast<const double*>(&sh_uhist[1][0]), pacc, bk);
+                    else
+                        staged_pair_block<T>(pv, sh_spec[pu], pu, sh_spec[pt], pt, sh_stg, pacc, bk);
                     double* r = sh_wd + pu * SPEC_WD + (pt == pu ? 6 : 14 + 4 * pt);
                     r[0] = bk[0]; r[1] = bk[1]; r[2] = bk[2]; r[3] = bk[3];
                 }
@@ -2671,64 +2751,84 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                     const int wr = wsp >= 0 ? 2 * wsp + (c & 1) : 0;
                     const size_t coff = (size_t)(wr >> 5) * 64 * KH + ((wr & 15) + 16 * (l >> 4)) * KH + ((wr >> 4) & 1) * 4;
                     auto comp = [](double4& v, int k) -> double& { return reinterpret_cast<double*>(&v)[k]; };
+                    // two tile rows per pass, the pending steps inside: each step's operand loads of
+                    // both row blocks are in flight together (a memory round trip per step and pair,
+                    // not per step and tile row); per accumulator the same MFMA sequence
 #pragma unroll 1
-                    for (int r4 = 0; r4 < 4; r4++) {
-                        const int rb = rb0 + r4;
+                    for (int r2 = 0; r2 < 4; r2 += 2) {
                         // (the last workgroup's waves may reach past the landmark block: no rows,
                         // no operand rows there)
-                        if (rb >= d.nb) break;
-                        const bool sw = wsp >= 0 && rb > (wr >> 5);   // stored transposed
-                        const bool nsw = wsp >= 0 && !sw;
-                        d64x4 acc[2], dac[2];
+                        if (rb0 + r2 >= d.nb) break;
+                        const bool two = rb0 + r2 + 1 < d.nb;   // (uniform)
+                        bool sw[2], nsw[2];
+                        d64x4 acc[2][2], dac[2][2];
 #pragma unroll
-                        for (int h = 0; h < 2; h++)
+                        for (int x = 0; x < 2; x++) {
+                            const int r4 = r2 + x, rb = rb0 + r4;
+                            sw[x] = wsp >= 0 && rb > (wr >> 5);   // stored transposed
+                            nsw[x] = wsp >= 0 && !sw[x];
 #pragma unroll
-                            for (int i = 0; i < 4; i++) {
-                                const int rl = 32 * r4 + 16 * h + 4 * i + (l >> 4);   // row in the wave (tile_off_f64)
-                                const int ow = wb + (rl >> 1);
-                                acc[h][i] = comp(sh_blk64[t][ow], (rl & 1) * 2 + (c & 1));
-                                const int cl = 32 * r4 + 16 * h + c;
-                                dac[h][i] = (rl >> 1) == (cl >> 1) ? comp(dg[ow], (rl & 1) * 2 + (cl & 1)) : 0.0;
-                            }
+                            for (int h = 0; h < 2; h++)
+#pragma unroll
+                                for (int i = 0; i < 4; i++) {
+                                    const int rl = 32 * r4 + 16 * h + 4 * i + (l >> 4);   // row in the wave (tile_off_f64)
+                                    const int ow = wb + (rl >> 1);
+                                    acc[x][h][i] = comp(sh_blk64[t][ow], (rl & 1) * 2 + (c & 1));
+                                    const int cl = 32 * r4 + 16 * h + c;
+                                    dac[x][h][i] = (rl >> 1) == (cl >> 1) ? comp(dg[ow], (rl & 1) * 2 + (cl & 1)) : 0.0;
+                                }
+                        }
                         for (int q = 0; q < p.npend; q++) {
                             if (sh_ctl[q].y <= 0) continue;   // no match, or rolled back: nothing
                             const double* Uq = reinterpret_cast<const double*>(p.pend[q].Uop) + e * opstride;
                             const double* Vq = reinterpret_cast<const double*>(p.pend[q].Vop) + e * opstride;
-                            const d64x2* uo = reinterpret_cast<const d64x2*>(Uq + (size_t)rb * 64 * KH + l * KH);
-                            const d64x2* vo = reinterpret_cast<const d64x2*>(Vq + (size_t)rb * 64 * KH + l * KH);
-                            d64x2 ua[4], va[4], cu[2], cv[2];
+                            d64x2 ua[2][4], va[2][4], cu[2], cv[2];
 #pragma unroll
-                            for (int k = 0; k < 4; k++) { ua[k] = uo[k]; va[k] = vo[k]; }
+                            for (int x = 0; x < 2; x++) {
+                                // (a second row block past the landmark block re-reads the first)
+                                const int rb = rb0 + r2 + (two ? x : 0);
+                                const d64x2* uo = reinterpret_cast<const d64x2*>(Uq + (size_t)rb * 64 * KH + l * KH);
+                                const d64x2* vo = reinterpret_cast<const d64x2*>(Vq + (size_t)rb * 64 * KH + l * KH);
+#pragma unroll
+                                for (int k = 0; k < 4; k++) { ua[x][k] = uo[k]; va[x][k] = vo[k]; }
+                            }
 #pragma unroll
                             for (int k = 0; k < 2; k++) {
                                 cu[k] = reinterpret_cast<const d64x2*>(Uq + coff)[k];
                                 cv[k] = reinterpret_cast<const d64x2*>(Vq + coff)[k];
                             }
 #pragma unroll
-                            for (int s4 = 0; s4 < 4; s4++) {
-                                const double bv = nsw ? cv[s4 >> 1][s4 & 1] : 0.0;
-                                const double bu = sw ? cu[s4 >> 1][s4 & 1] : 0.0;
+                            for (int x = 0; x < 2; x++)
 #pragma unroll
-                                for (int h = 0; h < 2; h++) {
-                                    const double au = ua[2 * h + (s4 >> 1)][s4 & 1];
-                                    const double av = va[2 * h + (s4 >> 1)][s4 & 1];
-                                    acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(au, bv, acc[h], 0, 0, 0);
-                                    acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bu, acc[h], 0, 0, 0);
-                                    dac[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(au, av, dac[h], 0, 0, 0);
+                                for (int s4 = 0; s4 < 4; s4++) {
+                                    const double bv = nsw[x] ? cv[s4 >> 1][s4 & 1] : 0.0;
+                                    const double bu = sw[x] ? cu[s4 >> 1][s4 & 1] : 0.0;
+#pragma unroll
+                                    for (int h = 0; h < 2; h++) {
+                                        const double au = ua[x][2 * h + (s4 >> 1)][s4 & 1];
+                                        const double av = va[x][2 * h + (s4 >> 1)][s4 & 1];
+                                        acc[x][h] = __builtin_amdgcn_mfma_f64_16x16x4f64(au, bv, acc[x][h], 0, 0, 0);
+                                        acc[x][h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bu, acc[x][h], 0, 0, 0);
+                                        dac[x][h] = __builtin_amdgcn_mfma_f64_16x16x4f64(au, av, dac[x][h], 0, 0, 0);
+                                    }
                                 }
-                            }
                         }
                         __builtin_amdgcn_wave_barrier();   // (every lane read its starting values)
 #pragma unroll
-                        for (int h = 0; h < 2; h++)
+                        for (int x = 0; x < 2; x++) {
+                            if (x == 1 && !two) break;
+                            const int r4 = r2 + x;
 #pragma unroll
-                            for (int i = 0; i < 4; i++) {
-                                const int rl = 32 * r4 + 16 * h + 4 * i + (l >> 4);
-                                const int ow = wb + (rl >> 1);
-                                comp(sh_blk64[t][ow], (rl & 1) * 2 + (c & 1)) = acc[h][i];
-                                const int cl = 32 * r4 + 16 * h + c;
-                                if ((rl >> 1) == (cl >> 1)) comp(dg[ow], (rl & 1) * 2 + (cl & 1)) = dac[h][i];
-                            }
+                            for (int h = 0; h < 2; h++)
+#pragma unroll
+                                for (int i = 0; i < 4; i++) {
+                                    const int rl = 32 * r4 + 16 * h + 4 * i + (l >> 4);
+                                    const int ow = wb + (rl >> 1);
+                                    comp(sh_blk64[t][ow], (rl & 1) * 2 + (c & 1)) = acc[x][h][i];
+                                    const int cl = 32 * r4 + 16 * h + c;
+                                    if ((rl >> 1) == (cl >> 1)) comp(dg[ow], (rl & 1) * 2 + (cl & 1)) = dac[x][h][i];
+                                }
+                        }
                     }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                     __builtin_amdgcn_wave_barrier();

@@ -839,12 +839,15 @@ def test_active_flush_equals_full_flush(ekf_mod, arith, N, active, T, extra_ever
     b.close()
 
 
-@pytest.mark.parametrize("N,T,lines", [(2000, 4, 8), (4096, 4, 8), (100, 8, 8), (300, 6, 5)])
+@pytest.mark.parametrize("N,T,lines", [(2000, 4, 8), (4096, 4, 8), (100, 8, 8), (300, 6, 5), (4096, 8, 8),
+                                        (1000, 8, 8), (520, 8, 3)])
 def test_f64_mfma_replay_equals_per_element_replay(ekf_mod, N, T, lines):
     """fp64 storage, speculative association with pending steps: the owned blocks of the guessed
     columns and the diagonal blocks replayed by v_mfma_f64_16x16x4f64 (EKF_OPT_MFMA_REPLAY = 1,
-    default) give the same matches, P and y bit for bit as the per-element FMA replay (0). N = 100
-    and 300 leave lanes without a landmark in the last wave; N = 4096 is the bench's shape."""
+    default; two tile rows per pass), and the winners' mutual blocks from their operand rows staged
+    in LDS, give the same matches, P and y bit for bit as the per-element FMA replay (0). N = 100,
+    300 and 520 leave lanes without a landmark in the last wave (and a lone last tile row of a
+    pass); N = 4096 at T = 8 is the bench's fp64 shape (up to seven pending steps)."""
     E = 3
     w = G.make_world(N)
     st = G.initial_state(w)
