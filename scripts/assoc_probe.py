@@ -14,7 +14,7 @@ NAMES = {0: "predict+state", 1: "diag+ctl", 5: "guess", 2: "exchange1", 10: "res
          4: "rw_gain+robot", 16: "lw_gate", 17: "lw_wait_pkg", 18: "lw_gain+store", 19: "lw_robot",
          14: "landmark_total", 6: "verdict", 27: "commit:augment", 28: "commit:state", 24: "commit:operands", 25: "commit:planes", 26: "commit:collect",
          7: "commit:record", 8: "total", 15: "fallbacks"}
-E = 8
+E = int(os.environ.get("PROBE_E", "8"))
 cfgs = sys.argv[1:] or ["4096:8", "4096:1", "1024:8"]
 for c in cfgs:
     N, T = (int(x) for x in c.split(":"))

@@ -88,9 +88,14 @@ struct ekf_ctx {
     int nwt24;
     ekf::WtEntry* wtq;        // split-fp16 quad form: groups of 2 × 2 wave-tiles (four entries each)
     int nwtq;
-    double* d_enc;
+    double* d_enc;            // the scan inputs: views of d_in, staged from h_in by one copy
     ekf_line* d_lines;
     int* d_nlines;
+    char* d_in;
+    char* h_in;               // pinned
+    size_t in_lines, in_nlines, in_bytes;   // byte offsets of the lines and counts, the total
+    int in_pending;           // a copy from h_in was enqueued (ev_in)
+    hipEvent_t ev_in;
     void* rccl_comm;          // ekf_shard_attach_rccl: the partitioned instance's own communicator
     double* sh_xbuf;          // ... and ekf_shard_localize's exchange buffers (device): [N][4] + flag,
     double* sh_xcols;         // [L][N][4] + flag + stopping line
@@ -98,6 +103,16 @@ struct ekf_ctx {
     int sh_dirty;             // a failed scan left nonzero flag words
     int* h_res;
     double* h_pose;
+    // the synchronous calls' result mirror (ScanParams::res_host): pinned, written by the scan's
+    // lead; h_r33 the robot block, h_ep the epoch of each instance's last mirrored commit
+    double* h_r33;
+    unsigned* h_ep;
+    int* hd_res;              // (their device pointers)
+    double* hd_pose;
+    double* hd_r33;
+    unsigned* hd_ep;
+    int mirror_on;            // the association launch being enqueued writes the mirror
+    unsigned mirror_epoch;    // scan_epoch of the mirrored robot blocks (0: none valid)
     int dd_grid;
     int dd_per_cu;            // flush workgroups per CU of the grid-strided forms (EKF_OPT_FLUSH_BLOCKS_PER_CU)
     int dd_variant;           // f32 flush kernel form (EKF_OPT_FLUSH_FORM)
@@ -196,7 +211,7 @@ int ekf_abi_version(void) { return SLAM_EKF_ABI_VERSION; }
 static void free_all(ekf_ctx* c)
 {
     std::vector<void*> ptrs = {c->X[0], c->X[1], c->Rs, c->y, c->cur, c->pose, c->xpre, c->saved, c->D,
-                               c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->wt24, c->wtq, c->d_enc, c->d_lines, c->d_nlines, c->dbg, c->pexp, c->sink, c->mbox,
+                               c->tile_rc, c->stile_rc, c->stile2_rc, c->wt, c->wt64, c->wt24, c->wtq, c->d_in, c->dbg, c->pexp, c->sink, c->mbox,
                                c->sync, c->Ust, c->Vst, c->dense, c->psig, c->pvmax,
                                c->sh_rob, c->sh_rec, c->sh_hist, c->sh_pkg, c->sh_flags, c->sh_ctl,
                                c->sh_null.res, c->sh_xbuf, c->sh_xcols};
@@ -213,6 +228,10 @@ static void free_all(ekf_ctx* c)
     if (c->h_agree) (void)hipHostFree(c->h_agree);
     if (c->h_res) (void)hipHostFree(c->h_res);
     if (c->h_pose) (void)hipHostFree(c->h_pose);
+    if (c->h_r33) (void)hipHostFree(c->h_r33);
+    if (c->h_in) (void)hipHostFree(c->h_in);
+    if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+    if (c->h_ep) (void)hipHostFree(c->h_ep);
     for (auto& v : c->ev)
         for (auto& pr : v) { (void)hipEventDestroy(pr.a); (void)hipEventDestroy(pr.b); }
     for (auto& pr : c->pool) { (void)hipEventDestroy(pr.a); (void)hipEventDestroy(pr.b); }
@@ -481,9 +500,13 @@ static int create_ctx(const ekf_config* cfg, int sh_rank, int sh_world, ekf_ctx*
         ALLOC(c->stile_rc, sizeof(int2) * (size_t)nsb * (nsb + 1) / 2);
         ALLOC(c->stile2_rc, sizeof(int2) * (size_t)nsb * ((d.nb + 1) / 2));
     }
-    ALLOC(c->d_enc, sizeof(double) * 3 * E);
-    ALLOC(c->d_lines, sizeof(ekf_line) * d.max_lines * E);
-    ALLOC(c->d_nlines, sizeof(int) * E);
+    c->in_lines = ((sizeof(double) * 3 * E + 15) / 16) * 16;
+    c->in_nlines = c->in_lines + ((sizeof(ekf_line) * d.max_lines * E + 15) / 16) * 16;
+    c->in_bytes = c->in_nlines + sizeof(int) * E;
+    ALLOC(c->d_in, c->in_bytes);
+    c->d_enc = reinterpret_cast<double*>(c->d_in);
+    c->d_lines = reinterpret_cast<ekf_line*>(c->d_in + c->in_lines);
+    c->d_nlines = reinterpret_cast<int*>(c->d_in + c->in_nlines);
     ALLOC(c->pexp, sizeof(int) * E);
     ALLOC(c->sink, 8 * ekf::TILE_ELEMS);
     c->pexp_h.assign(E, 0);
@@ -522,6 +545,16 @@ static int create_ctx(const ekf_config* cfg, int sh_rank, int sh_world, ekf_ctx*
 #undef ALLOC
     if (hipHostMalloc((void**)&c->h_res, sizeof(int) * ekf::RES_STRIDE * E) != hipSuccess) goto fail;
     if (hipHostMalloc((void**)&c->h_pose, sizeof(double) * 3 * E) != hipSuccess) goto fail;
+    if (hipHostMalloc((void**)&c->h_r33, sizeof(double) * 9 * E) != hipSuccess) goto fail;
+    if (hipHostMalloc((void**)&c->h_ep, sizeof(unsigned) * E) != hipSuccess) goto fail;
+    if (hipHostMalloc((void**)&c->h_in, c->in_bytes) != hipSuccess) goto fail;
+    if (hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess) goto fail;
+    memset(c->h_ep, 0, sizeof(unsigned) * E);
+    if (hipHostGetDevicePointer((void**)&c->hd_res, c->h_res, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&c->hd_pose, c->h_pose, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&c->hd_r33, c->h_r33, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&c->hd_ep, c->h_ep, 0) != hipSuccess)
+        goto fail;
     rc = EKF_EDEVICE;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) goto fail;
     if (hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking) != hipSuccess) goto fail;
@@ -846,6 +879,7 @@ extern "C" int ekf_get_option(const ekf_ctx* c, int opt, int* v)
 
 extern "C" int ekf_reset_instance(ekf_ctx* c, int e, double x, double y, double th)
 {
+    if (c) c->mirror_epoch = 0;   // (the robot block changes without a scan)
     if (!c) return EKF_EINVAL;
     if (e >= c->cfg.instances) return EKF_ERANGE;
     int rc = drain(c);
@@ -954,6 +988,12 @@ static ekf::ScanParams scan_params(ekf_ctx* c, int phase, const double* enc,
     p.mbox = c->mbox;
     p.sync = c->sync;
     p.sync_stride = c->sync_stride;
+    if (c->mirror_on) {
+        p.res_host = c->hd_res;
+        p.pose_host = c->hd_pose;
+        p.r33_host = c->hd_r33;
+        p.ep_host = c->hd_ep;
+    }
     return p;
 }
 
@@ -1083,7 +1123,7 @@ static int enqueue(ekf_ctx* c, int phase, const double* enc, const ekf_line* lin
     EvPair* pr = prof_begin(c, 0, c->stream);
     HIP_TRY(launch_scans(c, sp));
     prof_end(c, pr, c->stream);
-    if (c->cfg.pipeline) HIP_TRY(hipEventRecord(c->ev_scan, c->stream));
+    if (c->cfg.pipeline || c->mirror_on) HIP_TRY(hipEventRecord(c->ev_scan, c->stream));
     c->nsteps++;
     if (c->nsteps - c->unflushed0 >= c->T) return enqueue_flush(c);
     return EKF_OK;
@@ -1095,17 +1135,31 @@ static int stage_inputs(ekf_ctx* c, const double* enc, const ekf_line* lines, co
     if (nlines)
         for (int e = 0; e < E; e++)
             if (nlines[e] < 0 || nlines[e] > c->d.max_lines) return EKF_ERANGE;
-    // the previous step's association kernel may still read the staging buffers
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (enc)
-        HIP_TRY(hipMemcpyAsync(c->d_enc, enc, sizeof(double) * 3 * E, hipMemcpyHostToDevice,
-                               c->stream));
-    if (lines)
-        HIP_TRY(hipMemcpyAsync(c->d_lines, lines, sizeof(ekf_line) * c->d.max_lines * E,
-                               hipMemcpyHostToDevice, c->stream));
-    if (nlines)
-        HIP_TRY(hipMemcpyAsync(c->d_nlines, nlines, sizeof(int) * E, hipMemcpyHostToDevice,
-                               c->stream));
+    // into the pinned staging buffer (once the previous copy out of it has been done), then one
+    // stream-ordered copy of the sections given: the device buffers are rewritten after the
+    // association kernels that read them
+    if (c->in_pending) HIP_TRY(hipEventSynchronize(c->ev_in));
+    size_t lo = c->in_bytes, hi = 0;
+    if (enc) {
+        memcpy(c->h_in, enc, sizeof(double) * 3 * E);
+        lo = 0;
+        hi = sizeof(double) * 3 * E;
+    }
+    if (lines) {
+        memcpy(c->h_in + c->in_lines, lines, sizeof(ekf_line) * c->d.max_lines * E);
+        lo = std::min(lo, c->in_lines);
+        hi = c->in_nlines;
+    }
+    if (nlines) {
+        memcpy(c->h_in + c->in_nlines, nlines, sizeof(int) * E);
+        lo = std::min(lo, c->in_nlines);
+        hi = c->in_bytes;
+    }
+    if (hi > lo) {
+        HIP_TRY(hipMemcpyAsync(c->d_in + lo, c->h_in + lo, hi - lo, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipEventRecord(c->ev_in, c->stream));
+        c->in_pending = 1;
+    }
     return EKF_OK;
 }
 
@@ -1167,15 +1221,35 @@ static void fill_results(const ekf_ctx* c, ekf_result* out)
     }
 }
 
+// A synchronous call's update: the scan's lead mirrors a committed result into pinned host memory
+// (ScanParams::res_host), so the call waits for the association kernel only (not for a flush queued
+// behind it) and reads the result without a copy; the robot blocks it mirrored serve
+// ekf_get_pose_cov until the next launch. Any instance without this launch's epoch in its mirror
+// (a rollback, a lead that never finished) takes the copies and the host fold of ekf_read_results.
+static int enqueue_mirrored(ekf_ctx* c, int phase, ekf_result* out)
+{
+    c->mirror_on = 1;
+    const int rc = enqueue(c, phase, c->d_enc, c->d_lines, c->d_nlines);
+    c->mirror_on = 0;
+    if (rc) return rc;
+    c->mirror_epoch = 0;
+    HIP_TRY(hipEventSynchronize(c->ev_scan));
+    const int E = c->cfg.instances;
+    bool all = true;
+    for (int e = 0; e < E; e++) all = all && __atomic_load_n(c->h_ep + e, __ATOMIC_ACQUIRE) == c->scan_epoch;
+    if (!all) return ekf_read_results(c, out);
+    c->mirror_epoch = c->scan_epoch;
+    fill_results(c, out);
+    return EKF_OK;
+}
+
 extern "C" int ekf_localize(ekf_ctx* c, const double* enc, const ekf_line* lines,
                             const int32_t* nlines, ekf_result* out)
 {
     if (!c || !enc || !lines || !nlines || c->sh_world > 0) return EKF_EINVAL;
     int rc = stage_inputs(c, enc, lines, nlines);
     if (rc) return rc;
-    rc = enqueue(c, ekf::PHASE_BOTH, c->d_enc, c->d_lines, c->d_nlines);
-    if (rc) return rc;
-    return ekf_read_results(c, out);
+    return enqueue_mirrored(c, ekf::PHASE_BOTH, out);
 }
 
 extern "C" int ekf_localize_device(ekf_ctx* c, const double* d_enc, const ekf_line* d_lines,
@@ -1199,9 +1273,7 @@ extern "C" int ekf_update(ekf_ctx* c, const ekf_line* lines, const int32_t* nlin
     if (!c || !lines || !nlines || c->sh_world > 0) return EKF_EINVAL;
     int rc = stage_inputs(c, nullptr, lines, nlines);
     if (rc) return rc;
-    rc = enqueue(c, ekf::PHASE_UPDATE, c->d_enc, c->d_lines, c->d_nlines);
-    if (rc) return rc;
-    return ekf_read_results(c, out);
+    return enqueue_mirrored(c, ekf::PHASE_UPDATE, out);
 }
 
 // The dense n × n fp64 scratch of the state transfers: allocated on first use and kept, so that a
@@ -1222,6 +1294,7 @@ static hipError_t dense_scratch(ekf_ctx* c, double** out)
 extern "C" int ekf_upload_state(ekf_ctx* c, int e, const double* P, const double* y, int saved,
                                 const double pose[3])
 {
+    if (c) c->mirror_epoch = 0;   // (the robot block changes without a scan)
     if (!c) return EKF_EINVAL;
     if (e < 0 || e >= c->cfg.instances) return EKF_ERANGE;
     if (saved < 0 || saved > c->d.N) return EKF_ERANGE;
@@ -1304,6 +1377,7 @@ extern "C" int ekf_download_state(ekf_ctx* c, int e, double* P, double* y, int* 
 extern "C" int ekf_init_lowrank(ekf_ctx* c, int e, const double* diag, const double* U, int rank,
                                 const double* y, int saved, const double pose[3])
 {
+    if (c) c->mirror_epoch = 0;   // (the robot block changes without a scan)
     if (!c || !diag || (rank > 0 && !U) || rank < 0) return EKF_EINVAL;
     if (e < 0 || e >= c->cfg.instances) return EKF_ERANGE;
     int rc = drain(c);
@@ -1348,6 +1422,7 @@ extern "C" int ekf_storage_exponent(const ekf_ctx* c, int e)
 
 extern "C" int ekf_rescale(ekf_ctx* c, int e, int ex)
 {
+    if (c) c->mirror_epoch = 0;   // (the robot block changes without a scan)
     if (!c) return EKF_EINVAL;
     if (e < 0 || e >= c->cfg.instances) return EKF_ERANGE;
     if (c->cfg.precision != EKF_PREC_F16) return EKF_OK;
@@ -1386,6 +1461,11 @@ extern "C" int ekf_get_pose_cov(ekf_ctx* c, int e, double P33[9])
 {
     if (!c || !P33) return EKF_EINVAL;
     if (e < 0 || e >= c->cfg.instances) return EKF_ERANGE;
+    if (c->mirror_epoch != 0 && c->mirror_epoch == c->scan_epoch) {
+        // the robot block the last synchronous call's scan committed (no launch since)
+        memcpy(P33, c->h_r33 + 9 * (size_t)e, sizeof(double) * 9);
+        return EKF_OK;
+    }
     const Dims& d = c->d;
     int cb = 0;
     const int rc = strip_copy(c, e, &cb);

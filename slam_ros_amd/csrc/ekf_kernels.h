@@ -138,6 +138,13 @@ struct ScanParams {
     const int* nlines;    // [E]
     const int* pexp;      // [E] fp16 storage exponent (P stored as 2^pexp·P)
     unsigned long long* dbg;  // optional [E][16] phase timers (s_memrealtime ticks, 100 MHz)
+    // synchronous calls (ekf_localize / ekf_update): the lead also writes a committed step's result
+    // words and folded status, pose and robot 3×3 block into pinned host memory (device pointers of
+    // host-mapped buffers), then the launch epoch into ep_host[e] (system-scope release); nullptr: off
+    int* res_host;        // [Etot][RES_STRIDE]
+    double* pose_host;    // [Etot][3]
+    double* r33_host;     // [Etot][9]
+    unsigned* ep_host;    // [Etot]
 };
 
 // One instance whose landmark block is partitioned over ranks: rank r

@@ -3461,6 +3461,26 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
             res[RES_PSIG] = ploss ? PLANE_SIGMA_EXACT : psig;
             // nonzero operand rows only below zg workgroups' landmarks; new rows below s + nadd
             res[RES_ZMAX] = max(min(zg * SCAN_THREADS, N), reset ? 0 : s + nadd);
+            if (p.res_host) {
+                // the synchronous call's result without a copy: the words ekf_result takes (the
+                // status with every workgroup's bits, as the host's fold of the completion words
+                // would give: the lead collected them), the pose and the robot block, then the
+                // epoch. A rollback writes none of it (the host then reads the device copies)
+                int* rh = p.res_host + (size_t)e * RES_STRIDE;
+                rh[RES_NLINES] = L;
+                rh[RES_STATUS] = res[RES_STATUS] | (wgst & DONE_STATUS_MASK);
+                rh[RES_M] = m;
+                rh[RES_NEXTRA] = nextra;
+                rh[RES_SAVED] = reset ? 0 : s + nadd;
+                rh[RES_RESET] = reset;
+                for (int i = 0; i < L; i++) rh[RES_MATCH + i] = res[RES_MATCH + i];
+                p.pose_host[3 * e + 0] = pose[0];
+                p.pose_host[3 * e + 1] = pose[1];
+                p.pose_host[3 * e + 2] = pose[2];
+                for (int a = 0; a < 9; a++) p.r33_host[9 * e + a] = R33[a];
+                __threadfence_system();
+                __hip_atomic_store(p.ep_host + e, p.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             p.saved[e] = reset ? 0 : s + nadd;
             p.live[e] = 1 - cb;
             if (pf16) {

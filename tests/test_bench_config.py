@@ -376,8 +376,11 @@ def test_survey_world_parity_from_init(ekf_mod, oracle_mod, arith, T, rep):
     out = run_survey_parity(ekf_mod, oracle_mod, arith, T, 0, 48, options={"mfma_replay": rep})
     record(f"survey_parity_init_a{arith}_T{T}_rep{rep}", out)
     # from the initial state the restatement predicts one unresolved scan per instance (scan 30:
-    # instance 0's gate, instance 7's cancellation; CPU restatement alone): most is checked
-    assert out["assoc_checked"] >= 0.7 * out["instance_scans"], out
+    # instance 0's gate, instance 7's cancellation; CPU restatement alone): few predictions, each
+    # exempting at most the rest of its flush group (T − 1 scans); everything else is checked
+    assert out["oracle_predicted"] <= 0.05 * out["instance_scans"], out
+    assert out["exempt_after_prediction"] <= out["oracle_predicted"] * (T - 1), out
+    assert out["assoc_checked"] >= out["instance_scans"] - out["oracle_predicted"] * T, out
 
 
 @pytest.mark.parametrize("arith,T,rep", [(2, 20, 1), (2, 20, 2), (0, 16, 1)])

@@ -261,6 +261,43 @@ def test_predict_then_update_equals_localize(ekf_mod, prec):
         np.testing.assert_array_equal(pa, pb)
 
 
+@pytest.mark.parametrize("prec,T", [(0, 1), (1, 4), (0, 8)])
+def test_synchronous_result_mirror(ekf_mod, prec, T):
+    """ekf_localize / ekf_update read their result from the pinned mirror the scan's lead writes (no
+    copies; the call waits for the association kernel only) and ekf_get_pose_cov the mirrored robot
+    block until the next launch: equal to the device copies (ekf_read_results, the state's top-left
+    3 × 3), also after a state upload or an asynchronous launch invalidated the mirror."""
+    N, E = 300, 3
+    w = G.make_world(N)
+    st = G.initial_state(w)
+    ens = ekf_mod.Ensemble(N, E, prec, max_lines=8, flush_interval=T)
+    for e in range(E):
+        ens.init_lowrank(e, st.diag, st.U, st.y, st.saved, st.pose)
+    for step in range(1, 2 * T + 3):
+        enc, ln, nl = G.make_scan(w, step, instances=E)
+        if step % 3 == 0:
+            ens.predict(enc)
+            res = ens.update(ln, nl)
+        else:
+            res = ens.localize(enc, ln, nl)
+        p33 = [ens.pose_cov(e) for e in range(E)]   # (the mirror, before any other call)
+        dev = ens.read_results()                      # the device copies and the host fold
+        for e in range(E):
+            np.testing.assert_array_equal(res[e]["pose"], dev[e]["pose"])
+            assert ({k: v for k, v in res[e].items() if k != "pose"} ==
+                    {k: v for k, v in dev[e].items() if k != "pose"}), (step, e)
+            P, y, saved, pose = ens.download_state(e)
+            np.testing.assert_array_equal(p33[e], P[:3, :3])
+            np.testing.assert_array_equal(res[e]["pose"], pose)
+            assert res[e]["saved"] == saved and res[e]["matches"] == 8
+    # an upload changes the robot block without a scan: the mirror no longer serves it
+    P, y, saved, pose = ens.download_state(1)
+    P[:3, :3] *= 1.5
+    ens.upload_state(1, P, y, saved, pose)
+    np.testing.assert_array_equal(ens.pose_cov(1), P[:3, :3])
+    ens.close()
+
+
 @pytest.mark.parametrize("prec", [0, 1, 2])
 def test_ensemble_instances_are_independent(ekf_mod, prec):
     N, E = 64, 3
