@@ -1814,12 +1814,12 @@ extern "C" int ekf_shard_resume(ekf_ctx* c, int line)
     return EKF_OK;
 }
 
-extern "C" int ekf_shard_end(ekf_ctx* c, ekf_result* out)
+// SH_END with its results mirrored into the pinned host buffers (one instance), so the result
+// needs no copy: only the wait for this kernel, not for a flush behind it. gate (ekf_shard_localize):
+// the ranks' agreement [failure flag, stopping line] on the device; the phase commits only if it
+// says every line ran, and mirrors the pair into h_agree either way
+static int shard_end_launch(ekf_ctx* c, const double* gate)
 {
-    if (!c || c->sh_open != 1 || c->sh_line != c->sh_L) return EKF_EINVAL;
-    // (with no line, begin's exchange is not consumed: the end needs no diagonal block). The
-    // phase also writes the step's record and pose into the pinned host buffers (one instance),
-    // so the result needs no copy: only the wait for this kernel, not for a flush behind it
     ekf::ShardParams p = shard_params(c, ekf::SH_END, nullptr);
     int* rh = nullptr;
     double* ph = nullptr;
@@ -1827,18 +1827,39 @@ extern "C" int ekf_shard_end(ekf_ctx* c, ekf_result* out)
     HIP_TRY(hipHostGetDevicePointer((void**)&ph, c->h_pose, 0));
     p.res_host = rh;
     p.pose_host = ph;
+    if (gate) {
+        double* ah = nullptr;
+        HIP_TRY(hipHostGetDevicePointer((void**)&ah, c->h_agree, 0));
+        p.end_gate = gate;
+        p.end_gate_host = ah;
+    }
     SH_TRY(ekf::launch_shard(p, c->cfg.precision, c->stream));
     HIP_TRY(hipEventRecord(c->ev_scan, c->stream));
+    return EKF_OK;
+}
+
+// after a committed SH_END: the step joins the deferred flush of the rank's tiles; the results
+// from the mirror once the phase has finished (flushed: the wait was before the flush's launch)
+static int shard_end_finish(ekf_ctx* c, ekf_result* out, bool waited)
+{
     c->sh_open = 0;
-    // the step joins the deferred flush of the rank's tiles
     c->nsteps++;
     if (c->nsteps - c->unflushed0 >= c->T) {
         const int rc = enqueue_flush(c);
         if (rc) return rc;
     }
-    HIP_TRY(hipEventSynchronize(c->ev_scan));
+    if (!waited) HIP_TRY(hipEventSynchronize(c->ev_scan));
     fill_results(c, out);
     return EKF_OK;
+}
+
+extern "C" int ekf_shard_end(ekf_ctx* c, ekf_result* out)
+{
+    if (!c || c->sh_open != 1 || c->sh_line != c->sh_L) return EKF_EINVAL;
+    // (with no line, begin's exchange is not consumed: the end needs no diagonal block)
+    const int rc = shard_end_launch(c, nullptr);
+    if (rc) return rc;
+    return shard_end_finish(c, out, false);
 }
 
 extern "C" int ekf_shard_abort(ekf_ctx* c)
@@ -1991,10 +2012,22 @@ extern "C" int ekf_shard_localize(ekf_ctx* c, const double enc[3], const ekf_lin
             c->sh_dirty = 1;
         }
         if (!sum(agree, 2, ncclMax)) return EKF_EDEVICE;
-        HIP_TRY(hipMemcpyAsync(c->h_agree, agree, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        // the end phase goes behind the run before the host reads the agreement: it commits only if
+        // every line ran on every rank (the common case: one host round trip per scan), and leaves
+        // everything untouched otherwise, when the lines from the agreed one follow as below
+        bool gated = false;
+        if (!err) {
+            c->sh_line = L;
+            err = shard_end_launch(c, agree);
+            gated = !err;
+        }
+        if (!gated)
+            HIP_TRY(hipMemcpyAsync(c->h_agree, agree, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         abandon = c->h_agree[0] > 0.0 || c->h_agree[1] > (double)L;   // (past L: a run timed out)
         first = abandon ? L : (int)c->h_agree[1];
+        if (gated && !abandon && first == L) return shard_end_finish(c, out, true);
+        if (gated) c->sh_line = -1;   // (not committed: the run's state stands, as after ekf_shard_run)
         // (host bookkeeping only, on the agreed line: it fails on every rank alike or on none)
         if (!abandon && !err) err = ekf_shard_resume(c, first);
         spec_all = first == L;

@@ -201,6 +201,9 @@ struct ShardParams {
     int mbw;
     unsigned epoch;       // its tag epoch (one per launch)
     int spin_log2;        // its bounded waits
+    const double* end_gate;   // SH_END (ekf_shard_localize): commit only if the ranks' agreement
+    double* end_gate_host;    // [failure flag, stopping line] is [0, L]; the pair also into pinned host
+                              // memory (device pointer) either way (nullptr: commit unconditionally)
 };
 hipError_t launch_shard(const ShardParams& p, int precision, hipStream_t st);
 // lines [ctl[SC_NEXT], L) of the speculative path on shard_run_workgroups(N) cooperating
@@ -212,6 +215,9 @@ constexpr int SH_THREADS = 64;     // shard_kernel's workgroup
 #endif
 constexpr int SHR_THREADS = EKF_SHR_THREADS;   // shard_run_kernel's workgroup: landmarks per workgroup
 constexpr int SHR_GMAX = 64;       // ... and at most this many workgroups (more landmarks per thread past it)
+#ifndef EKF_SHARD_SPEC
+#define EKF_SHARD_SPEC 1           // launch_shard_run: shard_spec_kernel where it applies (0: shard_run_kernel always)
+#endif
 inline int shard_run_workgroups(int N)
 {
     const int g = (N + SHR_THREADS - 1) / SHR_THREADS;

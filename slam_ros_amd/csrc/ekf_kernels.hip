@@ -3866,6 +3866,17 @@ __device__ __forceinline__ void shard_step(const ShardParams& p, const int phase
     // to the step's patch buffer (every rank all of them: its flush takes the columns of its tiles),
     // the new landmarks' strip columns and mean, the 2×2 diagonal blocks; the capacity reset
     // (Robot.cpp:893-904)
+    if (p.end_gate) {
+        // (ekf_shard_localize) launched behind the speculative run before the host has read the
+        // agreement: a run that stopped short or failed on some rank leaves everything untouched
+        const double a0 = p.end_gate[0], a1 = p.end_gate[1];
+        if (j == 0) {
+            p.end_gate_host[0] = a0;
+            p.end_gate_host[1] = a1;
+            __threadfence_system();
+        }
+        if (a0 > 0.0 || a1 != (double)p.L) return;
+    }
     const int m = ctl[SC_M], nextra = ctl[SC_NEXTRA];
     double pose[3] = {xp[0], xp[1], xp[2]};
     if (p.L == 0 || m == 0) pose[2] = normalize_radian(xp[2]);
@@ -4126,6 +4137,344 @@ __global__ __launch_bounds__(SHR_THREADS) void shard_run_kernel(ShardParams p)
         for (int k = tid; k < SC_WORDS; k += SHR_THREADS)
             if (k != SC_STATUS) p.ctl[k] = sh_cw[k];
         if (tid < 12) p.rob[tid] = sh_rob[tid];
+    }
+}
+
+// The speculative path's lines in the association kernel's form (ekf_shard_run when
+// every landmark has its own thread, N <= shard_run_workgroups(N)·SHR_THREADS): instead of one
+// exchange among the workgroups per line, every workgroup replays the guessed winners' chain itself
+// from the exchanged guessed columns (p.cols, which hold every block (j, w_t), the winners' mutual
+// blocks among them) and checks each line's guess on its own landmarks; one verdict exchange at the
+// end. Per workgroup: two landmark waves (one landmark per thread, its record, history rows and
+// flags kept in registers and LDS) and a replay wave (lane u = line u's guessed winner). Line t:
+// the replay lane t evaluates its winner's gate at the state after lines < t (shard_step's
+// SH_GATE sequence) and, if it passes, builds the line's package (build_package and the winner's
+// V rows of the earlier matches, as SH_PACKAGE); every lane takes the robot update
+// (robot_update, as SH_ROBOT) and the later winners' lanes apply the line to their winners (gain
+// rows, as SH_APPLY). Meanwhile each landmark thread, per line as its package is published:
+// its gate at that state (SH_GATE), a violation if it passes before the guess or while the guess
+// fails, and the line's update (SH_APPLY: gain rows, history row, operand rows). The verdict (the
+// first violating line over all workgroups) decides: the records, flags, history rows, control
+// words and robot block are written as they stand after the lines before it (recomputed from the
+// run's start when a violation cut the lines short), and *next_out = that line; the caller runs
+// the per-line phases from there, as after shard_run_kernel. Every value comes from the same
+// functions on the same inputs as the per-line phases: bit-identical.
+constexpr int SPR_THREADS = SHR_THREADS + 64;   // two landmark waves + the replay wave
+template <typename T>
+__global__ __launch_bounds__(SPR_THREADS) void shard_spec_kernel(ShardParams p)
+{
+    using C = typename Stor<T>::C;
+    constexpr double ETA = gate_eta<T>();
+    constexpr int SPK = MB_VH + 4 * SH_MAX_LINES;   // a package: build_package's words + the V rows
+    __shared__ int sh_cw[SC_WORDS];
+    __shared__ double sh_pk[SH_MAX_LINES][SPK];          // line t's package
+    __shared__ double sh_robl[SH_MAX_LINES + 1][12];     // the robot block and x_pre before line t
+    __shared__ int sh_pass[SH_MAX_LINES];                // line t's guessed winner passed its gate
+    __shared__ int sh_ready;                              // packages published (lines < sh_ready)
+    __shared__ double sh_wh[SH_MAX_LINES][SH_MAX_LINES][8];   // replay lane u: winner u's history rows
+    __shared__ double sh_lh[SH_MAX_LINES][4][SHR_THREADS];    // landmark thread tid: its U rows
+    __shared__ int sh_red[SPR_THREADS / 64];
+    __shared__ int sh_to, sh_bad, sh_first;
+    const int tid = threadIdx.x, g = blockIdx.x, G = gridDim.x;
+    const Dims d = p.d;
+    const int N = d.N, L = p.L;
+    const bool sym = p.r_mode != 1 && sizeof(C) == 4;
+    for (int k = tid; k < SC_WORDS; k += SPR_THREADS) sh_cw[k] = p.ctl[k];
+    if (tid < 12) sh_robl[0][tid] = p.rob[tid];
+    if (tid == 0) {
+        sh_ready = 0;
+        sh_to = sh_bad = 0;
+        sh_first = L;
+    }
+    __syncthreads();
+    const int s = sh_cw[SC_S];
+    int tstatus = 0;
+
+    // the operand rows of match m of landmark j (SH_APPLY's stores)
+    auto store_ops = [&](int j, int m, const double (&kk)[4], const double (&uu)[4], const float (&F)[3]) {
+        C* Uop = reinterpret_cast<C*>(p.cur.Uop);
+        C* Vop = reinterpret_cast<C*>(p.cur.Vop);
+#pragma unroll
+        for (int pp = 0; pp < 2; pp++) {
+            const int lr = 2 * j + pp;
+            if constexpr (sizeof(C) == 4) {
+                double o0 = uu[2 * pp], o1 = uu[2 * pp + 1], v0 = kk[2 * pp], v1 = kk[2 * pp + 1];
+                if (sym) {
+                    v0 = kk[2 * pp] * (double)F[0] + kk[2 * pp + 1] * (double)F[1];
+                    v1 = kk[2 * pp + 1] * (double)F[2];
+                    o0 = (double)(float)v0;
+                    o1 = (double)(float)v1;
+                }
+                Uop[op_index_f32(lr, 2 * m, d.kmax)] = to_domain<T>(-o0, 0);
+                Uop[op_index_f32(lr, 2 * m + 1, d.kmax)] = to_domain<T>(-o1, 0);
+                Vop[op_index_f32(lr, 2 * m, d.kmax)] = (C)v0;
+                Vop[op_index_f32(lr, 2 * m + 1, d.kmax)] = (C)v1;
+            } else {
+                Uop[op_index_f64(lr, 2 * m, d.kmax)] = (C)(-uu[2 * pp]);
+                Uop[op_index_f64(lr, 2 * m + 1, d.kmax)] = (C)(-uu[2 * pp + 1]);
+                Vop[op_index_f64(lr, 2 * m, d.kmax)] = (C)kk[2 * pp];
+                Vop[op_index_f64(lr, 2 * m + 1, d.kmax)] = (C)kk[2 * pp + 1];
+            }
+        }
+    };
+    // the gate of one landmark at the robot state rob (SH_GATE's evaluation)
+    auto gate_of = [&](const double* rob, const double2& rr0, const double2& rr1, const double2& rr2,
+                       const double2& yb, const double (&Dj)[4], const double* rc, int line, Cand& c, bool& pass,
+                       bool& sing, bool& amb) {
+        const ekf_line ln = p.lines[line];
+        double Rm[4];
+        line_R(ln, line, p.r_mode, Rm);
+        double R33[9], xp[3];
+#pragma unroll
+        for (int a = 0; a < 9; a++) R33[a] = rob[a];
+        xp[0] = rob[9]; xp[1] = rob[10]; xp[2] = rob[11];
+        Block5 b5;
+        fill_block5(b5, R33, rr0, rr1, rr2, Dj);
+        double sn, cs;
+        pass = sing = amb = false;
+        if (!quick_reject(b5, yb.x, yb.y, rc[12], rc[15], rc[16], xp, ln.alpha, ln.r, Rm, p.gate, ETA) &&
+            (sincos_near(yb.x, rc[12], rc[13], rc[14], sn, cs),
+             !certified_reject(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, ETA))) {
+            eval_candidate(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, ETA, c);
+            sing = c.singular;
+            amb = c.amb;
+            pass = c.pass;
+        }
+    };
+
+    if (tid >= SHR_THREADS) {
+        // ---- the replay wave: lane u carries line u's guessed winner up to its line ----
+        const int u = tid - SHR_THREADS;
+        const int wu = u < L ? sh_cw[SC_GUESS + u] : 0x7fffffff;
+        const bool act = wu != 0x7fffffff && wu < N;
+        double rc[SH_REC];
+        if (act)
+            for (int k = 0; k < SH_REC; k++) rc[k] = p.rec[(size_t)wu * SH_REC + k];
+        else
+            for (int k = 0; k < SH_REC; k++) rc[k] = 0.0;
+        double2 rr0 = make_double2(rc[0], rc[1]), rr1 = make_double2(rc[2], rc[3]), rr2 = make_double2(rc[4], rc[5]);
+        double2 yb = make_double2(rc[6], rc[7]);
+        double Dj[4] = {rc[8], rc[9], rc[10], rc[11]};
+        bool matched = false;
+        int m = 0;
+        for (int t = 0; t < L; t++) {
+            const int wt = sh_cw[SC_GUESS + t];
+            bool pass = false;
+            if (u == t && act && !matched && wu < s) {
+                Cand c;
+                bool sing, amb;
+                gate_of(sh_robl[t], rr0, rr1, rr2, yb, Dj, rc, t, c, pass, sing, amb);
+                if (pass) {
+                    double R33[9];
+#pragma unroll
+                    for (int a = 0; a < 9; a++) R33[a] = sh_robl[t][a];
+                    build_package(c, R33, rr0, rr1, rr2, sh_pk[t]);
+                    for (int q = 0; q < m; q++)
+#pragma unroll
+                        for (int k = 0; k < 4; k++) sh_pk[t][MB_VH + 4 * q + k] = sh_wh[u][q][4 + k];
+                }
+                sh_pass[t] = pass ? 1 : 0;
+            } else if (u == t) {
+                sh_pass[t] = 0;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const bool pt = sh_pass[t] != 0;
+            // the robot block and x_pre after line t (SH_ROBOT; every lane the same bits)
+            {
+                double R33[9], xp[3];
+#pragma unroll
+                for (int a = 0; a < 9; a++) R33[a] = sh_robl[t][a];
+                xp[0] = sh_robl[t][9]; xp[1] = sh_robl[t][10]; xp[2] = sh_robl[t][11];
+                if (pt) robot_update(R33, xp, sh_pk[t]);
+                if (u == 0) {
+#pragma unroll
+                    for (int a = 0; a < 9; a++) sh_robl[t + 1][a] = R33[a];
+                    sh_robl[t + 1][9] = xp[0]; sh_robl[t + 1][10] = xp[1]; sh_robl[t + 1][11] = xp[2];
+                }
+            }
+            // the later winners take line t's update (SH_APPLY on their own landmark)
+            if (pt && act && u > t) {
+                const double4 cb = *reinterpret_cast<const double4*>(p.cols + 4 * ((size_t)t * N + wu));
+                double blk[4] = {cb.x, cb.y, cb.z, cb.w};
+                const double* pk = sh_pk[t];
+                double kk[4], uu[4];
+                gain_rows<0>(pk, m,
+                             [&](int q) { return make_double4(sh_wh[u][q][0], sh_wh[u][q][1], sh_wh[u][q][2], sh_wh[u][q][3]); },
+                             [&](int q) {
+                                 const double* vh = pk + MB_VH + 4 * q;
+                                 return make_double4(vh[0], vh[1], vh[2], vh[3]);
+                             },
+                             blk, rr0, rr1, rr2, yb, Dj, kk, uu);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    sh_wh[u][m][k] = uu[k];
+                    sh_wh[u][m][4 + k] = kk[k];
+                }
+                if (wu == wt) matched = true;
+            }
+            if (pt) m++;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            if (u == 0) __hip_atomic_store(&sh_ready, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+
+    // ---- the landmark waves: one landmark per thread ----
+    const int j = g * SHR_THREADS + tid;
+    const bool own = tid < SHR_THREADS && j < N;
+    double rc[SH_REC];
+    for (int k = 0; k < SH_REC; k++) rc[k] = own ? p.rec[(size_t)j * SH_REC + k] : 0.0;
+    int stacc = 0;   // the status bits of the lines run (SH_APPLY's)
+    int viol = L;    // this thread's first violating line
+    // one pass over lines [0, upto): gates (check: the violations), updates into the registers
+    // and the history rows; the operand rows stored as they come (the same rows are rewritten by
+    // the per-line phases for any line not kept)
+    auto run_lines = [&](int upto, bool check, double2& rr0, double2& rr1, double2& rr2, double2& yb,
+                         double (&Dj)[4], bool& matched, int& m) {
+        for (int i = 0; i < upto; i++) {
+            if (tid < SHR_THREADS) {
+                int polls = 0;
+                while (__hip_atomic_load(&sh_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= i) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if ((tstatus & EKF_ST_TIMEOUT_BIT) || ++polls > (1 << p.spin_log2)) {
+                        tstatus |= EKF_ST_TIMEOUT_BIT;
+                        break;
+                    }
+                }
+            }
+            if (!own) continue;
+            const int w = sh_cw[SC_GUESS + i];
+            const bool pt = sh_pass[i] != 0;
+            const int jstar = pt ? w : 0x7fffffff;
+            bool pass = false, sing = false, amb = false;
+            if (j < s && !matched) {
+                Cand c;
+                gate_of(sh_robl[i], rr0, rr1, rr2, yb, Dj, rc, i, c, pass, sing, amb);
+            }
+            if (check && pass && (!pt || j < w)) {   // the guess is not the line's first passing landmark
+                viol = i;
+                return;
+            }
+            int st = sing && j <= jstar ? (int)EKF_ST_SINGULAR : 0;
+            if (amb && j <= jstar) st |= EKF_ST_PRECISION_BIT;
+            if (p.r_mode == 1 && (i == 1 || i == 2)) st |= EKF_ST_NSYM;
+            stacc |= st;
+            if (!pt) continue;
+            const double4 cb = *reinterpret_cast<const double4*>(p.cols + 4 * ((size_t)i * N + j));
+            double blk[4] = {cb.x, cb.y, cb.z, cb.w};
+            const double* pk = sh_pk[i];
+            double kk[4], uu[4];
+            gain_rows<0>(pk, m,
+                         [&](int q) { return make_double4(sh_lh[q][0][tid], sh_lh[q][1][tid], sh_lh[q][2][tid], sh_lh[q][3][tid]); },
+                         [&](int q) {
+                             const double* vh = pk + MB_VH + 4 * q;
+                             return make_double4(vh[0], vh[1], vh[2], vh[3]);
+                         },
+                         blk, rr0, rr1, rr2, yb, Dj, kk, uu);
+            float F[3] = {0.f, 0.f, 0.f};
+            if (sym) sym_factor(pk, F);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                sh_lh[m][k][tid] = uu[k];
+            }
+            double* h = p.hist + ((size_t)j * d.max_lines + m) * 8;   // (SH_APPLY's history row)
+            h[0] = uu[0]; h[1] = uu[1]; h[2] = uu[2]; h[3] = uu[3];
+            h[4] = kk[0]; h[5] = kk[1]; h[6] = kk[2]; h[7] = kk[3];
+            store_ops(j, m, kk, uu, F);
+            if (j == w) matched = true;
+            m++;
+        }
+    };
+    double2 rr0 = make_double2(rc[0], rc[1]), rr1 = make_double2(rc[2], rc[3]), rr2 = make_double2(rc[4], rc[5]);
+    double2 yb = make_double2(rc[6], rc[7]);
+    double Dj[4] = {rc[8], rc[9], rc[10], rc[11]};
+    const bool matched0 = own && (p.flags[j] & 1);
+    bool matched = matched0;
+    int m = 0;   // (the run starts at line 0: ekf_shard_run)
+    run_lines(L, true, rr0, rr1, rr2, yb, Dj, matched, m);
+    // ---- the verdict: the first violating line over every workgroup (one exchange) ----
+    {
+        int v = viol;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
+        if ((tid & 63) == 0) sh_red[tid >> 6] = v;
+        __syncthreads();
+        int wv = L;
+        for (int w = 0; w < SHR_THREADS / 64; w++) wv = min(wv, sh_red[w]);
+        double* slot = p.mbox + (size_t)g * p.mbw;
+        if (tid == 0) mb_tag(slot, p.epoch, TAG_SPEC_VERDICT, (unsigned)(wv + 1));
+        for (int k = tid; k < G; k += SPR_THREADS) {
+            const int bq = mb_poll(p.mbox, 0, G, k, p.mbw, p.epoch, TAG_SPEC_VERDICT, tstatus, p.spin_log2);
+            if (bq <= 0) sh_to = 1;
+            else atomicMin(&sh_first, bq - 1);
+        }
+        if (tstatus & EKF_ST_TIMEOUT_BIT) sh_to = 1;
+        __syncthreads();
+    }
+    const int first = sh_to ? 0 : sh_first;
+    // the state after the lines before `first` (recomputed when the run was cut short)
+    if (first < L && !sh_to) {
+        rr0 = make_double2(rc[0], rc[1]); rr1 = make_double2(rc[2], rc[3]); rr2 = make_double2(rc[4], rc[5]);
+        yb = make_double2(rc[6], rc[7]);
+        Dj[0] = rc[8]; Dj[1] = rc[9]; Dj[2] = rc[10]; Dj[3] = rc[11];
+        matched = matched0;
+        m = 0;
+        stacc = 0;
+        run_lines(first, false, rr0, rr1, rr2, yb, Dj, matched, m);
+    }
+    if (own && !sh_to) {
+        double* r = p.rec + (size_t)j * SH_REC;
+        const double v[12] = {rr0.x, rr0.y, rr1.x, rr1.y, rr2.x, rr2.y, yb.x, yb.y, Dj[0], Dj[1], Dj[2], Dj[3]};
+        for (int k = 0; k < 12; k++) r[k] = v[k];
+        p.flags[j] = matched ? 1 : 0;
+    }
+    int st = own ? stacc : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) st |= __shfl_xor(st, off, 64);
+    __syncthreads();
+    if ((tid & 63) == 0) sh_red[tid >> 6] = st;
+    __syncthreads();
+    // every workgroup's outcome to workgroup 0 (as shard_run_kernel): a workgroup whose verdict
+    // poll timed out makes the run report L + 1, and the scan is abandoned on every rank
+    if (tid == 0) {
+        int wst = 0;
+        for (int w = 0; w < SPR_THREADS / 64; w++) wst |= sh_red[w];
+        atomicOr(p.ctl + SC_STATUS, wst | (sh_to ? (int)EKF_ST_TIMEOUT_BIT : 0));
+        mb_store_tagged(p.mbox + (size_t)g * p.mbw + p.mbw - 1, p.epoch,
+                        ((unsigned long long)first << 1) | (sh_to ? 1ull : 0ull));
+    }
+    if (g == 0) {
+        for (int k = tid; k < G; k += SPR_THREADS) {
+            int stw = sh_to ? (int)EKF_ST_TIMEOUT_BIT : 0;
+            const unsigned long long w = mb_wait_tagged(p.mbox + (size_t)k * p.mbw + p.mbw - 1, p.epoch, stw, p.spin_log2);
+            if (stw || (w & 1ull) || (int)(w >> 1) != first) atomicOr(&sh_bad, 1);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            // the control words after the lines kept (SH_ROBOT's bookkeeping, line by line)
+            int mm = 0, nx = sh_cw[SC_NEXTRA];
+            for (int i = 0; i < first; i++) {
+                if (sh_pass[i]) {
+                    sh_cw[SC_MATCH + i] = sh_cw[SC_GUESS + i];
+                    mm++;
+                } else {
+                    sh_cw[SC_MATCH + i] = -1;
+                    sh_cw[SC_EXTRA + nx] = i;
+                    nx++;
+                }
+            }
+            sh_cw[SC_M] += mm;
+            sh_cw[SC_NEXTRA] = nx;
+            sh_cw[SC_WIN] = 0x7fffffff;
+            sh_cw[SC_NEXT] = first;
+            *p.next_out = (sh_to || sh_bad) ? (double)(L + 1) : (double)first;
+        }
+        __syncthreads();
+        for (int k = tid; k < SC_WORDS; k += SPR_THREADS)
+            if (k != SC_STATUS) p.ctl[k] = sh_cw[k];
+        if (tid < 12) p.rob[tid] = sh_robl[first][tid];
     }
 }
 
@@ -6476,6 +6825,14 @@ size_t scan_lds_bytes(int precision)
 hipError_t launch_shard_run(const ShardParams& p, int precision, hipStream_t st)
 {
     const unsigned G = (unsigned)shard_run_workgroups(p.d.N);
+    // one landmark per thread and at most SH_MAX_LINES lines: one verdict exchange for the run
+    // (shard_spec_kernel); otherwise one exchange per line (shard_run_kernel)
+    if (EKF_SHARD_SPEC && p.d.N <= (int)G * SHR_THREADS && p.L <= SH_MAX_LINES && p.d.max_lines <= SH_MAX_LINES) {
+        if (precision == EKF_PREC_F64) hipLaunchKernelGGL(shard_spec_kernel<double>, dim3(G), dim3(SPR_THREADS), 0, st, p);
+        else if (precision == EKF_PREC_F32) hipLaunchKernelGGL(shard_spec_kernel<float>, dim3(G), dim3(SPR_THREADS), 0, st, p);
+        else return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
     if (precision == EKF_PREC_F64) hipLaunchKernelGGL(shard_run_kernel<double>, dim3(G), dim3(SHR_THREADS), 0, st, p);
     else if (precision == EKF_PREC_F32) hipLaunchKernelGGL(shard_run_kernel<float>, dim3(G), dim3(SHR_THREADS), 0, st, p);
     else return hipErrorInvalidValue;
