@@ -186,7 +186,9 @@ int ekf_sync(ekf_ctx* ctx);
 enum {
     /* association path: 1 speculative (default), 0 the sequential chain on every scan (one
      * cross-workgroup exchange per line), 2 test hook: every guess wrong (the speculative path,
-     * a failed verdict and the sequential restart on every scan). Identical results. */
+     * a failed verdict and the sequential restart on every scan), 3 test hook: the guesses of
+     * lines L/2 .. L-1 wrong (a failed verdict keeps the lines before the first wrong one).
+     * Identical results. */
     EKF_OPT_SPECULATE = 1,
     /* spin bound of the association's cross-workgroup waits: 2^v polls, 8 <= v <= 24 (24) */
     EKF_OPT_SPIN_LOG2 = 2,

@@ -806,7 +806,7 @@ extern "C" int ekf_set_option(ekf_ctx* c, int opt, int v)
     if (!c) return EKF_EINVAL;
     const int E = c->cfg.instances;
     switch (opt) {
-    case EKF_OPT_SPECULATE: if (v < 0 || v > 2) return EKF_ERANGE; break;
+    case EKF_OPT_SPECULATE: if (v < 0 || v > 3) return EKF_ERANGE; break;
     case EKF_OPT_SPIN_LOG2: if (v < 8 || v > 24) return EKF_ERANGE; break;
     case EKF_OPT_FLUSH_FORM:
         if (v != 0 && v != 2 && v != 8 && v != 24 && v != 44) return EKF_ERANGE;

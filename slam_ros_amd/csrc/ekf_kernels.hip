@@ -862,6 +862,21 @@ __device__ __forceinline__ int wave_min(int v)
     return v;
 }
 
+// The status bits a speculative line can raise (GSL_EDOM, the gate's precision margin, the
+// as-written R), three per line (line i at bits 3i .. 3i + 2 of one word, SPEC_L = 8 lines), so that
+// a restart after a failed verdict keeps those of the lines before the first violating one
+__device__ __forceinline__ int st_line(int st, int i)
+{
+    return (((st & EKF_ST_SINGULAR) ? 1 : 0) | ((st & EKF_ST_PRECISION_BIT) ? 2 : 0) | ((st & EKF_ST_NSYM) ? 4 : 0))
+           << (3 * i);
+}
+__device__ __forceinline__ int st_lines(int packed, int upto)   // the bits of lines < upto
+{
+    const int w = upto >= 8 ? packed : packed & ((1 << (3 * upto)) - 1);
+    return ((w & 0x249249) ? (int)EKF_ST_SINGULAR : 0) | ((w & 0x492492) ? (int)EKF_ST_PRECISION_BIT : 0) |
+           ((w & 0x924924) ? (int)EKF_ST_NSYM : 0);
+}
+
 // ---------------------------------------------------------------------------------------
 // 1. association + gain chain + augmentation: ⌈N/256⌉ cooperating workgroups per instance
 // ---------------------------------------------------------------------------------------
@@ -2201,6 +2216,10 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                      // 64-256: rpath)
     int par0 = 0;   // mailbox parity of line 0 on the sequential path
     bool sequential = true;
+    // a restart after a failed verdict keeps the lines before the first violating one: every
+    // workgroup replays them from the speculative packages (no gate, no exchange; the state, rows
+    // and status bits the sequential path computes for them), then the sequential path takes over
+    int keep = 0;
     // a restart after a failed verdict: the owned blocks of the guessed columns as the speculative
     // pass computed them (scan start, pending steps applied) serve the lines whose winner was guessed
     bool blk_cached = false;
@@ -2224,6 +2243,13 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
             }
             if (p.spec == 2 && L > 1)   // test hook: every guess taken from the next line
                 gp = ((gp >> 1) | (gp << (L - 1))) & ((1u << L) - 1u);
+            if (p.spec == 3 && L > 3) {
+                // test hook: the guesses of lines L/2 .. L − 1 taken from the next of them (the
+                // lines before stay right: a failed verdict keeps them)
+                const int h = L / 2, nh = L - h;
+                const unsigned hi = (gp >> h) & ((1u << nh) - 1u);
+                gp = (gp & ((1u << h) - 1u)) | ((((hi >> 1) | (hi << (nh - 1))) & ((1u << nh) - 1u)) << h);
+            }
         }
         // per wave and line the guessed candidates (ballot), then the workgroup's first SPEC_K
         // in landmark order: word A = 8-bit local indices 0..3 | count << 32 | more << 36, word B =
@@ -2544,6 +2570,8 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
             // then the later winners' lanes apply their gain rows. Meanwhile (g) the landmark
             // waves run every line as soon as its package is published (sh_ready). ----
             int viol = 0;
+            int vline = L;   // the line of this thread's violation
+            int stp = 0;     // its status bits per line (st_line)
             if (tid >= SCAN_THREADS) {
                 const int u = tid - SCAN_THREADS;
                 const unsigned long long t_l0 = __builtin_amdgcn_s_memrealtime();
@@ -2616,8 +2644,8 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                     if (u == t) {
                         // GSL_EDOM of the winner (the reference evaluated it: Robot.cpp:454) and the
                         // gate's storage precision (gate_eta), off the line's chain
-                        if (c.singular) atomicOr(&sh_rwst, (int)EKF_ST_SINGULAR);
-                        if (cand_amb(b5, c, p.gate, ETA)) atomicOr(&sh_rwst, (int)EKF_ST_PRECISION_BIT);
+                        if (c.singular) atomicOr(&sh_rwst, st_line(EKF_ST_SINGULAR, t));
+                        if (cand_amb(b5, c, p.gate, ETA)) atomicOr(&sh_rwst, st_line(EKF_ST_PRECISION_BIT, t));
                     }
                     if (!ok) continue;   // (ml counts matches: unchanged)
                     if (u != t) {   // (lane t has them)
@@ -2919,12 +2947,12 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                         int polls = 0;
                         while (__hip_atomic_load(&sh_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= i) {
                             __builtin_amdgcn_s_sleep(1);
-                            if ((tstatus & EKF_ST_TIMEOUT_BIT) || ++polls > (1 << p.spin_log2)) { tstatus |= EKF_ST_TIMEOUT_BIT; viol = 1; break; }
+                            if ((tstatus & EKF_ST_TIMEOUT_BIT) || ++polls > (1 << p.spin_log2)) { tstatus |= EKF_ST_TIMEOUT_BIT; viol = 1; vline = i; break; }
                         }
                         sub(17);
                         pk = sh_pk[i];
                         wok = __builtin_amdgcn_readfirstlane(pk[PK_OK] != 0.0 ? 1 : 0) != 0;
-                        if (r_mode == 1 && (i == 1 || i == 2) && wok) status |= EKF_ST_NSYM;
+                        if (r_mode == 1 && (i == 1 || i == 2) && wok) stp |= st_line(EKF_ST_NSYM, i);
                         if (own) {
                             // the quick filter and the gain rows in one block (independent chains);
                             // the gain rows take effect only if the guessed winner passed (wok,
@@ -2967,13 +2995,16 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                             eval_candidate(b5, ybx, yby, sn, cs, xpg, ln.alpha, ln.r, Rm, p.gate, ETA, c);
                             // GSL_EDOM counts only for candidates the reference evaluates: the
                             // unmatched ones up to the winner (Robot.cpp:313-498 stops there)
-                            if (c.singular && (w < 0 || !wok || j <= w)) status |= EKF_ST_SINGULAR;
-                            if (c.amb && (w < 0 || !wok || j <= w)) status |= EKF_ST_PRECISION_BIT;
+                            if (c.singular && (w < 0 || !wok || j <= w)) stp |= st_line(EKF_ST_SINGULAR, i);
+                            if (c.amb && (w < 0 || !wok || j <= w)) stp |= st_line(EKF_ST_PRECISION_BIT, i);
                             pass = c.pass;
                         }
                         // the guess must be the first passing unmatched landmark; a guessed
                         // winner that failed leaves the line unmatched only if none passes
-                        if (pass && (w < 0 || !wok || j < w)) viol = 1;
+                        if (pass && (w < 0 || !wok || j < w)) {
+                            viol = 1;
+                            vline = i;
+                        }
                     }
                     if (pdbg && g == 0) {   // waves of workgroup 0 whose lanes went deeper
                         const bool d1 = __any(deep >= 1), d2 = __any(deep >= 2), d3 = __any(deep >= 3);
@@ -3012,48 +3043,63 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
             }
             if (dbg) sh_stamp[31] += __builtin_amdgcn_s_memrealtime() - sh_trec;   // landmark wave 0 done
             __syncthreads();
-            viol |= sh_flag;
-            status |= sh_rwst;
+            if (sh_flag) vline = 0;
+            const int rwp = sh_rwst;
             EKF_STAMP(14);
-            // ---- (h) verdict (exchange 3, parity 0): any flag restarts on the sequential path ----
-            const int wv = __any(viol) ? 1 : 0;
+            // ---- (h) verdict (exchange 3, parity 0): the first violating line over the workgroups
+            // (payload line + 1, 0: none); a violation restarts on the sequential path from there ----
+            const int wv = wave_min(tid < SCAN_THREADS ? vline : L);
             __syncthreads();
             if ((tid & 63) == 0 && tid < SCAN_THREADS) sh_red[tid >> 6] = wv;
             __syncthreads();
-            int any = 0;
+            int first = L;
 #pragma unroll
-            for (int w = 0; w < SCAN_THREADS / 64; w++) any |= sh_red[w];
+            for (int w = 0; w < SCAN_THREADS / 64; w++) first = min(first, sh_red[w]);
             if (G > 1) {
-                if (tid == 0) mb_tag(mbox + (size_t)g * p.mbw, p.epoch, TAG_SPEC_VERDICT, (unsigned)any);
+                if (tid == 0) mb_tag(mbox + (size_t)g * p.mbw, p.epoch, TAG_SPEC_VERDICT, (unsigned)(first < L ? first + 1 : 0));
                 if (tid < G) {
                     int v = mb_poll(mbox, 0, G, tid, p.mbw, p.epoch, TAG_SPEC_VERDICT, tstatus, p.spin_log2);
                     if (p.test_verdict == e + 1 && g == 1 && tid == 0) {   // test hook: this poll timed out
                         tstatus |= EKF_ST_TIMEOUT_BIT;
                         v = -1;
                     }
-                    sh_best[tid] = v != 0;
+                    sh_best[tid] = v > 0 ? v - 1 : L;
                     if (v < 0) sh_vto = 1;
                 }
                 __syncthreads();
-                for (int k = 0; k < G; k++) any |= sh_best[k];
+                for (int k = 0; k < G; k++) first = min(first, sh_best[k]);
                 if (sh_vto) {
                     // a verdict that never arrived: this workgroup does not restart (its peers
                     // may have committed their halves already); it finishes with the timeout bit
                     // in its completion word, and the lead, which collects every word, rolls the
                     // instance's call back
                     tstatus |= EKF_ST_TIMEOUT_BIT;
-                    any = 0;
+                    first = L;
                 }
             }
             EKF_STAMP(6);
-            if (any) {
-                dpath |= 8;
+            if (first >= L) {
+                status |= st_lines(stp, L) | st_lines(rwp, L);
+            } else {
+                dpath |= (first > 0 ? 8 | 512 : 8) | (first << 10);   // (512: lines kept; bits 10..12 the line)
                 if (dbg) sh_stamp[15] += 1;
                 sequential = true;
-                par0 = 1;
+                keep = first;
+                // the first kept line's exchange on parity 1: the verdict tags (parity 0) may still
+                // be polled until every workgroup has passed it
+                par0 = (first + 1) & 1;
                 init_state();
                 Dj[0] = Dj[1] = Dj[2] = Dj[3] = 0.0;
-                if (own && j < s) pll_block(pv, 2 * j, 2 * j, Dj);
+                if (own && j < s) {
+                    if (mf && p.npend > 0) {
+                        // the diagonal block the speculative pass started from (Dd, exact), which
+                        // the kept lines' packages were computed against
+                        const double4 b = Ddr[j];
+                        Dj[0] = b.x; Dj[1] = b.y; Dj[2] = b.z; Dj[3] = b.w;
+                    } else {
+                        pll_block(pv, 2 * j, 2 * j, Dj);
+                    }
+                }
                 // fp32 operands: out of sh_blk, which aliases the V history the restart writes, into
                 // the stage (free once the speculative pass is over); fp64: sh_blk64 as it is
                 if constexpr (!kB64)
@@ -3063,7 +3109,8 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
                             if (t < L && sh_spec[t] >= 0) sh_cblk[t][tid] = sh_blk[t][tid];
                 blk_cached = true;
                 matched = false;
-                m = nextra = status = 0;
+                m = nextra = 0;
+                status = st_lines(stp, first) | st_lines(rwp, first);
                 dsq = 0.0;
                 ops_early = 0;   // (the sequential path rewrites every operand row)
                 __syncthreads();   // sh_extra, sh_vhist reuse
@@ -3077,6 +3124,45 @@ __global__ __launch_bounds__(NT + 64) void scan_kernel(ScanParams p)
     }
 
     for (int i = 0; sequential && i < L; ++i) {
+        if (i < keep) {
+            // a kept line (restart): its guessed winner and package, verified by the verdict
+            const int w = __builtin_amdgcn_readfirstlane(sh_spec[i]);
+            const double* pk = sh_pk[i];
+            if (w < 0 || __builtin_amdgcn_readfirstlane(pk[PK_OK] != 0.0 ? 1 : 0) == 0) {
+                if (lead) {
+                    res[RES_MATCH + i] = -1;
+                    res[RES_EXTRA + nextra] = i;
+                }
+                if (tid == 0) sh_extra[nextra] = i;
+                nextra++;
+                continue;
+            }
+            if (own) {
+                // the owned block of column w: the speculative pass's (scan start, pending steps
+                // applied), as the sequential lines take it (owned_block, blk_cached)
+                double blk[4];
+                if constexpr (kB64) {
+                    const double4 b = sh_blk64[i][tid];
+                    blk[0] = b.x; blk[1] = b.y; blk[2] = b.z; blk[3] = b.w;
+                } else {
+                    const float4 b = sh_cblk[i][tid];
+                    blk[0] = b.x; blk[1] = b.y; blk[2] = b.z; blk[3] = b.w;
+                }
+                double kk[4], uu[4];
+                gain_rows<0>(pk, m, uq_owned, [&](int q) { return sh_wh[i][q][1]; }, blk, rr0, rr1, rr2, yb, Dj, kk, uu);
+                float F[3] = {0.f, 0.f, 0.f};
+                if (sym) sym_factor(pk, F);
+                store_rows(m, kk, uu, true, F, true);
+            }
+            // = robot_update(R33, xp, pk), computed by the replay wave
+#pragma unroll
+            for (int a = 0; a < 9; a++) R33[a] = pk[PK_R33 + a];
+            xp[0] = pk[PK_XP + 0]; xp[1] = pk[PK_XP + 1]; xp[2] = pk[PK_XP + 2];
+            if (j == w) matched = true;
+            if (lead) res[RES_MATCH + i] = w;
+            m++;
+            continue;
+        }
         const ekf_line ln = sh_lines[i];
         double Rm[4];
         line_R(ln, i, r_mode, Rm);

@@ -490,13 +490,14 @@ def _spec_scans(w, rng, steps, L=8):
 def test_speculative_association_identical(ekf_mod, oracle_mod, monkeypatch, prec, N, T):
     """The speculative association (guessed winners, three exchanges per scan, exact local
     re-check) gives bit-identical state and results to the per-line sequential exchange, also
-    when every guess is wrong (EKF_OPT_SPECULATE = 2: every scan falls back); association vs the
-    restatement."""
+    when every guess is wrong (EKF_OPT_SPECULATE = 2: every scan falls back) and when only the
+    later lines' guesses are (3: the restart keeps the lines before the first wrong one, from the
+    speculative packages); association vs the restatement."""
     w = G.make_world(N, active=N - 30)
     st = G.initial_state(w)
     scans = _spec_scans(w, np.random.default_rng(3), 8)
     runs = {}
-    for mode in (0, 1, 2):
+    for mode in (0, 1, 2, 3):
         ens = ekf_mod.Ensemble(N, 1, prec, max_lines=8, flush_interval=T,
                                options={"scan_stamps": 1, "speculate": mode})
         ens.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
@@ -504,17 +505,21 @@ def test_speculative_association_identical(ekf_mod, oracle_mod, monkeypatch, pre
             ref = oracle_mod.OracleRobot(N)
             ref.set_state(*ens.download_state(0))
         results = []
+        kept = 0   # restarts that kept the lines before the first wrong guess (RES_DBG bit 512)
         for enc, ln in scans:
             r = ens.localize(enc, ln[None], [len(ln)])[0]
             results.append((r["match"], r["matches"], r["new_landmarks"], r["status"]))
+            ens.read_results()   # (the full record: a synchronous call mirrors only ekf_result's words)
+            kept += 1 if int(ens.result_words(0)[9]) & 512 else 0
             if mode == 1:
                 assert r["match"] == ref.localize(ln, enc[0]), r["match"]
         stamps = ens.scan_stamps()
-        runs[mode] = (results, ens.download_state(0), stamps[15])
+        runs[mode] = (results, ens.download_state(0), stamps[15], kept)
         ens.close()
     assert runs[1][2] == 0, "speculation fell back on ordinary scans"
     assert runs[2][2] >= 4, "wrong guesses did not fall back"
-    for mode in (1, 2):
+    assert runs[3][2] >= 2 and runs[3][3] >= 1, "wrong late guesses did not keep the lines before them"
+    for mode in (1, 2, 3):
         assert runs[mode][0] == runs[0][0], mode
         P, y, s, pose = runs[mode][1]
         P0, y0, s0, pose0 = runs[0][1]
@@ -540,7 +545,7 @@ def test_hot_scan_kernel_equals_generic(ekf_mod, monkeypatch, prec, arith):
     scans = _spec_scans(w, np.random.default_rng(5), 10)
     runs = {}
     for stamps in ("0", "1"):
-        for spec in ("1", "2"):
+        for spec in ("1", "2", "3"):
             ens = ekf_mod.Ensemble(N, 1, prec, max_lines=8, flush_interval=T, arith=arith,
                                    options={"scan_stamps": int(stamps), "speculate": int(spec)})
             ens.init_lowrank(0, st.diag, st.U, st.y, st.saved, st.pose)
@@ -550,7 +555,7 @@ def test_hot_scan_kernel_equals_generic(ekf_mod, monkeypatch, prec, arith):
                 results.append((r["match"], r["matches"], r["new_landmarks"], r["status"]))
             runs[(stamps, spec)] = (results, ens.download_state(0))
             ens.close()
-    for spec in ("1", "2"):
+    for spec in ("1", "2", "3"):
         hot, gen = runs[("0", spec)], runs[("1", spec)]
         assert hot[0] == gen[0], spec
         P, y, s, pose = hot[1]
