@@ -346,9 +346,10 @@ int ekf_shard_abort(ekf_ctx* ctx);
 /* The same scan as one call, with the exchanges on the library's own RCCL communicator (RCCL is
  * loaded on first use; EKF_EDEVICE if it is not available): rank 0 gets an id with
  * ekf_rccl_unique_id, the host hands it to every rank, and each attaches with its (rank, world)
- * of ekf_shard_create. ekf_shard_localize then runs begin, SUM, speculate, SUM, run, MAX, resume /
- * the per-line phases and end on the context's stream, with two host reads (the agreement pair
- * and the results), and is bit-identical to the sequence above (Robot::localize,
+ * of ekf_shard_create. ekf_shard_localize then runs begin, SUM, speculate, SUM, run, MAX, end on
+ * the context's stream before its one host read: the end phase commits only if the agreement says
+ * every line ran on every rank, and otherwise changes nothing, when resume / the per-line phases
+ * and the end follow (a second host read). It is bit-identical to the sequence above (Robot::localize,
  * Robot.cpp:126-904). A phase failing on any rank, or a run whose workgroups timed out, abandons
  * the scan on every rank alike (the error, or EKF_EDEVICE on the ranks where nothing failed);
  * a failed collective returns EKF_EDEVICE. */
