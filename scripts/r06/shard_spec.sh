@@ -5,11 +5,11 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 out=gpurun_out/${TAG:-r06_shardspec}; mkdir -p $out
-timeout -k 10 400 python -u -m pytest tests/test_rowshard_gpu.py -x -v -s --timeout 120 --timeout-method thread > $out/pytest.log 2>&1 || exit 1
+timeout -k 10 800 python -u -m pytest tests/test_rowshard_gpu.py -x -v -s --timeout 300 --timeout-method thread > $out/pytest.log 2>&1 || exit 1
 export MASTER_ADDR=127.0.0.1 MASTER_PORT=29619 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0
 for rep in 1 2; do
-  for lib in product shrun; do
-    for cfg in "1024|1" "4096|1" "1024|0"; do
+  for lib in ${LIBS:-product shrun}; do
+    for cfg in "1024|1" "4096|1" "1024|0" "16384|1"; do
       N="${cfg%%|*}"; prec="${cfg#*|}"
       d=$out/$lib${N}p$prec; mkdir -p $d
       if [ $lib = product ]; then L=slam_ros_amd/lib/libslam_ekf.so; else L=slam_ros_amd/lib/xp_$lib.so; fi

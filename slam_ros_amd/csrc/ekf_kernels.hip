@@ -4226,8 +4226,8 @@ __global__ __launch_bounds__(SHR_THREADS) void shard_run_kernel(ShardParams p)
     }
 }
 
-// The speculative path's lines in the association kernel's form (ekf_shard_run when
-// every landmark has its own thread, N <= shard_run_workgroups(N)·SHR_THREADS): instead of one
+// The speculative path's lines in the association kernel's form (ekf_shard_run with
+// at most SH_MAX_LINES lines; K = ⌈N / (G·SHR_THREADS)⌉ landmarks per thread): instead of one
 // exchange among the workgroups per line, every workgroup replays the guessed winners' chain itself
 // from the exchanged guessed columns (p.cols, which hold every block (j, w_t), the winners' mutual
 // blocks among them) and checks each line's guess on its own landmarks; one verdict exchange at the
@@ -4243,8 +4243,10 @@ __global__ __launch_bounds__(SHR_THREADS) void shard_run_kernel(ShardParams p)
 // first violating line over all workgroups) decides: the records, flags, history rows, control
 // words and robot block are written as they stand after the lines before it (recomputed from the
 // run's start when a violation cut the lines short), and *next_out = that line; the caller runs
-// the per-line phases from there, as after shard_run_kernel. Every value comes from the same
-// functions on the same inputs as the per-line phases: bit-identical.
+// the per-line phases from there, as after shard_run_kernel. With several landmarks per thread
+// (N > G·SHR_THREADS) each thread checks its landmarks one after the other without stores, and
+// after the verdict runs each again over the lines kept, with the stores. Every value comes from
+// the same functions on the same inputs as the per-line phases: bit-identical.
 constexpr int SPR_THREADS = SHR_THREADS + 64;   // two landmark waves + the replay wave
 template <typename T>
 __global__ __launch_bounds__(SPR_THREADS) void shard_spec_kernel(ShardParams p)
@@ -4407,18 +4409,17 @@ __global__ __launch_bounds__(SPR_THREADS) void shard_spec_kernel(ShardParams p)
         }
     }
 
-    // ---- the landmark waves: one landmark per thread ----
-    const int j = g * SHR_THREADS + tid;
-    const bool own = tid < SHR_THREADS && j < N;
-    double rc[SH_REC];
-    for (int k = 0; k < SH_REC; k++) rc[k] = own ? p.rec[(size_t)j * SH_REC + k] : 0.0;
+    // ---- the landmark waves: landmark j = g·SHR_THREADS + tid + k·G·SHR_THREADS, k < K ----
+    const int K = (N + G * SHR_THREADS - 1) / (G * SHR_THREADS);   // landmarks per thread (uniform)
+    const int j0 = g * SHR_THREADS + tid;
     int stacc = 0;   // the status bits of the lines run (SH_APPLY's)
     int viol = L;    // this thread's first violating line
-    // one pass over lines [0, upto): gates (check: the violations), updates into the registers
-    // and the history rows; the operand rows stored as they come (the same rows are rewritten by
-    // the per-line phases for any line not kept)
-    auto run_lines = [&](int upto, bool check, double2& rr0, double2& rr1, double2& rr2, double2& yb,
-                         double (&Dj)[4], bool& matched, int& m) {
+    // one pass over lines [0, upto) for landmark j: gates (check: the violations), updates into
+    // the registers; store: the history and operand rows as they come (the same rows are
+    // rewritten by the per-line phases for any line not kept)
+    auto run_lines = [&](int j, const double* rc, int upto, bool check, bool store, double2& rr0, double2& rr1,
+                         double2& rr2, double2& yb, double (&Dj)[4], bool& matched, int& m) {
+        const bool own = tid < SHR_THREADS && j < N;
         for (int i = 0; i < upto; i++) {
             if (tid < SHR_THREADS) {
                 int polls = 0;
@@ -4440,7 +4441,7 @@ __global__ __launch_bounds__(SPR_THREADS) void shard_spec_kernel(ShardParams p)
                 gate_of(sh_robl[i], rr0, rr1, rr2, yb, Dj, rc, i, c, pass, sing, amb);
             }
             if (check && pass && (!pt || j < w)) {   // the guess is not the line's first passing landmark
-                viol = i;
+                viol = min(viol, i);
                 return;
             }
             int st = sing && j <= jstar ? (int)EKF_ST_SINGULAR : 0;
@@ -4459,27 +4460,61 @@ __global__ __launch_bounds__(SPR_THREADS) void shard_spec_kernel(ShardParams p)
                              return make_double4(vh[0], vh[1], vh[2], vh[3]);
                          },
                          blk, rr0, rr1, rr2, yb, Dj, kk, uu);
-            float F[3] = {0.f, 0.f, 0.f};
-            if (sym) sym_factor(pk, F);
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 sh_lh[m][k][tid] = uu[k];
             }
-            double* h = p.hist + ((size_t)j * d.max_lines + m) * 8;   // (SH_APPLY's history row)
-            h[0] = uu[0]; h[1] = uu[1]; h[2] = uu[2]; h[3] = uu[3];
-            h[4] = kk[0]; h[5] = kk[1]; h[6] = kk[2]; h[7] = kk[3];
-            store_ops(j, m, kk, uu, F);
+            if (store) {
+                float F[3] = {0.f, 0.f, 0.f};
+                if (sym) sym_factor(pk, F);
+                double* h = p.hist + ((size_t)j * d.max_lines + m) * 8;   // (SH_APPLY's history row)
+                h[0] = uu[0]; h[1] = uu[1]; h[2] = uu[2]; h[3] = uu[3];
+                h[4] = kk[0]; h[5] = kk[1]; h[6] = kk[2]; h[7] = kk[3];
+                store_ops(j, m, kk, uu, F);
+            }
             if (j == w) matched = true;
             m++;
         }
     };
-    double2 rr0 = make_double2(rc[0], rc[1]), rr1 = make_double2(rc[2], rc[3]), rr2 = make_double2(rc[4], rc[5]);
-    double2 yb = make_double2(rc[6], rc[7]);
-    double Dj[4] = {rc[8], rc[9], rc[10], rc[11]};
-    const bool matched0 = own && (p.flags[j] & 1);
-    bool matched = matched0;
-    int m = 0;   // (the run starts at line 0: ekf_shard_run)
-    run_lines(L, true, rr0, rr1, rr2, yb, Dj, matched, m);
+    // one landmark's pass from its record at the run's start (the run starts at line 0:
+    // ekf_shard_run, no match yet), its record and flag written at the end (write)
+    auto run_landmark = [&](int j, int upto, bool check, bool store, bool write) {
+        const bool own = tid < SHR_THREADS && j < N;
+        double rc[SH_REC];
+        for (int k = 0; k < SH_REC; k++) rc[k] = own ? p.rec[(size_t)j * SH_REC + k] : 0.0;
+        double2 rr0 = make_double2(rc[0], rc[1]), rr1 = make_double2(rc[2], rc[3]), rr2 = make_double2(rc[4], rc[5]);
+        double2 yb = make_double2(rc[6], rc[7]);
+        double Dj[4] = {rc[8], rc[9], rc[10], rc[11]};
+        bool matched = own && (p.flags[j] & 1);
+        int m = 0;
+        run_lines(j, rc, upto, check, store, rr0, rr1, rr2, yb, Dj, matched, m);
+        if (write && own) {
+            double* r = p.rec + (size_t)j * SH_REC;
+            const double v[12] = {rr0.x, rr0.y, rr1.x, rr1.y, rr2.x, rr2.y, yb.x, yb.y, Dj[0], Dj[1], Dj[2], Dj[3]};
+            for (int k = 0; k < 12; k++) r[k] = v[k];
+            p.flags[j] = matched ? 1 : 0;
+        }
+    };
+    // one landmark per thread (K = 1): its state stays in registers across the verdict and is
+    // recomputed only when a violation cut the run short
+    double2 rr0 = make_double2(0, 0), rr1 = rr0, rr2 = rr0, yb = rr0;
+    double Dj[4] = {0, 0, 0, 0};
+    bool matched = false;
+    int m = 0;
+    double rc0[SH_REC];
+    const bool own0 = tid < SHR_THREADS && j0 < N;
+    if (K == 1) {
+        for (int k = 0; k < SH_REC; k++) rc0[k] = own0 ? p.rec[(size_t)j0 * SH_REC + k] : 0.0;
+        rr0 = make_double2(rc0[0], rc0[1]); rr1 = make_double2(rc0[2], rc0[3]); rr2 = make_double2(rc0[4], rc0[5]);
+        yb = make_double2(rc0[6], rc0[7]);
+        Dj[0] = rc0[8]; Dj[1] = rc0[9]; Dj[2] = rc0[10]; Dj[3] = rc0[11];
+        matched = own0 && (p.flags[j0] & 1);
+        run_lines(j0, rc0, L, true, true, rr0, rr1, rr2, yb, Dj, matched, m);
+    } else {
+        // several landmarks per thread: check each in turn (no stores; lines at or past an earlier
+        // violation of this thread are never kept), the stores after the verdict
+        for (int k = 0; k < K; k++) run_landmark(j0 + k * G * SHR_THREADS, viol, true, false, false);
+    }
     // ---- the verdict: the first violating line over every workgroup (one exchange) ----
     {
         int v = viol;
@@ -4500,22 +4535,28 @@ __global__ __launch_bounds__(SPR_THREADS) void shard_spec_kernel(ShardParams p)
         __syncthreads();
     }
     const int first = sh_to ? 0 : sh_first;
-    // the state after the lines before `first` (recomputed when the run was cut short)
-    if (first < L && !sh_to) {
-        rr0 = make_double2(rc[0], rc[1]); rr1 = make_double2(rc[2], rc[3]); rr2 = make_double2(rc[4], rc[5]);
-        yb = make_double2(rc[6], rc[7]);
-        Dj[0] = rc[8]; Dj[1] = rc[9]; Dj[2] = rc[10]; Dj[3] = rc[11];
-        matched = matched0;
-        m = 0;
+    if (K == 1) {
+        // the state after the lines before `first` (recomputed when the run was cut short)
+        if (first < L && !sh_to) {
+            rr0 = make_double2(rc0[0], rc0[1]); rr1 = make_double2(rc0[2], rc0[3]); rr2 = make_double2(rc0[4], rc0[5]);
+            yb = make_double2(rc0[6], rc0[7]);
+            Dj[0] = rc0[8]; Dj[1] = rc0[9]; Dj[2] = rc0[10]; Dj[3] = rc0[11];
+            matched = own0 && (p.flags[j0] & 1);
+            m = 0;
+            stacc = 0;
+            run_lines(j0, rc0, first, false, true, rr0, rr1, rr2, yb, Dj, matched, m);
+        }
+        if (own0 && !sh_to) {
+            double* r = p.rec + (size_t)j0 * SH_REC;
+            const double v[12] = {rr0.x, rr0.y, rr1.x, rr1.y, rr2.x, rr2.y, yb.x, yb.y, Dj[0], Dj[1], Dj[2], Dj[3]};
+            for (int k = 0; k < 12; k++) r[k] = v[k];
+            p.flags[j0] = matched ? 1 : 0;
+        }
+    } else if (!sh_to) {
         stacc = 0;
-        run_lines(first, false, rr0, rr1, rr2, yb, Dj, matched, m);
+        for (int k = 0; k < K; k++) run_landmark(j0 + k * G * SHR_THREADS, first, false, true, true);
     }
-    if (own && !sh_to) {
-        double* r = p.rec + (size_t)j * SH_REC;
-        const double v[12] = {rr0.x, rr0.y, rr1.x, rr1.y, rr2.x, rr2.y, yb.x, yb.y, Dj[0], Dj[1], Dj[2], Dj[3]};
-        for (int k = 0; k < 12; k++) r[k] = v[k];
-        p.flags[j] = matched ? 1 : 0;
-    }
+    const bool own = own0 || (K > 1 && tid < SHR_THREADS);
     int st = own ? stacc : 0;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) st |= __shfl_xor(st, off, 64);
@@ -6911,9 +6952,9 @@ size_t scan_lds_bytes(int precision)
 hipError_t launch_shard_run(const ShardParams& p, int precision, hipStream_t st)
 {
     const unsigned G = (unsigned)shard_run_workgroups(p.d.N);
-    // one landmark per thread and at most SH_MAX_LINES lines: one verdict exchange for the run
-    // (shard_spec_kernel); otherwise one exchange per line (shard_run_kernel)
-    if (EKF_SHARD_SPEC && p.d.N <= (int)G * SHR_THREADS && p.L <= SH_MAX_LINES && p.d.max_lines <= SH_MAX_LINES) {
+    // at most SH_MAX_LINES lines: one verdict exchange for the run (shard_spec_kernel); otherwise
+    // one exchange per line (shard_run_kernel)
+    if (EKF_SHARD_SPEC && p.L <= SH_MAX_LINES && p.d.max_lines <= SH_MAX_LINES) {
         if (precision == EKF_PREC_F64) hipLaunchKernelGGL(shard_spec_kernel<double>, dim3(G), dim3(SPR_THREADS), 0, st, p);
         else if (precision == EKF_PREC_F32) hipLaunchKernelGGL(shard_spec_kernel<float>, dim3(G), dim3(SPR_THREADS), 0, st, p);
         else return hipErrorInvalidValue;

@@ -49,13 +49,15 @@ def test_two_rank_shard_equals_single_context(ekf_mod, oracle_mod, tmp_path, pre
                          [(1, 1024, 4, 9, 1000, 3, 3, "spec"), (0, 512, 4, 6, 0, 0, 0, "wrong"),
                           (1, 1024, 4, 9, 1000, 3, 0, "perline"),
                           (1, 1024, 4, 9, 1000, 3, 3, "native"), (0, 480, 4, 7, 400, 2, 3, "native-wrong"),
-                          (1, 512, 4, 6, 0, 0, 2, "native-perline"), (1, 4096, 4, 6, 0, 0, 0, "native")])
+                          (1, 512, 4, 6, 0, 0, 2, "native-perline"), (1, 4096, 4, 6, 0, 0, 0, "native"),
+                          (1, 8500, 4, 4, 0, 0, 2, "native"), (1, 8500, 4, 3, 0, 0, 0, "native-wrong")])
 def test_rccl_device_sum_world1(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_every, dup, mode):
     """The nccl (RCCL) backend's path: the exchange buffers all-reduced in place on the device, on
     the context's stream, with no host staging. One GPU holds one RCCL rank, so this runs a world of
     one (the partition is the whole block); the two-rank protocol itself is covered over gloo.
     native*: the whole scan as one library call (ekf_shard_localize) on the library's own RCCL
-    communicator (ekf_shard_attach_rccl), every protocol variant."""
+    communicator (ekf_shard_attach_rccl), every protocol variant; N = 8500 puts two landmarks on
+    each of the run's threads (shard_spec_kernel with K = 2)."""
     run_sharded(ekf_mod, oracle_mod, tmp_path, prec, N, T, scans, active, extra_every, world=1, backend="nccl",
                 dup=dup, mode=mode)
 
