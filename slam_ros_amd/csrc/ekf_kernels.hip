@@ -4349,13 +4349,24 @@ __global__ __launch_bounds__(SPR_THREADS) void shard_spec_kernel(ShardParams p)
             const int wt = sh_cw[SC_GUESS + t];
             bool pass = false;
             if (u == t && act && !matched && wu < s) {
+                // the exact evaluation without the reject filters, which never reject a landmark
+                // that passes (the association kernel's replay wave does the same); its status
+                // bits come from the landmark's own thread
                 Cand c;
-                bool sing, amb;
-                gate_of(sh_robl[t], rr0, rr1, rr2, yb, Dj, rc, t, c, pass, sing, amb);
-                if (pass) {
-                    double R33[9];
+                const ekf_line ln = p.lines[t];
+                double Rm[4];
+                line_R(ln, t, p.r_mode, Rm);
+                double R33[9], xp[3];
 #pragma unroll
-                    for (int a = 0; a < 9; a++) R33[a] = sh_robl[t][a];
+                for (int a = 0; a < 9; a++) R33[a] = sh_robl[t][a];
+                xp[0] = sh_robl[t][9]; xp[1] = sh_robl[t][10]; xp[2] = sh_robl[t][11];
+                Block5 b5;
+                fill_block5(b5, R33, rr0, rr1, rr2, Dj);
+                double sn, cs;
+                sincos_near(yb.x, rc[12], rc[13], rc[14], sn, cs);
+                eval_candidate<false>(b5, yb.x, yb.y, sn, cs, xp, ln.alpha, ln.r, Rm, p.gate, ETA, c);
+                pass = c.pass;
+                if (pass) {
                     build_package(c, R33, rr0, rr1, rr2, sh_pk[t]);
                     for (int q = 0; q < m; q++)
 #pragma unroll
